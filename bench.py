@@ -1,0 +1,129 @@
+#!/usr/bin/env python
+"""Headline benchmark: K-Means Lloyd iterations, k=200, 100M x 50 dense fp32 (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]            # 1 GPU
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+
+A "step" is one full Lloyd iteration of the distributed fit (fused MFMA assign kernel over every
+local row + one RCCL allreduce of the fixed-point centroid statistics + the finalize kernel +
+the convergence read-back) — nothing is skipped: tol=0 keeps every iteration doing full work.
+Scaling is STRONG: the global dataset is 100M rows for every N, each rank generating its own
+contiguous shard directly in HBM (synthetic Gaussian blobs, identical values for any N).
+The timed region is bracketed by a barrier + device synchronize on both sides and the MAX over
+ranks is reported.  `value` is whole-job samples/s = global_rows * K / t.  The end-to-end fit()
+wall clock (k-means|| init + Lloyd to convergence, maxIter=20) is reported alongside.
+Other BASELINE configs: --config pca | als | kmeans_bf16 (see bench/).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def _barrier_sync(w):
+    import torch
+
+    if w.size > 1:
+        w.barrier()
+    torch.cuda.synchronize()
+    if w.ctx is not None:
+        w.ctx.sync()
+
+
+def bench_kmeans(args, w):
+    from oap_mllib_amd import _loader
+
+    N = _loader.load()
+    rows_total, d, k = args.rows, args.dim, args.k
+    base, rem = divmod(rows_total, w.size)
+    local = base + (1 if w.rank < rem else 0)
+    row0 = w.rank * base + min(w.rank, rem)
+    ld = N.kmeans_ld(d)
+    t_ing = time.time()
+    table = N.synth_blobs(w.ctx, local, d, ld, row0, k, 10.0, 1.0, 20240917)
+    table.set_global(row0, rows_total)
+    _barrier_sync(w)
+    ingest_s = time.time() - t_ing
+    # initial centers: k-means|| (identical for any world size), untimed
+    t0 = time.time()
+    init = N.kmeans_init(w.ctx, w.comm, table, k, "k-means||", 2, 7)
+    init_s = time.time() - t0
+    # warmup iterations
+    if args.warmup > 0:
+        N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, 0.0)
+    _barrier_sync(w)
+    t0 = time.perf_counter()
+    r = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, 0.0)
+    _barrier_sync(w)
+    el = time.perf_counter() - t0
+    el_max = float(w.allreduce_np(np.array([el]), "max")[0])
+    assert r["num_iter"] == args.steps, r["num_iter"]
+    # end-to-end fit(): init + Lloyd to convergence (maxIter 20, tol 1e-4)
+    fit_s = None
+    if not args.skip_fit:
+        _barrier_sync(w)
+        t1 = time.perf_counter()
+        rf = N.kmeans_fit(w.ctx, w.comm, table, None, k, 20, 1e-4, "k-means||", 2, 7)
+        _barrier_sync(w)
+        fit_s = float(w.allreduce_np(np.array([time.perf_counter() - t1]), "max")[0])
+        fit_iters = rf["num_iter"]
+    m = w.ctx.metrics()["phases"]
+    ak = m.get("kmeans/assign_kernel", {"total_us": 0, "count": 1})
+    ar = m.get("kmeans/allreduce", {"total_us": 0, "count": 1})
+    samples = rows_total * args.steps / el_max
+    flops = 2.0 * rows_total * k * d
+    out = {
+        "metric": "kmeans_samples_per_sec", "value": samples, "unit": "samples/s",
+        "n_gpus": w.size, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": el_max / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (gaussian blobs, on-device)",
+        "config": {"model": "kmeans k=200 d=50 (Lloyd, euclidean)", "global_batch": rows_total,
+                   "seq_len": d, "parallelism": f"dp{w.size}", "k": k,
+                   "rows": rows_total, "dim": d},
+        "extra": {"fit_wall_s_end_to_end": fit_s,
+                  "fit_iters": fit_iters if fit_s is not None else None,
+                  "init_kmeans_parallel_s": init_s, "ingest_synth_s": ingest_s,
+                  "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
+                  "allreduce_us": ar["total_us"] / max(ar["count"], 1),
+                  "achieved_tflops": flops / (el_max / args.steps) / 1e12,
+                  "cost": r["cost"]},
+    }
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="kmeans", choices=["kmeans"])
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--dim", type=int, default=50)
+    ap.add_argument("--k", type=int, default=200)
+    ap.add_argument("--skip-fit", action="store_true")
+    args = ap.parse_args(argv)
+
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and ws != args.gpus:
+        print(f"--gpus {args.gpus} requires a launcher with WORLD_SIZE={args.gpus} "
+              f"(python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py ...)",
+              file=sys.stderr)
+        return 2
+    import oap_mllib_amd as O
+
+    w = O.init_world(O.get_config().replace(device="gpu"))
+    out = bench_kmeans(args, w)
+    if w.rank == 0:
+        print(json.dumps(out), flush=True)
+    O.shutdown_world()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

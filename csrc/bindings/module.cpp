@@ -1,0 +1,442 @@
+// Python bindings for the MI355X-native MLlib engine (pybind11).
+//
+// Plays the role of the reference's JNI surface (mllib-dal/src/main/native/javah/*.h; SURVEY.md
+// §2.8) for the Python API layer: native handles are RAII objects owned by Python (no leaked
+// `new SharedPtr<...>` as in KMeansDALImpl.cpp:245), arrays cross as numpy buffers, and native
+// exceptions become oap_mllib_amd.errors.* Python exceptions instead of exit().
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "bindings/bindings.h"
+#include "comm/comm.h"
+#include "drivers/kmeans.h"
+#include "kernels/kernels.h"
+#include "runtime/context.h"
+#include "runtime/table.h"
+
+namespace py = pybind11;
+using namespace oap;
+
+namespace oap {
+namespace py_bind {
+
+py::dtype np_dtype(DType t) {
+  switch (t) {
+    case DType::F32: return py::dtype::of<float>();
+    case DType::F64: return py::dtype::of<double>();
+    case DType::BF16: return py::dtype("uint16");
+    case DType::I32: return py::dtype::of<int32_t>();
+    case DType::I64: return py::dtype::of<int64_t>();
+    case DType::U8: return py::dtype::of<uint8_t>();
+  }
+  return py::dtype::of<uint8_t>();
+}
+
+const char* op_name(ReduceOp op) {
+  switch (op) {
+    case ReduceOp::Sum: return "sum";
+    case ReduceOp::Max: return "max";
+    case ReduceOp::Min: return "min";
+  }
+  return "sum";
+}
+
+// Non-owning numpy view over a host pointer.
+py::array host_view(void* p, size_t count, DType t) {
+  py::capsule nothing(p, [](void*) {});
+  return py::array(np_dtype(t), {static_cast<py::ssize_t>(count)}, {}, p, nothing);
+}
+
+// Comm implemented by a Python object (torch.distributed / gloo on CPU, or anything exposing
+// allreduce/allgather/alltoallv/bcast/barrier over numpy arrays).
+class HostComm final : public Comm {
+ public:
+  HostComm(py::object impl, int rank, int world) : impl_(std::move(impl)), rank_(rank), world_(world) {}
+  ~HostComm() override {
+    py::gil_scoped_acquire g;
+    impl_ = py::object();
+  }
+  int rank() const override { return rank_; }
+  int size() const override { return world_; }
+  bool on_device() const override { return false; }
+  const char* name() const override { return "host"; }
+  void allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    call("allreduce", host_view(buf, count, dt), op_name(op));
+  }
+  void allgather(const void* send, void* recv, size_t count, DType dt, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    call("allgather", host_view(const_cast<void*>(send), count, dt),
+         host_view(recv, count * world_, dt));
+  }
+  void alltoallv(const void* send, const std::vector<size_t>& sc, void* recv,
+                 const std::vector<size_t>& rc, DType dt, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    size_t sn = 0, rn = 0;
+    for (auto c : sc) sn += c;
+    for (auto c : rc) rn += c;
+    call("alltoallv", host_view(const_cast<void*>(send), sn, dt), py::cast(sc),
+         host_view(recv, rn, dt), py::cast(rc));
+  }
+  void bcast(void* buf, size_t count, DType dt, int root, hipStream_t) override {
+    py::gil_scoped_acquire g;
+    call("bcast", host_view(buf, count, dt), root);
+  }
+  void barrier() override {
+    py::gil_scoped_acquire g;
+    call("barrier");
+  }
+
+ private:
+  template <typename... A>
+  void call(const char* m, A&&... args) {
+    try {
+      impl_.attr(m)(std::forward<A>(args)...);
+    } catch (py::error_already_set& e) {
+      throw CommError(std::string("host comm ") + m + " failed: " + e.what());
+    }
+  }
+  py::object impl_;
+  int rank_, world_;
+};
+
+DType parse_dtype(const std::string& s) {
+  if (s == "f32" || s == "float32") return DType::F32;
+  if (s == "f64" || s == "float64") return DType::F64;
+  if (s == "bf16" || s == "bfloat16") return DType::BF16;
+  if (s == "i32" || s == "int32") return DType::I32;
+  if (s == "i64" || s == "int64") return DType::I64;
+  throw ConfigError("unknown dtype '" + s + "'");
+}
+
+py::dict metrics_dict(Context& ctx) {
+  py::dict phases;
+  for (auto& kv : ctx.metrics().phases()) {
+    py::dict e;
+    e["count"] = kv.second.count;
+    e["total_us"] = kv.second.total_us;
+    e["max_us"] = kv.second.max_us;
+    e["bytes"] = kv.second.bytes;
+    phases[py::str(kv.first)] = e;
+  }
+  py::dict vals;
+  for (auto& kv : ctx.metrics().values()) vals[py::str(kv.first)] = kv.second;
+  py::dict out;
+  out["phases"] = phases;
+  out["values"] = vals;
+  if (ctx.is_gpu()) {
+    py::dict arena;
+    arena["used"] = ctx.arena()->used();
+    arena["peak"] = ctx.arena()->peak();
+    arena["reserved"] = ctx.arena()->reserved();
+    arena["budget"] = ctx.arena()->budget();
+    out["arena"] = arena;
+  }
+  return out;
+}
+
+}  // namespace py_bind
+}  // namespace oap
+
+using namespace oap::py_bind;
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "MI355X-native (gfx950) K-Means / PCA / ALS engine";
+
+  // ---------------------------------------------------------------- exceptions
+  static py::exception<Error> exc_base(m, "OapError");
+  static py::exception<DeviceError> exc_dev(m, "DeviceError", exc_base.ptr());
+  static py::exception<CommError> exc_comm(m, "CommError", exc_base.ptr());
+  static py::exception<ConfigError> exc_cfg(m, "ConfigError", exc_base.ptr());
+  static py::exception<OutOfMemoryError> exc_oom(m, "OutOfMemoryError", exc_base.ptr());
+  py::register_exception_translator([](std::exception_ptr p) {
+    try {
+      if (p) std::rethrow_exception(p);
+    } catch (const OutOfMemoryError& e) {
+      py::set_error(exc_oom, e.what());
+    } catch (const ConfigError& e) {
+      py::set_error(exc_cfg, e.what());
+    } catch (const CommError& e) {
+      py::set_error(exc_comm, e.what());
+    } catch (const DeviceError& e) {
+      py::set_error(exc_dev, e.what());
+    } catch (const Error& e) {
+      py::set_error(exc_base, e.what());
+    }
+  });
+
+  // ---------------------------------------------------------------- runtime
+  m.def("visible_device_count", &visible_device_count);
+  m.def("rccl_available", &rccl_available);
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def(
+      "configure_logging",
+      [](int rank, int device, const std::string& level, const std::string& path) {
+        LogLevel l = LogLevel::Warn;
+        if (level == "debug") l = LogLevel::Debug;
+        else if (level == "info") l = LogLevel::Info;
+        else if (level == "warn") l = LogLevel::Warn;
+        else if (level == "error") l = LogLevel::Error;
+        else if (level == "off") l = LogLevel::Off;
+        Logger::instance().configure(rank, device, l, path);
+      },
+      py::arg("rank"), py::arg("device"), py::arg("level") = "warn", py::arg("path") = "");
+  m.def("log", [](const std::string& level, const std::string& phase, const std::string& fields) {
+    LogLevel l = level == "error" ? LogLevel::Error
+                 : level == "warn" ? LogLevel::Warn
+                 : level == "debug" ? LogLevel::Debug
+                                    : LogLevel::Info;
+    Logger::instance().log(l, phase, fields);
+  });
+  m.def("roctx_push", [](const std::string& s) { roctx_push(s.c_str()); });
+  m.def("roctx_pop", []() { roctx_pop(); });
+
+  py::class_<Context, std::shared_ptr<Context>>(m, "Context")
+      .def(py::init<int, double, int>(), py::arg("device") = -1, py::arg("hbm_fraction") = 0.9,
+           py::arg("cpu_threads") = 0)
+      .def_property_readonly("is_gpu", &Context::is_gpu)
+      .def_property_readonly("device", &Context::device)
+      .def_property_readonly("info",
+                             [](Context& c) {
+                               py::dict d;
+                               auto& i = c.info();
+                               d["id"] = i.id;
+                               d["name"] = i.name;
+                               d["arch"] = i.arch;
+                               d["cu_count"] = i.cu_count;
+                               d["total_mem"] = i.total_mem;
+                               d["free_mem"] = i.free_mem;
+                               d["lds_per_block"] = i.lds_per_block;
+                               d["warp_size"] = i.warp_size;
+                               return d;
+                             })
+      .def("metrics", [](Context& c) { return metrics_dict(c); })
+      .def("reset_metrics", [](Context& c) { c.metrics().reset(); })
+      .def("sync", [](Context& c) {
+        py::gil_scoped_release r;
+        c.sync_all();
+      })
+      .def("trim", [](Context& c) {
+        if (c.is_gpu()) c.arena()->trim();
+      });
+
+  // ---------------------------------------------------------------- comms
+  py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("size", &Comm::size)
+      .def_property_readonly("on_device", &Comm::on_device)
+      .def_property_readonly("name", [](Comm& c) { return std::string(c.name()); })
+      .def("barrier",
+           [](Comm& c) {
+             py::gil_scoped_release r;
+             c.barrier();
+           })
+      .def("abort", &Comm::abort)
+      .def(
+          "allreduce_f64",
+          [](Comm& c, std::shared_ptr<Context> ctx, py::array_t<double> a, const std::string& op) {
+            auto buf = a.request(true);
+            ReduceOp o = op == "max" ? ReduceOp::Max : op == "min" ? ReduceOp::Min : ReduceOp::Sum;
+            double* p = static_cast<double*>(buf.ptr);
+            size_t n = static_cast<size_t>(buf.size);
+            py::gil_scoped_release r;
+            if (!c.on_device()) {
+              c.allreduce(p, n, DType::F64, o, nullptr);
+            } else {
+              Buffer d = ctx->alloc(n * 8);
+              hipStream_t s = ctx->comm_stream();
+              OAP_HIP_CHECK(hipMemcpyAsync(d.data(), p, n * 8, hipMemcpyHostToDevice, s));
+              c.allreduce(d.data(), n, DType::F64, o, s);
+              OAP_HIP_CHECK(hipMemcpyAsync(p, d.data(), n * 8, hipMemcpyDeviceToHost, s));
+              c.wait(s);
+            }
+          },
+          py::arg("ctx"), py::arg("array"), py::arg("op") = "sum");
+  py::class_<LocalComm, Comm, std::shared_ptr<LocalComm>>(m, "LocalComm")
+      .def(py::init<bool>(), py::arg("device") = false);
+  py::class_<RcclComm, Comm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int world, int rank, int device, double timeout) {
+             std::string id = uid;
+             py::gil_scoped_release r;
+             return std::make_shared<RcclComm>(id, world, rank, device, timeout);
+           }),
+           py::arg("unique_id"), py::arg("world"), py::arg("rank"), py::arg("device"),
+           py::arg("timeout_s") = 600.0);
+  py::class_<HostComm, Comm, std::shared_ptr<HostComm>>(m, "HostComm")
+      .def(py::init<py::object, int, int>(), py::arg("impl"), py::arg("rank"), py::arg("world"));
+
+  // ---------------------------------------------------------------- tables
+  py::class_<DenseTable, std::shared_ptr<DenseTable>>(m, "DenseTable")
+      .def_readonly("rows", &DenseTable::rows)
+      .def_readonly("cols", &DenseTable::cols)
+      .def_readonly("ld", &DenseTable::ld)
+      .def_readonly("global_offset", &DenseTable::global_offset)
+      .def_readonly("global_rows", &DenseTable::global_rows)
+      .def_property_readonly("dtype", [](DenseTable& t) { return std::string(dtype_name(t.dtype)); })
+      .def_property_readonly("nbytes", &DenseTable::bytes)
+      .def_property_readonly("on_gpu", [](DenseTable& t) { return t.backend == Backend::GPU; })
+      .def("to_numpy",
+           [](DenseTable& t, std::shared_ptr<Context> ctx, int64_t r0, int64_t n) {
+             if (n < 0) n = t.rows - r0;
+             std::vector<double> v;
+             {
+               py::gil_scoped_release r;
+               v = table_rows_f64(*ctx, t, r0, n);
+             }
+             py::array_t<double> out({n, int64_t(t.cols)});
+             if (!v.empty()) std::memcpy(out.mutable_data(), v.data(), v.size() * 8);
+             return out;
+           },
+           py::arg("ctx"), py::arg("start") = 0, py::arg("count") = -1)
+      .def("set_global", [](DenseTable& t, int64_t off, int64_t tot) {
+        t.global_offset = off;
+        t.global_rows = tot;
+      });
+
+  m.def(
+      "upload_dense",
+      [](std::shared_ptr<Context> ctx, py::array arr, const std::string& storage, int64_t ld) {
+        py::buffer_info bi = arr.request();
+        if (bi.ndim != 2) throw ConfigError("upload_dense expects a 2-D array");
+        DType src;
+        if (bi.format == py::format_descriptor<double>::format()) src = DType::F64;
+        else if (bi.format == py::format_descriptor<float>::format()) src = DType::F32;
+        else throw ConfigError("upload_dense: array must be float32 or float64");
+        int64_t rows = bi.shape[0], cols = bi.shape[1];
+        size_t es = static_cast<size_t>(bi.itemsize);
+        if (bi.strides[1] != static_cast<py::ssize_t>(es) ||
+            bi.strides[0] % static_cast<py::ssize_t>(es) != 0)
+          throw ConfigError("upload_dense: array must be row-major (C-contiguous rows)");
+        int64_t src_ld = bi.strides[0] / static_cast<int64_t>(es);
+        if (ld <= 0) ld = cols;
+        DType st = parse_dtype(storage);
+        auto t = std::make_shared<DenseTable>();
+        {
+          py::gil_scoped_release r;
+          *t = upload_dense(*ctx, bi.ptr, src, rows, static_cast<int>(cols), src_ld, st, ld);
+        }
+        return t;
+      },
+      py::arg("ctx"), py::arg("array"), py::arg("storage") = "f32", py::arg("ld") = 0);
+  m.def(
+      "synth_blobs",
+      [](std::shared_ptr<Context> ctx, int64_t rows, int cols, int64_t ld, int64_t row0,
+         int ncenters, double box, double sigma, uint64_t seed) {
+        auto t = std::make_shared<DenseTable>();
+        py::gil_scoped_release r;
+        *t = synth_blobs_table(*ctx, rows, cols, ld <= 0 ? cols : ld, row0, ncenters, box, sigma,
+                               seed);
+        return t;
+      },
+      py::arg("ctx"), py::arg("rows"), py::arg("cols"), py::arg("ld") = 0, py::arg("row0") = 0,
+      py::arg("ncenters") = 8, py::arg("box") = 10.0, py::arg("sigma") = 1.0,
+      py::arg("seed") = 42);
+  m.def("assign_global_offsets",
+        [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t) {
+          py::gil_scoped_release r;
+          assign_global_offsets(*ctx, *comm, *t);
+        });
+
+  // ---------------------------------------------------------------- K-Means
+  m.def("kmeans_ld", &kern::kmeans_ld);
+  m.def(
+      "kmeans_fit",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
+         py::object init_centers, int k, int max_iter, double tol, const std::string& init_mode,
+         int init_steps, uint64_t seed) {
+        KMeansParams p;
+        p.k = k;
+        p.max_iter = max_iter;
+        p.tol = tol;
+        p.init_steps = init_steps;
+        p.seed = seed;
+        std::vector<double> init;
+        if (!init_centers.is_none()) {
+          auto a = py::array_t<double, py::array::c_style | py::array::forcecast>(init_centers);
+          init.assign(a.data(), a.data() + a.size());
+          p.init = KMeansInit::Given;
+        } else if (init_mode == "random") {
+          p.init = KMeansInit::Random;
+        } else if (init_mode == "k-means||") {
+          p.init = KMeansInit::Parallel;
+        } else {
+          throw ConfigError("unknown initMode '" + init_mode + "'");
+        }
+        KMeansResult r;
+        {
+          py::gil_scoped_release rel;
+          r = kmeans_fit(*ctx, *comm, *t, init, p);
+        }
+        py::dict out;
+        py::array_t<double> c({int64_t(r.k), int64_t(r.d)});
+        if (!r.centers.empty()) std::memcpy(c.mutable_data(), r.centers.data(), r.centers.size() * 8);
+        out["centers"] = c;
+        out["cost"] = r.cost;
+        out["num_iter"] = r.num_iter;
+        out["converged"] = r.converged;
+        out["cost_history"] = r.cost_history;
+        out["last_counts"] = r.last_counts;
+        out["init_seconds"] = r.init_seconds;
+        out["iter_seconds"] = r.iter_seconds;
+        out["global_rows"] = r.global_rows;
+        return out;
+      },
+      py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),
+      py::arg("k") = 2, py::arg("max_iter") = 20, py::arg("tol") = 1e-4,
+      py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1);
+  m.def(
+      "kmeans_init",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
+         int k, const std::string& init_mode, int init_steps, uint64_t seed) {
+        KMeansParams p;
+        p.k = k;
+        p.init_steps = init_steps;
+        p.seed = seed;
+        p.init = init_mode == "random" ? KMeansInit::Random : KMeansInit::Parallel;
+        int keff = 0;
+        std::vector<double> c;
+        {
+          py::gil_scoped_release rel;
+          c = kmeans_init_centers(*ctx, *comm, *t, p, &keff);
+        }
+        py::array_t<double> out({int64_t(keff), int64_t(t->cols)});
+        if (!c.empty()) std::memcpy(out.mutable_data(), c.data(), c.size() * 8);
+        return out;
+      },
+      py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("k"),
+      py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1);
+  m.def(
+      "kmeans_predict",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> centers) {
+        auto c = py::array_t<double, py::array::c_style | py::array::forcecast>(centers);
+        if (c.ndim() != 2 || c.shape(1) != t->cols)
+          throw ConfigError("centers must be k x d with d == table cols");
+        int k = static_cast<int>(c.shape(0));
+        std::vector<double> cv(c.data(), c.data() + c.size());
+        py::array_t<int32_t> labels(t->rows);
+        py::array_t<double> dist(t->rows);
+        int32_t* lp = labels.mutable_data();
+        double* dp = dist.mutable_data();
+        {
+          py::gil_scoped_release rel;
+          kmeans_predict(*ctx, *t, cv, k, lp, dp);
+        }
+        return py::make_tuple(labels, dist);
+      });
+  m.def("local_kmeans_pp",
+        [](py::array_t<double> pts, py::array_t<double> w, int k, int max_iter, uint64_t seed) {
+          auto p = py::array_t<double, py::array::c_style | py::array::forcecast>(pts);
+          std::vector<double> pv(p.data(), p.data() + p.size()), wv(w.data(), w.data() + w.size());
+          int d = static_cast<int>(p.shape(1));
+          auto c = local_kmeans_pp(pv, wv, d, k, max_iter, seed);
+          py::array_t<double> out({int64_t(k), int64_t(d)});
+          std::memcpy(out.mutable_data(), c.data(), c.size() * 8);
+          return out;
+        });
+
+  register_pca(m);
+  register_als(m);
+}

@@ -1,0 +1,322 @@
+#include "comm/comm.h"
+
+#include <rccl/rccl.h>
+#include <unistd.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <sstream>
+#include <thread>
+
+namespace oap {
+
+// ------------------------------------------------------------------------------------ Comm
+void Comm::wait(hipStream_t s) {
+  if (s) OAP_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+// ------------------------------------------------------------------------------- LocalComm
+void LocalComm::allgather(const void* send, void* recv, size_t count, DType dt, hipStream_t s) {
+  size_t bytes = count * dtype_size(dt);
+  if (send == recv || bytes == 0) return;
+  if (device_) {
+    OAP_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+  } else {
+    std::memmove(recv, send, bytes);
+  }
+}
+
+void LocalComm::alltoallv(const void* send, const std::vector<size_t>& send_counts, void* recv,
+                          const std::vector<size_t>& recv_counts, DType dt, hipStream_t s) {
+  OAP_CHECK(send_counts.size() == 1 && recv_counts.size() == 1 &&
+                send_counts[0] == recv_counts[0],
+            "LocalComm::alltoallv: inconsistent counts");
+  allgather(send, recv, send_counts[0], dt, s);
+}
+
+// -------------------------------------------------------------------------------- RCCL
+namespace {
+ncclDataType_t to_nccl(DType t) {
+  switch (t) {
+    case DType::F32: return ncclFloat32;
+    case DType::F64: return ncclFloat64;
+    case DType::BF16: return ncclBfloat16;
+    case DType::I32: return ncclInt32;
+    case DType::I64: return ncclInt64;
+    case DType::U8: return ncclUint8;
+  }
+  return ncclUint8;
+}
+ncclRedOp_t to_nccl(ReduceOp op) {
+  switch (op) {
+    case ReduceOp::Sum: return ncclSum;
+    case ReduceOp::Max: return ncclMax;
+    case ReduceOp::Min: return ncclMin;
+  }
+  return ncclSum;
+}
+#define OAP_NCCL_CHECK(expr)                                                                   \
+  do {                                                                                         \
+    ncclResult_t _r = (expr);                                                                  \
+    if (_r != ncclSuccess)                                                                     \
+      ::oap::detail::raise<::oap::CommError>(__FILE__, __LINE__,                               \
+                                             std::string(#expr) + ": " +                       \
+                                                 ncclGetErrorString(_r));                      \
+  } while (0)
+}  // namespace
+
+bool rccl_available() {
+  int v = 0;
+  return ncclGetVersion(&v) == ncclSuccess && v > 0;
+}
+
+std::string rccl_unique_id() {
+  ncclUniqueId id;
+  OAP_NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+RcclComm::RcclComm(const std::string& unique_id, int world, int rank, int device,
+                   double timeout_s)
+    : world_(world), rank_(rank), device_(device), timeout_s_(timeout_s) {
+  OAP_CHECK(unique_id.size() == sizeof(ncclUniqueId),
+            "RCCL unique id must be " << sizeof(ncclUniqueId) << " bytes, got "
+                                      << unique_id.size());
+  OAP_CHECK(rank >= 0 && rank < world, "bad rank " << rank << " for world " << world);
+  ncclUniqueId id;
+  std::memcpy(id.internal, unique_id.data(), sizeof(id.internal));
+  OAP_HIP_CHECK(hipSetDevice(device));
+  ncclComm_t c = nullptr;
+  OAP_NCCL_CHECK(ncclCommInitRank(&c, world, id, rank));
+  comm_ = c;
+  OAP_HIP_CHECK(hipMalloc(&barrier_buf_, 64));
+  OAP_HIP_CHECK(hipStreamCreateWithFlags(&barrier_stream_, hipStreamNonBlocking));
+  std::ostringstream os;
+  os << "\"world\":" << world << ",\"device\":" << device;
+  Logger::instance().log(LogLevel::Info, "comm/rccl_init", os.str());
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ && !aborted_) (void)ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+  if (barrier_buf_) (void)hipFree(barrier_buf_);
+  if (barrier_stream_) (void)hipStreamDestroy(barrier_stream_);
+}
+
+void RcclComm::check_async() {
+  if (aborted_) OAP_THROW(CommError, "RCCL communicator was aborted");
+  ncclResult_t r = ncclSuccess;
+  OAP_NCCL_CHECK(ncclCommGetAsyncError(static_cast<ncclComm_t>(comm_), &r));
+  if (r != ncclSuccess && r != ncclInProgress)
+    OAP_THROW(CommError, "RCCL async error: " << ncclGetErrorString(r));
+}
+
+void RcclComm::allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t s) {
+  check_async();
+  if (count == 0) return;
+  OAP_NCCL_CHECK(ncclAllReduce(buf, buf, count, to_nccl(dt), to_nccl(op),
+                               static_cast<ncclComm_t>(comm_), s));
+}
+
+void RcclComm::allgather(const void* send, void* recv, size_t count, DType dt, hipStream_t s) {
+  check_async();
+  if (count == 0) return;
+  OAP_NCCL_CHECK(
+      ncclAllGather(send, recv, count, to_nccl(dt), static_cast<ncclComm_t>(comm_), s));
+}
+
+void RcclComm::alltoallv(const void* send, const std::vector<size_t>& send_counts, void* recv,
+                         const std::vector<size_t>& recv_counts, DType dt, hipStream_t s) {
+  check_async();
+  OAP_CHECK(static_cast<int>(send_counts.size()) == world_ &&
+                static_cast<int>(recv_counts.size()) == world_,
+            "alltoallv: counts must have one entry per rank");
+  size_t es = dtype_size(dt);
+  auto c = static_cast<ncclComm_t>(comm_);
+  OAP_NCCL_CHECK(ncclGroupStart());
+  size_t soff = 0, roff = 0;
+  for (int p = 0; p < world_; ++p) {
+    if (send_counts[p])
+      OAP_NCCL_CHECK(ncclSend(static_cast<const char*>(send) + soff * es, send_counts[p],
+                              to_nccl(dt), p, c, s));
+    if (recv_counts[p])
+      OAP_NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + roff * es, recv_counts[p], to_nccl(dt),
+                              p, c, s));
+    soff += send_counts[p];
+    roff += recv_counts[p];
+  }
+  OAP_NCCL_CHECK(ncclGroupEnd());
+}
+
+void RcclComm::bcast(void* buf, size_t count, DType dt, int root, hipStream_t s) {
+  check_async();
+  if (count == 0) return;
+  OAP_NCCL_CHECK(
+      ncclBroadcast(buf, buf, count, to_nccl(dt), root, static_cast<ncclComm_t>(comm_), s));
+}
+
+void RcclComm::group_start() { OAP_NCCL_CHECK(ncclGroupStart()); }
+void RcclComm::group_end() { OAP_NCCL_CHECK(ncclGroupEnd()); }
+
+void RcclComm::barrier() {
+  OAP_HIP_CHECK(hipSetDevice(device_));
+  allreduce(barrier_buf_, 1, DType::I32, ReduceOp::Sum, barrier_stream_);
+  wait(barrier_stream_);
+}
+
+void RcclComm::wait(hipStream_t s) {
+  if (timeout_s_ <= 0) {
+    OAP_HIP_CHECK(hipStreamSynchronize(s));
+    check_async();
+    return;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  int spins = 0;
+  for (;;) {
+    hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) OAP_HIP_CHECK(q);
+    check_async();
+    double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > timeout_s_) {
+      std::ostringstream os;
+      os << "\"timeout_s\":" << timeout_s_;
+      Logger::instance().log(LogLevel::Error, "comm/watchdog_timeout", os.str());
+      abort();
+      OAP_THROW(CommError, "collective watchdog: stream not finished after "
+                               << timeout_s_ << " s (rank " << rank_
+                               << "); communicator aborted");
+    }
+    // Spin briefly (collectives are usually µs), then back off to keep a core free.
+    if (++spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+void RcclComm::abort() {
+  if (comm_ && !aborted_) {
+    (void)ncclCommAbort(static_cast<ncclComm_t>(comm_));
+    aborted_ = true;
+  }
+}
+
+// -------------------------------------------------------------------------------- helpers
+namespace {
+bool need_stage(Context& ctx, Comm& comm) { return ctx.is_gpu() && !comm.on_device(); }
+}  // namespace
+
+void comm_allreduce(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, ReduceOp op,
+                    hipStream_t s) {
+  if (comm.size() == 1 || count == 0) return;
+  if (!need_stage(ctx, comm)) {
+    comm.allreduce(buf, count, dt, op, s);
+    return;
+  }
+  size_t bytes = count * dtype_size(dt);
+  Buffer h = Buffer::pinned(bytes);
+  OAP_HIP_CHECK(hipMemcpyAsync(h.data(), buf, bytes, hipMemcpyDeviceToHost, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+  comm.allreduce(h.data(), count, dt, op, nullptr);
+  OAP_HIP_CHECK(hipMemcpyAsync(buf, h.data(), bytes, hipMemcpyHostToDevice, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void comm_allgather(Context& ctx, Comm& comm, const void* send, void* recv, size_t count,
+                    DType dt, hipStream_t s) {
+  size_t bytes = count * dtype_size(dt);
+  if (!need_stage(ctx, comm)) {
+    comm.allgather(send, recv, count, dt, s);
+    return;
+  }
+  Buffer hs = Buffer::pinned(bytes), hr = Buffer::pinned(bytes * comm.size());
+  OAP_HIP_CHECK(hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+  comm.allgather(hs.data(), hr.data(), count, dt, nullptr);
+  OAP_HIP_CHECK(
+      hipMemcpyAsync(recv, hr.data(), bytes * comm.size(), hipMemcpyHostToDevice, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void comm_alltoallv(Context& ctx, Comm& comm, const void* send,
+                    const std::vector<size_t>& send_counts, void* recv,
+                    const std::vector<size_t>& recv_counts, DType dt, hipStream_t s) {
+  if (!need_stage(ctx, comm)) {
+    comm.alltoallv(send, send_counts, recv, recv_counts, dt, s);
+    return;
+  }
+  size_t es = dtype_size(dt), sn = 0, rn = 0;
+  for (auto c : send_counts) sn += c;
+  for (auto c : recv_counts) rn += c;
+  Buffer hs = Buffer::pinned(sn * es), hr = Buffer::pinned(rn * es);
+  OAP_HIP_CHECK(hipMemcpyAsync(hs.data(), send, sn * es, hipMemcpyDeviceToHost, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+  comm.alltoallv(hs.data(), send_counts, hr.data(), recv_counts, dt, nullptr);
+  OAP_HIP_CHECK(hipMemcpyAsync(recv, hr.data(), rn * es, hipMemcpyHostToDevice, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void comm_bcast(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, int root,
+                hipStream_t s) {
+  if (comm.size() == 1 || count == 0) return;
+  if (!need_stage(ctx, comm)) {
+    comm.bcast(buf, count, dt, root, s);
+    return;
+  }
+  size_t bytes = count * dtype_size(dt);
+  Buffer h = Buffer::pinned(bytes);
+  OAP_HIP_CHECK(hipMemcpyAsync(h.data(), buf, bytes, hipMemcpyDeviceToHost, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+  comm.bcast(h.data(), count, dt, root, nullptr);
+  OAP_HIP_CHECK(hipMemcpyAsync(buf, h.data(), bytes, hipMemcpyHostToDevice, s));
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+}
+
+double comm_allreduce_scalar(Context& ctx, Comm& comm, double v, ReduceOp op) {
+  if (comm.size() == 1) return v;
+  if (comm.on_device()) {
+    Buffer d = ctx.alloc(sizeof(double));
+    hipStream_t s = ctx.comm_stream();
+    OAP_HIP_CHECK(hipMemcpyAsync(d.data(), &v, sizeof(double), hipMemcpyHostToDevice, s));
+    comm.allreduce(d.data(), 1, DType::F64, op, s);
+    OAP_HIP_CHECK(hipMemcpyAsync(&v, d.data(), sizeof(double), hipMemcpyDeviceToHost, s));
+    comm.wait(s);
+    return v;
+  }
+  comm.allreduce(&v, 1, DType::F64, op, nullptr);
+  return v;
+}
+
+std::vector<int64_t> comm_allgather_i64(Context& ctx, Comm& comm, int64_t v) {
+  std::vector<int64_t> out(comm.size(), v);
+  if (comm.size() == 1) return out;
+  if (comm.on_device()) {
+    Buffer d = ctx.alloc(sizeof(int64_t) * (comm.size() + 1));
+    hipStream_t s = ctx.comm_stream();
+    int64_t* dp = d.as<int64_t>();
+    OAP_HIP_CHECK(hipMemcpyAsync(dp, &v, sizeof(int64_t), hipMemcpyHostToDevice, s));
+    comm.allgather(dp, dp + 1, 1, DType::I64, s);
+    OAP_HIP_CHECK(hipMemcpyAsync(out.data(), dp + 1, sizeof(int64_t) * comm.size(),
+                                 hipMemcpyDeviceToHost, s));
+    comm.wait(s);
+    return out;
+  }
+  comm.allgather(&v, out.data(), 1, DType::I64, nullptr);
+  return out;
+}
+
+// ------------------------------------------------------------------------- fault injection
+void maybe_inject_fault(int rank, const char* phase, int iteration) {
+  static const char* spec = std::getenv("OAP_MLLIB_FAULT");
+  if (!spec || !*spec) return;
+  int r = -1, it = -1;
+  char ph[64] = {0};
+  if (std::sscanf(spec, "%d:%63[^:]:%d", &r, ph, &it) != 3) return;
+  if (r != rank || it != iteration || std::strcmp(ph, phase) != 0) return;
+  const char* mode = std::getenv("OAP_MLLIB_FAULT_MODE");
+  std::ostringstream os;
+  os << "\"iteration\":" << iteration << ",\"mode\":\"" << (mode ? mode : "raise") << "\"";
+  Logger::instance().log(LogLevel::Error, std::string("fault/") + phase, os.str());
+  if (mode && std::strcmp(mode, "exit") == 0) _exit(17);
+  OAP_THROW(CommError, "injected fault at rank " << rank << " phase " << phase << " iteration "
+                                                   << iteration);
+}
+
+}  // namespace oap

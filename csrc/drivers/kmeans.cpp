@@ -1,0 +1,771 @@
+#include "drivers/kmeans.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <random>
+#include <set>
+#include <sstream>
+#include <unordered_map>
+
+#include "kernels/kernels.h"
+
+namespace oap {
+
+namespace {
+
+using u64 = unsigned long long;
+
+double seconds_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// Host buffer collectives that work with device- or host-buffer comms.
+void host_allreduce(Context& ctx, Comm& comm, void* host, size_t count, DType dt, ReduceOp op) {
+  if (comm.size() == 1 || count == 0) return;
+  if (!comm.on_device()) {
+    comm.allreduce(host, count, dt, op, nullptr);
+    return;
+  }
+  size_t bytes = count * dtype_size(dt);
+  Buffer d = ctx.alloc(bytes);
+  hipStream_t s = ctx.comm_stream();
+  OAP_HIP_CHECK(hipMemcpyAsync(d.data(), host, bytes, hipMemcpyHostToDevice, s));
+  comm.allreduce(d.data(), count, dt, op, s);
+  OAP_HIP_CHECK(hipMemcpyAsync(host, d.data(), bytes, hipMemcpyDeviceToHost, s));
+  comm.wait(s);
+}
+
+// Gathers a variable number of f64 rows (cols wide) from every rank, rank-major.
+std::vector<double> host_allgatherv_rows(Context& ctx, Comm& comm, const std::vector<double>& mine,
+                                         int cols) {
+  int64_t my_rows = cols ? int64_t(mine.size()) / cols : 0;
+  if (comm.size() == 1) return mine;
+  auto counts = comm_allgather_i64(ctx, comm, my_rows);
+  int64_t mx = 0;
+  for (auto c : counts) mx = std::max(mx, c);
+  if (mx == 0) return {};
+  std::vector<double> send(size_t(mx) * cols, 0.0), recv(size_t(mx) * cols * comm.size());
+  std::copy(mine.begin(), mine.end(), send.begin());
+  size_t cnt = size_t(mx) * cols;
+  if (comm.on_device()) {
+    Buffer ds = ctx.alloc(cnt * 8), dr = ctx.alloc(cnt * 8 * comm.size());
+    hipStream_t s = ctx.comm_stream();
+    OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send.data(), cnt * 8, hipMemcpyHostToDevice, s));
+    comm.allgather(ds.data(), dr.data(), cnt, DType::F64, s);
+    OAP_HIP_CHECK(
+        hipMemcpyAsync(recv.data(), dr.data(), recv.size() * 8, hipMemcpyDeviceToHost, s));
+    comm.wait(s);
+  } else {
+    comm.allgather(send.data(), recv.data(), cnt, DType::F64, nullptr);
+  }
+  std::vector<double> out;
+  for (int r = 0; r < comm.size(); ++r)
+    out.insert(out.end(), recv.begin() + size_t(r) * cnt,
+               recv.begin() + size_t(r) * cnt + size_t(counts[r]) * cols);
+  return out;
+}
+
+struct FixedPoint {
+  std::vector<float> scale;       // 2^e_f
+  std::vector<double> inv_scale;  // 2^-e_f
+};
+
+FixedPoint fixed_point_scales(const std::vector<double>& absmax, int64_t global_rows) {
+  FixedPoint fp;
+  int d = static_cast<int>(absmax.size());
+  fp.scale.resize(d);
+  fp.inv_scale.resize(d);
+  int ln = static_cast<int>(std::ceil(std::log2(double(std::max<int64_t>(global_rows, 2)))));
+  for (int f = 0; f < d; ++f) {
+    int e = 0;
+    if (absmax[f] > 0 && std::isfinite(absmax[f])) {
+      int lm = static_cast<int>(std::ceil(std::log2(absmax[f])));
+      e = 61 - ln - lm;
+      e = std::max(-100, std::min(120, e));
+    }
+    fp.scale[f] = std::ldexp(1.0f, e);
+    fp.inv_scale[f] = std::ldexp(1.0, -e);
+  }
+  return fp;
+}
+
+inline double table_at(const DenseTable& t, int64_t r, int c) {
+  return t.dtype == DType::F64 ? t.data.as<double>()[size_t(r) * t.ld + c]
+                               : double(t.data.as<float>()[size_t(r) * t.ld + c]);
+}
+
+// ---------------------------------------------------------------------------- CPU engine
+struct CpuAssignOut {
+  std::vector<int64_t> sums;    // k*d fixed point (when accumulate)
+  std::vector<int64_t> counts;  // k
+  double cost = 0.0;
+};
+
+// Exact fp64 distances; lowest index wins ties (Spark findClosest semantics).
+CpuAssignOut cpu_assign(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
+                        int k, const FixedPoint* fp, bool accumulate, bool sums_too,
+                        int32_t* labels, double* dist2) {
+  const int d = x.cols;
+  const int P = ctx.pool().size();
+  std::vector<CpuAssignOut> part(P);
+  ctx.pool().parallel_for(x.rows, [&](int ci, int64_t b, int64_t e) {
+    CpuAssignOut& o = part[ci];
+    if (accumulate) {
+      o.counts.assign(k, 0);
+      if (sums_too) o.sums.assign(size_t(k) * d, 0);
+    }
+    std::vector<double> xr(d);
+    for (int64_t r = b; r < e; ++r) {
+      for (int f = 0; f < d; ++f) xr[f] = table_at(x, r, f);
+      double best = std::numeric_limits<double>::infinity();
+      int bi = 0;
+      for (int c = 0; c < k; ++c) {
+        const double* cr = centers.data() + size_t(c) * d;
+        double acc = 0.0;
+        for (int f = 0; f < d; ++f) {
+          double df = xr[f] - cr[f];
+          acc += df * df;
+        }
+        if (acc < best) {
+          best = acc;
+          bi = c;
+        }
+      }
+      if (labels) labels[r] = bi;
+      if (dist2) dist2[r] = best;
+      o.cost += best;
+      if (accumulate) {
+        o.counts[bi] += 1;
+        if (sums_too)
+          for (int f = 0; f < d; ++f)
+            o.sums[size_t(bi) * d + f] += static_cast<int64_t>(
+                std::llrint(xr[f] * double(fp->scale[f])));
+      }
+    }
+  });
+  CpuAssignOut out;
+  if (accumulate) {
+    out.counts.assign(k, 0);
+    if (sums_too) out.sums.assign(size_t(k) * d, 0);
+  }
+  for (auto& o : part) {  // chunk order => deterministic cost
+    out.cost += o.cost;
+    if (!accumulate || o.counts.empty()) continue;
+    for (int c = 0; c < k; ++c) out.counts[c] += o.counts[c];
+    if (sums_too)
+      for (size_t i = 0; i < out.sums.size(); ++i)
+        out.sums[i] = static_cast<int64_t>(static_cast<u64>(out.sums[i]) +
+                                           static_cast<u64>(o.sums[i]));
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------- GPU helpers
+struct GpuCenters {
+  Buffer c32, cnorm;
+  int k = 0, kpad = 0;
+};
+
+GpuCenters upload_centers(Context& ctx, const std::vector<double>& centers, int k, int d) {
+  GpuCenters g;
+  g.k = k;
+  g.kpad = static_cast<int>(round_up(std::max(k, 1), 32));
+  Buffer c64 = ctx.alloc(sizeof(double) * size_t(k) * d);
+  ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * size_t(k) * d);
+  g.c32 = ctx.alloc(sizeof(float) * size_t(k) * d);
+  g.cnorm = ctx.alloc(sizeof(float) * g.kpad);
+  kern::kmeans_prepare_centers(c64.as<double>(), k, d, g.c32.as<float>(), g.cnorm.as<float>(),
+                               g.kpad, ctx.compute());
+  OAP_HIP_CHECK(hipStreamSynchronize(ctx.compute()));
+  return g;
+}
+
+kern::KMeansAssignArgs base_args(const DenseTable& x, const GpuCenters& g) {
+  kern::KMeansAssignArgs a;
+  a.x = x.data.as<float>();
+  a.n = x.rows;
+  a.ld = static_cast<int>(x.ld);
+  a.d = x.cols;
+  a.centers = g.c32.as<float>();
+  a.cnorm = g.cnorm.as<float>();
+  a.k = g.k;
+  a.kpad = g.kpad;
+  return a;
+}
+
+void check_gpu_table(const DenseTable& x) {
+  OAP_CHECK(x.dtype == DType::F32, "GPU K-Means expects an f32 table");
+  OAP_CHECK(x.ld == kern::kmeans_ld(x.cols), "table row stride " << x.ld
+                                                                 << " does not match the K-Means "
+                                                                    "layout "
+                                                                 << kern::kmeans_ld(x.cols));
+}
+
+// Operations the initialisers need, on either backend.
+class InitOps {
+ public:
+  InitOps(Context& ctx, DenseTable& x) : ctx_(ctx), x_(x) {
+    if (ctx.is_gpu()) {
+      check_gpu_table(x);
+      costs_ = ctx.alloc(sizeof(float) * std::max<int64_t>(x.rows, 1));
+      tmp_ = ctx.alloc(sizeof(float) * std::max<int64_t>(x.rows, 1));
+      slab_ = ctx.alloc(sizeof(double) * std::max(kern::kmeans_cost_slab_size(256), 512));
+      ctx.memset(costs_.data(), 0x7f, sizeof(float) * std::max<int64_t>(x.rows, 1));
+    } else {
+      hcost_.assign(x.rows, std::numeric_limits<double>::infinity());
+    }
+  }
+
+  // costs = min(costs, dist^2 to `centers`)
+  void update_costs(const std::vector<double>& centers, int m) {
+    if (m == 0 || x_.rows == 0) return;
+    if (ctx_.is_gpu()) {
+      GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
+      kern::KMeansAssignArgs a = base_args(x_, g);
+      a.accumulate = false;
+      a.mindist = tmp_.as<float>();
+      a.cost_slab = slab_.as<double>();
+      kern::kmeans_assign(a, ctx_.info().cu_count, ctx_.compute());
+      kern::elementwise_min(costs_.as<float>(), tmp_.as<float>(), x_.rows, ctx_.compute());
+      OAP_HIP_CHECK(hipStreamSynchronize(ctx_.compute()));
+    } else {
+      std::vector<double> d2(x_.rows);
+      cpu_assign(ctx_, x_, centers, m, nullptr, false, false, nullptr, d2.data());
+      for (int64_t i = 0; i < x_.rows; ++i) hcost_[i] = std::min(hcost_[i], d2[i]);
+    }
+  }
+
+  double local_cost_sum() {
+    if (x_.rows == 0) return 0.0;
+    if (ctx_.is_gpu()) {
+      Buffer out = ctx_.alloc(sizeof(double));
+      int m = kern::reduce_sum_f32(costs_.as<float>(), x_.rows, slab_.as<double>(),
+                                   ctx_.compute());
+      kern::sum_f64(slab_.as<double>(), m, out.as<double>(), ctx_.compute());
+      double v = 0.0;
+      ctx_.copy_to_host(&v, out.data(), sizeof(double));
+      return v;
+    }
+    double s = 0.0;
+    for (double c : hcost_) s += c;
+    return s;
+  }
+
+  // Local row indices whose Bernoulli draw succeeds, sorted ascending.
+  std::vector<int64_t> select(double factor, uint64_t seed, int step) {
+    std::vector<int64_t> idx;
+    if (x_.rows == 0) return idx;
+    if (ctx_.is_gpu()) {
+      Buffer flag = ctx_.alloc(sizeof(int32_t) * x_.rows);
+      Buffer out = ctx_.alloc(sizeof(int64_t) * x_.rows);
+      Buffer cnt = ctx_.alloc(sizeof(u64));
+      ctx_.memset(cnt.data(), 0, sizeof(u64));
+      kern::bernoulli_select(costs_.as<float>(), x_.rows, x_.global_offset, factor, seed, step,
+                             flag.as<int32_t>(), ctx_.compute());
+      kern::compact_flags(flag.as<int32_t>(), x_.rows, out.as<int64_t>(), cnt.as<u64>(),
+                          ctx_.compute());
+      u64 n = 0;
+      ctx_.copy_to_host(&n, cnt.data(), sizeof(u64));
+      idx.resize(n);
+      ctx_.copy_to_host(idx.data(), out.data(), sizeof(int64_t) * n);
+      std::sort(idx.begin(), idx.end());
+      return idx;
+    }
+    for (int64_t i = 0; i < x_.rows; ++i) {
+      uint64_t h = mix64(seed ^ (uint64_t(step) << 48) ^ uint64_t(x_.global_offset + i));
+      double u = double(h >> 11) * (1.0 / 9007199254740992.0);
+      // same float rounding of the cost as the GPU path keeps the two engines aligned
+      if (u < factor * double(float(hcost_[i]))) idx.push_back(i);
+    }
+    return idx;
+  }
+
+  std::vector<double> rows(const std::vector<int64_t>& local_idx) {
+    const int d = x_.cols;
+    std::vector<double> out(local_idx.size() * d);
+    if (local_idx.empty()) return out;
+    if (ctx_.is_gpu()) {
+      Buffer di = ctx_.alloc(sizeof(int64_t) * local_idx.size());
+      Buffer dv = ctx_.alloc(sizeof(float) * local_idx.size() * d);
+      ctx_.copy_to_backend(di.data(), local_idx.data(), sizeof(int64_t) * local_idx.size());
+      kern::gather_rows(x_.data.as<float>(), x_.ld, d, di.as<int64_t>(),
+                        int64_t(local_idx.size()), dv.as<float>(), ctx_.compute());
+      std::vector<float> h(local_idx.size() * d);
+      ctx_.copy_to_host(h.data(), dv.data(), sizeof(float) * h.size());
+      for (size_t i = 0; i < h.size(); ++i) out[i] = h[i];
+      return out;
+    }
+    for (size_t i = 0; i < local_idx.size(); ++i)
+      for (int f = 0; f < d; ++f) out[i * d + f] = table_at(x_, local_idx[i], f);
+    return out;
+  }
+
+  std::vector<int64_t> count_closest(const std::vector<double>& centers, int m) {
+    std::vector<int64_t> cnt(m, 0);
+    if (x_.rows == 0) return cnt;
+    if (ctx_.is_gpu()) {
+      GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
+      Buffer dc = ctx_.alloc(sizeof(u64) * m);
+      ctx_.memset(dc.data(), 0, sizeof(u64) * m);
+      kern::KMeansAssignArgs a = base_args(x_, g);
+      a.accumulate = true;
+      a.sums_too = false;
+      a.counts = dc.as<u64>();
+      a.cost_slab = slab_.as<double>();
+      kern::kmeans_assign(a, ctx_.info().cu_count, ctx_.compute());
+      ctx_.copy_to_host(cnt.data(), dc.data(), sizeof(u64) * m);
+      return cnt;
+    }
+    auto o = cpu_assign(ctx_, x_, centers, m, nullptr, true, false, nullptr, nullptr);
+    return o.counts;
+  }
+
+ private:
+  Context& ctx_;
+  DenseTable& x_;
+  Buffer costs_, tmp_, slab_;
+  std::vector<double> hcost_;
+};
+
+// Fetch rows by GLOBAL index; every rank ends with all of them (owner fills, allreduce SUM).
+std::vector<double> fetch_global_rows(Context& ctx, Comm& comm, DenseTable& x, InitOps& ops,
+                                      const std::vector<int64_t>& gidx) {
+  const int d = x.cols;
+  std::vector<double> out(gidx.size() * d, 0.0);
+  std::vector<int64_t> mine;
+  std::vector<size_t> pos;
+  for (size_t i = 0; i < gidx.size(); ++i) {
+    int64_t l = gidx[i] - x.global_offset;
+    if (l >= 0 && l < x.rows) {
+      mine.push_back(l);
+      pos.push_back(i);
+    }
+  }
+  auto vals = ops.rows(mine);
+  for (size_t i = 0; i < mine.size(); ++i)
+    std::copy(vals.begin() + i * d, vals.begin() + (i + 1) * d, out.begin() + pos[i] * d);
+  host_allreduce(ctx, comm, out.data(), out.size(), DType::F64, ReduceOp::Sum);
+  return out;
+}
+
+std::vector<double> distinct_rows(const std::vector<double>& pts, int d) {
+  std::vector<double> out;
+  std::set<std::vector<double>> seen;
+  size_t m = d ? pts.size() / d : 0;
+  for (size_t i = 0; i < m; ++i) {
+    std::vector<double> r(pts.begin() + i * d, pts.begin() + (i + 1) * d);
+    for (auto& v : r)
+      if (v == 0.0) v = 0.0;  // -0.0 == 0.0 as in Spark's Vector equality
+    if (seen.insert(r).second) out.insert(out.end(), r.begin(), r.end());
+  }
+  return out;
+}
+
+// Uniform sample of m distinct indices of [0, n) in draw order (partial Fisher-Yates).
+std::vector<int64_t> sample_without_replacement(int64_t n, int64_t m, uint64_t seed) {
+  std::mt19937_64 rng(mix64(seed));
+  std::unordered_map<int64_t, int64_t> swp;
+  std::vector<int64_t> out;
+  m = std::min(m, n);
+  for (int64_t i = 0; i < m; ++i) {
+    std::uniform_int_distribution<int64_t> u(i, n - 1);
+    int64_t j = u(rng);
+    int64_t vi = swp.count(i) ? swp[i] : i;
+    int64_t vj = swp.count(j) ? swp[j] : j;
+    swp[j] = vi;
+    out.push_back(vj);
+  }
+  return out;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------ local k-means++
+namespace {
+// One greedy k-means++ seeding (2 + ln k candidate draws per step, keep the one that lowers the
+// weighted potential most) followed by weighted Lloyd; returns the weighted cost.
+double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>& w, int d, int k,
+                      int max_iter, std::mt19937_64& rng, std::vector<double>& centers) {
+  const size_t n = pts.size() / d;
+  std::uniform_real_distribution<double> U(0.0, 1.0);
+  auto dist2 = [&](size_t i, const double* c) {
+    double s = 0.0;
+    for (int f = 0; f < d; ++f) {
+      double df = pts[i * d + f] - c[f];
+      s += df * df;
+    }
+    return s;
+  };
+  auto pick = [&](const std::vector<double>& mass) {  // Spark pickWeighted semantics
+    double tot = 0.0;
+    for (double v : mass) tot += v;
+    double r = U(rng) * tot, cum = 0.0;
+    size_t j = 0;
+    while (j < n && cum < r) cum += mass[j++];
+    return j == 0 ? size_t(0) : j - 1;
+  };
+  centers.assign(size_t(k) * d, 0.0);
+  auto set_center = [&](int c, size_t i) {
+    std::copy(pts.begin() + i * d, pts.begin() + (i + 1) * d, centers.begin() + size_t(c) * d);
+  };
+  set_center(0, pick(w));
+  std::vector<double> cost(n), mass(n), trial(n);
+  for (size_t i = 0; i < n; ++i) cost[i] = dist2(i, centers.data());
+  const int trials = 2 + static_cast<int>(std::log(double(k)));
+  for (int c = 1; c < k; ++c) {
+    for (size_t i = 0; i < n; ++i) mass[i] = w[i] * cost[i];
+    size_t best_i = 0;
+    double best_pot = std::numeric_limits<double>::infinity();
+    std::vector<double> best_cost;
+    for (int t = 0; t < trials; ++t) {
+      size_t cand = pick(mass);
+      double pot = 0.0;
+      const double* cc = pts.data() + cand * d;
+      for (size_t i = 0; i < n; ++i) {
+        trial[i] = std::min(cost[i], dist2(i, cc));
+        pot += w[i] * trial[i];
+      }
+      if (pot < best_pot) {
+        best_pot = pot;
+        best_i = cand;
+        best_cost = trial;
+      }
+    }
+    set_center(c, best_i);
+    cost = best_cost;
+  }
+  std::vector<int> old(n, -1);
+  std::vector<int> lab(n, 0);
+  bool moved = true;
+  for (int it = 0; moved && it < max_iter; ++it) {
+    moved = false;
+    std::vector<double> cnt(k, 0.0), sums(size_t(k) * d, 0.0);
+    for (size_t i = 0; i < n; ++i) {
+      int best = 0;
+      double bd = std::numeric_limits<double>::infinity();
+      for (int c = 0; c < k; ++c) {
+        double v = dist2(i, centers.data() + size_t(c) * d);
+        if (v < bd) {
+          bd = v;
+          best = c;
+        }
+      }
+      for (int f = 0; f < d; ++f) sums[size_t(best) * d + f] += w[i] * pts[i * d + f];
+      cnt[best] += w[i];
+      if (best != old[i]) {
+        moved = true;
+        old[i] = best;
+      }
+    }
+    for (int c = 0; c < k; ++c) {
+      if (cnt[c] == 0.0) {
+        std::uniform_int_distribution<size_t> ui(0, n - 1);
+        set_center(c, ui(rng));
+      } else {
+        for (int f = 0; f < d; ++f) centers[size_t(c) * d + f] = sums[size_t(c) * d + f] / cnt[c];
+      }
+    }
+  }
+  double total = 0.0;
+  for (size_t i = 0; i < n; ++i) {
+    double bd = std::numeric_limits<double>::infinity();
+    for (int c = 0; c < k; ++c) bd = std::min(bd, dist2(i, centers.data() + size_t(c) * d));
+    total += w[i] * bd;
+  }
+  return total;
+}
+}  // namespace
+
+// Spark's LocalKMeans.kMeansPlusPlus runs ONE plain k-means++ seeding + Lloyd; here the seeding
+// is greedy (sklearn-style local trials) and the best of 3 restarts by weighted cost is kept —
+// a strictly better local optimum for the same candidate set (deterministic given the seed).
+std::vector<double> local_kmeans_pp(const std::vector<double>& pts, const std::vector<double>& w,
+                                    int d, int k, int max_iter, uint64_t seed) {
+  const size_t n = d ? pts.size() / d : 0;
+  OAP_CHECK(n > 0 && w.size() == n, "local_kmeans_pp: bad inputs");
+  std::mt19937_64 rng(mix64(seed));
+  std::vector<double> best, cur;
+  double best_cost = std::numeric_limits<double>::infinity();
+  for (int r = 0; r < 3; ++r) {
+    double c = kmeans_pp_once(pts, w, d, k, max_iter, rng, cur);
+    if (c < best_cost) {
+      best_cost = c;
+      best = cur;
+    }
+  }
+  return best;
+}
+
+// ------------------------------------------------------------------------------- init
+std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
+                                        const KMeansParams& p, int* k_eff) {
+  TraceRange tr(&ctx.metrics(), "kmeans/init");
+  if (x.global_offset < 0) assign_global_offsets(ctx, comm, x);
+  const int d = x.cols;
+  const int64_t N = x.global_rows;
+  OAP_CHECK(N > 0, "K-Means needs at least one row");
+  InitOps ops(ctx, x);
+  const uint64_t seed = mix64(p.seed ^ 0x5DEECE66Dull);
+  std::vector<double> centers;
+  if (p.init == KMeansInit::Random) {
+    auto gidx = sample_without_replacement(N, p.k, seed);
+    centers = distinct_rows(fetch_global_rows(ctx, comm, x, ops, gidx), d);
+  } else {
+    auto first = sample_without_replacement(N, 1, seed);
+    std::vector<double> cand = fetch_global_rows(ctx, comm, x, ops, first);
+    std::vector<double> newc = cand;
+    for (int step = 0; step < p.init_steps; ++step) {
+      ops.update_costs(newc, static_cast<int>(newc.size() / d));
+      double sum = comm_allreduce_scalar(ctx, comm, ops.local_cost_sum(), ReduceOp::Sum);
+      if (!(sum > 0.0)) break;  // every point already a center
+      auto local = ops.select(2.0 * p.k / sum, seed, step);
+      newc = host_allgatherv_rows(ctx, comm, ops.rows(local), d);
+      cand.insert(cand.end(), newc.begin(), newc.end());
+      if (newc.empty()) break;
+    }
+    centers = distinct_rows(cand, d);
+    int m = static_cast<int>(centers.size() / d);
+    if (m > p.k) {
+      auto cnt = ops.count_closest(centers, m);
+      host_allreduce(ctx, comm, cnt.data(), cnt.size(), DType::I64, ReduceOp::Sum);
+      std::vector<double> w(cnt.begin(), cnt.end());
+      centers = local_kmeans_pp(centers, w, d, p.k, 30, seed ^ 0x1234567ull);
+    }
+  }
+  *k_eff = static_cast<int>(centers.size() / d);
+  std::ostringstream os;
+  os << "\"k\":" << p.k << ",\"k_eff\":" << *k_eff << ",\"mode\":" << int(p.init);
+  Logger::instance().log(LogLevel::Info, "kmeans/init", os.str());
+  return centers;
+}
+
+// ------------------------------------------------------------------------------- fit
+KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
+                        const std::vector<double>& init_centers, const KMeansParams& p) {
+  OAP_CHECK(p.k > 1 || p.init == KMeansInit::Given, "k must be > 1");
+  OAP_CHECK(p.max_iter >= 0, "maxIter must be >= 0");
+  if (ctx.is_gpu()) check_gpu_table(x);
+  ctx.activate();
+  KMeansResult res;
+  const int d = x.cols;
+  res.d = d;
+  auto t_init = std::chrono::steady_clock::now();
+  if (x.global_offset < 0) assign_global_offsets(ctx, comm, x);
+  res.global_rows = x.global_rows;
+  std::vector<double> centers;
+  int k = 0;
+  if (p.init == KMeansInit::Given) {
+    OAP_CHECK(!init_centers.empty() && init_centers.size() % d == 0,
+              "initial centers must be k x d");
+    centers = init_centers;
+    k = static_cast<int>(centers.size() / d);
+  } else {
+    centers = kmeans_init_centers(ctx, comm, x, p, &k);
+  }
+  res.init_seconds = seconds_since(t_init);
+  res.k = k;
+
+  auto absmax = global_column_absmax(ctx, comm, x);
+  FixedPoint fp = fixed_point_scales(absmax, x.global_rows);
+  const size_t kd = size_t(k) * d;
+  auto t_iter = std::chrono::steady_clock::now();
+  Metrics& M = ctx.metrics();
+
+  if (!ctx.is_gpu()) {
+    // ------------------------------------------------------------------ CPU engine
+    std::vector<int64_t> stats(kd + k);
+    for (int it = 0; it < p.max_iter; ++it) {
+      maybe_inject_fault(comm.rank(), "kmeans_iter", it);
+      TraceRange tr(&M, "kmeans/iteration");
+      auto o = cpu_assign(ctx, x, centers, k, &fp, true, true, nullptr, nullptr);
+      std::copy(o.sums.begin(), o.sums.end(), stats.begin());
+      std::copy(o.counts.begin(), o.counts.end(), stats.begin() + kd);
+      double cost = o.cost;
+      {
+        TraceRange tc(&M, "kmeans/allreduce", int64_t(stats.size() * 8 + 8));
+        host_allreduce(ctx, comm, stats.data(), stats.size(), DType::I64, ReduceOp::Sum);
+        host_allreduce(ctx, comm, &cost, 1, DType::F64, ReduceOp::Sum);
+      }
+      bool conv = true;
+      for (int c = 0; c < k; ++c) {
+        int64_t cnt = stats[kd + c];
+        if (cnt <= 0) continue;
+        double sh = 0.0;
+        for (int f = 0; f < d; ++f) {
+          double nv = double(stats[size_t(c) * d + f]) * fp.inv_scale[f] / double(cnt);
+          double df = nv - centers[size_t(c) * d + f];
+          sh += df * df;
+          centers[size_t(c) * d + f] = nv;
+        }
+        if (sh > p.tol * p.tol) conv = false;
+      }
+      res.cost = cost;
+      res.cost_history.push_back(cost);
+      res.last_counts.assign(stats.begin() + kd, stats.end());
+      res.num_iter = it + 1;
+      if (conv) {
+        res.converged = true;
+        break;
+      }
+    }
+    res.centers = centers;
+    res.iter_seconds = seconds_since(t_iter);
+    return res;
+  }
+
+  // -------------------------------------------------------------------- GPU engine
+  hipStream_t s = ctx.compute();
+  const int kpad = static_cast<int>(round_up(k, 32));
+  Buffer c64 = ctx.alloc(sizeof(double) * kd);
+  Buffer c32 = ctx.alloc(sizeof(float) * kd);
+  Buffer cnorm = ctx.alloc(sizeof(float) * kpad);
+  Buffer stats = ctx.alloc(sizeof(u64) * (kd + k));
+  const int nslab = kern::kmeans_cost_slab_size(ctx.info().cu_count);
+  Buffer slab = ctx.alloc(sizeof(double) * nslab);
+  Buffer cost_d = ctx.alloc(sizeof(double));
+  Buffer scale = ctx.alloc(sizeof(float) * d);
+  Buffer inv_scale = ctx.alloc(sizeof(double) * d);
+  Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags));
+  Buffer flags_h = ctx.alloc_pinned(sizeof(kern::KMeansFlags));
+  Buffer counts_h = ctx.alloc_pinned(sizeof(u64) * k);
+  ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * kd, s);
+  ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d, s);
+  ctx.copy_to_backend(inv_scale.data(), fp.inv_scale.data(), sizeof(double) * d, s);
+  kern::kmeans_prepare_centers(c64.as<double>(), k, d, c32.as<float>(), cnorm.as<float>(), kpad,
+                               s);
+  u64* sums = stats.as<u64>();
+  u64* counts = sums + kd;
+
+  kern::KMeansAssignArgs a;
+  a.x = x.data.as<float>();
+  a.n = x.rows;
+  a.ld = static_cast<int>(x.ld);
+  a.d = d;
+  a.centers = c32.as<float>();
+  a.cnorm = cnorm.as<float>();
+  a.k = k;
+  a.kpad = kpad;
+  a.scale = scale.as<float>();
+  a.sums = sums;
+  a.counts = counts;
+  a.cost_slab = slab.as<double>();
+  a.accumulate = true;
+  a.sums_too = true;
+
+  kern::KMeansFinalizeArgs fa;
+  fa.sums = sums;
+  fa.counts = counts;
+  fa.inv_scale = inv_scale.as<double>();
+  fa.centers64 = c64.as<double>();
+  fa.centers32 = c32.as<float>();
+  fa.cnorm = cnorm.as<float>();
+  fa.k = k;
+  fa.d = d;
+  fa.tol = p.tol;
+  fa.cost_in = cost_d.as<double>();
+  fa.flags = flags_d.data();
+
+  RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
+  Event e0, e1, e2, e3;
+  const int64_t flops_per_iter = 2 * int64_t(x.rows) * k * d;
+  for (int it = 0; it < p.max_iter; ++it) {
+    maybe_inject_fault(comm.rank(), "kmeans_iter", it);
+    roctx_push("kmeans/iteration");
+    e0.record(s);
+    OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
+    int nb = kern::kmeans_assign(a, ctx.info().cu_count, s);
+    kern::sum_f64(slab.as<double>(), std::max(nb, 0), cost_d.as<double>(), s);
+    if (nb == 0) OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+    e1.record(s);
+    if (comm.size() > 1) {
+      if (comm.on_device()) {
+        if (rccl) rccl->group_start();
+        comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
+        comm.allreduce(cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+        if (rccl) rccl->group_end();
+      } else {
+        comm_allreduce(ctx, comm, stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
+        comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+      }
+    }
+    e2.record(s);
+    kern::kmeans_finalize(fa, s);
+    OAP_HIP_CHECK(hipMemcpyAsync(flags_h.data(), flags_d.data(), sizeof(kern::KMeansFlags),
+                                 hipMemcpyDeviceToHost, s));
+    OAP_HIP_CHECK(
+        hipMemcpyAsync(counts_h.data(), counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
+    e3.record(s);
+    comm.wait(s);
+    roctx_pop();
+    float ms_assign = Event::elapsed_ms(e0, e1), ms_comm = Event::elapsed_ms(e1, e2),
+          ms_all = Event::elapsed_ms(e0, e3);
+    M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.rows) * x.ld * 4);
+    M.add("kmeans/allreduce", ms_comm * 1e3, int64_t(kd + k) * 8 + 8);
+    M.add("kmeans/iteration", ms_all * 1e3);
+    auto* fl = flags_h.as<kern::KMeansFlags>();
+    if (Logger::instance().level() <= LogLevel::Info) {
+      std::ostringstream os;
+      os << "\"iter\":" << it << ",\"cost\":" << fl->cost << ",\"assign_us\":" << ms_assign * 1e3
+         << ",\"allreduce_us\":" << ms_comm * 1e3 << ",\"tflops\":"
+         << (ms_assign > 0 ? double(flops_per_iter) / (ms_assign * 1e-3) / 1e12 : 0.0);
+      Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
+    }
+    res.cost = fl->cost;
+    res.cost_history.push_back(fl->cost);
+    res.num_iter = it + 1;
+    if (fl->converged) {
+      res.converged = true;
+      break;
+    }
+  }
+  res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);
+  res.centers.resize(kd);
+  ctx.copy_to_host(res.centers.data(), c64.data(), sizeof(double) * kd, s);
+  res.iter_seconds = seconds_since(t_iter);
+  M.set_value("kmeans/iter_seconds", res.iter_seconds);
+  M.set_value("kmeans/samples_per_sec",
+              res.iter_seconds > 0 ? double(x.global_rows) * res.num_iter / res.iter_seconds : 0);
+  return res;
+}
+
+void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>& centers, int k,
+                    int32_t* labels, double* dist2) {
+  OAP_CHECK(centers.size() == size_t(k) * x.cols, "centers must be k x d");
+  TraceRange tr(&ctx.metrics(), "kmeans/predict");
+  if (!ctx.is_gpu()) {
+    cpu_assign(ctx, x, centers, k, nullptr, false, false, labels, dist2);
+    return;
+  }
+  check_gpu_table(x);
+  ctx.activate();
+  if (x.rows == 0) return;
+  GpuCenters g = upload_centers(ctx, centers, k, x.cols);
+  Buffer dl = ctx.alloc(sizeof(int32_t) * x.rows);
+  Buffer dd = ctx.alloc(sizeof(float) * x.rows);
+  Buffer slab = ctx.alloc(sizeof(double) * kern::kmeans_cost_slab_size(ctx.info().cu_count));
+  kern::KMeansAssignArgs a = base_args(x, g);
+  a.accumulate = false;
+  a.labels = dl.as<int32_t>();
+  a.mindist = dd.as<float>();
+  a.cost_slab = slab.as<double>();
+  kern::kmeans_assign(a, ctx.info().cu_count, ctx.compute());
+  if (labels) ctx.copy_to_host(labels, dl.data(), sizeof(int32_t) * x.rows);
+  if (dist2) {
+    std::vector<float> h(x.rows);
+    ctx.copy_to_host(h.data(), dd.data(), sizeof(float) * x.rows);
+    for (int64_t i = 0; i < x.rows; ++i) dist2[i] = h[i];
+  }
+}
+
+}  // namespace oap

@@ -1,0 +1,65 @@
+// Distributed K-Means driver (native Lloyd loop + k-means|| / random initialisation).
+//
+// MI355X-native counterpart of the reference's K-Means JNI driver
+// (mllib-dal/src/main/native/KMeansDALImpl.cpp:34-249) and of the initialisation the reference
+// leaves on Spark (spark-3.1.1/mllib/clustering/KMeans.scala:354-432).  Per iteration the
+// reference does 4 blocking collectives through rank 0 (bcast length, bcast centroids,
+// allgatherv partials, bcast converged — SURVEY.md §2.7 C2-C5); here each rank runs the fused
+// assign kernel, ONE grouped allreduce of [fixed-point sums | counts] + cost, and the finalize
+// kernel, and evaluates convergence redundantly — no root, no broadcast.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "comm/comm.h"
+#include "runtime/context.h"
+#include "runtime/table.h"
+
+namespace oap {
+
+enum class KMeansInit : int { Given = 0, Random = 1, Parallel = 2 };
+
+struct KMeansParams {
+  int k = 2;
+  int max_iter = 20;
+  double tol = 1e-4;
+  KMeansInit init = KMeansInit::Parallel;
+  int init_steps = 2;
+  uint64_t seed = 1;
+};
+
+struct KMeansResult {
+  std::vector<double> centers;  // k_eff x d, row-major
+  int k = 0;                    // k_eff (may be < requested k when fewer distinct points)
+  int d = 0;
+  double cost = 0.0;            // cost of the last assignment step (Spark semantics)
+  int num_iter = 0;
+  bool converged = false;
+  std::vector<double> cost_history;
+  std::vector<int64_t> last_counts;  // cluster sizes of the last assignment step
+  double init_seconds = 0.0;
+  double iter_seconds = 0.0;
+  int64_t global_rows = 0;
+};
+
+// Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for
+// any world size / sharding (every random draw is keyed by the GLOBAL row index).
+std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
+                                        const KMeansParams& params, int* k_eff);
+
+// Full fit: init (unless params.init == Given, in which case init_centers is used) + Lloyd.
+KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
+                        const std::vector<double>& init_centers, const KMeansParams& params);
+
+// Nearest-center labels and exact squared distances for the local rows (host outputs).
+void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>& centers, int k,
+                    int32_t* labels, double* dist2);
+
+// k-means++ over weighted candidates, then up to max_iter weighted Lloyd iterations (host).
+// Mirrors the semantics of Spark's LocalKMeans.kMeansPlusPlus (RNG stream is our own).
+std::vector<double> local_kmeans_pp(const std::vector<double>& pts, const std::vector<double>& w,
+                                    int d, int k, int max_iter, uint64_t seed);
+
+}  // namespace oap

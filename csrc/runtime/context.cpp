@@ -1,0 +1,211 @@
+#include "runtime/context.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace oap {
+
+// -------------------------------------------------------------------------------- Stream/Event
+Stream::Stream(int device, int priority) : device_(device) {
+  OAP_HIP_CHECK(hipSetDevice(device));
+  OAP_HIP_CHECK(hipStreamCreateWithPriority(&s_, hipStreamNonBlocking, priority));
+}
+Stream::~Stream() {
+  if (s_) (void)hipStreamDestroy(s_);
+}
+void Stream::sync() const { OAP_HIP_CHECK(hipStreamSynchronize(s_)); }
+
+Event::Event(bool timing) {
+  OAP_HIP_CHECK(hipEventCreateWithFlags(&e_, timing ? hipEventDefault : hipEventDisableTiming));
+}
+Event::~Event() {
+  if (e_) (void)hipEventDestroy(e_);
+}
+void Event::record(hipStream_t s) { OAP_HIP_CHECK(hipEventRecord(e_, s)); }
+void Event::wait_on(hipStream_t s) const { OAP_HIP_CHECK(hipStreamWaitEvent(s, e_, 0)); }
+void Event::sync() const { OAP_HIP_CHECK(hipEventSynchronize(e_)); }
+float Event::elapsed_ms(const Event& a, const Event& b) {
+  float ms = 0.f;
+  OAP_HIP_CHECK(hipEventElapsedTime(&ms, a.e_, b.e_));
+  return ms;
+}
+
+// -------------------------------------------------------------------------------- ThreadPool
+ThreadPool::ThreadPool(int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  for (int i = 1; i < nthreads; ++i) workers_.emplace_back([this, i] { worker(i); });
+}
+
+ThreadPool::~ThreadPool() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : workers_) t.join();
+}
+
+void ThreadPool::worker(int idx) {
+  int64_t seen = 0;
+  for (;;) {
+    const std::function<void(int, int64_t, int64_t)>* job;
+    int64_t n;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || generation_ != seen; });
+      if (stop_) return;
+      seen = generation_;
+      job = job_;
+      n = job_n_;
+    }
+    int parts = size();
+    int64_t b = n * idx / parts, e = n * (idx + 1) / parts;
+    if (b < e) (*job)(idx, b, e);
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+}
+
+void ThreadPool::parallel_for(int64_t n, const std::function<void(int, int64_t, int64_t)>& fn) {
+  int parts = size();
+  if (parts == 1 || n < 2) {
+    if (n > 0) fn(0, 0, n);
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    job_ = &fn;
+    job_n_ = n;
+    pending_ = parts - 1;
+    ++generation_;
+  }
+  cv_.notify_all();
+  int64_t e = n / parts;
+  if (e > 0) fn(0, 0, e);
+  std::unique_lock<std::mutex> lk(mu_);
+  done_cv_.wait(lk, [&] { return pending_ == 0; });
+  job_ = nullptr;
+}
+
+// -------------------------------------------------------------------------------- devices
+int visible_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+DeviceInfo query_device(int device) {
+  DeviceInfo d;
+  hipDeviceProp_t p;
+  OAP_HIP_CHECK(hipGetDeviceProperties(&p, device));
+  d.id = device;
+  d.name = p.name;
+  d.arch = p.gcnArchName;
+  d.cu_count = p.multiProcessorCount;
+  d.total_mem = p.totalGlobalMem;
+  d.lds_per_block = static_cast<int>(p.sharedMemPerBlock);
+  d.warp_size = p.warpSize;
+  int prev = 0;
+  OAP_HIP_CHECK(hipGetDevice(&prev));
+  OAP_HIP_CHECK(hipSetDevice(device));
+  size_t fr = 0, tot = 0;
+  OAP_HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  OAP_HIP_CHECK(hipSetDevice(prev));
+  d.free_mem = fr;
+  return d;
+}
+
+// -------------------------------------------------------------------------------- Context
+Context::Context(int device, double hbm_fraction, int cpu_threads)
+    : backend_(device >= 0 ? Backend::GPU : Backend::CPU), device_(device) {
+  if (cpu_threads <= 0) {
+    unsigned hc = std::thread::hardware_concurrency();
+    cpu_threads = static_cast<int>(std::min<unsigned>(hc == 0 ? 1 : hc, 16));
+  }
+  pool_ = std::make_unique<ThreadPool>(cpu_threads);
+  if (backend_ == Backend::GPU) {
+    int n = visible_device_count();
+    OAP_CHECK(device < n, "device " << device << " requested but only " << n << " visible");
+    info_ = query_device(device);
+    OAP_HIP_CHECK(hipSetDevice(device));
+    if (hbm_fraction <= 0.0 || hbm_fraction > 1.0) hbm_fraction = 0.9;
+    size_t budget = static_cast<size_t>(static_cast<double>(info_.free_mem) * hbm_fraction);
+    // 1 GiB segments: few hipMallocs for 288 GB-class devices, little waste for small fits.
+    arena_ = std::make_shared<DeviceArena>(device, budget, size_t(1) << 30);
+    int lo = 0, hi = 0;
+    OAP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    compute_ = std::make_unique<Stream>(device, 0);
+    comm_ = std::make_unique<Stream>(device, hi);  // collectives get the higher priority
+    h2d_ = std::make_unique<Stream>(device, 0);
+  } else {
+    info_.id = -1;
+    info_.name = "cpu";
+    info_.arch = "x86_64";
+    info_.cu_count = pool_->size();
+  }
+}
+
+Context::~Context() {
+  if (backend_ == Backend::GPU) {
+    (void)hipSetDevice(device_);
+    (void)hipDeviceSynchronize();
+  }
+}
+
+void Context::activate() const {
+  if (backend_ == Backend::GPU) OAP_HIP_CHECK(hipSetDevice(device_));
+}
+
+void Context::sync_all() const {
+  if (backend_ != Backend::GPU) return;
+  OAP_HIP_CHECK(hipSetDevice(device_));
+  compute_->sync();
+  comm_->sync();
+  h2d_->sync();
+}
+
+Buffer Context::alloc(size_t bytes) {
+  if (backend_ == Backend::GPU) return Buffer::device(arena_, bytes);
+  return Buffer::host(bytes);
+}
+
+Buffer Context::alloc_pinned(size_t bytes) {
+  if (backend_ == Backend::GPU) return Buffer::pinned(bytes);
+  return Buffer::host(bytes);
+}
+
+void Context::copy_to_backend(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  if (backend_ == Backend::GPU) {
+    OAP_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s ? s : compute()));
+  } else {
+    std::memcpy(dst, src, bytes);
+  }
+}
+
+void Context::copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  if (backend_ == Backend::GPU) {
+    hipStream_t st = s ? s : compute();
+    OAP_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+    OAP_HIP_CHECK(hipStreamSynchronize(st));
+  } else {
+    std::memcpy(dst, src, bytes);
+  }
+}
+
+void Context::memset(void* dst, int value, size_t bytes, hipStream_t s) {
+  if (bytes == 0) return;
+  if (backend_ == Backend::GPU) {
+    OAP_HIP_CHECK(hipMemsetAsync(dst, value, bytes, s ? s : compute()));
+  } else {
+    std::memset(dst, value, bytes);
+  }
+}
+
+}  // namespace oap

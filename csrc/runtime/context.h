@@ -1,0 +1,130 @@
+// Per-process execution context: backend (GPU or CPU), device pinning, HBM arena, HIP streams,
+// host thread pool and metrics.  One Context per (process, device); it replaces the
+// reference's process-global oneDAL/oneCCL state (mllib-dal/src/main/native/OneCCL.cpp:35-38,
+// ALSDALImpl.cpp:37-51) with an explicit, reentrant object.
+#pragma once
+
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "runtime/common.h"
+#include "runtime/log.h"
+#include "runtime/memory.h"
+
+namespace oap {
+
+// RAII HIP stream.
+class Stream {
+ public:
+  Stream() = default;
+  explicit Stream(int device, int priority = 0);
+  ~Stream();
+  Stream(const Stream&) = delete;
+  Stream& operator=(const Stream&) = delete;
+  hipStream_t get() const { return s_; }
+  void sync() const;
+
+ private:
+  hipStream_t s_ = nullptr;
+  int device_ = -1;
+};
+
+// RAII HIP event (timing-enabled by default).
+class Event {
+ public:
+  explicit Event(bool timing = true);
+  ~Event();
+  Event(const Event&) = delete;
+  Event& operator=(const Event&) = delete;
+  hipEvent_t get() const { return e_; }
+  void record(hipStream_t s);
+  void wait_on(hipStream_t s) const;  // make stream s wait for this event
+  void sync() const;
+  static float elapsed_ms(const Event& a, const Event& b);
+
+ private:
+  hipEvent_t e_ = nullptr;
+};
+
+// Static-partition thread pool for the CPU engine: deterministic chunking so results do not
+// depend on scheduling.
+class ThreadPool {
+ public:
+  explicit ThreadPool(int nthreads);
+  ~ThreadPool();
+  int size() const { return static_cast<int>(workers_.size()) + 1; }
+  // Runs fn(chunk_index, begin, end) over [0, n) split into size() contiguous chunks.
+  void parallel_for(int64_t n, const std::function<void(int, int64_t, int64_t)>& fn);
+
+ private:
+  void worker(int idx);
+  std::vector<std::thread> workers_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int, int64_t, int64_t)>* job_ = nullptr;
+  int64_t job_n_ = 0;
+  int64_t generation_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
+struct DeviceInfo {
+  int id = -1;
+  std::string name;
+  std::string arch;
+  int cu_count = 0;
+  size_t total_mem = 0;
+  size_t free_mem = 0;
+  int lds_per_block = 0;
+  int warp_size = 64;
+};
+
+class Context {
+ public:
+  // device < 0 => CPU backend.  hbm_fraction: share of currently-free HBM the arena may use.
+  Context(int device, double hbm_fraction, int cpu_threads);
+  ~Context();
+
+  Backend backend() const { return backend_; }
+  bool is_gpu() const { return backend_ == Backend::GPU; }
+  int device() const { return device_; }
+  const DeviceInfo& info() const { return info_; }
+  DeviceArena* arena() { return arena_.get(); }
+  ThreadPool& pool() { return *pool_; }
+  Metrics& metrics() { return metrics_; }
+
+  hipStream_t compute() const { return compute_ ? compute_->get() : nullptr; }
+  hipStream_t comm_stream() const { return comm_ ? comm_->get() : nullptr; }
+  hipStream_t h2d() const { return h2d_ ? h2d_->get() : nullptr; }
+  void sync_all() const;
+  void activate() const;  // hipSetDevice(device_) for the calling thread
+
+  // Allocate on this context's backend (device arena for GPU, aligned host memory for CPU).
+  Buffer alloc(size_t bytes);
+  Buffer alloc_pinned(size_t bytes);
+
+  // Generic copies; kinds inferred from the context's backend.
+  void copy_to_backend(void* dst, const void* host_src, size_t bytes, hipStream_t s = nullptr);
+  void copy_to_host(void* host_dst, const void* src, size_t bytes, hipStream_t s = nullptr);
+  void memset(void* dst, int value, size_t bytes, hipStream_t s = nullptr);
+
+ private:
+  Backend backend_;
+  int device_;
+  DeviceInfo info_;
+  std::shared_ptr<DeviceArena> arena_;
+  std::unique_ptr<Stream> compute_, comm_, h2d_;
+  std::unique_ptr<ThreadPool> pool_;
+  Metrics metrics_;
+};
+
+// Number of visible HIP devices (0 when no GPU / no driver).
+int visible_device_count();
+DeviceInfo query_device(int device);
+
+}  // namespace oap

@@ -1,0 +1,216 @@
+#include "runtime/table.h"
+
+#include <cmath>
+#include <cstring>
+
+#include "kernels/kernels.h"
+
+namespace oap {
+
+namespace {
+// CPU helpers ---------------------------------------------------------------------------
+double read_elem(const void* p, DType t, size_t i) {
+  switch (t) {
+    case DType::F32: return static_cast<const float*>(p)[i];
+    case DType::F64: return static_cast<const double*>(p)[i];
+    default: OAP_THROW(ConfigError, "unsupported element type " << dtype_name(t));
+  }
+}
+uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+float u01(uint64_t h) { return static_cast<float>(h >> 40) * (1.0f / 16777216.0f); }
+}  // namespace
+
+DenseTable upload_dense(Context& ctx, const void* host, DType src_t, int64_t rows, int cols,
+                        int64_t src_ld, DType storage, int64_t ld, int64_t chunk_rows) {
+  OAP_CHECK(src_t == DType::F32 || src_t == DType::F64, "source must be f32 or f64");
+  OAP_CHECK(ld >= cols, "ld (" << ld << ") < cols (" << cols << ")");
+  OAP_CHECK(rows >= 0 && cols > 0, "bad shape " << rows << "x" << cols);
+  DenseTable t;
+  t.rows = rows;
+  t.cols = cols;
+  t.ld = ld;
+  t.dtype = storage;
+  t.backend = ctx.backend();
+  TraceRange tr(&ctx.metrics(), "ingest/upload_dense", int64_t(rows) * cols * dtype_size(src_t));
+  if (!ctx.is_gpu()) {
+    OAP_CHECK(storage == DType::F64 || storage == DType::F32,
+              "CPU tables are f32 or f64, got " << dtype_name(storage));
+    t.data = Buffer::host(t.bytes());
+    ctx.pool().parallel_for(rows, [&](int, int64_t b, int64_t e) {
+      for (int64_t r = b; r < e; ++r)
+        for (int c = 0; c < ld; ++c) {
+          double v = c < cols ? read_elem(host, src_t, size_t(r) * src_ld + c) : 0.0;
+          if (storage == DType::F64)
+            t.data.as<double>()[size_t(r) * ld + c] = v;
+          else
+            t.data.as<float>()[size_t(r) * ld + c] = static_cast<float>(v);
+        }
+    });
+    return t;
+  }
+  OAP_CHECK(storage == DType::F32 || storage == DType::BF16,
+            "GPU tables are f32 or bf16, got " << dtype_name(storage));
+  ctx.activate();
+  t.data = ctx.alloc(t.bytes() == 0 ? 256 : t.bytes());
+  if (rows == 0) return t;
+  // Double-buffered pipeline: host memcpy into pinned[i%2] -> H2D into staging[i%2] -> device
+  // convert/pad into the final layout; the event on each slot protects it from being refilled
+  // while its copy is still in flight.
+  const size_t es = dtype_size(src_t);
+  if (chunk_rows > rows) chunk_rows = rows;
+  const size_t chunk_bytes = size_t(chunk_rows) * cols * es;
+  Buffer pinned[2] = {ctx.alloc_pinned(chunk_bytes), ctx.alloc_pinned(chunk_bytes)};
+  Buffer stage[2] = {ctx.alloc(chunk_bytes), ctx.alloc(chunk_bytes)};
+  Event done[2];
+  bool used[2] = {false, false};
+  hipStream_t s = ctx.h2d();
+  int slot = 0;
+  for (int64_t r0 = 0; r0 < rows; r0 += chunk_rows, slot ^= 1) {
+    int64_t n = std::min<int64_t>(chunk_rows, rows - r0);
+    if (used[slot]) done[slot].sync();
+    const char* src = static_cast<const char*>(host) + size_t(r0) * src_ld * es;
+    char* dst = pinned[slot].as<char>();
+    if (src_ld == cols) {
+      std::memcpy(dst, src, size_t(n) * cols * es);
+    } else {
+      for (int64_t r = 0; r < n; ++r)
+        std::memcpy(dst + size_t(r) * cols * es, src + size_t(r) * src_ld * es, cols * es);
+    }
+    OAP_HIP_CHECK(hipMemcpyAsync(stage[slot].data(), dst, size_t(n) * cols * es,
+                                 hipMemcpyHostToDevice, s));
+    char* out = t.data.as<char>() + size_t(r0) * ld * dtype_size(storage);
+    kern::convert_pad(stage[slot].data(), src_t, n, cols, cols, out, storage, ld, s);
+    done[slot].record(s);
+    used[slot] = true;
+  }
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+  return t;
+}
+
+DenseTable synth_blobs_table(Context& ctx, int64_t rows, int cols, int64_t ld, int64_t row0,
+                             int ncenters, double box, double sigma, uint64_t seed) {
+  DenseTable t;
+  t.rows = rows;
+  t.cols = cols;
+  t.ld = ld;
+  t.backend = ctx.backend();
+  TraceRange tr(&ctx.metrics(), "ingest/synth_blobs", int64_t(rows) * ld * 4);
+  if (ctx.is_gpu()) {
+    t.dtype = DType::F32;
+    ctx.activate();
+    t.data = ctx.alloc(t.bytes() == 0 ? 256 : t.bytes());
+    kern::synth_blobs(t.data.as<float>(), rows, cols, ld, row0, ncenters, float(box),
+                      float(sigma), seed, ctx.compute());
+    OAP_HIP_CHECK(hipStreamSynchronize(ctx.compute()));
+    return t;
+  }
+  // Same generator on the CPU, in float32 arithmetic, cast to f64 storage.
+  t.dtype = DType::F64;
+  t.data = Buffer::host(t.bytes());
+  double* x = t.data.as<double>();
+  ctx.pool().parallel_for(rows, [&](int, int64_t b, int64_t e) {
+    for (int64_t r = b; r < e; ++r) {
+      int64_t grow = row0 + r;
+      uint64_t lab = splitmix64(seed ^ (uint64_t(grow) * 0x2545F4914F6CDD1Dull)) %
+                     uint64_t(ncenters);
+      for (int c = 0; c < ld; ++c) {
+        if (c >= cols) {
+          x[size_t(r) * ld + c] = 0.0;
+          continue;
+        }
+        uint64_t hc = splitmix64(seed * 31ull + lab * 1315423911ull + uint64_t(c) * 2654435761ull);
+        float center = (u01(hc) * 2.f - 1.f) * float(box);
+        uint64_t h1 = splitmix64(seed ^ 0xABCDEFull ^ (uint64_t(grow) << 20) ^ uint64_t(c));
+        uint64_t h2 = splitmix64(h1);
+        float u1 = std::fmax(u01(h1), 1e-7f), u2 = u01(h2);
+        float g = std::sqrt(-2.f * std::log(u1)) * std::cos(6.2831853f * u2);
+        x[size_t(r) * ld + c] = double(center + float(sigma) * g);
+      }
+    }
+  });
+  return t;
+}
+
+void assign_global_offsets(Context& ctx, Comm& comm, DenseTable& t) {
+  auto counts = comm_allgather_i64(ctx, comm, t.rows);
+  int64_t off = 0, tot = 0;
+  for (int r = 0; r < comm.size(); ++r) {
+    if (r < comm.rank()) off += counts[r];
+    tot += counts[r];
+  }
+  t.global_offset = off;
+  t.global_rows = tot;
+}
+
+std::vector<double> global_column_absmax(Context& ctx, Comm& comm, const DenseTable& t) {
+  std::vector<double> mx(t.cols, 0.0);
+  if (ctx.is_gpu()) {
+    OAP_CHECK(t.dtype == DType::F32, "column_absmax expects an f32 table");
+    Buffer d = ctx.alloc(sizeof(float) * t.cols);
+    ctx.memset(d.data(), 0, sizeof(float) * t.cols);
+    kern::column_absmax(t.data.as<float>(), t.rows, t.cols, t.ld, d.as<float>(), ctx.compute());
+    std::vector<float> h(t.cols);
+    ctx.copy_to_host(h.data(), d.data(), sizeof(float) * t.cols);
+    for (int c = 0; c < t.cols; ++c) mx[c] = h[c];
+  } else {
+    std::vector<std::vector<double>> part(ctx.pool().size(), std::vector<double>(t.cols, 0.0));
+    ctx.pool().parallel_for(t.rows, [&](int ci, int64_t b, int64_t e) {
+      auto& p = part[ci];
+      for (int64_t r = b; r < e; ++r)
+        for (int c = 0; c < t.cols; ++c) {
+          double v = t.dtype == DType::F64 ? t.data.as<double>()[size_t(r) * t.ld + c]
+                                           : t.data.as<float>()[size_t(r) * t.ld + c];
+          p[c] = std::max(p[c], std::fabs(v));
+        }
+    });
+    for (auto& p : part)
+      for (int c = 0; c < t.cols; ++c) mx[c] = std::max(mx[c], p[c]);
+  }
+  if (comm.size() > 1) {
+    if (comm.on_device() && ctx.is_gpu()) {
+      Buffer d = ctx.alloc(sizeof(double) * t.cols);
+      ctx.copy_to_backend(d.data(), mx.data(), sizeof(double) * t.cols, ctx.comm_stream());
+      comm.allreduce(d.data(), t.cols, DType::F64, ReduceOp::Max, ctx.comm_stream());
+      OAP_HIP_CHECK(hipMemcpyAsync(mx.data(), d.data(), sizeof(double) * t.cols,
+                                   hipMemcpyDeviceToHost, ctx.comm_stream()));
+      comm.wait(ctx.comm_stream());
+    } else {
+      comm.allreduce(mx.data(), t.cols, DType::F64, ReduceOp::Max, nullptr);
+    }
+  }
+  return mx;
+}
+
+std::vector<double> table_rows_f64(Context& ctx, const DenseTable& t, int64_t r0, int64_t n) {
+  OAP_CHECK(r0 >= 0 && r0 + n <= t.rows, "row range out of bounds");
+  std::vector<double> out(size_t(n) * t.cols);
+  size_t es = dtype_size(t.dtype);
+  std::vector<char> raw(size_t(n) * t.ld * es);
+  if (n == 0) return out;
+  ctx.copy_to_host(raw.data(), t.data.as<char>() + size_t(r0) * t.ld * es, raw.size());
+  for (int64_t r = 0; r < n; ++r)
+    for (int c = 0; c < t.cols; ++c) {
+      size_t i = size_t(r) * t.ld + c;
+      double v;
+      if (t.dtype == DType::F64)
+        v = reinterpret_cast<double*>(raw.data())[i];
+      else if (t.dtype == DType::F32)
+        v = reinterpret_cast<float*>(raw.data())[i];
+      else {
+        uint16_t b = reinterpret_cast<uint16_t*>(raw.data())[i];
+        uint32_t u = uint32_t(b) << 16;
+        float f;
+        std::memcpy(&f, &u, 4);
+        v = f;
+      }
+      out[size_t(r) * t.cols + c] = v;
+    }
+  return out;
+}
+
+}  // namespace oap

@@ -1,0 +1,78 @@
+"""Worker functions executed inside multi-process test worlds (see mp_util.run_world)."""
+import os
+
+import numpy as np
+
+
+def _blobs(n, d, k, seed, sigma=1.0):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-10, 10, size=(k, d))
+    return c[rng.integers(0, k, n)] + rng.normal(0, sigma, size=(n, d))
+
+
+def _shard(X, rank, world):
+    base, rem = divmod(len(X), world)
+    lo = rank * base + min(rank, rem)
+    return X[lo: lo + base + (1 if rank < rem else 0)]
+
+
+def kmeans_native(n=4000, d=6, k=5, seed=7, device="cpu", use_rccl=True, init_mode="k-means||"):
+    import oap_mllib_amd as O
+
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl, device_id=0))
+    X = _blobs(n, d, k, seed)
+    local = _shard(X, w.rank, w.size)
+    m = O.KMeans(k=k, seed=seed, maxIter=25, initMode=init_mode).fit(local)
+    out = {"rank": w.rank, "size": w.size, "engine": m.fit_info["engine"],
+           "comm": w.comm.name if w.comm is not None else None,
+           "centers": np.array(m.clusterCenters()).tolist(), "cost": m.trainingCost,
+           "iters": m.numIter}
+    O.shutdown_world()
+    return out
+
+
+def kmeans_vanilla(n=2000, d=4, k=3, seed=3):
+    import oap_mllib_amd as O
+
+    w = O.init_world(O.get_config().replace(device="vanilla"))
+    X = _blobs(n, d, k, seed)
+    local = _shard(X, w.rank, w.size)
+    init = X[:k]
+    from oap_mllib_amd.fallback import kmeans_vanilla as V
+
+    r = V.fit(local, k, 10, 0.0, init_centers=init, allreduce=lambda a: w.allreduce_np(a))
+    O.shutdown_world()
+    return {"centers": r.centers.tolist(), "cost": r.cost}
+
+
+def fault_injection(device="cpu"):
+    """Rank 1 raises at iteration 0; rank 0 must not hang (gloo timeout / error)."""
+    import oap_mllib_amd as O
+
+    w = O.init_world(O.get_config().replace(device=device, comm_timeout_s=30.0))
+    X = _shard(_blobs(2000, 4, 3, 1), w.rank, w.size)
+    try:
+        O.KMeans(k=3, seed=1, maxIter=10, tol=0.0).fit(X)
+        status = "finished"
+    except Exception as e:  # noqa: BLE001
+        status = type(e).__name__
+    os._exit(3 if status != "finished" else 0)
+
+
+def host_comm_collectives():
+    """Exercises every HostComm collective through the native layer."""
+    import oap_mllib_amd as O
+    from oap_mllib_amd import _loader
+
+    N = _loader.load()
+    w = O.init_world(O.get_config().replace(device="cpu"))
+    a = np.arange(5, dtype=np.float64) * (w.rank + 1)
+    w.comm.allreduce_f64(w.ctx, a, "sum")
+    b = np.array([float(w.rank)])
+    w.comm.allreduce_f64(w.ctx, b, "max")
+    t = N.upload_dense(w.ctx, np.ones((3 + w.rank, 2)), "f64", 2)
+    N.assign_global_offsets(w.ctx, w.comm, t)
+    out = {"sum": a.tolist(), "max": b.tolist(), "offset": t.global_offset,
+           "total": t.global_rows}
+    O.shutdown_world()
+    return out

@@ -1,0 +1,67 @@
+"""Multi-process (gloo, world size 2-3) tests of the distributed paths on CPU.
+
+The reference's only multi-rank coverage is a pseudo-YARN cluster that runs the examples without
+assertions.  Here real multi-process worlds check that the distributed fit equals
+the single-process fit: with fixed-point centroid accumulation the result is BITWISE identical
+for any world size (the sums are integers), which is asserted directly."""
+import numpy as np
+import pytest
+
+from mp_util import run_world
+
+
+def _single(**kw):
+    import oap_mllib_amd as O
+    from dist_workers import kmeans_native
+
+    O.shutdown_world()
+    r = kmeans_native(**kw)
+    O.shutdown_world()
+    return r
+
+
+@pytest.mark.parametrize("nproc", [2, 3])
+def test_kmeans_native_cpu_world_matches_single_process(nproc):
+    rc, outs = run_world("dist_workers", "kmeans_native", nproc=nproc, device="cpu")
+    assert rc == 0, outs
+    ref = _single(device="cpu")
+    for o in outs:
+        assert o["size"] == nproc and o["engine"] == "cpu" and o["comm"] == "host"
+        assert o["iters"] == ref["iters"]
+        assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
+        np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-12)
+
+
+def test_kmeans_random_init_world_size_independent():
+    rc, outs = run_world("dist_workers", "kmeans_native", nproc=2, device="cpu",
+                         init_mode="random")
+    assert rc == 0
+    ref = _single(device="cpu", init_mode="random")
+    assert np.array_equal(np.array(outs[0]["centers"]), np.array(ref["centers"]))
+
+
+def test_vanilla_distributed_allreduce():
+    rc, outs = run_world("dist_workers", "kmeans_vanilla", nproc=2)
+    assert rc == 0
+    from dist_workers import _blobs
+    from oap_mllib_amd.fallback import kmeans_vanilla as V
+
+    X = _blobs(2000, 4, 3, 3)
+    ref = V.fit(X, 3, 10, 0.0, init_centers=X[:3])
+    np.testing.assert_allclose(np.array(outs[0]["centers"]), ref.centers, rtol=1e-10)
+
+
+def test_host_comm_collectives():
+    rc, outs = run_world("dist_workers", "host_comm_collectives", nproc=2)
+    assert rc == 0
+    assert outs[0]["sum"] == [0.0, 3.0, 6.0, 9.0, 12.0]
+    assert outs[1]["max"] == [1.0]
+    assert (outs[0]["offset"], outs[1]["offset"]) == (0, 3)
+    assert outs[0]["total"] == outs[1]["total"] == 7
+
+
+def test_fault_injection_no_hang():
+    """A rank that fails mid-fit must not leave its peer hanging (launcher gang-kills)."""
+    rc, _ = run_world("dist_workers", "fault_injection", nproc=2, timeout=120,
+                      env={"OAP_MLLIB_FAULT": "1:kmeans_iter:0"})
+    assert rc not in (0, 124), rc

@@ -1,0 +1,106 @@
+"""K-Means on the MI355X engine: HIP kernel numerics vs an fp64 oracle, engine equivalence,
+determinism and the multi-rank paths.  Run on the GPU box: ``pytest -m gpu``."""
+import numpy as np
+import pytest
+
+import oap_mllib_amd as O
+from mp_util import run_world
+from oap_mllib_amd.fallback import kmeans_vanilla as vanilla
+
+pytestmark = pytest.mark.gpu
+
+
+def f32_blobs(n, d, k, seed, sigma=0.5, box=10.0):
+    rng = np.random.default_rng(seed)
+    c = rng.uniform(-box, box, size=(k, d))
+    X = c[rng.integers(0, k, n)] + rng.normal(0, sigma, size=(n, d))
+    return X.astype(np.float32).astype(np.float64)  # exactly representable in fp32
+
+
+@pytest.mark.parametrize("n,d,k", [(5000, 3, 4), (20000, 8, 33), (30000, 50, 200),
+                                    (10000, 64, 17), (8000, 100, 40), (6000, 130, 9),
+                                    (12000, 50, 500), (777, 26, 2)])
+def test_assign_kernel_matches_fp64_oracle(gpu_world, native, n, d, k):
+    X = f32_blobs(n, d, k, seed=d * 1000 + k, sigma=0.3)
+    rng = np.random.default_rng(1)
+    C = X[rng.choice(n, k, replace=False)] + 1e-3
+    w = gpu_world
+    t = native.upload_dense(w.ctx, X, "f32", native.kmeans_ld(d))
+    lab, dist = native.kmeans_predict(w.ctx, t, C)
+    ref_lab, ref_cost = vanilla.find_closest(X, C)
+    # fp32 expansion vs exact fp64: allow label flips only where the top-2 gap is ~fp32 eps
+    bad = np.nonzero(lab != ref_lab)[0]
+    if len(bad):
+        D = ((X[bad][:, None, :] - C[None]) ** 2).sum(-1)
+        r = np.arange(len(bad))
+        gap = np.abs(D[r, lab[bad]] - D[r, ref_lab[bad]])
+        assert (gap <= 1e-4 * (1 + D.min(1))).all()
+    assert len(bad) <= max(2, n // 2000)
+    np.testing.assert_allclose(dist[lab == ref_lab], ref_cost[lab == ref_lab], rtol=2e-5,
+                               atol=1e-4)
+
+
+@pytest.mark.parametrize("d,k", [(8, 5), (50, 200), (100, 40), (130, 7)])
+def test_gpu_fit_bitwise_equals_cpu_engine(native, d, k):
+    """Same inputs, same assignments => identical fixed-point sums => identical centers."""
+    X = f32_blobs(20000, d, k, seed=k + d, sigma=0.2)
+    init = X[np.random.default_rng(2).choice(len(X), k, replace=False)]
+    g = native.Context(0, 0.5, 0)
+    c = native.Context(-1)
+    tg = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
+    tc = native.upload_dense(c, X, "f64", d)
+    rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, 8, 0.0)
+    rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, 8, 0.0)
+    assert rg["last_counts"] == rc["last_counts"]
+    assert np.array_equal(rg["centers"], rc["centers"])
+    np.testing.assert_allclose(rg["cost"], rc["cost"], rtol=1e-5)
+
+
+def test_gpu_fit_deterministic(native):
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, 2_000_000, 50, native.kmeans_ld(50), 0, 64, 10.0, 2.0, 5)
+    init = t.to_numpy(g, 0, 64)
+    r1 = native.kmeans_fit(g, native.LocalComm(True), t, init, 64, 5, 0.0)
+    r2 = native.kmeans_fit(g, native.LocalComm(True), t, init, 64, 5, 0.0)
+    assert np.array_equal(r1["centers"], r2["centers"]) and r1["cost"] == r2["cost"]
+
+
+def test_gpu_init_matches_cpu_engine(native):
+    X = f32_blobs(30000, 10, 12, seed=4, sigma=1.0)
+    g, c = native.Context(0, 0.5, 0), native.Context(-1)
+    tg = native.upload_dense(g, X, "f32", native.kmeans_ld(10))
+    tc = native.upload_dense(c, X, "f64", 10)
+    for mode in ("random", "k-means||"):
+        cg = native.kmeans_init(g, native.LocalComm(True), tg, 12, mode, 2, 11)
+        cc = native.kmeans_init(c, native.LocalComm(False), tc, 12, mode, 2, 11)
+        np.testing.assert_array_equal(cg, cc)
+
+
+def test_api_uses_gpu_engine(gpu_world):
+    X = f32_blobs(10000, 16, 6, seed=9)
+    m = O.KMeans(k=6, seed=3).fit(X)
+    assert m.fit_info["engine"] == "gpu"
+    ref = vanilla.fit(X, 6, 20, 1e-4, init_centers=None, seed=3)
+    assert abs(m.summary.trainingCost - ref.cost) / ref.cost < 1e-3
+    assert sum(m.summary.clusterSizes) == len(X)
+
+
+def test_synth_blobs_shard_independent(native):
+    g = native.Context(0, 0.5, 0)
+    full = native.synth_blobs(g, 1000, 7, native.kmeans_ld(7), 0, 5, 10.0, 1.0, 3)
+    part = native.synth_blobs(g, 400, 7, native.kmeans_ld(7), 600, 5, 10.0, 1.0, 3)
+    np.testing.assert_array_equal(full.to_numpy(g, 600, 400), part.to_numpy(g))
+
+
+def test_gpu_world_two_ranks_host_comm_bitwise():
+    """Two ranks on GPU 0 with host (gloo) collectives staged through pinned memory."""
+    rc, outs = run_world("dist_workers", "kmeans_native", nproc=2, device="gpu",
+                         use_rccl=False, n=20000, d=12, k=7)
+    assert rc == 0, outs
+    from dist_workers import kmeans_native
+
+    O.shutdown_world()
+    ref = kmeans_native(device="gpu", n=20000, d=12, k=7)
+    for o in outs:
+        assert o["engine"] == "gpu" and o["comm"] == "host"
+        assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
