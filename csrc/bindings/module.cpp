@@ -346,8 +346,9 @@ PYBIND11_MODULE(_native, m) {
       "kmeans_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
          py::object init_centers, int k, int max_iter, double tol, const std::string& init_mode,
-         int init_steps, uint64_t seed) {
+         int init_steps, uint64_t seed, bool precise) {
         KMeansParams p;
+        p.precise = precise;
         p.k = k;
         p.max_iter = max_iter;
         p.tol = tol;
@@ -382,11 +383,13 @@ PYBIND11_MODULE(_native, m) {
         out["init_seconds"] = r.init_seconds;
         out["iter_seconds"] = r.iter_seconds;
         out["global_rows"] = r.global_rows;
+        out["refine_tiles"] = r.refine_tiles;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),
       py::arg("k") = 2, py::arg("max_iter") = 20, py::arg("tol") = 1e-4,
-      py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1);
+      py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1,
+      py::arg("precise") = false);
   m.def(
       "kmeans_init",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,

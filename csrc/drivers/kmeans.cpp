@@ -172,26 +172,52 @@ CpuAssignOut cpu_assign(Context& ctx, const DenseTable& x, const std::vector<dou
 }
 
 // ---------------------------------------------------------------------------- GPU helpers
+// Device-resident centers in the padded kernel layout.
 struct GpuCenters {
-  Buffer c32, cnorm;
-  int k = 0, kpad = 0;
+  Buffer c32, cnorm, cstat;
+  int k = 0, kpad = 0, dp = 0;
 };
 
-GpuCenters upload_centers(Context& ctx, const std::vector<double>& centers, int k, int d) {
+GpuCenters alloc_centers(Context& ctx, int k, int d) {
   GpuCenters g;
   g.k = k;
   g.kpad = static_cast<int>(round_up(std::max(k, 1), 32));
-  Buffer c64 = ctx.alloc(sizeof(double) * size_t(k) * d);
-  ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * size_t(k) * d);
-  g.c32 = ctx.alloc(sizeof(float) * size_t(k) * d);
+  g.dp = kern::kmeans_dp(d);
+  g.c32 = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
   g.cnorm = ctx.alloc(sizeof(float) * g.kpad);
-  kern::kmeans_prepare_centers(c64.as<double>(), k, d, g.c32.as<float>(), g.cnorm.as<float>(),
-                               g.kpad, ctx.compute());
+  g.cstat = ctx.alloc(sizeof(float) * 4);
+  return g;
+}
+
+GpuCenters upload_centers(Context& ctx, const std::vector<double>& centers, int k, int d) {
+  GpuCenters g = alloc_centers(ctx, k, d);
+  Buffer c64 = ctx.alloc(sizeof(double) * size_t(std::max(k, 1)) * d);
+  ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * size_t(k) * d);
+  kern::kmeans_prepare_centers(c64.as<double>(), k, d, g.dp, g.c32.as<float>(),
+                               g.cnorm.as<float>(), g.cstat.as<float>(), g.kpad, ctx.compute());
   OAP_HIP_CHECK(hipStreamSynchronize(ctx.compute()));
   return g;
 }
 
-kern::KMeansAssignArgs base_args(const DenseTable& x, const GpuCenters& g) {
+// One assignment pass over the local rows.  Uses the fused single-launch kernel when the
+// centroids fit the LDS plan, otherwise walks centroid chunks (merge mode: exact-cost argmin
+// across chunks, earlier chunk wins ties) and accumulates from the labels afterwards.
+struct AssignReq {
+  bool accumulate = false;
+  bool sums_too = true;
+  bool precise = false;
+  const float* scale = nullptr;
+  u64* sums = nullptr;
+  u64* counts = nullptr;
+  int32_t* labels = nullptr;  // device, optional
+  float* mindist = nullptr;   // device, optional
+  double* cost_slab = nullptr;
+  u64* refine_tiles = nullptr;
+};
+
+// Returns the number of cost partials written to req.cost_slab.
+int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const AssignReq& req,
+               hipStream_t s) {
   kern::KMeansAssignArgs a;
   a.x = x.data.as<float>();
   a.n = x.rows;
@@ -199,9 +225,53 @@ kern::KMeansAssignArgs base_args(const DenseTable& x, const GpuCenters& g) {
   a.d = x.cols;
   a.centers = g.c32.as<float>();
   a.cnorm = g.cnorm.as<float>();
+  a.cstat = g.cstat.as<float>();
   a.k = g.k;
   a.kpad = g.kpad;
-  return a;
+  a.scale = req.scale;
+  a.sums = req.sums;
+  a.counts = req.counts;
+  a.cost_slab = req.cost_slab;
+  a.labels = req.labels;
+  a.mindist = req.mindist;
+  a.accumulate = req.accumulate;
+  a.sums_too = req.sums_too;
+  a.precise = req.precise;
+  a.refine_tiles = req.refine_tiles;
+  const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
+  if (x.cols > 128 || g.kpad <= kmax || kmax == 0)
+    return kern::kmeans_assign(a, ctx.info().cu_count, s);
+  // ---- chunked path (more centroids than one LDS plan holds)
+  Buffer lab, dist;
+  int32_t* labels = req.labels;
+  float* mind = req.mindist;
+  if (!labels) {
+    lab = ctx.alloc(sizeof(int32_t) * std::max<int64_t>(x.rows, 1));
+    labels = lab.as<int32_t>();
+  }
+  if (!mind) {
+    dist = ctx.alloc(sizeof(float) * std::max<int64_t>(x.rows, 1));
+    mind = dist.as<float>();
+  }
+  a.labels = labels;
+  a.mindist = mind;
+  a.accumulate = false;
+  a.cost_slab = nullptr;
+  for (int c = 0; c < g.k; c += kmax) {
+    const int kc = std::min(kmax, g.k - c);
+    a.centers = g.c32.as<float>() + size_t(c) * g.dp;
+    a.cnorm = g.cnorm.as<float>() + c;
+    a.k = kc;
+    a.kpad = static_cast<int>(round_up(kc, 32));
+    a.base = c;
+    a.merge = c > 0;
+    kern::kmeans_assign(a, ctx.info().cu_count, s);
+  }
+  if (req.accumulate)
+    kern::kmeans_accumulate(x.data.as<float>(), x.rows, static_cast<int>(x.ld), x.cols, labels,
+                            g.k, req.scale, req.sums_too ? req.sums : nullptr, req.counts, s);
+  if (req.cost_slab) return kern::reduce_sum_f32(mind, x.rows, req.cost_slab, s);
+  return 0;
 }
 
 void check_gpu_table(const DenseTable& x) {
@@ -232,11 +302,9 @@ class InitOps {
     if (m == 0 || x_.rows == 0) return;
     if (ctx_.is_gpu()) {
       GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
-      kern::KMeansAssignArgs a = base_args(x_, g);
-      a.accumulate = false;
-      a.mindist = tmp_.as<float>();
-      a.cost_slab = slab_.as<double>();
-      kern::kmeans_assign(a, ctx_.info().cu_count, ctx_.compute());
+      AssignReq req;
+      req.mindist = tmp_.as<float>();
+      gpu_assign(ctx_, x_, g, req, ctx_.compute());
       kern::elementwise_min(costs_.as<float>(), tmp_.as<float>(), x_.rows, ctx_.compute());
       OAP_HIP_CHECK(hipStreamSynchronize(ctx_.compute()));
     } else {
@@ -318,12 +386,11 @@ class InitOps {
       GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
       Buffer dc = ctx_.alloc(sizeof(u64) * m);
       ctx_.memset(dc.data(), 0, sizeof(u64) * m);
-      kern::KMeansAssignArgs a = base_args(x_, g);
-      a.accumulate = true;
-      a.sums_too = false;
-      a.counts = dc.as<u64>();
-      a.cost_slab = slab_.as<double>();
-      kern::kmeans_assign(a, ctx_.info().cu_count, ctx_.compute());
+      AssignReq req;
+      req.accumulate = true;
+      req.sums_too = false;
+      req.counts = dc.as<u64>();
+      gpu_assign(ctx_, x_, g, req, ctx_.compute());
       ctx_.copy_to_host(cnt.data(), dc.data(), sizeof(u64) * m);
       return cnt;
     }
@@ -626,52 +693,50 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
 
   // -------------------------------------------------------------------- GPU engine
   hipStream_t s = ctx.compute();
-  const int kpad = static_cast<int>(round_up(k, 32));
+  GpuCenters g = alloc_centers(ctx, k, d);
   Buffer c64 = ctx.alloc(sizeof(double) * kd);
-  Buffer c32 = ctx.alloc(sizeof(float) * kd);
-  Buffer cnorm = ctx.alloc(sizeof(float) * kpad);
   Buffer stats = ctx.alloc(sizeof(u64) * (kd + k));
   const int nslab = kern::kmeans_cost_slab_size(ctx.info().cu_count);
   Buffer slab = ctx.alloc(sizeof(double) * nslab);
   Buffer cost_d = ctx.alloc(sizeof(double));
-  Buffer scale = ctx.alloc(sizeof(float) * d);
+  Buffer scale = ctx.alloc(sizeof(float) * (round_up(d, 4) + 4));
   Buffer inv_scale = ctx.alloc(sizeof(double) * d);
   Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags));
+  Buffer refine_d = ctx.alloc(sizeof(u64));
   Buffer flags_h = ctx.alloc_pinned(sizeof(kern::KMeansFlags));
   Buffer counts_h = ctx.alloc_pinned(sizeof(u64) * k);
+  Buffer refine_h = ctx.alloc_pinned(sizeof(u64));
+  ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4), s);
+  ctx.memset(refine_d.data(), 0, sizeof(u64), s);
   ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * kd, s);
   ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d, s);
   ctx.copy_to_backend(inv_scale.data(), fp.inv_scale.data(), sizeof(double) * d, s);
-  kern::kmeans_prepare_centers(c64.as<double>(), k, d, c32.as<float>(), cnorm.as<float>(), kpad,
-                               s);
+  kern::kmeans_prepare_centers(c64.as<double>(), k, d, g.dp, g.c32.as<float>(),
+                               g.cnorm.as<float>(), g.cstat.as<float>(), g.kpad, s);
   u64* sums = stats.as<u64>();
   u64* counts = sums + kd;
 
-  kern::KMeansAssignArgs a;
-  a.x = x.data.as<float>();
-  a.n = x.rows;
-  a.ld = static_cast<int>(x.ld);
-  a.d = d;
-  a.centers = c32.as<float>();
-  a.cnorm = cnorm.as<float>();
-  a.k = k;
-  a.kpad = kpad;
-  a.scale = scale.as<float>();
-  a.sums = sums;
-  a.counts = counts;
-  a.cost_slab = slab.as<double>();
-  a.accumulate = true;
-  a.sums_too = true;
+  AssignReq req;
+  req.accumulate = true;
+  req.sums_too = true;
+  req.precise = p.precise;
+  req.scale = scale.as<float>();
+  req.sums = sums;
+  req.counts = counts;
+  req.cost_slab = slab.as<double>();
+  req.refine_tiles = refine_d.as<u64>();
 
   kern::KMeansFinalizeArgs fa;
   fa.sums = sums;
   fa.counts = counts;
   fa.inv_scale = inv_scale.as<double>();
   fa.centers64 = c64.as<double>();
-  fa.centers32 = c32.as<float>();
-  fa.cnorm = cnorm.as<float>();
+  fa.centers32 = g.c32.as<float>();
+  fa.cnorm = g.cnorm.as<float>();
+  fa.cstat = g.cstat.as<float>();
   fa.k = k;
   fa.d = d;
+  fa.dp = g.dp;
   fa.tol = p.tol;
   fa.cost_in = cost_d.as<double>();
   fa.flags = flags_d.data();
@@ -684,9 +749,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     roctx_push("kmeans/iteration");
     e0.record(s);
     OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
-    int nb = kern::kmeans_assign(a, ctx.info().cu_count, s);
-    kern::sum_f64(slab.as<double>(), std::max(nb, 0), cost_d.as<double>(), s);
-    if (nb == 0) OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+    int nb = gpu_assign(ctx, x, g, req, s);
+    if (nb > 0)
+      kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
+    else
+      OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
     e1.record(s);
     if (comm.size() > 1) {
       if (comm.on_device()) {
@@ -732,8 +799,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);
   res.centers.resize(kd);
   ctx.copy_to_host(res.centers.data(), c64.data(), sizeof(double) * kd, s);
+  ctx.copy_to_host(refine_h.data(), refine_d.data(), sizeof(u64), s);
+  res.refine_tiles = static_cast<int64_t>(*refine_h.as<u64>());
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
+  M.set_value("kmeans/refine_tiles", double(res.refine_tiles));
   M.set_value("kmeans/samples_per_sec",
               res.iter_seconds > 0 ? double(x.global_rows) * res.num_iter / res.iter_seconds : 0);
   return res;
@@ -753,13 +823,10 @@ void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>
   GpuCenters g = upload_centers(ctx, centers, k, x.cols);
   Buffer dl = ctx.alloc(sizeof(int32_t) * x.rows);
   Buffer dd = ctx.alloc(sizeof(float) * x.rows);
-  Buffer slab = ctx.alloc(sizeof(double) * kern::kmeans_cost_slab_size(ctx.info().cu_count));
-  kern::KMeansAssignArgs a = base_args(x, g);
-  a.accumulate = false;
-  a.labels = dl.as<int32_t>();
-  a.mindist = dd.as<float>();
-  a.cost_slab = slab.as<double>();
-  kern::kmeans_assign(a, ctx.info().cu_count, ctx.compute());
+  AssignReq req;
+  req.labels = dl.as<int32_t>();
+  req.mindist = dd.as<float>();
+  gpu_assign(ctx, x, g, req, ctx.compute());
   if (labels) ctx.copy_to_host(labels, dl.data(), sizeof(int32_t) * x.rows);
   if (dist2) {
     std::vector<float> h(x.rows);

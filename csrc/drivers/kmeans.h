@@ -28,6 +28,9 @@ struct KMeansParams {
   KMeansInit init = KMeansInit::Parallel;
   int init_steps = 2;
   uint64_t seed = 1;
+  // exact-fp32 MFMA distances only (default: bf16-split fast path + exact refinement, which
+  // yields the same assignments)
+  bool precise = false;
 };
 
 struct KMeansResult {
@@ -42,6 +45,7 @@ struct KMeansResult {
   double init_seconds = 0.0;
   double iter_seconds = 0.0;
   int64_t global_rows = 0;
+  int64_t refine_tiles = 0;  // 32-row tiles re-decided by the exact pass (GPU fast path)
 };
 
 // Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for

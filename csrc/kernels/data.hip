@@ -1,0 +1,217 @@
+// Data-movement / utility kernels: ingestion conversion + padding, column statistics, on-device
+// synthetic data, deterministic reductions, row gathers and stream compaction.
+//
+// Ingestion replaces the reference's row-by-row JNI copies into oneDAL tables
+// (mllib-dal/src/main/native/OneDAL.cpp:50-60): the host streams raw chunks,
+// the device converts dtype and applies the padded row layout the MFMA kernels expect.
+#include <hip/hip_bf16.h>
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "kernels/device_utils.h"
+#include "kernels/kernels.h"
+
+namespace oap {
+namespace kern {
+
+namespace {
+
+template <typename Src, typename Dst>
+__device__ inline Dst cvt(Src v) {
+  return static_cast<Dst>(static_cast<float>(v));
+}
+template <>
+__device__ inline double cvt<double, double>(double v) {
+  return v;
+}
+
+template <typename Src, typename Dst>
+__global__ void oap_convert_pad(const Src* src, int64_t rows, int cols, int64_t src_ld, Dst* dst,
+                                int64_t dst_ld) {
+  const int64_t total = rows * dst_ld;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t r = i / dst_ld;
+    int c = static_cast<int>(i - r * dst_ld);
+    dst[i] = c < cols ? cvt<Src, Dst>(src[r * src_ld + c]) : cvt<Src, Dst>(Src(0));
+  }
+}
+
+__global__ void oap_column_absmax(const float* x, int64_t rows, int cols, int64_t ld,
+                                  float* out) {
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    float m = 0.f;
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) m = fmaxf(m, fabsf(x[r * ld + c]));
+    atomicMax(reinterpret_cast<int*>(out) + c, __float_as_int(m));  // m >= 0: int order == float
+  }
+}
+
+__global__ void oap_synth_blobs(float* x, int64_t rows, int cols, int64_t ld, int64_t row0,
+                                int ncenters, float box, float sigma, uint64_t seed) {
+  const int64_t total = rows * ld;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t r = i / ld;
+    int c = static_cast<int>(i - r * ld);
+    if (c >= cols) {
+      x[i] = 0.f;
+      continue;
+    }
+    int64_t grow = row0 + r;
+    uint64_t lab = splitmix64(seed ^ (uint64_t(grow) * 0x2545F4914F6CDD1Dull)) % uint64_t(ncenters);
+    uint64_t hc = splitmix64(seed * 31ull + lab * 1315423911ull + uint64_t(c) * 2654435761ull);
+    float center = (u01_24(hc) * 2.f - 1.f) * box;
+    uint64_t h1 = splitmix64(seed ^ 0xABCDEFull ^ (uint64_t(grow) << 20) ^ uint64_t(c));
+    uint64_t h2 = splitmix64(h1);
+    float u1 = fmaxf(u01_24(h1), 1e-7f), u2 = u01_24(h2);
+    float gauss = sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2);
+    x[i] = center + sigma * gauss;
+  }
+}
+
+__global__ void oap_elementwise_min(float* acc, const float* v, int64_t n) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x)
+    acc[i] = fminf(acc[i], v[i]);
+}
+
+__global__ void oap_bernoulli_select(const float* cost, int64_t n, int64_t row0, double factor,
+                                     uint64_t seed, int step, int32_t* flag) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    uint64_t hsh = splitmix64(seed ^ (uint64_t(step) << 48) ^ uint64_t(row0 + i));
+    double u = double(hsh >> 11) * (1.0 / 9007199254740992.0);
+    flag[i] = (u < factor * double(cost[i])) ? 1 : 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void oap_reduce_sum_f32(const float* v, int64_t n,
+                                                          double* slab) {
+  __shared__ double ws[4];
+  double acc = 0.0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x)
+    acc += double(v[i]);
+  acc = wave_sum_f64(acc);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) slab[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void oap_sum_f64(const double* in, int m, double* out) {
+  double v = 0.0;  // single wave, fixed order
+  for (int i = threadIdx.x; i < m; i += 64) v += in[i];
+  v = wave_sum_f64(v);
+  if (threadIdx.x == 0) out[0] = v;
+}
+
+__global__ void oap_gather_rows(const float* x, int64_t ld, int cols, const int64_t* idx,
+                                int64_t m, float* out) {
+  const int64_t total = m * cols;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t r = i / cols;
+    int c = static_cast<int>(i - r * cols);
+    out[i] = x[idx[r] * ld + c];
+  }
+}
+
+__global__ void oap_compact_flags(const int32_t* flag, int64_t n, int64_t* out,
+                                  unsigned long long* counter) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x)
+    if (flag[i]) out[atomicAdd(counter, 1ull)] = i;
+}
+
+template <typename Src, typename Dst>
+void launch_convert(const void* src, int64_t rows, int cols, int64_t src_ld, void* dst,
+                    int64_t dst_ld, hipStream_t s) {
+  hipLaunchKernelGGL((oap_convert_pad<Src, Dst>), dim3(grid_for(rows * dst_ld, 256)), dim3(256), 0,
+                     s, static_cast<const Src*>(src), rows, cols, src_ld, static_cast<Dst*>(dst),
+                     dst_ld);
+}
+
+}  // namespace
+
+void convert_pad(const void* src, DType src_t, int64_t rows, int cols, int64_t src_ld, void* dst,
+                 DType dst_t, int64_t dst_ld, hipStream_t s) {
+  if (rows == 0) return;
+  if (src_t == DType::F64 && dst_t == DType::F32)
+    launch_convert<double, float>(src, rows, cols, src_ld, dst, dst_ld, s);
+  else if (src_t == DType::F32 && dst_t == DType::F32)
+    launch_convert<float, float>(src, rows, cols, src_ld, dst, dst_ld, s);
+  else if (src_t == DType::F64 && dst_t == DType::BF16)
+    launch_convert<double, __bf16>(src, rows, cols, src_ld, dst, dst_ld, s);
+  else if (src_t == DType::F32 && dst_t == DType::BF16)
+    launch_convert<float, __bf16>(src, rows, cols, src_ld, dst, dst_ld, s);
+  else if (src_t == DType::F64 && dst_t == DType::F64)
+    launch_convert<double, double>(src, rows, cols, src_ld, dst, dst_ld, s);
+  else if (src_t == DType::F32 && dst_t == DType::F64)
+    launch_convert<float, double>(src, rows, cols, src_ld, dst, dst_ld, s);
+  else
+    OAP_THROW(ConfigError, "convert_pad: unsupported " << dtype_name(src_t) << " -> "
+                                                       << dtype_name(dst_t));
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void column_absmax(const float* x, int64_t rows, int cols, int64_t ld, float* out,
+                   hipStream_t s) {
+  if (rows == 0) return;
+  int grid = static_cast<int>(rows < 2048 ? rows : 2048);
+  hipLaunchKernelGGL(oap_column_absmax, dim3(grid), dim3(256), 0, s, x, rows, cols, ld, out);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void synth_blobs(float* x, int64_t rows, int cols, int64_t ld, int64_t row0, int ncenters,
+                 float box, float sigma, uint64_t seed, hipStream_t s) {
+  if (rows == 0) return;
+  hipLaunchKernelGGL(oap_synth_blobs, dim3(grid_for(rows * ld, 256)), dim3(256), 0, s, x, rows,
+                     cols, ld, row0, ncenters, box, sigma, seed);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void elementwise_min(float* acc, const float* v, int64_t n, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(oap_elementwise_min, dim3(grid_for(n, 256)), dim3(256), 0, s, acc, v, n);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void bernoulli_select(const float* cost, int64_t n, int64_t row0, double factor, uint64_t seed,
+                      int step, int32_t* flag, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(oap_bernoulli_select, dim3(grid_for(n, 256)), dim3(256), 0, s, cost, n,
+                     row0, factor, seed, step, flag);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+int reduce_sum_f32(const float* v, int64_t n, double* slab, hipStream_t s) {
+  const int grid = 256;
+  hipLaunchKernelGGL(oap_reduce_sum_f32, dim3(grid), dim3(256), 0, s, v, n, slab);
+  OAP_HIP_CHECK(hipGetLastError());
+  return grid;
+}
+
+void sum_f64(const double* in, int m, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(oap_sum_f64, dim3(1), dim3(64), 0, s, in, m, out);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void gather_rows(const float* x, int64_t ld, int cols, const int64_t* idx, int64_t m, float* out,
+                 hipStream_t s) {
+  if (m == 0) return;
+  hipLaunchKernelGGL(oap_gather_rows, dim3(grid_for(m * cols, 256)), dim3(256), 0, s, x, ld,
+                     cols, idx, m, out);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void compact_flags(const int32_t* flag, int64_t n, int64_t* out_idx, unsigned long long* counter,
+                   hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(oap_compact_flags, dim3(grid_for(n, 256)), dim3(256), 0, s, flag, n,
+                     out_idx, counter);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace kern
+}  // namespace oap

@@ -1,0 +1,59 @@
+// Device-side helpers shared by the HIP kernels (wave64 reductions, hashing RNG, bf16 splits).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace oap {
+namespace kern {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned long long u64;
+
+__device__ inline double wave_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+__device__ inline float wave_sum_f32(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+__device__ inline float wave_max_f32(float v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+__host__ __device__ inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ inline float u01_24(uint64_t h) {  // [0,1) with 24 random bits
+  return static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
+}
+
+// x = hi + lo + O(2^-18 |x|): the 2-term bf16 split used by the "bf16x3" MFMA products.
+__device__ inline void bf16_split(float x, __bf16& hi, __bf16& lo) {
+  hi = static_cast<__bf16>(x);
+  lo = static_cast<__bf16>(x - static_cast<float>(hi));
+}
+
+inline int grid_for(int64_t n, int block, int cap = 8192) {
+  int64_t g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return static_cast<int>(g);
+}
+
+}  // namespace kern
+}  // namespace oap

@@ -43,8 +43,11 @@ def test_assign_kernel_matches_fp64_oracle(gpu_world, native, n, d, k):
 @pytest.mark.parametrize("d,k", [(8, 5), (50, 200), (100, 40), (130, 7)])
 def test_gpu_fit_bitwise_equals_cpu_engine(native, d, k):
     """Same inputs, same assignments => identical fixed-point sums => identical centers."""
-    X = f32_blobs(20000, d, k, seed=k + d, sigma=0.2)
-    init = X[np.random.default_rng(2).choice(len(X), k, replace=False)]
+    rng = np.random.default_rng(k + d)
+    C = rng.uniform(-10, 10, size=(k, d))
+    X = (C[rng.integers(0, k, 20000)] + rng.normal(0, 0.2, size=(20000, d)))
+    X = X.astype(np.float32).astype(np.float64)
+    init = (C + rng.normal(0, 0.05, size=C.shape)).astype(np.float32).astype(np.float64)
     g = native.Context(0, 0.5, 0)
     c = native.Context(-1)
     tg = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
@@ -104,3 +107,51 @@ def test_gpu_world_two_ranks_host_comm_bitwise():
     for o in outs:
         assert o["engine"] == "gpu" and o["comm"] == "host"
         assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
+
+
+@pytest.mark.parametrize("d,k", [(50, 200), (16, 64), (100, 30)])
+def test_fast_path_bitwise_equals_precise(native, d, k):
+    """bf16-split + refinement must reproduce the exact-fp32 kernel's assignments exactly."""
+    X = f32_blobs(60000, d, k, seed=d + 7 * k, sigma=3.0, box=4.0)  # heavily overlapping
+    init = X[np.random.default_rng(5).choice(len(X), k, replace=False)]
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
+    rf = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 4, 0.0, precise=False)
+    rp = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 4, 0.0, precise=True)
+    assert rf["last_counts"] == rp["last_counts"]
+    assert np.array_equal(rf["centers"], rp["centers"])
+    assert rf["cost"] == rp["cost"]
+
+
+def test_refinement_triggers_on_near_ties(native):
+    """Rows exactly between two centers must take the exact pass (and still match precise)."""
+    rng = np.random.default_rng(0)
+    d, k = 32, 8
+    C = rng.uniform(-5, 5, size=(k, d))
+    mids = 0.5 * (C[rng.integers(0, k, 5000)] + C[rng.integers(0, k, 5000)])
+    X = np.concatenate([mids, C[rng.integers(0, k, 5000)] + rng.normal(0, 0.1, (5000, d))])
+    X = X.astype(np.float32).astype(np.float64)
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
+    rf = native.kmeans_fit(g, native.LocalComm(True), t, C, k, 1, 0.0, precise=False)
+    rp = native.kmeans_fit(g, native.LocalComm(True), t, C, k, 1, 0.0, precise=True)
+    assert rf["refine_tiles"] > 0
+    assert rf["last_counts"] == rp["last_counts"]
+    assert np.array_equal(rf["centers"], rp["centers"])
+
+
+def test_many_centroids_chunked_path(gpu_world, native):
+    """k beyond one LDS plan: centroid chunks + merge + label-driven accumulation."""
+    d, k = 50, 1500
+    X = f32_blobs(40000, d, k, seed=1, sigma=0.05)
+    C = X[np.random.default_rng(3).choice(len(X), k, replace=False)]
+    t = native.upload_dense(gpu_world.ctx, X, "f32", native.kmeans_ld(d))
+    lab, dist = native.kmeans_predict(gpu_world.ctx, t, C)
+    ref_lab, ref_d = vanilla.find_closest(X, C)
+    assert (lab == ref_lab).mean() > 0.9999
+    r = native.kmeans_fit(gpu_world.ctx, gpu_world.comm, t, C, k, 2, 0.0)
+    c = native.Context(-1)
+    tc = native.upload_dense(c, X, "f64", d)
+    rc = native.kmeans_fit(c, native.LocalComm(False), tc, C, k, 2, 0.0)
+    assert r["last_counts"] == rc["last_counts"]
+    assert np.array_equal(r["centers"], rc["centers"])
