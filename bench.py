@@ -58,7 +58,7 @@ def bench_kmeans(args, w):
         N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, 0.0)
     _barrier_sync(w)
     t0 = time.perf_counter()
-    r = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, 0.0)
+    r = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, 0.0, precise=args.precise)
     _barrier_sync(w)
     el = time.perf_counter() - t0
     el_max = float(w.allreduce_np(np.array([el]), "max")[0])
@@ -91,6 +91,9 @@ def bench_kmeans(args, w):
                   "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
                   "allreduce_us": ar["total_us"] / max(ar["count"], 1),
                   "achieved_tflops": flops / (el_max / args.steps) / 1e12,
+                  "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
+                  "distance_path": "fp32-exact MFMA" if args.precise else
+                  "bf16-split MFMA + exact-fp32 refinement (assignments identical to fp32)",
                   "cost": r["cost"]},
     }
     return out
@@ -107,6 +110,8 @@ def main(argv=None):
     ap.add_argument("--dim", type=int, default=50)
     ap.add_argument("--k", type=int, default=200)
     ap.add_argument("--skip-fit", action="store_true")
+    ap.add_argument("--precise", action="store_true",
+                    help="exact-fp32 MFMA distances only (no bf16-split fast path)")
     args = ap.parse_args(argv)
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))

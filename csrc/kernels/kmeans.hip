@@ -66,7 +66,7 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
   m.cn = off;
   off = round16(off + size_t(kpad) * 4);
   m.acc = off;
-  if (lds_acc) off += size_t(k) * d * 8;
+  if (lds_acc) off += size_t(k) * (d | 1) * 8;  // odd row stride: conflict-free ds_add_u64
   m.cnt = off;
   if (lds_acc) off += size_t(k) * 8;
   off = round16(off);
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   }
   for (int c = tid; c < kpad; c += kThreads) cn[c] = (c < k) ? a.cnorm[c] : INFINITY;
   if (lds_acc && accumulate) {
-    for (int i = tid; i < k * d; i += kThreads) acc_l[i] = 0ull;
+    for (int i = tid; i < k * (d | 1); i += kThreads) acc_l[i] = 0ull;
     for (int i = tid; i < k; i += kThreads) cnt_l[i] = 0ull;
   }
   __syncthreads();
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     if (accumulate) {
       if (h == 0) atomicAdd(lds_acc ? &cnt_l[bidx] : &a.counts[bidx], 1ull);
       if (a.sums_too) {
-        u64* ap = (lds_acc ? acc_l : a.sums) + size_t(bidx) * d;
+        u64* ap = lds_acc ? acc_l + size_t(bidx) * (d | 1) : a.sums + size_t(bidx) * d;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
 #pragma unroll
@@ -350,7 +350,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   if (lds_acc && accumulate) {
     if (a.sums_too)
       for (int i = tid; i < k * d; i += kThreads) {
-        u64 v = acc_l[i];
+        const int b = i / d, f = i - b * d;
+        u64 v = acc_l[b * (d | 1) + f];
         if (v) atomicAdd(&a.sums[i], v);
       }
     for (int i = tid; i < k; i += kThreads) {
@@ -442,10 +443,9 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
     double shift2 = 0.0, nrm = 0.0;
     if (cntv > 0) {
       atomicAdd(&s_nonempty, 1);
-      const double inv_n = 1.0 / double(cntv);
       for (int f = 0; f < a.d; ++f) {
         long long sv = static_cast<long long>(a.sums[size_t(c) * a.d + f]);
-        double nv = double(sv) * a.inv_scale[f] * inv_n;
+        double nv = double(sv) * a.inv_scale[f] / double(cntv);  // same formula as the CPU engine
         double df = nv - c64[f];
         shift2 += df * df;
         c64[f] = nv;
