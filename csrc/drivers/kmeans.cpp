@@ -681,7 +681,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       res.cost_history.push_back(cost);
       res.last_counts.assign(stats.begin() + kd, stats.end());
       res.num_iter = it + 1;
-      if (conv) {
+      if (conv && p.tol >= 0) {  // tol < 0: run exactly max_iter iterations
         res.converged = true;
         break;
       }
@@ -791,7 +791,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     res.cost = fl->cost;
     res.cost_history.push_back(fl->cost);
     res.num_iter = it + 1;
-    if (fl->converged) {
+    if (fl->converged && p.tol >= 0) {  // tol < 0: run exactly max_iter iterations
       res.converged = true;
       break;
     }

@@ -143,12 +143,16 @@ def test_refinement_triggers_on_near_ties(native):
 def test_many_centroids_chunked_path(gpu_world, native):
     """k beyond one LDS plan: centroid chunks + merge + label-driven accumulation."""
     d, k = 50, 1500
-    X = f32_blobs(40000, d, k, seed=1, sigma=0.05)
-    C = X[np.random.default_rng(3).choice(len(X), k, replace=False)]
+    rng = np.random.default_rng(1)
+    centers = rng.uniform(-10, 10, size=(k, d))
+    X = (centers[rng.integers(0, k, 40000)] + rng.normal(0, 0.05, size=(40000, d)))
+    X = X.astype(np.float32).astype(np.float64)
+    C = (centers + rng.normal(0, 0.01, size=centers.shape)).astype(np.float32).astype(np.float64)
     t = native.upload_dense(gpu_world.ctx, X, "f32", native.kmeans_ld(d))
     lab, dist = native.kmeans_predict(gpu_world.ctx, t, C)
     ref_lab, ref_d = vanilla.find_closest(X, C)
-    assert (lab == ref_lab).mean() > 0.9999
+    assert (lab == ref_lab).all()
+    np.testing.assert_allclose(dist, ref_d, rtol=1e-4, atol=1e-5)
     r = native.kmeans_fit(gpu_world.ctx, gpu_world.comm, t, C, k, 2, 0.0)
     c = native.Context(-1)
     tc = native.upload_dense(c, X, "f64", d)
