@@ -429,6 +429,18 @@ PYBIND11_MODULE(_native, m) {
         }
         return py::make_tuple(labels, dist);
       });
+  m.def(
+      "kmeans_assign_timing",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> centers,
+         int reps, bool precise, int ablate) {
+        auto c = py::array_t<double, py::array::c_style | py::array::forcecast>(centers);
+        std::vector<double> cv(c.data(), c.data() + c.size());
+        int k = static_cast<int>(c.shape(0));
+        py::gil_scoped_release rel;
+        return kmeans_assign_timing(*ctx, *t, cv, k, reps, precise, ablate);
+      },
+      py::arg("ctx"), py::arg("table"), py::arg("centers"), py::arg("reps") = 10,
+      py::arg("precise") = false, py::arg("ablate") = 0);
   m.def("local_kmeans_pp",
         [](py::array_t<double> pts, py::array_t<double> w, int k, int max_iter, uint64_t seed) {
           auto p = py::array_t<double, py::array::c_style | py::array::forcecast>(pts);

@@ -81,17 +81,25 @@ struct FixedPoint {
   std::vector<double> inv_scale;  // 2^-e_f
 };
 
-FixedPoint fixed_point_scales(const std::vector<double>& absmax, int64_t global_rows) {
+// Per-feature fixed-point exponents e_f: every |rint(x * 2^e_f)| summed over the whole dataset
+// stays below 2^61 (int64 global sums, any rank count), and over one assign workgroup's rows
+// below 2^52 (exact integer partial sums in the GPU kernel's fp64 LDS accumulator).  The same
+// function serves both engines so CPU and GPU produce identical integers.
+FixedPoint fixed_point_scales(const std::vector<double>& absmax, int64_t global_rows,
+                              int64_t max_local_rows) {
   FixedPoint fp;
   int d = static_cast<int>(absmax.size());
   fp.scale.resize(d);
   fp.inv_scale.resize(d);
-  int ln = static_cast<int>(std::ceil(std::log2(double(std::max<int64_t>(global_rows, 2)))));
+  auto clog2 = [](double v) { return static_cast<int>(std::ceil(std::log2(std::max(v, 2.0)))); };
+  const int ln = clog2(double(global_rows));
+  const int lb = clog2(double(kern::kmeans_rows_per_block_bound(max_local_rows)));
+  const int budget = std::min(61 - ln, 52 - lb);
   for (int f = 0; f < d; ++f) {
     int e = 0;
     if (absmax[f] > 0 && std::isfinite(absmax[f])) {
       int lm = static_cast<int>(std::ceil(std::log2(absmax[f])));
-      e = 61 - ln - lm;
+      e = budget - lm;
       e = std::max(-100, std::min(120, e));
     }
     fp.scale[f] = std::ldexp(1.0f, e);
@@ -644,7 +652,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   res.k = k;
 
   auto absmax = global_column_absmax(ctx, comm, x);
-  FixedPoint fp = fixed_point_scales(absmax, x.global_rows);
+  const int64_t max_local =
+      static_cast<int64_t>(comm_allreduce_scalar(ctx, comm, double(x.rows), ReduceOp::Max));
+  FixedPoint fp = fixed_point_scales(absmax, x.global_rows, max_local);
   const size_t kd = size_t(k) * d;
   auto t_iter = std::chrono::steady_clock::now();
   Metrics& M = ctx.metrics();
@@ -833,6 +843,51 @@ void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>
     ctx.copy_to_host(h.data(), dd.data(), sizeof(float) * x.rows);
     for (int64_t i = 0; i < x.rows; ++i) dist2[i] = h[i];
   }
+}
+
+}  // namespace oap
+
+namespace oap {
+
+double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
+                            int k, int reps, bool precise, int ablate) {
+  OAP_CHECK(ctx.is_gpu(), "kmeans_assign_timing needs a GPU context");
+  check_gpu_table(x);
+  ctx.activate();
+  const int d = x.cols;
+  GpuCenters g = upload_centers(ctx, centers, k, d);
+  std::vector<double> absmax(d, 1.0);
+  for (int f = 0; f < d; ++f) absmax[f] = 64.0;
+  FixedPoint fp = fixed_point_scales(absmax, x.rows, x.rows);
+  Buffer scale = ctx.alloc(sizeof(float) * (round_up(d, 4) + 4));
+  ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4));
+  ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d);
+  Buffer stats = ctx.alloc(sizeof(u64) * (size_t(k) * d + k));
+  Buffer slab = ctx.alloc(sizeof(double) * kern::kmeans_cost_slab_size(ctx.info().cu_count));
+  kern::KMeansAssignArgs a;
+  a.x = x.data.as<float>();
+  a.n = x.rows;
+  a.ld = static_cast<int>(x.ld);
+  a.d = d;
+  a.centers = g.c32.as<float>();
+  a.cnorm = g.cnorm.as<float>();
+  a.cstat = g.cstat.as<float>();
+  a.k = k;
+  a.kpad = g.kpad;
+  a.scale = scale.as<float>();
+  a.sums = stats.as<u64>();
+  a.counts = stats.as<u64>() + size_t(k) * d;
+  a.cost_slab = slab.as<double>();
+  a.precise = precise;
+  a.ablate = ablate;
+  hipStream_t s = ctx.compute();
+  Event e0, e1;
+  kern::kmeans_assign(a, ctx.info().cu_count, s);  // warm
+  e0.record(s);
+  for (int i = 0; i < reps; ++i) kern::kmeans_assign(a, ctx.info().cu_count, s);
+  e1.record(s);
+  e1.sync();
+  return Event::elapsed_ms(e0, e1) / std::max(reps, 1);
 }
 
 }  // namespace oap

@@ -61,6 +61,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
 void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>& centers, int k,
                     int32_t* labels, double* dist2);
 
+// Average device time (ms) of the fused assign kernel over `reps` launches with optional timing
+// ablations (kern::KMeansAssignArgs::ablate) — the per-phase cost breakdown used for tuning.
+double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
+                            int k, int reps, bool precise, int ablate);
+
 // k-means++ over weighted candidates, then up to max_iter weighted Lloyd iterations (host).
 // Mirrors the semantics of Spark's LocalKMeans.kMeansPlusPlus (RNG stream is our own).
 std::vector<double> local_kmeans_pp(const std::vector<double>& pts, const std::vector<double>& w,

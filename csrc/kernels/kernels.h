@@ -63,7 +63,11 @@ struct KMeansAssignArgs {
   bool precise = false;                  // exact-fp32 MFMA only (no bf16x3 fast path)
   bool merge = false;                    // keep labels/mindist from earlier chunks unless beaten
   unsigned long long* refine_tiles = nullptr;  // optional: tiles that took the exact pass
+  int ablate = 0;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work
 };
+// Upper bound on rows one assign workgroup processes for n local rows (device independent); the
+// fixed-point scale keeps per-workgroup LDS partial sums below 2^53 with it.
+int64_t kmeans_rows_per_block_bound(int64_t n);
 // Largest centroid count one launch can hold in LDS for d features (0 => generic kernel).
 int kmeans_lds_kmax(int d, bool precise);
 // Returns the number of blocks used (== entries written to cost_slab).

@@ -1,0 +1,471 @@
+// oap_kmeans_assign_mfma — the fused K-Means hot kernel for MI355X (gfx950, CDNA4).
+//
+// One launch per Lloyd iteration replaces oneDAL's step1Local (mllib-dal/src/main/native/
+// KMeansDALImpl.cpp:70-77): distance cross-term on the matrix cores, argmin in
+// registers, exact per-row cost, and per-cluster fixed-point sums/counts.
+//
+// * Layout: a wave owns a 32-row tile; lane (r = l&31, h = l>>5) holds features f = 16s + 8h + j
+//   (s < KS, j < 8) of row r in registers.  Centroids are the MFMA A operand, staged ONCE per
+//   workgroup in LDS with an odd-16B-slot row stride (conflict-free ds_read_b128); data rows are
+//   the B operand straight from registers.  The 32x32 accumulator holds one data row x 16
+//   centroids per lane, so the argmin is a per-lane scan plus one cross-half exchange.
+// * Fast path: the cross term x.c on the bf16 matrix cores as a 3-product split
+//   (x_hi c_hi + x_hi c_lo + x_lo c_hi, operands split as hi + lo bf16, fp32 accumulation):
+//   3 x v_mfma_f32_32x32x16_bf16 replace 8 x v_mfma_f32_32x32x2_f32 per 16 features.  The split's
+//   error is bounded by 4.6e-5 |x||c| per distance; every tile holding a row whose best/2nd-best
+//   gap is inside that bound (+ the fp32 path's own bound) is re-decided by the exact-fp32 MFMA
+//   pass, so assignments are IDENTICAL to the exact kernel (tested bitwise) at bf16-split speed.
+// * Exact path (PRECISE and refinement): v_mfma_f32_32x32x2_f32 in the same feature order.
+// * Exact per-row cost |x - c_best|^2 from the fp32 center; in the fast path the c_best rows are
+//   fetched from L2 one tile ahead (software pipelined) so their latency hides under the next
+//   tile's MFMAs.
+// * Centroid sums in FIXED POINT: v = rint(x * 2^e_f) is an integer; the per-workgroup LDS
+//   accumulator adds these integers as doubles (ds_add_f64) — exact while |partial| < 2^53,
+//   which the driver's choice of e_f guarantees — so the order of the LDS atomics cannot change a
+//   bit.  The flush converts to int64 and adds across workgroups, ranks (RCCL) in integer
+//   arithmetic: results are bitwise identical for any schedule and any world size.
+// * Persistent grid (>= 256 workgroups of 512 threads, one per CU: 2 waves per SIMD so one wave's
+//   VALU epilogue overlaps the other's MFMAs), register prefetch of the next tile.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "kernels/device_utils.h"
+#include "kernels/kmeans_internal.h"
+
+namespace oap {
+namespace kern {
+
+namespace {
+
+constexpr int kThreads = kAssignThreads;
+constexpr int kWaves = kThreads / 64;
+
+__host__ __device__ inline size_t round16(size_t v) { return (v + 15) / 16 * 16; }
+__host__ __device__ inline int stride_bf16(int dp) { return dp + 8; }  // (dp+8)/8 odd slots
+__host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)/4 odd slots
+
+struct Smem {
+  size_t planes, cn, sc, acc, cnt, wcost, total;
+};
+__host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool precise,
+                                          bool lds_acc) {
+  Smem m;
+  size_t off = 0;
+  m.planes = 0;
+  off += precise ? size_t(kpad) * stride_f32(dp) * 4 : size_t(2) * kpad * stride_bf16(dp) * 2;
+  off = round16(off);
+  m.cn = off;
+  off = round16(off + size_t(kpad) * 4);
+  m.sc = off;
+  off = round16(off + size_t(dp) * 4);
+  m.acc = off;
+  if (lds_acc) off += size_t(k) * (d | 1) * 8;  // odd row stride => conflict-free ds_add_f64
+  off = round16(off);
+  m.cnt = off;
+  if (lds_acc) off += size_t(k) * 4;
+  off = round16(off);
+  m.wcost = off;
+  off += kWaves * 8;
+  m.total = round16(off);
+  return m;
+}
+
+// Exact fp32 argmin over kpad centroids for the lane's row (both halves get the result).
+template <int KS>
+__device__ inline void exact_argmin(const float* __restrict__ cbase, int stride,
+                                    const float (&x)[KS][8], const float* __restrict__ cn,
+                                    int kpad, int d, int r, int h, int& bidx) {
+  float best = INFINITY;
+  bidx = 0x7fffffff;
+  for (int c0 = 0; c0 < kpad; c0 += 32) {
+    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* cp = cbase + size_t(c0 + r) * stride + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (16 * s + 4 * q < d) {  // wave-uniform: skip all-padding groups
+          float4 a4 = *reinterpret_cast<const float4*>(cp + 16 * s + 4 * q);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, x[s][4 * q + 0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, x[s][4 * q + 1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, x[s][4 * q + 2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, x[s][4 * q + 3], acc, 0, 0, 0);
+        }
+      }
+    }
+    // accumulator element 4g+q <-> centroid c0 + 8g + 4h + q, data row r
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
+      float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float dist = fmaf(-2.f, acc[4 * g + q], cv[q]);
+        if (dist < best) {
+          best = dist;
+          bidx = c0 + 8 * g + 4 * h + q;
+        }
+      }
+    }
+  }
+  float ob = __shfl_xor(best, 32, 64);
+  int oi = __shfl_xor(bidx, 32, 64);
+  if (ob < best || (ob == best && oi < bidx)) bidx = oi;
+}
+
+template <int KS>
+__device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8]) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float4 v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+      dst[s][4 * q + 0] = v.x;
+      dst[s][4 * q + 1] = v.y;
+      dst[s][4 * q + 2] = v.z;
+      dst[s][4 * q + 3] = v.w;
+    }
+}
+
+template <int KS, bool PRECISE, bool LDSACC>
+__global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssignArgs a) {
+  constexpr int DP = 16 * KS;
+  constexpr bool PIPE = !PRECISE && KS <= 5;  // register budget for one tile of look-ahead
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int kpad = a.kpad, k = a.k, d = a.d;
+  const Smem L = smem_plan(DP, kpad, k, d, PRECISE, LDSACC);
+  const int sb = stride_bf16(DP), s32 = stride_f32(DP);
+  __bf16* ph = reinterpret_cast<__bf16*>(smem + L.planes);
+  __bf16* pl = ph + size_t(kpad) * sb;
+  float* p32 = reinterpret_cast<float*>(smem + L.planes);
+  float* cn = reinterpret_cast<float*>(smem + L.cn);
+  float* sc_l = reinterpret_cast<float*>(smem + L.sc);
+  double* acc_l = reinterpret_cast<double*>(smem + L.acc);
+  unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
+  double* wcost = reinterpret_cast<double*>(smem + L.wcost);
+  const int tid = threadIdx.x;
+  const bool accumulate = a.accumulate && !a.merge && !(a.ablate & 1);
+  const bool do_cost = !(a.ablate & 2);
+
+  // ---- stage centroids (+ norms, fixed-point scales) once per workgroup
+  for (int idx = tid; idx < kpad * DP; idx += kThreads) {
+    const int c = idx / DP, f = idx - c * DP;
+    const float v = a.centers[idx];
+    if constexpr (PRECISE) {
+      p32[c * s32 + f] = v;
+    } else {
+      __bf16 hi, lo;
+      bf16_split(v, hi, lo);
+      ph[c * sb + f] = hi;
+      pl[c * sb + f] = lo;
+    }
+  }
+  for (int c = tid; c < kpad; c += kThreads) cn[c] = (c < k) ? a.cnorm[c] : INFINITY;
+  for (int f = tid; f < DP; f += kThreads)
+    sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
+  if (LDSACC && accumulate) {
+    for (int i = tid; i < k * (d | 1); i += kThreads) acc_l[i] = 0.0;
+    for (int i = tid; i < k; i += kThreads) cnt_l[i] = 0u;
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  float thr1 = 0.f, thr0 = 0.f;
+  if constexpr (!PRECISE) {
+    const float cmax = a.cstat ? a.cstat[0] : 0.f;
+    thr1 = 1.25e-4f * cmax;  // 2 candidates x (bf16 split + accumulation) + fp32-path bound
+    thr0 = 2e-6f * cmax * cmax + 1e-30f;
+  }
+  double my_cost = 0.0;
+
+  // ---- per-row epilogue: exact cost, outputs, fixed-point accumulation
+  auto finish = [&](const float (&xv)[KS][8], const float (&cv)[KS][8], int b, int64_t row,
+                    bool valid) {
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      if (16 * s < d)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float e = xv[s][j] - cv[s][j];
+          part = fmaf(e, e, part);
+        }
+    const float rowcost = part + __shfl_xor(part, 32, 64);
+    if (!valid) return;
+    if (h == 0) {
+      if (a.merge) {
+        if (rowcost < a.mindist[row]) {
+          a.mindist[row] = rowcost;
+          a.labels[row] = a.base + b;
+        }
+      } else {
+        if (a.labels) a.labels[row] = a.base + b;
+        if (a.mindist) a.mindist[row] = rowcost;
+      }
+      my_cost += double(rowcost);
+    }
+    if (!accumulate) return;
+    if constexpr (LDSACC) {
+      if (h == 0) atomicAdd(&cnt_l[b], 1u);
+      double* ap = acc_l + b * (d | 1) + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int f0 = 16 * s + 8 * h;
+        if (16 * s + 16 <= d || f0 < d) {
+          const float4 s0 = *reinterpret_cast<const float4*>(sc_l + f0);
+          const float4 s1 = *reinterpret_cast<const float4*>(sc_l + f0 + 4);
+          const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (16 * s + 16 <= d || f0 + j < d)
+              atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv[s][j] * scv[j])));
+        }
+      }
+    } else {
+      if (h == 0) atomicAdd(&a.counts[b], 1ull);
+      if (a.sums_too) {
+        u64* gp = a.sums + size_t(b) * d;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int f = 16 * s + 8 * h + j;
+            if (f < d) {
+              const long long qv = static_cast<long long>(rintf(xv[s][j] * sc_l[f]));
+              atomicAdd(gp + f, static_cast<u64>(qv));
+            }
+          }
+      }
+    }
+  };
+
+  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t stride = int64_t(gridDim.x) * kWaves;
+  int64_t t = int64_t(blockIdx.x) * kWaves + wave;
+
+  auto load_tile = [&](int64_t tt, float (&dst)[KS][8]) {
+    const int64_t row = tt * 32 + r;
+    const bool ok = tt < ntiles && row < a.n;
+    const float* p = a.x + (ok ? row : 0) * a.ld + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int f = 16 * s + 8 * h + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok && f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+        dst[s][4 * q + 0] = v.x;
+        dst[s][4 * q + 1] = v.y;
+        dst[s][4 * q + 2] = v.z;
+        dst[s][4 * q + 3] = v.w;
+      }
+  };
+
+  float xn[KS][8];
+  load_tile(t, xn);
+  float xp[KS][8], cp[KS][8];
+  int bp = 0;
+  int64_t rowp = 0;
+  bool validp = false, havep = false;
+
+  for (; t < ntiles; t += stride) {
+    float x[KS][8];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[s][j] = xn[s][j];
+    const int64_t row = t * 32 + r;
+    const bool valid = row < a.n;
+    load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
+
+    int bidx;
+    if (a.ablate & 8) {
+      bidx = r % k;  // timing ablation: no distance work
+    } else if constexpr (PRECISE) {
+      exact_argmin<KS>(p32, s32, x, cn, kpad, d, r, h, bidx);
+    } else {
+      bf16x8 xh[KS], xl[KS];
+      float nx2 = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 hi, lo;
+          bf16_split(x[s][j], hi, lo);
+          xh[s][j] = hi;
+          xl[s][j] = lo;
+          nx2 = fmaf(x[s][j], x[s][j], nx2);
+        }
+      nx2 += __shfl_xor(nx2, 32, 64);
+      float b1 = INFINITY, b2 = INFINITY;
+      int bi = 0x7fffffff;
+      for (int c0 = 0; c0 < kpad; c0 += 32) {
+        f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                      0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
+        const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          if (16 * s < d) {
+            const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
+            const bf16x8 al = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[s], acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
+          const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float dist = fmaf(-2.f, acc[4 * g + q], cv[q]);
+            b2 = fminf(b2, fmaxf(b1, dist));
+            if (dist < b1) bi = c0 + 8 * g + 4 * h + q;
+            b1 = fminf(b1, dist);
+          }
+        }
+      }
+      {  // merge the two halves' top-2
+        const float o1 = __shfl_xor(b1, 32, 64), o2 = __shfl_xor(b2, 32, 64);
+        const int oi = __shfl_xor(bi, 32, 64);
+        if (o1 < b1 || (o1 == b1 && oi < bi)) {
+          b2 = fminf(b1, o2);
+          b1 = o1;
+          bi = oi;
+        } else {
+          b2 = fminf(o1, b2);
+        }
+      }
+      const bool unsure = valid && !(b2 - b1 > fmaf(thr1, sqrtf(nx2), thr0));
+      if (__any(unsure)) {
+        // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
+        exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bi);
+        if (lane == 0 && a.refine_tiles) atomicAdd(a.refine_tiles, 1ull);
+      }
+      bidx = bi;
+    }
+    if (bidx >= k || bidx < 0) bidx = 0;  // only for degenerate (NaN / all-inf) inputs
+
+    float cb[KS][8];
+    if (!do_cost) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
+    } else if constexpr (PRECISE) {
+      load_row8<KS>(p32 + size_t(bidx) * s32 + 8 * h, cb);
+    } else {
+      load_row8<KS>(a.centers + size_t(bidx) * DP + 8 * h, cb);  // L2-resident
+    }
+    if constexpr (PIPE) {
+      if (havep) finish(xp, cp, bp, rowp, validp);
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xp[s][j] = x[s][j];
+          cp[s][j] = cb[s][j];
+        }
+      bp = bidx;
+      rowp = row;
+      validp = valid;
+      havep = true;
+    } else {
+      finish(x, cb, bidx, row, valid);
+    }
+  }
+  if constexpr (PIPE) {
+    if (havep) finish(xp, cp, bp, rowp, validp);
+  }
+
+  // ---- deterministic per-block cost: fixed shuffle tree, waves in index order
+  const double wsum = wave_sum_f64(my_cost);
+  if (lane == 0) wcost[wave] = wsum;
+  __syncthreads();
+  if (tid == 0 && a.cost_slab) {
+    double tot = 0.0;
+    for (int w = 0; w < kWaves; ++w) tot += wcost[w];
+    a.cost_slab[blockIdx.x] = tot;
+  }
+  if (LDSACC && accumulate) {
+    for (int i = tid; i < k * d; i += kThreads) {
+      const int b = i / d, f = i - b * d;
+      const double v = acc_l[b * (d | 1) + f];  // an exact integer, |v| < 2^53
+      if (v != 0.0) atomicAdd(&a.sums[i], static_cast<u64>(static_cast<long long>(v)));
+    }
+    for (int i = tid; i < k; i += kThreads) {
+      const unsigned c = cnt_l[i];
+      if (c) atomicAdd(&a.counts[i], static_cast<u64>(c));
+    }
+  }
+}
+
+template <int KS, bool P, bool LA>
+void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA);
+  static bool attr_set = false;
+  if (!attr_set) {
+    OAP_HIP_CHECK(hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA>), dim3(grid), dim3(kThreads), L.total, s,
+                     a);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+template <int KS>
+void launch_ks(const KMeansAssignArgs& a, int grid, hipStream_t s, bool lds_acc) {
+  if (a.precise) {
+    if (lds_acc) launch3<KS, true, true>(a, grid, s);
+    else launch3<KS, true, false>(a, grid, s);
+  } else {
+    if (lds_acc) launch3<KS, false, true>(a, grid, s);
+    else launch3<KS, false, false>(a, grid, s);
+  }
+}
+
+}  // namespace
+
+int kmeans_mfma_kmax(int d, bool precise) {
+  if (d > 128) return 0;
+  const int dp = (d + 15) / 16 * 16;
+  int kp = 32;
+  if (smem_plan(dp, kp, 0, d, precise, false).total > kLdsLimit) return 0;
+  while (smem_plan(dp, kp + 32, 0, d, precise, false).total <= kLdsLimit) kp += 32;
+  return kp;
+}
+
+int kmeans_mfma_grid(int64_t n, int num_cus) {
+  const int64_t tiles = (n + 31) / 32;
+  const int64_t want = (tiles + kWaves - 1) / kWaves;
+  const int64_t cap = num_cus > 256 ? num_cus : 256;
+  return static_cast<int>(want < cap ? (want < 1 ? 1 : want) : cap);
+}
+
+void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  const int dp = (a.d + 15) / 16 * 16;
+  const bool acc = a.accumulate && !a.merge;
+  const bool lds_acc =
+      acc && a.sums_too && smem_plan(dp, a.kpad, a.k, a.d, a.precise, true).total <= kLdsLimit;
+  switch (dp / 16) {
+    case 1: launch_ks<1>(a, grid, s, lds_acc); break;
+    case 2: launch_ks<2>(a, grid, s, lds_acc); break;
+    case 3: launch_ks<3>(a, grid, s, lds_acc); break;
+    case 4: launch_ks<4>(a, grid, s, lds_acc); break;
+    case 5: launch_ks<5>(a, grid, s, lds_acc); break;
+    case 6: launch_ks<6>(a, grid, s, lds_acc); break;
+    case 7: launch_ks<7>(a, grid, s, lds_acc); break;
+    case 8: launch_ks<8>(a, grid, s, lds_acc); break;
+    default: OAP_THROW(ConfigError, "kmeans_assign: unsupported d=" << a.d);
+  }
+}
+
+}  // namespace kern
+}  // namespace oap

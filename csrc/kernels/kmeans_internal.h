@@ -1,0 +1,21 @@
+// Internal interface between the K-Means kernel translation units.
+#pragma once
+
+#include "kernels/kernels.h"
+
+namespace oap {
+namespace kern {
+
+constexpr int kAssignThreads = 512;  // 8 waves: 2 per SIMD with one workgroup per CU
+constexpr size_t kLdsLimit = 160 * 1024;
+
+// Launches the MFMA assign kernel (d <= 128, centroids fit the LDS plan).  `grid` blocks.
+void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s);
+// Largest kpad (multiple of 32) whose centroid planes fit LDS for d features.
+int kmeans_mfma_kmax(int d, bool precise);
+// Grid the MFMA assign kernel uses for n rows (>= 256 blocks once there is work for them, so the
+// per-block row bound used by the fixed-point scale is device independent).
+int kmeans_mfma_grid(int64_t n, int num_cus);
+
+}  // namespace kern
+}  // namespace oap
