@@ -38,6 +38,38 @@ __global__ void oap_convert_pad(const Src* src, int64_t rows, int cols, int64_t 
   }
 }
 
+// Column max |x| when ld % 4 == 0: the matrix is read as a flat float4 stream (fully coalesced);
+// the thread stride is a multiple of ld/4, so every thread always sees the same 4 columns.
+__global__ __launch_bounds__(256) void oap_column_absmax4(const float4* x, int64_t rows,
+                                                          int ld4, int cols, float* out) {
+  __shared__ float part[256 * 4];
+  const int per_block = (256 / ld4) * ld4;  // threads with a fixed column group
+  const int t = threadIdx.x;
+  float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < per_block) {
+    const int cg = t % ld4;
+    const int64_t rstride = int64_t(gridDim.x) * (per_block / ld4);
+    for (int64_t r = int64_t(blockIdx.x) * (per_block / ld4) + t / ld4; r < rows; r += rstride) {
+      const float4 v = x[r * ld4 + cg];
+      m.x = fmaxf(m.x, fabsf(v.x));
+      m.y = fmaxf(m.y, fabsf(v.y));
+      m.z = fmaxf(m.z, fabsf(v.z));
+      m.w = fmaxf(m.w, fabsf(v.w));
+    }
+  }
+  part[t * 4 + 0] = m.x;
+  part[t * 4 + 1] = m.y;
+  part[t * 4 + 2] = m.z;
+  part[t * 4 + 3] = m.w;
+  __syncthreads();
+  for (int c = t; c < ld4 * 4 && c < cols; c += blockDim.x) {
+    float mm = 0.f;
+    const int cg = c / 4, lane = c % 4;
+    for (int i = cg; i < per_block; i += ld4) mm = fmaxf(mm, part[i * 4 + lane]);
+    atomicMax(reinterpret_cast<int*>(out) + c, __float_as_int(mm));  // mm >= 0: int order
+  }
+}
+
 __global__ void oap_column_absmax(const float* x, int64_t rows, int cols, int64_t ld,
                                   float* out) {
   for (int c = threadIdx.x; c < cols; c += blockDim.x) {
@@ -158,6 +190,13 @@ void convert_pad(const void* src, DType src_t, int64_t rows, int cols, int64_t s
 void column_absmax(const float* x, int64_t rows, int cols, int64_t ld, float* out,
                    hipStream_t s) {
   if (rows == 0) return;
+  if (ld % 4 == 0 && ld / 4 <= 256 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    hipLaunchKernelGGL(oap_column_absmax4, dim3(2048), dim3(256), 0, s,
+                       reinterpret_cast<const float4*>(x), rows, static_cast<int>(ld / 4), cols,
+                       out);
+    OAP_HIP_CHECK(hipGetLastError());
+    return;
+  }
   int grid = static_cast<int>(rows < 2048 ? rows : 2048);
   hipLaunchKernelGGL(oap_column_absmax, dim3(grid), dim3(256), 0, s, x, rows, cols, ld, out);
   OAP_HIP_CHECK(hipGetLastError());

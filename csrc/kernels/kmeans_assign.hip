@@ -49,8 +49,9 @@ __host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)
 struct Smem {
   size_t planes, cn, sc, acc, cnt, wcost, total;
 };
+// lds_acc: LDS counters (+ the fp64 fixed-point sum accumulator when lds_sums).
 __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool precise,
-                                          bool lds_acc) {
+                                          bool lds_acc, bool lds_sums = true) {
   Smem m;
   size_t off = 0;
   m.planes = 0;
@@ -61,7 +62,8 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
   m.sc = off;
   off = round16(off + size_t(dp) * 4);
   m.acc = off;
-  if (lds_acc) off += size_t(k) * (d | 1) * 8;  // odd row stride => conflict-free ds_add_f64
+  if (lds_acc && lds_sums)
+    off += size_t(k) * (d | 1) * 8;  // odd row stride => conflict-free ds_add_f64
   off = round16(off);
   m.cnt = off;
   if (lds_acc) off += size_t(k) * 4;
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   constexpr bool PIPE = !PRECISE && KS <= 5;  // register budget for one tile of look-ahead
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
-  const Smem L = smem_plan(DP, kpad, k, d, PRECISE, LDSACC);
+  const Smem L = smem_plan(DP, kpad, k, d, PRECISE, LDSACC, a.sums_too);
   const int sb = stride_bf16(DP), s32 = stride_f32(DP);
   __bf16* ph = reinterpret_cast<__bf16*>(smem + L.planes);
   __bf16* pl = ph + size_t(kpad) * sb;
@@ -166,7 +168,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   for (int f = tid; f < DP; f += kThreads)
     sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
   if (LDSACC && accumulate) {
-    for (int i = tid; i < k * (d | 1); i += kThreads) acc_l[i] = 0.0;
+    if (a.sums_too)
+      for (int i = tid; i < k * (d | 1); i += kThreads) acc_l[i] = 0.0;
     for (int i = tid; i < k; i += kThreads) cnt_l[i] = 0u;
   }
   __syncthreads();
@@ -210,6 +213,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     if (!accumulate) return;
     if constexpr (LDSACC) {
       if (h == 0) atomicAdd(&cnt_l[b], 1u);
+      if (!a.sums_too) return;
       double* ap = acc_l + b * (d | 1) + 8 * h;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -393,7 +397,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     a.cost_slab[blockIdx.x] = tot;
   }
   if (LDSACC && accumulate) {
-    for (int i = tid; i < k * d; i += kThreads) {
+    for (int i = tid; a.sums_too && i < k * d; i += kThreads) {
       const int b = i / d, f = i - b * d;
       const double v = acc_l[b * (d | 1) + f];  // an exact integer, |v| < 2^53
       if (v != 0.0) atomicAdd(&a.sums[i], static_cast<u64>(static_cast<long long>(v)));
@@ -407,7 +411,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 
 template <int KS, bool P, bool LA>
 void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
-  const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA);
+  const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA, a.sums_too);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
@@ -453,7 +457,7 @@ void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t 
   const int dp = (a.d + 15) / 16 * 16;
   const bool acc = a.accumulate && !a.merge;
   const bool lds_acc =
-      acc && a.sums_too && smem_plan(dp, a.kpad, a.k, a.d, a.precise, true).total <= kLdsLimit;
+      acc && smem_plan(dp, a.kpad, a.k, a.d, a.precise, true, a.sums_too).total <= kLdsLimit;
   switch (dp / 16) {
     case 1: launch_ks<1>(a, grid, s, lds_acc); break;
     case 2: launch_ks<2>(a, grid, s, lds_acc); break;

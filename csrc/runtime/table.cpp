@@ -147,9 +147,11 @@ void assign_global_offsets(Context& ctx, Comm& comm, DenseTable& t) {
   t.global_rows = tot;
 }
 
-std::vector<double> global_column_absmax(Context& ctx, Comm& comm, const DenseTable& t) {
+std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t) {
   std::vector<double> mx(t.cols, 0.0);
-  if (ctx.is_gpu()) {
+  if (!t.local_absmax.empty()) {
+    mx = t.local_absmax;
+  } else if (ctx.is_gpu()) {
     OAP_CHECK(t.dtype == DType::F32, "column_absmax expects an f32 table");
     Buffer d = ctx.alloc(sizeof(float) * t.cols);
     ctx.memset(d.data(), 0, sizeof(float) * t.cols);
@@ -171,6 +173,7 @@ std::vector<double> global_column_absmax(Context& ctx, Comm& comm, const DenseTa
     for (auto& p : part)
       for (int c = 0; c < t.cols; ++c) mx[c] = std::max(mx[c], p[c]);
   }
+  t.local_absmax = mx;
   if (comm.size() > 1) {
     if (comm.on_device() && ctx.is_gpu()) {
       Buffer d = ctx.alloc(sizeof(double) * t.cols);

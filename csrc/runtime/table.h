@@ -23,6 +23,7 @@ struct DenseTable {
   Backend backend = Backend::CPU;
   int64_t global_offset = -1;  // global row index of local row 0 (-1 = not yet known)
   int64_t global_rows = -1;
+  std::vector<double> local_absmax;  // cached per-column max |x| over the local rows
 
   size_t bytes() const { return size_t(rows) * size_t(ld) * dtype_size(dtype); }
 };
@@ -41,7 +42,8 @@ DenseTable synth_blobs_table(Context& ctx, int64_t rows, int cols, int64_t ld, i
 void assign_global_offsets(Context& ctx, Comm& comm, DenseTable& t);
 
 // Per-column max |x| over the GLOBAL dataset (local kernel + allreduce MAX).
-std::vector<double> global_column_absmax(Context& ctx, Comm& comm, const DenseTable& t);
+// The local pass runs once per table (cached in t.local_absmax).
+std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t);
 
 // Copies rows [r0, r0+n) (first `cols` columns) back to host as float64.
 std::vector<double> table_rows_f64(Context& ctx, const DenseTable& t, int64_t r0, int64_t n);

@@ -2,7 +2,10 @@
 import json
 import sys
 
-import torch  # noqa: F401
+import os
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: F401,E402
 
 from oap_mllib_amd import _loader
 
