@@ -134,7 +134,9 @@ __device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8
 template <int KS, bool PRECISE, bool LDSACC>
 __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
-  constexpr bool PIPE = !PRECISE && KS <= 5;  // register budget for one tile of look-ahead
+  // One tile of c_best look-ahead costs 2*8*KS VGPRs; the partner wave on the SIMD already
+  // covers the L2 latency with its MFMA chain, so the look-ahead is only used for tiny KS.
+  constexpr bool PIPE = !PRECISE && KS <= 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
   const Smem L = smem_plan(DP, kpad, k, d, PRECISE, LDSACC, a.sums_too);
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       p32[c * s32 + f] = v;
     } else {
       __bf16 hi, lo;
-      bf16_split(v, hi, lo);
+      bf16_split(-2.f * v, hi, lo);  // exact scaling: split(-2c) == -2 split(c)
       ph[c * sb + f] = hi;
       pl[c * sb + f] = lo;
     }
@@ -304,11 +306,21 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
           nx2 = fmaf(x[s][j], x[s][j], nx2);
         }
       nx2 += __shfl_xor(nx2, 32, 64);
-      float b1 = INFINITY, b2 = INFINITY;
-      int bi = 0x7fffffff;
-      for (int c0 = 0; c0 < kpad; c0 += 32) {
-        f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
-                      0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      // The accumulator is seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
+      // ends at |x - c|^2 directly.  Top-2 tracking runs on integer KEYS: the float's bits with
+      // the low 10 mantissa bits replaced by the centroid index (kpad <= 1024), so min/max on
+      // ints gives value order + lowest-index tie-break in 4 VALU ops per candidate.  Two
+      // accumulators let chunk c's key epilogue interleave with chunk c+1's MFMAs.
+      int k1 = 0x7fffffff, k2 = 0x7fffffff;
+      auto mfma_chunk = [&](int c0, f32x16& acc) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
+          acc[4 * g + 0] = c4.x + nx2;
+          acc[4 * g + 1] = c4.y + nx2;
+          acc[4 * g + 2] = c4.z + nx2;
+          acc[4 * g + 3] = c4.w + nx2;
+        }
         const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
         const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
 #pragma unroll
@@ -321,31 +333,36 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[s], acc, 0, 0, 0);
           }
         }
+      };
+      auto epilogue = [&](int c0, const f32x16& acc) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
-          const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float dist = fmaf(-2.f, acc[4 * g + q], cv[q]);
-            b2 = fminf(b2, fmaxf(b1, dist));
-            if (dist < b1) bi = c0 + 8 * g + 4 * h + q;
-            b1 = fminf(b1, dist);
-          }
+        for (int e = 0; e < 16; ++e) {
+          const int ci = c0 + 8 * (e >> 2) + 4 * h + (e & 3);
+          const int key = (__float_as_int(acc[e]) & ~0x3ff) | ci;
+          k2 = min(k2, max(k1, key));
+          k1 = min(k1, key);
         }
+      };
+      f32x16 accA, accB;
+      bool pend = false;
+      for (int c0 = 0; c0 < kpad; c0 += 64) {
+        mfma_chunk(c0, accA);
+        if (pend) epilogue(c0 - 32, accB);
+        pend = c0 + 32 < kpad;
+        if (pend) mfma_chunk(c0 + 32, accB);
+        epilogue(c0, accA);
       }
-      {  // merge the two halves' top-2
-        const float o1 = __shfl_xor(b1, 32, 64), o2 = __shfl_xor(b2, 32, 64);
-        const int oi = __shfl_xor(bi, 32, 64);
-        if (o1 < b1 || (o1 == b1 && oi < bi)) {
-          b2 = fminf(b1, o2);
-          b1 = o1;
-          bi = oi;
-        } else {
-          b2 = fminf(o1, b2);
-        }
+      if (pend) epilogue(kpad - 32, accB);
+      {  // merge the two halves' top-2 keys
+        const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
+        k2 = min(max(k1, o1), min(k2, o2));
+        k1 = min(k1, o1);
       }
-      const bool unsure = valid && !(b2 - b1 > fmaf(thr1, sqrtf(nx2), thr0));
+      int bi = k1 & 0x3ff;
+      const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
+      // gap must beat: split+accumulation error, |c|^2+|x|^2 seed rounding, key truncation
+      const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
+      const bool unsure = valid && !(b2 - b1 > thr);
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bi);
@@ -443,7 +460,7 @@ int kmeans_mfma_kmax(int d, bool precise) {
   int kp = 32;
   if (smem_plan(dp, kp, 0, d, precise, false).total > kLdsLimit) return 0;
   while (smem_plan(dp, kp + 32, 0, d, precise, false).total <= kLdsLimit) kp += 32;
-  return kp;
+  return precise ? kp : (kp < 1024 ? kp : 1024);  // fast path keys carry a 10-bit index
 }
 
 int kmeans_mfma_grid(int64_t n, int num_cus) {
