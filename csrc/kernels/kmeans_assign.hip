@@ -134,9 +134,6 @@ __device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8
 template <int KS, bool PRECISE, bool LDSACC>
 __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
-  // One tile of c_best look-ahead costs 2*8*KS VGPRs; the partner wave on the SIMD already
-  // covers the L2 latency with its MFMA chain, so the look-ahead is only used for tiny KS.
-  constexpr bool PIPE = !PRECISE && KS <= 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
   const Smem L = smem_plan(DP, kpad, k, d, PRECISE, LDSACC, a.sums_too);
@@ -272,27 +269,37 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 
   float xn[KS][8];
   load_tile(t, xn);
-  float xp[KS][8], cp[KS][8];
-  int bp = 0;
-  int64_t rowp = 0;
-  bool validp = false, havep = false;
 
   for (; t < ntiles; t += stride) {
-    float x[KS][8];
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[s][j] = xn[s][j];
     const int64_t row = t * 32 + r;
     const bool valid = row < a.n;
-    load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
-
     int bidx;
-    if (a.ablate & 8) {
-      bidx = r % k;  // timing ablation: no distance work
-    } else if constexpr (PRECISE) {
-      exact_argmin<KS>(p32, s32, x, cn, kpad, d, r, h, bidx);
+    if constexpr (PRECISE) {
+      float x[KS][8];
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[s][j] = xn[s][j];
+      load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
+      if (a.ablate & 8)
+        bidx = r % k;  // timing ablation: no distance work
+      else
+        exact_argmin<KS>(p32, s32, x, cn, kpad, d, r, h, bidx);
+      if (bidx >= k || bidx < 0) bidx = 0;
+      float cb[KS][8];
+      if (do_cost) {
+        load_row8<KS>(p32 + size_t(bidx) * s32 + 8 * h, cb);
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
+      }
+      finish(x, cb, bidx, row, valid);
     } else {
+      // split the row into bf16 hi/lo MFMA operands; the fp32 copy is NOT kept live through the
+      // MFMA phase (registers go to the fragment reads and the two accumulators instead) — it is
+      // re-read from L2 for the epilogue.
       bf16x8 xh[KS], xl[KS];
       float nx2 = 0.f;
 #pragma unroll
@@ -300,19 +307,29 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           __bf16 hi, lo;
-          bf16_split(x[s][j], hi, lo);
+          bf16_split(xn[s][j], hi, lo);
           xh[s][j] = hi;
           xl[s][j] = lo;
-          nx2 = fmaf(x[s][j], x[s][j], nx2);
+          nx2 = fmaf(xn[s][j], xn[s][j], nx2);
         }
       nx2 += __shfl_xor(nx2, 32, 64);
-      // The accumulator is seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
-      // ends at |x - c|^2 directly.  Top-2 tracking runs on integer KEYS: the float's bits with
-      // the low 10 mantissa bits replaced by the centroid index (kpad <= 1024), so min/max on
-      // ints gives value order + lowest-index tie-break in 4 VALU ops per candidate.  Two
-      // accumulators let chunk c's key epilogue interleave with chunk c+1's MFMAs.
+      load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
+
+      // Accumulators are seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
+      // ends at |x - c|^2.  Top-2 tracking runs on integer KEYS: the float's bits with the low 10
+      // mantissa bits replaced by the centroid index (kpad <= 1024) — int min/max give value
+      // order plus lowest-index tie-break in 4 VALU ops per candidate.  Two accumulators let chunk
+      // c's key epilogue (VALU) interleave with chunk c+1's MFMAs.
       int k1 = 0x7fffffff, k2 = 0x7fffffff;
       auto mfma_chunk = [&](int c0, f32x16& acc) {
+        const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
+        const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
+        bf16x8 ah[KS], al[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
+          al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
@@ -321,17 +338,12 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
           acc[4 * g + 2] = c4.z + nx2;
           acc[4 * g + 3] = c4.w + nx2;
         }
-        const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
-        const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
+        // KS = ceil(d/16): every k-step holds real features, so there is no runtime guard here
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          if (16 * s < d) {
-            const bf16x8 ah = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
-            const bf16x8 al = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xh[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, xl[s], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, xh[s], acc, 0, 0, 0);
-          }
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xl[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], xh[s], acc, 0, 0, 0);
         }
       };
       auto epilogue = [&](int c0, const f32x16& acc) {
@@ -343,65 +355,56 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
           k1 = min(k1, key);
         }
       };
-      f32x16 accA, accB;
-      bool pend = false;
-      for (int c0 = 0; c0 < kpad; c0 += 64) {
-        mfma_chunk(c0, accA);
-        if (pend) epilogue(c0 - 32, accB);
-        pend = c0 + 32 < kpad;
-        if (pend) mfma_chunk(c0 + 32, accB);
-        epilogue(c0, accA);
+      if (a.ablate & 8) {
+        k1 = r % k;  // timing ablation: no distance work
+        k2 = 0x7fffffff;
+      } else {
+        f32x16 accA, accB;
+        mfma_chunk(0, accA);
+        int c0 = 32;
+        for (; c0 + 32 < kpad; c0 += 64) {  // branch-free body: chunk pairs
+          mfma_chunk(c0, accB);
+          epilogue(c0 - 32, accA);
+          mfma_chunk(c0 + 32, accA);
+          epilogue(c0, accB);
+        }
+        if (c0 < kpad) {  // one chunk left (wave-uniform)
+          mfma_chunk(c0, accB);
+          epilogue(c0 - 32, accA);
+          epilogue(c0, accB);
+        } else {
+          epilogue(c0 - 32, accA);
+        }
       }
-      if (pend) epilogue(kpad - 32, accB);
       {  // merge the two halves' top-2 keys
         const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
         k2 = min(max(k1, o1), min(k2, o2));
         k1 = min(k1, o1);
       }
-      int bi = k1 & 0x3ff;
+      bidx = k1 & 0x3ff;
       const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
-      // gap must beat: split+accumulation error, |c|^2+|x|^2 seed rounding, key truncation
+      // the gap must beat: split + accumulation error, seed rounding, key truncation
       const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
-      const bool unsure = valid && !(b2 - b1 > thr);
+      const bool unsure = valid && !(a.ablate & 8) && !(b2 - b1 > thr);
+      float x[KS][8];
+      load_tile(t, x);  // fp32 row again (L2/L1-resident: read a few microseconds ago)
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
-        exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bi);
+        exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);
         if (lane == 0 && a.refine_tiles) atomicAdd(a.refine_tiles, 1ull);
       }
-      bidx = bi;
-    }
-    if (bidx >= k || bidx < 0) bidx = 0;  // only for degenerate (NaN / all-inf) inputs
-
-    float cb[KS][8];
-    if (!do_cost) {
+      if (bidx >= k || bidx < 0) bidx = 0;  // only for degenerate (NaN / all-inf) inputs
+      float cb[KS][8];
+      if (do_cost) {
+        load_row8<KS>(a.centers + size_t(bidx) * DP + 8 * h, cb);  // L2-resident
+      } else {
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
+        for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
-    } else if constexpr (PRECISE) {
-      load_row8<KS>(p32 + size_t(bidx) * s32 + 8 * h, cb);
-    } else {
-      load_row8<KS>(a.centers + size_t(bidx) * DP + 8 * h, cb);  // L2-resident
-    }
-    if constexpr (PIPE) {
-      if (havep) finish(xp, cp, bp, rowp, validp);
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xp[s][j] = x[s][j];
-          cp[s][j] = cb[s][j];
-        }
-      bp = bidx;
-      rowp = row;
-      validp = valid;
-      havep = true;
-    } else {
+          for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
+      }
       finish(x, cb, bidx, row, valid);
     }
-  }
-  if constexpr (PIPE) {
-    if (havep) finish(xp, cp, bp, rowp, validp);
   }
 
   // ---- deterministic per-block cost: fixed shuffle tree, waves in index order
