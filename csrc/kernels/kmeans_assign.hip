@@ -297,20 +297,20 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       }
       finish(x, cb, bidx, row, valid);
     } else {
-      // split the row into bf16 hi/lo MFMA operands; the fp32 copy is NOT kept live through the
-      // MFMA phase (registers go to the fragment reads and the two accumulators instead) — it is
-      // re-read from L2 for the epilogue.
+      // split the row into bf16 hi/lo MFMA operands (the fp32 copy stays live for the epilogue)
       bf16x8 xh[KS], xl[KS];
+      float x[KS][8];
       float nx2 = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+          x[s][j] = xn[s][j];
           __bf16 hi, lo;
-          bf16_split(xn[s][j], hi, lo);
+          bf16_split(x[s][j], hi, lo);
           xh[s][j] = hi;
           xl[s][j] = lo;
-          nx2 = fmaf(xn[s][j], xn[s][j], nx2);
+          nx2 = fmaf(x[s][j], x[s][j], nx2);
         }
       nx2 += __shfl_xor(nx2, 32, 64);
       load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
@@ -322,14 +322,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       // c's key epilogue (VALU) interleave with chunk c+1's MFMAs.
       int k1 = 0x7fffffff, k2 = 0x7fffffff;
       auto mfma_chunk = [&](int c0, f32x16& acc) {
-        const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
-        const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
-        bf16x8 ah[KS], al[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
-          al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
-        }
+        // norms first: the first MFMA needs the seeded accumulator + fragment 0 only
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
@@ -337,6 +330,14 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
           acc[4 * g + 1] = c4.y + nx2;
           acc[4 * g + 2] = c4.z + nx2;
           acc[4 * g + 3] = c4.w + nx2;
+        }
+        const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
+        const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
+        bf16x8 ah[KS], al[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
+          al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
         }
         // KS = ceil(d/16): every k-step holds real features, so there is no runtime guard here
 #pragma unroll
@@ -386,8 +387,6 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       // the gap must beat: split + accumulation error, seed rounding, key truncation
       const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
       const bool unsure = valid && !(a.ablate & 8) && !(b2 - b1 > thr);
-      float x[KS][8];
-      load_tile(t, x);  // fp32 row again (L2/L1-resident: read a few microseconds ago)
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);

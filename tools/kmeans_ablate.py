@@ -11,6 +11,8 @@ from oap_mllib_amd import _loader
 
 N = _loader.load()
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
+reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 d, k = 50, 200
 g = N.Context(0, 0.9, 0)
 t = N.synth_blobs(g, rows, d, N.kmeans_ld(d), 0, k, 10.0, 1.0, 20240917)
@@ -20,6 +22,8 @@ for name, precise, ab in [("full", False, 0), ("no_accumulate", False, 1), ("no_
                           ("no_acc_no_cost", False, 3), ("no_distance", False, 8),
                           ("loads_only", False, 11), ("precise_full", True, 0),
                           ("precise_no_acc_no_cost", True, 3)]:
-    ms = N.kmeans_assign_timing(g, t, C, 10, precise, ab)
+    if only and name not in only:
+        continue
+    ms = N.kmeans_assign_timing(g, t, C, reps, precise, ab)
     out[name] = round(ms * 100e6 / rows, 3)  # normalised to 100M rows
 print(json.dumps({"rows": rows, "ms_per_100M_rows": out}))
