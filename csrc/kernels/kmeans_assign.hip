@@ -267,19 +267,13 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       }
   };
 
-  float xn[KS][8];
-  load_tile(t, xn);
-
-  for (; t < ntiles; t += stride) {
+  // One tile: `x` holds its rows (loaded one tile earlier), `xn` receives the next tile's prefetch.
+  // The loop below alternates two named buffers, so no register copies are needed.
+  auto process = [&](const int64_t t, float (&x)[KS][8], float (&xn)[KS][8]) {
     const int64_t row = t * 32 + r;
     const bool valid = row < a.n;
     int bidx;
     if constexpr (PRECISE) {
-      float x[KS][8];
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[s][j] = xn[s][j];
       load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
       if (a.ablate & 8)
         bidx = r % k;  // timing ablation: no distance work
@@ -299,13 +293,11 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     } else {
       // split the row into bf16 hi/lo MFMA operands (the fp32 copy stays live for the epilogue)
       bf16x8 xh[KS], xl[KS];
-      float x[KS][8];
       float nx2 = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          x[s][j] = xn[s][j];
           __bf16 hi, lo;
           bf16_split(x[s][j], hi, lo);
           xh[s][j] = hi;
@@ -348,13 +340,21 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         }
       };
       auto epilogue = [&](int c0, const f32x16& acc) {
+        // chunk-local keys carry the in-chunk offset 8(e>>2)+(e&3) (an inline constant: one
+        // v_bfi_b32 per candidate); the lane's chunk base c0+4h is OR-ed in once per chunk.
+        int q1 = 0x7fffffff, q2 = 0x7fffffff;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int ci = c0 + 8 * (e >> 2) + 4 * h + (e & 3);
-          const int key = (__float_as_int(acc[e]) & ~0x3ff) | ci;
-          k2 = min(k2, max(k1, key));
-          k1 = min(k1, key);
+          const int off = 8 * (e >> 2) + (e & 3);
+          const int key = (__float_as_int(acc[e]) & ~0x3ff) | (off & 0x3ff);
+          q2 = max(q1, min(q2, key));  // second smallest of {q1, q2, key} (q1 <= q2)
+          q1 = min(q1, key);
         }
+        const int base = c0 + 4 * h;  // disjoint from every in-chunk offset's bits
+        q1 |= base;
+        q2 |= base;
+        k2 = min(max(k1, q1), min(k2, q2));
+        k1 = min(k1, q1);
       };
       if (a.ablate & 8) {
         k1 = r % k;  // timing ablation: no distance work
@@ -404,6 +404,14 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       }
       finish(x, cb, bidx, row, valid);
     }
+  };
+
+  float xa[KS][8], xb[KS][8];
+  load_tile(t, xa);
+  for (; t < ntiles; t += 2 * stride) {  // t is wave-uniform: both branches stay uniform
+    process(t, xa, xb);
+    if (t + stride >= ntiles) break;
+    process(t + stride, xb, xa);
   }
 
   // ---- deterministic per-block cost: fixed shuffle tree, waves in index order
