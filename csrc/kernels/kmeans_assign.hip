@@ -131,7 +131,10 @@ __device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8
     }
 }
 
-template <int KS, bool PRECISE, bool LDSACC>
+// BIAS (fast path, d + 2 <= 16*KS): two padding features carry the norms through the MFMAs —
+// x' = [x, 1, |x|^2], c' = [-2c, |c|^2, 1] — so accumulators start at zero and the chunk loop
+// reads only the operand fragments from LDS (no norm loads / seeding VALU).
+template <int KS, bool PRECISE, bool LDSACC, bool BIAS>
 __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -158,7 +161,10 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       p32[c * s32 + f] = v;
     } else {
       __bf16 hi, lo;
-      bf16_split(-2.f * v, hi, lo);  // exact scaling: split(-2c) == -2 split(c)
+      float w = -2.f * v;  // exact scaling: split(-2c) == -2 split(c)
+      if (BIAS && f == d) w = (c < k) ? a.cnorm[c] : 1e30f;
+      if (BIAS && f == d + 1) w = 1.f;
+      bf16_split(w, hi, lo);
       ph[c * sb + f] = hi;
       pl[c * sb + f] = lo;
     }
@@ -179,7 +185,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   if constexpr (!PRECISE) {
     const float cmax = a.cstat ? a.cstat[0] : 0.f;
     thr1 = 1.25e-4f * cmax;  // 2 candidates x (bf16 split + accumulation) + fp32-path bound
-    thr0 = 2e-6f * cmax * cmax + 1e-30f;
+    // bias feature: |c|^2 enters as a bf16 hi/lo pair (error <= 2^-18 |c|^2 per candidate)
+    thr0 = (BIAS ? 1e-5f : 2e-6f) * cmax * cmax + 1e-30f;
   }
   double my_cost = 0.0;
 
@@ -297,14 +304,23 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
+        for (int j = 0; j < 8; ++j) nx2 = fmaf(x[s][j], x[s][j], nx2);
+      nx2 += __shfl_xor(nx2, 32, 64);
+      const int jb = d - 16 * (KS - 1) - 8 * h;  // lane-local slot of bias feature d (if in range)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
         for (int j = 0; j < 8; ++j) {
+          float v = x[s][j];
+          if (BIAS && s == KS - 1) {
+            v = (j == jb) ? 1.f : v;
+            v = (j == jb + 1) ? nx2 : v;
+          }
           __bf16 hi, lo;
-          bf16_split(x[s][j], hi, lo);
+          bf16_split(v, hi, lo);
           xh[s][j] = hi;
           xl[s][j] = lo;
-          nx2 = fmaf(x[s][j], x[s][j], nx2);
         }
-      nx2 += __shfl_xor(nx2, 32, 64);
       load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
 
       // Accumulators are seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
@@ -314,14 +330,19 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       // c's key epilogue (VALU) interleave with chunk c+1's MFMAs.
       int k1 = 0x7fffffff, k2 = 0x7fffffff;
       auto mfma_chunk = [&](int c0, f32x16& acc) {
-        // norms first: the first MFMA needs the seeded accumulator + fragment 0 only
+        if constexpr (BIAS) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
-          acc[4 * g + 0] = c4.x + nx2;
-          acc[4 * g + 1] = c4.y + nx2;
-          acc[4 * g + 2] = c4.z + nx2;
-          acc[4 * g + 3] = c4.w + nx2;
+          for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+        } else {
+          // norms first: the first MFMA needs the seeded accumulator + fragment 0 only
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
+            acc[4 * g + 0] = c4.x + nx2;
+            acc[4 * g + 1] = c4.y + nx2;
+            acc[4 * g + 2] = c4.z + nx2;
+            acc[4 * g + 3] = c4.w + nx2;
+          }
         }
         const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
         const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
@@ -436,17 +457,17 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   }
 }
 
-template <int KS, bool P, bool LA>
+template <int KS, bool P, bool LA, bool B>
 void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA, a.sums_too);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA>),
+        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA, B>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA>), dim3(grid), dim3(kThreads), L.total, s,
+  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA, B>), dim3(grid), dim3(kThreads), L.total, s,
                      a);
   OAP_HIP_CHECK(hipGetLastError());
 }
@@ -454,11 +475,14 @@ void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
 template <int KS>
 void launch_ks(const KMeansAssignArgs& a, int grid, hipStream_t s, bool lds_acc) {
   if (a.precise) {
-    if (lds_acc) launch3<KS, true, true>(a, grid, s);
-    else launch3<KS, true, false>(a, grid, s);
+    if (lds_acc) launch3<KS, true, true, false>(a, grid, s);
+    else launch3<KS, true, false, false>(a, grid, s);
+  } else if (a.d + 2 <= 16 * KS) {
+    if (lds_acc) launch3<KS, false, true, true>(a, grid, s);
+    else launch3<KS, false, false, true>(a, grid, s);
   } else {
-    if (lds_acc) launch3<KS, false, true>(a, grid, s);
-    else launch3<KS, false, false>(a, grid, s);
+    if (lds_acc) launch3<KS, false, true, false>(a, grid, s);
+    else launch3<KS, false, false, false>(a, grid, s);
   }
 }
 

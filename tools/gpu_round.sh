@@ -1,11 +1,32 @@
 #!/bin/bash
-# usage: scratch/gpu_round.sh <tag>  -- build, gpu tests, bench (fast+precise), rocprof stats
+# usage: tools/gpu_round.sh <tag> [steps...]  -- on the GPU box: build, then the named steps
+# (default: test bench precise prof).  Any step ending in a fault/abort/timeout stops the script.
 set -u
-R=$GRAFT_REPO_ROOT; T=${1:-run}
+R=$GRAFT_REPO_ROOT; T=${1:-run}; shift || true
+STEPS=${*:-test bench precise prof}
 cd $R
 python -m oap_mllib_amd.build > gpurun_out/build_$T.log 2>&1 || { echo build_failed; exit 1; }
-timeout -k 10 600 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$T.log 2>&1; echo pytest_rc=$?; tail -4 gpurun_out/pytest_gpu_$T.log
-timeout -k 10 240 python bench.py > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err; echo bench_rc=$?; cat gpurun_out/bench_$T.json
-timeout -k 10 240 python bench.py --precise --skip-fit > gpurun_out/bench_precise_$T.json 2>> gpurun_out/bench_$T.err; echo benchp_rc=$?; cat gpurun_out/bench_precise_$T.json
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- python3 $R/bench.py --rows 20000000 --steps 5 --warmup 1 --skip-fit > $R/gpurun_out/prof_$T.log 2>&1; echo prof_rc=$?
+fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2: stopping"; exit $1;; esac; }
+for st in $STEPS; do
+  case $st in
+    test)
+      timeout -k 10 600 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$T.log 2>&1
+      rc=$?; echo pytest_rc=$rc; tail -4 gpurun_out/pytest_gpu_$T.log; fatal $rc pytest;;
+    bench)
+      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err
+      rc=$?; echo bench_rc=$rc; cat gpurun_out/bench_$T.json; fatal $rc bench;;
+    precise)
+      timeout -k 10 240 python bench.py --precise --skip-fit > gpurun_out/bench_precise_$T.json 2>> gpurun_out/bench_$T.err
+      rc=$?; echo benchp_rc=$rc; cat gpurun_out/bench_precise_$T.json; fatal $rc precise;;
+    ablate)
+      timeout -k 10 300 python tools/kmeans_ablate.py > gpurun_out/ablate_$T.json 2>&1
+      rc=$?; echo ablate_rc=$rc; tail -2 gpurun_out/ablate_$T.json; fatal $rc ablate;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- python3 $R/bench.py --rows 20000000 --steps 5 --warmup 1 --skip-fit > $R/gpurun_out/prof_$T.log 2>&1)
+      rc=$?; echo prof_rc=$rc; fatal $rc prof;;
+    *)
+      # any other step is a python script path relative to the repo, with output to a log
+      timeout -k 10 600 python $st > gpurun_out/$(basename $st .py)_$T.log 2>&1
+      rc=$?; echo "$st rc=$rc"; tail -5 gpurun_out/$(basename $st .py)_$T.log; fatal $rc $st;;
+  esac
+done
