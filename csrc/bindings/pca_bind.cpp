@@ -1,3 +1,92 @@
-#include "bindings/bindings.h"
+// PCA bindings: the role of the reference's JNI entry PCADALImpl.cPCATrainDAL
+// (mllib-dal/src/main/native/javah/org_apache_spark_ml_feature_PCADALImpl.h:12-16), returning
+// arrays instead of filling PCAResult fields with leaked native table handles.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
-void register_pca(pybind11::module_& m) { (void)m; }
+#include <cstring>
+
+#include "bindings/bindings.h"
+#include "drivers/pca.h"
+#include "linalg/eigen.h"
+
+namespace py = pybind11;
+using namespace oap;
+
+namespace {
+
+py::array_t<double> to_array(const std::vector<double>& v, int64_t rows, int64_t cols) {
+  py::array_t<double> a({rows, cols});
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(double));
+  return a;
+}
+
+}  // namespace
+
+void register_pca(py::module_& m) {
+  m.def(
+      "pca_fit",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
+         int k, bool precise) {
+        PcaParams p;
+        p.k = k;
+        p.precise = precise;
+        PcaResult r;
+        {
+          py::gil_scoped_release rel;
+          r = pca_fit(*ctx, *comm, *t, p);
+        }
+        py::dict out;
+        out["pc"] = to_array(r.pc, r.d, r.k);
+        out["explained_variance"] = r.explained;
+        out["eigenvalues"] = r.eigenvalues;
+        out["mean"] = r.mean;
+        out["n"] = r.n;
+        out["stats_ms"] = r.stats_ms;
+        out["allreduce_ms"] = r.allreduce_ms;
+        out["eig_ms"] = r.eig_ms;
+        out["total_ms"] = r.total_ms;
+        return out;
+      },
+      py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("k"),
+      py::arg("precise") = false);
+  m.def(
+      "pca_covariance",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
+         bool precise) {
+        PcaParams p;
+        p.precise = precise;
+        PcaCovariance c;
+        {
+          py::gil_scoped_release rel;
+          c = pca_covariance(*ctx, *comm, *t, p);
+        }
+        py::dict out;
+        out["cov"] = to_array(c.cov, c.d, c.d);
+        out["mean"] = c.mean;
+        out["n"] = c.n;
+        out["stats_ms"] = c.stats_ms;
+        out["allreduce_ms"] = c.allreduce_ms;
+        return out;
+      },
+      py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("precise") = false);
+  m.def(
+      "sym_eig",
+      [](py::array_t<double, py::array::c_style | py::array::forcecast> a, int k, int threads) {
+        if (a.ndim() != 2 || a.shape(0) != a.shape(1))
+          throw ConfigError("sym_eig expects a square matrix");
+        const int n = static_cast<int>(a.shape(0));
+        if (k <= 0 || k > n) k = n;
+        std::vector<double> A(a.data(), a.data() + a.size());
+        SymEig e;
+        {
+          py::gil_scoped_release rel;
+          ThreadPool pool(threads > 0 ? threads : 1);
+          e = sym_eig_topk(A, n, k, &pool);
+        }
+        return py::make_tuple(e.values, to_array(e.vectors, n, k));
+      },
+      py::arg("a"), py::arg("k") = 0, py::arg("threads") = 4,
+      "Eigen-decomposition of a symmetric matrix: (values sorted by |.| desc, vectors n x k).");
+}

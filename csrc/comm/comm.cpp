@@ -269,6 +269,22 @@ void comm_bcast(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, int
   OAP_HIP_CHECK(hipStreamSynchronize(s));
 }
 
+void comm_allreduce_host(Context& ctx, Comm& comm, void* host, size_t count, DType dt,
+                         ReduceOp op) {
+  if (comm.size() == 1 || count == 0) return;
+  if (!comm.on_device()) {
+    comm.allreduce(host, count, dt, op, nullptr);
+    return;
+  }
+  const size_t bytes = count * dtype_size(dt);
+  Buffer d = ctx.alloc(bytes);
+  hipStream_t s = ctx.comm_stream();
+  OAP_HIP_CHECK(hipMemcpyAsync(d.data(), host, bytes, hipMemcpyHostToDevice, s));
+  comm.allreduce(d.data(), count, dt, op, s);
+  OAP_HIP_CHECK(hipMemcpyAsync(host, d.data(), bytes, hipMemcpyDeviceToHost, s));
+  comm.wait(s);
+}
+
 double comm_allreduce_scalar(Context& ctx, Comm& comm, double v, ReduceOp op) {
   if (comm.size() == 1) return v;
   if (comm.on_device()) {

@@ -32,18 +32,7 @@ uint64_t mix64(uint64_t z) {
 
 // Host buffer collectives that work with device- or host-buffer comms.
 void host_allreduce(Context& ctx, Comm& comm, void* host, size_t count, DType dt, ReduceOp op) {
-  if (comm.size() == 1 || count == 0) return;
-  if (!comm.on_device()) {
-    comm.allreduce(host, count, dt, op, nullptr);
-    return;
-  }
-  size_t bytes = count * dtype_size(dt);
-  Buffer d = ctx.alloc(bytes);
-  hipStream_t s = ctx.comm_stream();
-  OAP_HIP_CHECK(hipMemcpyAsync(d.data(), host, bytes, hipMemcpyHostToDevice, s));
-  comm.allreduce(d.data(), count, dt, op, s);
-  OAP_HIP_CHECK(hipMemcpyAsync(host, d.data(), bytes, hipMemcpyDeviceToHost, s));
-  comm.wait(s);
+  comm_allreduce_host(ctx, comm, host, count, dt, op);
 }
 
 // Gathers a variable number of f64 rows (cols wide) from every rank, rank-major.

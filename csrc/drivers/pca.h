@@ -1,0 +1,50 @@
+// Distributed PCA driver.
+//
+// MI355X-native counterpart of the reference's PCA path: Spark-side mean centring
+// (mllib-dal/src/main/scala/org/apache/spark/ml/feature/PCADALImpl.scala:101-106), oneDAL
+// step1Local on every rank + allgatherv of serialized partials + step2Master on rank 0
+// (native/PCADALImpl.cpp:63-153), then top-k extraction and explained variance on the driver
+// (PCADALImpl.scala:108-135).  Here: one fused shifted SYRK pass per rank (kernels/pca.hip),
+// ONE allreduce of [S | column sums] (d^2 + d doubles), the fp64 covariance correction and the
+// hand-written symmetric eigensolver (linalg/eigen.cpp) evaluated redundantly on every rank —
+// no root and no broadcast.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "comm/comm.h"
+#include "runtime/context.h"
+#include "runtime/table.h"
+
+namespace oap {
+
+struct PcaParams {
+  int k = 1;
+  bool precise = false;  // 4-term bf16 split products (adds lo*lo); default 3-term
+  int flush_rows = 4096; // rows accumulated in fp32 before the fp64 flush (GPU)
+};
+
+struct PcaCovariance {
+  int d = 0;
+  int64_t n = 0;             // global rows
+  std::vector<double> cov;   // d x d sample covariance (divided by n - 1), row-major
+  std::vector<double> mean;  // d
+  double stats_ms = 0.0;     // local SYRK + reduce (device time on GPU)
+  double allreduce_ms = 0.0;
+};
+
+struct PcaResult {
+  int d = 0, k = 0;
+  int64_t n = 0;
+  std::vector<double> pc;           // d x k row-major (column j = j-th principal component)
+  std::vector<double> explained;    // k: |lambda_j| / sum_i |lambda_i|
+  std::vector<double> eigenvalues;  // all d, |.|-descending
+  std::vector<double> mean;
+  double stats_ms = 0.0, allreduce_ms = 0.0, eig_ms = 0.0, total_ms = 0.0;
+};
+
+PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p);
+PcaResult pca_fit(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p);
+
+}  // namespace oap

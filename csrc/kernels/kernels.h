@@ -105,5 +105,22 @@ void kmeans_finalize(const KMeansFinalizeArgs& a, hipStream_t s);
 void kmeans_prepare_centers(const double* centers64, int k, int d, int dp, float* centers32,
                             float* cnorm, float* cstat, int kpad, hipStream_t s);
 
+// ---- PCA (kernels/pca.hip) ------------------------------------------------------------------
+struct PcaPlan {
+  int nb = 0;      // 128-feature blocks
+  int tiles = 0;   // upper-triangular 128x128 tiles
+  int splits = 0;  // row splits (one fp64 slab each)
+  int64_t rows_per_split = 0;
+  size_t part_elems = 0, cpart_elems = 0, shift_elems = 0;
+  int grid = 0;
+};
+PcaPlan pca_syrk_plan(int64_t n, int d, int num_cus);
+// part/cpart: fp64 slabs of p.part_elems / p.cpart_elems; shift: [p.shift_elems] zero padded.
+void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, const PcaPlan& p,
+              double* part, double* cpart, bool four, int flush_rows, hipStream_t s);
+// out: d x d symmetric (both triangles written), colsum: [d]
+void pca_reduce(const PcaPlan& p, const double* part, const double* cpart, int d, double* out,
+                double* colsum, hipStream_t s);
+
 }  // namespace kern
 }  // namespace oap

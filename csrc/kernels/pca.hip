@@ -1,0 +1,290 @@
+// PCA covariance statistics: fused shifted SYRK + column sums on MFMA.
+//
+// Replaces the reference's two passes — Spark StandardScaler centring (mllib-dal/src/main/scala/
+// org/apache/spark/ml/feature/PCADALImpl.scala:101-106) followed by oneDAL's fp64 step1Local
+// cross-product (native/PCADALImpl.cpp:63-69) — with ONE pass over the HBM-resident fp32 rows:
+//
+//   S = sum_rows (x - s)(x - s)^T      (upper 128x128 tiles only)
+//   c = sum_rows (x - s)               (diagonal tiles)
+//
+// where s is a global shift close to the mean, so the later correction
+// cov = (S - c c^T / n) / (n - 1) has no catastrophic cancellation.
+//
+// Products run on v_mfma_f32_32x32x16_bf16 with the 2-term bf16 split of (x - s):
+// hi*hi + hi*lo + lo*hi (+ lo*lo with `four`), i.e. ~2^-17 relative per product, accumulated in
+// fp32 for at most `flush_chunks` x 32 rows and then added into a per-workgroup fp64 slab that
+// only this workgroup owns (deterministic); a second kernel sums the slabs in split order.
+//
+// Workgroup = 4 waves on one 128x128 output tile (each wave 64x64 = 2x2 MFMA blocks); rows are
+// staged 32 at a time through LDS transposed to [feature][row] bf16 hi/lo planes (40 KB), so
+// A and B fragments are single 16-byte LDS reads.  Blocks are remapped so that all tiles of one
+// row split land on one XCD and share its L2.
+#include "kernels/device_utils.h"
+#include "kernels/kernels.h"
+#include "runtime/common.h"
+
+namespace oap {
+namespace kern {
+
+namespace {
+
+constexpr int kTile = 128;
+constexpr int kChunk = 32;             // rows per LDS stage
+constexpr int kPS = kChunk + 8;        // plane row stride in bf16 (80 B: conflict-free b128 reads)
+constexpr int kPlane = kTile * kPS;    // bf16 elements per plane
+constexpr int kSyrkThreads = 256;
+
+struct SyrkArgs {
+  const float* x;
+  int64_t n, ld;
+  int d;
+  const float* shift;  // [nb*128], zero padded
+  int nb, tiles, splits, flush_chunks;
+  int64_t rows_per_split;
+  double* part;   // [splits][tiles][128*128]
+  double* cpart;  // [splits][nb][128]
+};
+
+__device__ inline void tile_coords(int tile, int nb, int& ti, int& tj) {
+  int t = 0, rem = tile;
+  while (rem >= nb - t) {
+    rem -= nb - t;
+    ++t;
+  }
+  ti = t;
+  tj = t + rem;
+}
+
+template <bool FOUR>
+__global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * kPlane];  // [side][plane hi/lo]
+  const int G = a.splits * a.tiles;
+  const int per = gridDim.x / 8;  // gridDim.x is a multiple of 8
+  const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= G) return;
+  const int split = L / a.tiles, tile = L - split * a.tiles;
+  int ti, tj;
+  tile_coords(tile, a.nb, ti, tj);
+  const bool diag = ti == tj;
+  const int64_t r_begin = int64_t(split) * a.rows_per_split;
+  const int64_t r_end = min(a.n, r_begin + a.rows_per_split);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wi = wave >> 1, wj = wave & 1;
+  // loader: rows 4*lg .. 4*lg+3 of the stage, features 4*lq .. 4*lq+3 of each side
+  const int lg = tid & 7, lq = tid >> 3;
+  const int fi = ti * kTile + 4 * lq, fj = tj * kTile + 4 * lq;
+  const bool okI = fi < a.ld, okJ = fj < a.ld;
+  const float4 shI = *reinterpret_cast<const float4*>(a.shift + fi);
+  const float4 shJ = *reinterpret_cast<const float4*>(a.shift + fj);
+
+  float4 vI[4], vJ[4];
+  double cs[4] = {0.0, 0.0, 0.0, 0.0};
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = r0 + 4 * lg + i;
+      const bool ok = row < r_end;
+      const float* p = a.x + (ok ? row : 0) * a.ld;
+      vI[i] = (ok && okI) ? *reinterpret_cast<const float4*>(p + fi) : make_float4(0, 0, 0, 0);
+      if (!diag)
+        vJ[i] = (ok && okJ) ? *reinterpret_cast<const float4*>(p + fj) : make_float4(0, 0, 0, 0);
+    }
+  };
+  // centre, split, transpose into the planes; rows past r_end contribute exact zeros
+  auto stage = [&](int64_t r0, int side, const float4 (&v)[4], const float4 sh, bool sums) {
+    __bf16* hi = lds + (2 * side) * kPlane;
+    __bf16* lo = hi + kPlane;
+    float c[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = r0 + 4 * lg + i < r_end;
+      c[0][i] = ok ? v[i].x - sh.x : 0.f;
+      c[1][i] = ok ? v[i].y - sh.y : 0.f;
+      c[2][i] = ok ? v[i].z - sh.z : 0.f;
+      c[3][i] = ok ? v[i].w - sh.w : 0.f;
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 ph, pl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __bf16 a_, b_;
+        bf16_split(c[f][i], a_, b_);
+        ph[i] = a_;
+        pl[i] = b_;
+        if (sums) cs[f] += static_cast<double>(c[f][i]);
+      }
+      const int off = (4 * lq + f) * kPS + 4 * lg;
+      *reinterpret_cast<bf16x4*>(hi + off) = ph;
+      *reinterpret_cast<bf16x4*>(lo + off) = pl;
+    }
+  };
+
+  f32x16 acc[2][2];
+  auto zero = [&]() {
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
+  };
+  zero();
+  double* slab = a.part + (size_t(split) * a.tiles + tile) * (kTile * kTile);
+  bool first = true;
+  auto flush = [&]() {
+    // laundered per-lane base: keeps the 64 element addresses from being hoisted out of the row
+    // loop as live registers
+    double* base = slab + (64 * wi + 4 * h) * kTile + 64 * wj + r;
+    asm volatile("" : "+v"(base));
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          double* p = base + (32 * x + (e & 3) + 8 * (e >> 2)) * kTile + 32 * y;
+          const double v = static_cast<double>(acc[x][y][e]);
+          *p = first ? v : *p + v;
+          if ((e & 3) == 3) asm volatile("" ::: "memory");  // bound the loads in flight
+        }
+    first = false;
+    zero();
+  };
+
+  const __bf16* aH = lds + (64 * wi + r) * kPS + 8 * h;
+  const __bf16* bH = lds + (diag ? 0 : 2 * kPlane) + (64 * wj + r) * kPS + 8 * h;
+  int since = 0;
+  if (r_begin < r_end) load(r_begin);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk) {
+    stage(r0, 0, vI, shI, diag);
+    if (!diag) stage(r0, 1, vJ, shJ, false);
+    __syncthreads();
+    if (r0 + kChunk < r_end) load(r0 + kChunk);  // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int x = 0; x < 2; ++x) {
+        ah[x] = *reinterpret_cast<const bf16x8*>(aH + 32 * x * kPS + 16 * ks);
+        al[x] = *reinterpret_cast<const bf16x8*>(aH + kPlane + 32 * x * kPS + 16 * ks);
+        bh[x] = *reinterpret_cast<const bf16x8*>(bH + 32 * x * kPS + 16 * ks);
+        bl[x] = *reinterpret_cast<const bf16x8*>(bH + kPlane + 32 * x * kPS + 16 * ks);
+      }
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bl[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bh[y], acc[x][y], 0, 0, 0);
+          if (FOUR)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (++since == a.flush_chunks) {
+      flush();
+      since = 0;
+    }
+  }
+  if (first || since > 0) flush();
+  if (diag) {  // column sums: the 8 loader lanes of one feature group are adjacent
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      double v = cs[f];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (lg == 0) a.cpart[(size_t(split) * a.nb + ti) * kTile + 4 * lq + f] = v;
+    }
+  }
+}
+
+__global__ void oap_pca_reduce(const double* __restrict__ part, const double* __restrict__ cpart,
+                               int splits, int tiles, int nb, int d, double* __restrict__ out,
+                               double* __restrict__ colsum) {
+  const int64_t total = int64_t(tiles) * kTile * kTile;
+  for (int64_t idx = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    const int tile = static_cast<int>(idx / (kTile * kTile));
+    const int e = static_cast<int>(idx - int64_t(tile) * kTile * kTile);
+    int ti, tj;
+    tile_coords(tile, nb, ti, tj);
+    const int ii = e / kTile, jj = e - ii * kTile;
+    const int i = ti * kTile + ii, j = tj * kTile + jj;
+    if (i >= d || j >= d || (ti == tj && ii > jj)) continue;
+    double s = 0.0;
+    for (int sp = 0; sp < splits; ++sp) s += part[(size_t(sp) * tiles + tile) * kTile * kTile + e];
+    out[size_t(i) * d + j] = s;
+    out[size_t(j) * d + i] = s;
+  }
+  for (int64_t f = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; f < d;
+       f += int64_t(gridDim.x) * blockDim.x) {
+    double s = 0.0;
+    for (int sp = 0; sp < splits; ++sp) s += cpart[(size_t(sp) * nb + f / kTile) * kTile + f % kTile];
+    colsum[f] = s;
+  }
+}
+
+}  // namespace
+
+PcaPlan pca_syrk_plan(int64_t n, int d, int num_cus) {
+  PcaPlan p;
+  p.nb = (d + kTile - 1) / kTile;
+  p.tiles = p.nb * (p.nb + 1) / 2;
+  const int64_t want = int64_t(std::max(num_cus, 64)) * 6;  // ~2 resident workgroups per CU x 3
+  int64_t s = (want + p.tiles - 1) / p.tiles;
+  const int64_t max_s = std::max<int64_t>(1, (n + 4 * kChunk - 1) / (4 * kChunk));
+  s = std::max<int64_t>(1, std::min(s, max_s));
+  // bound the fp64 slab (splits x tiles x 128 KB) to 1 GiB unless one split already exceeds it
+  const int64_t slab_tile = int64_t(kTile) * kTile * 8;
+  while (s > 1 && s * p.tiles * slab_tile > (int64_t(1) << 30)) --s;
+  p.splits = static_cast<int>(s);
+  p.rows_per_split = round_up((n + s - 1) / s, kChunk);
+  if (p.rows_per_split == 0) p.rows_per_split = kChunk;
+  p.part_elems = size_t(p.splits) * p.tiles * kTile * kTile;
+  p.cpart_elems = size_t(p.splits) * p.nb * kTile;
+  p.shift_elems = size_t(p.nb) * kTile;
+  const int64_t g = int64_t(p.splits) * p.tiles;
+  p.grid = static_cast<int>(round_up(g, 8));
+  return p;
+}
+
+void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, const PcaPlan& p,
+              double* part, double* cpart, bool four, int flush_rows, hipStream_t s) {
+  OAP_CHECK(ld % 4 == 0 && ld >= d, "pca_syrk: ld must be a multiple of 4 and >= d");
+  OAP_CHECK(reinterpret_cast<uintptr_t>(x) % 16 == 0, "pca_syrk: rows must be 16-byte aligned");
+  SyrkArgs a;
+  a.x = x;
+  a.n = n;
+  a.ld = ld;
+  a.d = d;
+  a.shift = shift;
+  a.nb = p.nb;
+  a.tiles = p.tiles;
+  a.splits = p.splits;
+  a.flush_chunks = std::max(1, flush_rows / kChunk);
+  a.rows_per_split = p.rows_per_split;
+  a.part = part;
+  a.cpart = cpart;
+  if (four)
+    hipLaunchKernelGGL(oap_pca_syrk<true>, dim3(p.grid), dim3(kSyrkThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(oap_pca_syrk<false>, dim3(p.grid), dim3(kSyrkThreads), 0, s, a);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void pca_reduce(const PcaPlan& p, const double* part, const double* cpart, int d, double* out,
+                double* colsum, hipStream_t s) {
+  const int64_t total = int64_t(p.tiles) * kTile * kTile;
+  hipLaunchKernelGGL(oap_pca_reduce, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s, part,
+                     cpart, p.splits, p.tiles, p.nb, d, out, colsum);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace kern
+}  // namespace oap

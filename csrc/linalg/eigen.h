@@ -1,0 +1,30 @@
+// Dense symmetric eigensolver (fp64, host, thread-parallel) — the replacement for the reference's
+// oneDAL `pca::Distributed<step2Master, svdDense>` finalisation (mllib-dal/src/main/native/
+// PCADALImpl.cpp:127-153), which returned the full eigenvalue vector and eigenvector matrix.
+//
+// Algorithm: Householder tridiagonalisation (Q explicit), implicit-shift QL on the tridiagonal
+// matrix with the Givens rotation sequence recorded, then the rotations applied to Q^T in
+// column slices on the thread pool (rows of the eigenvector matrix are independent).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "runtime/context.h"
+
+namespace oap {
+
+struct SymEig {
+  int n = 0;
+  std::vector<double> values;   // n eigenvalues, sorted by |lambda| descending (SVD order)
+  std::vector<double> vectors;  // n x n row-major, column j = unit eigenvector of values[j]
+};
+
+// A: n x n symmetric, row-major (only read).  Eigenvector signs are normalised so that the
+// largest-magnitude component of each vector is positive (deterministic across runs and ranks).
+SymEig sym_eig(const std::vector<double>& A, int n, ThreadPool* pool);
+
+// Same, only the first `k` eigenvectors are kept (values still hold all n eigenvalues).
+SymEig sym_eig_topk(const std::vector<double>& A, int n, int k, ThreadPool* pool);
+
+}  // namespace oap

@@ -8,6 +8,7 @@ from . import _loader  # imports torch first (single HIP runtime per process)
 from .config import Config, get_config, set_config
 from .linalg import DenseMatrix, DenseVector, Matrices, SparseVector, Vectors
 from .models.clustering import KMeans, KMeansModel, KMeansSummary
+from .models.feature import PCA, PCAModel
 from .parallel.world import get_world, init_world, shutdown_world
 
 __version__ = "0.1.0"
@@ -15,5 +16,5 @@ __version__ = "0.1.0"
 _loader.require_on_gpu_hosts()
 
 __all__ = ["Config", "get_config", "set_config", "DenseMatrix", "DenseVector", "Matrices",
-           "SparseVector", "Vectors", "KMeans", "KMeansModel", "KMeansSummary", "get_world",
+           "SparseVector", "Vectors", "KMeans", "KMeansModel", "KMeansSummary", "PCA", "PCAModel", "get_world",
            "init_world", "shutdown_world", "__version__"]

@@ -84,6 +84,8 @@ def _compile(src: Path, debug: bool) -> tuple[Path, str]:
         cmd += ["-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
     else:
         cmd += ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+        if "linalg" in src.parts:  # host fp64 dense kernels: x86-64-v3 (both hosts have it)
+            cmd += ["-mavx2", "-mfma", "-fopenmp-simd"]
     cmd += ["-MMD", "-MF", str(obj.with_suffix(".d")), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

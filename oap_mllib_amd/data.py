@@ -33,9 +33,19 @@ def _row_to_array(v: Any) -> np.ndarray:
     return np.asarray(v, dtype=np.float64)
 
 
+def _columns_to_frame(dataset: Any) -> Any:
+    """A {column: values} mapping is accepted wherever a DataFrame is."""
+    if isinstance(dataset, dict):
+        import pandas as pd
+
+        return pd.DataFrame({k: list(v) for k, v in dataset.items()})
+    return dataset
+
+
 def to_matrix(dataset: Any, features_col: str = "features",
               dtype=np.float64) -> np.ndarray:
     """Returns a C-contiguous (n, d) matrix for `dataset`."""
+    dataset = _columns_to_frame(dataset)
     if isinstance(dataset, np.ndarray):
         m = dataset
         if m.ndim == 1:
@@ -80,6 +90,7 @@ def as_frame(dataset: Any, features_col: str = "features"):
     """pandas view of a dataset (numpy matrices become a single vector column)."""
     import pandas as pd
 
+    dataset = _columns_to_frame(dataset)
     if isinstance(dataset, pd.DataFrame):
         return dataset.copy()
     if isinstance(dataset, np.ndarray):
@@ -103,6 +114,7 @@ def as_frame(dataset: Any, features_col: str = "features"):
 def column(dataset: Any, name: str) -> np.ndarray:
     import pandas as pd
 
+    dataset = _columns_to_frame(dataset)
     if isinstance(dataset, pd.DataFrame):
         return dataset[name].to_numpy()
     try:

@@ -115,6 +115,18 @@ class Params:
     def __init__(self, uid: str | None = None):
         self.uid = uid or f"{self._uid_prefix}_{uuid.uuid4().hex[-12:]}"
         self._paramMap: dict[str, Any] = {}
+        self._defaults: dict[str, Any] = {}  # per-instance defaults (e.g. outputCol = uid__output)
+
+    def _setDefault(self, **kw) -> "Params":  # noqa: N802
+        for name, value in kw.items():
+            self.getParam(name)
+            self._defaults[name] = value
+        return self
+
+    def _default_of(self, name: str) -> Any:
+        if name in getattr(self, "_defaults", {}):
+            return self._defaults[name]
+        return self.getParam(name).default
 
     # -- introspection -----------------------------------------------------------------
     @classmethod
@@ -143,7 +155,7 @@ class Params:
         return name in self._paramMap
 
     def hasDefault(self, name: str) -> bool:  # noqa: N802
-        return self.getParam(name).default is not NO_DEFAULT
+        return self._default_of(name) is not NO_DEFAULT
 
     def isDefined(self, name: str) -> bool:  # noqa: N802
         return self.isSet(name) or self.hasDefault(name)
@@ -151,13 +163,13 @@ class Params:
     def getOrDefault(self, name: str) -> Any:  # noqa: N802
         if name in self._paramMap:
             return self._paramMap[name]
-        p = self.getParam(name)
-        if p.default is NO_DEFAULT:
+        v = self._default_of(name)
+        if v is NO_DEFAULT:
             raise KeyError(f"Failed to find a default value for {name}")
-        return p.default
+        return v
 
     def getDefault(self, name: str) -> Any:  # noqa: N802
-        return self.getParam(name).default
+        return self._default_of(name)
 
     def _set(self, **kw) -> "Params":
         for name, value in kw.items():
@@ -173,19 +185,24 @@ class Params:
         return self
 
     def extractParamMap(self, extra: dict | None = None) -> dict[str, Any]:  # noqa: N802
-        out = {p.name: p.default for p in self.params if p.default is not NO_DEFAULT}
+        out = self.defaultParamMap()
         out.update(self._paramMap)
         out.update(extra or {})
         return out
 
     def defaultParamMap(self) -> dict[str, Any]:  # noqa: N802
-        return {p.name: p.default for p in self.params if p.default is not NO_DEFAULT}
+        out = {}
+        for p in self.params:
+            v = self._default_of(p.name)
+            if v is not NO_DEFAULT:
+                out[p.name] = v
+        return out
 
     def explainParam(self, name: str) -> str:  # noqa: N802
         p = self.getParam(name)
         parts = []
-        if p.default is not NO_DEFAULT:
-            parts.append(f"default: {p.default}")
+        if self._default_of(name) is not NO_DEFAULT:
+            parts.append(f"default: {self._default_of(name)}")
         if name in self._paramMap:
             parts.append(f"current: {self._paramMap[name]}")
         extra = f" ({', '.join(parts)})" if parts else " (undefined)"
@@ -197,6 +214,7 @@ class Params:
     def copy(self, extra: dict | None = None) -> "Params":
         that = _copy.copy(self)
         that._paramMap = dict(self._paramMap)
+        that._defaults = dict(getattr(self, "_defaults", {}))
         for k, v in (extra or {}).items():
             that._set(**{k: v})
         return that

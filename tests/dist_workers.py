@@ -76,3 +76,17 @@ def host_comm_collectives():
            "total": t.global_rows}
     O.shutdown_world()
     return out
+
+
+def pca_native(n=3000, d=12, k=4, seed=5, device="cpu", use_rccl=True):
+    import oap_mllib_amd as O
+
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl, device_id=0))
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, d)) @ rng.normal(size=(d, d)) + 50.0
+    local = _shard(X, w.rank, w.size)
+    m = O.PCA(k=k, inputCol="features").fit(local)
+    out = {"rank": w.rank, "engine": m.fit_info["engine"], "pc": m.pc.toArray().tolist(),
+           "ev": m.explainedVariance.toArray().tolist()}
+    O.shutdown_world()
+    return out

@@ -1,0 +1,93 @@
+"""PCA on the MI355X: the fused shifted-SYRK MFMA kernel (kernels/pca.hip) against an fp64
+numpy oracle computed on the SAME fp32-rounded rows the GPU sees."""
+import numpy as np
+import pytest
+
+import oap_mllib_amd as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _f32(X):
+    return np.asarray(X, np.float32).astype(np.float64)
+
+
+def _cov_gpu(native, w, X, precise=False):
+    from oap_mllib_amd.models.clustering import upload_table
+
+    t = upload_table(w, np.asarray(X, np.float32))
+    r = native.pca_covariance(w.ctx, w.comm, t, precise)
+    return np.asarray(r["cov"]), np.asarray(r["mean"]), r
+
+
+@pytest.mark.parametrize("n,d", [(5, 3), (31, 7), (1000, 50), (4099, 127), (3000, 128),
+                                 (2500, 129), (2000, 300), (20000, 1000)])
+def test_covariance_matches_fp64(native, gpu_world, n, d):
+    rng = np.random.default_rng(n * 7 + d)
+    X = _f32(rng.normal(size=(n, d)) @ (rng.normal(size=(d, d)) / np.sqrt(d)) + rng.normal(size=d))
+    C, mu, _ = _cov_gpu(native, gpu_world, X)
+    Cr = np.cov(X.T, ddof=1)
+    scale = np.sqrt(np.outer(np.diag(Cr), np.diag(Cr))) + 1e-30
+    assert np.max(np.abs(C - Cr) / scale) < 3e-5
+    np.testing.assert_allclose(mu, X.mean(axis=0), atol=1e-6 * (1 + np.abs(X).max()))
+    assert np.array_equal(C, C.T)
+
+
+def test_precise_mode_tighter(native, gpu_world):
+    rng = np.random.default_rng(11)
+    X = _f32(rng.normal(size=(5000, 96)) * rng.uniform(0.1, 10, size=96))
+    Cr = np.cov(X.T, ddof=1)
+    scale = np.sqrt(np.outer(np.diag(Cr), np.diag(Cr)))
+    C3, _, _ = _cov_gpu(native, gpu_world, X, precise=False)
+    C4, _, _ = _cov_gpu(native, gpu_world, X, precise=True)
+    e3 = np.max(np.abs(C3 - Cr) / scale)
+    e4 = np.max(np.abs(C4 - Cr) / scale)
+    assert e4 < 2e-6 and e4 <= e3 * 1.01
+
+
+def test_large_offset_no_cancellation(native, gpu_world):
+    rng = np.random.default_rng(5)
+    X = _f32(rng.normal(size=(30000, 20)) * np.linspace(0.01, 1, 20) + 3e3)
+    C, mu, _ = _cov_gpu(native, gpu_world, X)
+    Cr = np.cov(X.T, ddof=1)
+    scale = np.sqrt(np.outer(np.diag(Cr), np.diag(Cr)))
+    assert np.max(np.abs(C - Cr) / scale) < 5e-5
+
+
+def test_deterministic(native, gpu_world):
+    rng = np.random.default_rng(2)
+    X = rng.normal(size=(70000, 200)).astype(np.float32)
+    a, _, _ = _cov_gpu(native, gpu_world, X)
+    b, _, _ = _cov_gpu(native, gpu_world, X)
+    assert np.array_equal(a, b)
+
+
+def test_fit_api_gpu_engine(gpu_world):
+    rng = np.random.default_rng(9)
+    d, k = 40, 5
+    lat = rng.normal(size=(20000, d)) * np.geomspace(10, 0.1, d)
+    Q, _ = np.linalg.qr(rng.normal(size=(d, d)))
+    X = _f32(lat @ Q.T + 7.0)
+    m = O.PCA(k=k, inputCol="features").fit(X)
+    assert m.fit_info["engine"] == "gpu"
+    Cr = np.cov(X.T, ddof=1)
+    wr, Vr = np.linalg.eigh(Cr)
+    o = np.argsort(-wr)
+    wr, Vr = wr[o], Vr[:, o]
+    np.testing.assert_allclose(m.explainedVariance.toArray(), wr[:k] / wr.sum(), atol=1e-5)
+    np.testing.assert_allclose(np.abs(m.pc.toArray()), np.abs(Vr[:, :k]), atol=1e-4)
+
+
+def test_gpu_close_to_cpu_engine(native, gpu_world):
+    from oap_mllib_amd.models.clustering import upload_table
+
+    rng = np.random.default_rng(4)
+    X = rng.normal(size=(8000, 33)).astype(np.float32) * np.arange(1, 34, dtype=np.float32)
+    r_gpu = native.pca_fit(gpu_world.ctx, gpu_world.comm, upload_table(gpu_world, X), 6, False)
+    cpu = native.Context(-1, 1.0, 4)
+    lc = native.LocalComm()
+    t = native.upload_dense(cpu, X.astype(np.float64), "f64", 33)
+    r_cpu = native.pca_fit(cpu, lc, t, 6, False)
+    np.testing.assert_allclose(r_gpu["explained_variance"], r_cpu["explained_variance"],
+                               atol=2e-6)
+    np.testing.assert_allclose(np.abs(r_gpu["pc"]), np.abs(r_cpu["pc"]), atol=1e-4)
