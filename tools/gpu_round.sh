@@ -21,6 +21,12 @@ for st in $STEPS; do
     ablate)
       timeout -k 10 300 python tools/kmeans_ablate.py > gpurun_out/ablate_$T.json 2>&1
       rc=$?; echo ablate_rc=$rc; tail -2 gpurun_out/ablate_$T.json; fatal $rc ablate;;
+    smoke)
+      timeout -k 10 180 python __graft_entry__.py smoke > gpurun_out/smoke_$T.log 2>&1
+      rc=$?; echo smoke_rc=$rc; tail -2 gpurun_out/smoke_$T.log; fatal $rc smoke;;
+    pcabench)
+      timeout -k 10 400 python benchmarks/bench_pca.py ${PCA_ARGS:-} > gpurun_out/bench_pca_$T.json 2> gpurun_out/bench_pca_$T.err
+      rc=$?; echo pcabench_rc=$rc; cat gpurun_out/bench_pca_$T.json; tail -3 gpurun_out/bench_pca_$T.err; fatal $rc pcabench;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- python3 $R/bench.py --rows 20000000 --steps 5 --warmup 1 --skip-fit > $R/gpurun_out/prof_$T.log 2>&1)
       rc=$?; echo prof_rc=$rc; fatal $rc prof;;
