@@ -1,3 +1,70 @@
-#include "bindings/bindings.h"
+// ALS bindings: the role of the reference's JNI entries ALSDALImpl.cShuffleData and
+// cDALImplictALS (mllib-dal/src/main/native/javah/org_apache_spark_ml_recommendation_
+// ALSDALImpl.h:12-24) — one call takes this rank's ratings (any partition) and returns the full
+// id-indexed factor matrices instead of per-rank native tables plus offsets.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
-void register_als(pybind11::module_& m) { (void)m; }
+#include <cstring>
+
+#include "bindings/bindings.h"
+#include "drivers/als.h"
+#include "kernels/kernels.h"
+
+namespace py = pybind11;
+using namespace oap;
+
+void register_als(py::module_& m) {
+  m.def(
+      "als_fit",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> users,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> items,
+         py::array_t<float, py::array::c_style | py::array::forcecast> ratings, int rank,
+         int max_iter, double reg, double alpha, bool implicit, uint64_t seed) {
+        const int64_t n = users.size();
+        if (items.size() != n || ratings.size() != n)
+          throw ConfigError("users, items and ratings must have the same length");
+        AlsParams p;
+        p.rank = rank;
+        p.max_iter = max_iter;
+        p.reg = reg;
+        p.alpha = alpha;
+        p.implicit = implicit;
+        p.seed = seed;
+        AlsResult r;
+        {
+          py::gil_scoped_release rel;
+          r = als_fit(*ctx, *comm, users.data(), items.data(), ratings.data(), n, p);
+        }
+        auto ids = [](const std::vector<int32_t>& v) {
+          py::array_t<int32_t> a(int64_t(v.size()));
+          if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
+          return a;
+        };
+        auto fac = [&](const std::vector<float>& v, size_t rows) {
+          py::array_t<float> a({int64_t(rows), int64_t(r.rank)});
+          if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
+          return a;
+        };
+        py::dict out;
+        out["user_ids"] = ids(r.user_ids);
+        out["item_ids"] = ids(r.item_ids);
+        out["user_factors"] = fac(r.user_factors, r.user_ids.size());
+        out["item_factors"] = fac(r.item_factors, r.item_ids.size());
+        out["nnz"] = r.nnz;
+        out["setup_ms"] = r.setup_ms;
+        out["train_ms"] = r.train_ms;
+        out["iter_ms"] = r.iter_ms;
+        out["gram_ms"] = r.gram_ms;
+        out["solve_ms"] = r.solve_ms;
+        out["comm_ms"] = r.comm_ms;
+        out["failed_rows"] = r.failed_rows;
+        return out;
+      },
+      py::arg("ctx"), py::arg("comm"), py::arg("users"), py::arg("items"), py::arg("ratings"),
+      py::arg("rank") = 10, py::arg("max_iter") = 10, py::arg("reg") = 0.1,
+      py::arg("alpha") = 1.0, py::arg("implicit") = true, py::arg("seed") = 0);
+  m.def("als_max_rank", &kern::als_max_rank);
+}

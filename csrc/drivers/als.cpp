@@ -1,0 +1,483 @@
+#include "drivers/als.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+
+#include "kernels/rng.h"
+#include "kernels/kernels.h"
+#include "runtime/log.h"
+
+namespace oap {
+
+namespace {
+
+struct Rec {
+  int32_t a, b;
+  float r;
+};
+static_assert(sizeof(Rec) == 12, "Rec must be packed");
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+int owner_of(int32_t id, int P) { return int(((int64_t(id) % P) + P) % P); }
+
+// ---- host-memory collectives that work with any comm ------------------------------------
+std::vector<int64_t> allgather_i64(Context& ctx, Comm& comm, const std::vector<int64_t>& mine) {
+  const int P = comm.size();
+  std::vector<int64_t> all(mine.size() * P);
+  if (P == 1) {
+    std::copy(mine.begin(), mine.end(), all.begin());
+    return all;
+  }
+  if (comm.on_device()) {
+    Buffer s = ctx.alloc(mine.size() * 8), r = ctx.alloc(all.size() * 8);
+    hipStream_t st = ctx.comm_stream();
+    OAP_HIP_CHECK(hipMemcpyAsync(s.data(), mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st));
+    comm.allgather(s.data(), r.data(), mine.size(), DType::I64, st);
+    OAP_HIP_CHECK(hipMemcpyAsync(all.data(), r.data(), all.size() * 8, hipMemcpyDeviceToHost, st));
+    comm.wait(st);
+  } else {
+    comm.allgather(mine.data(), all.data(), mine.size(), DType::I64, nullptr);
+  }
+  return all;
+}
+
+// Ratings to their owners: out[p] goes to rank p; returns what this rank received, in source
+// rank order.
+std::vector<Rec> exchange(Context& ctx, Comm& comm, std::vector<std::vector<Rec>>& out) {
+  const int P = comm.size(), me = comm.rank();
+  if (P == 1) return std::move(out[0]);
+  std::vector<int64_t> mine(P);
+  for (int p = 0; p < P; ++p) mine[p] = int64_t(out[p].size());
+  const std::vector<int64_t> all = allgather_i64(ctx, comm, mine);
+  std::vector<size_t> sc(P), rc(P);
+  size_t stot = 0, rtot = 0;
+  for (int p = 0; p < P; ++p) {
+    sc[p] = out[p].size() * sizeof(Rec);
+    rc[p] = size_t(all[size_t(p) * P + me]) * sizeof(Rec);
+    stot += sc[p];
+    rtot += rc[p];
+  }
+  std::vector<char> send(stot);
+  size_t off = 0;
+  for (int p = 0; p < P; ++p) {
+    if (!out[p].empty()) std::memcpy(send.data() + off, out[p].data(), sc[p]);
+    off += sc[p];
+    std::vector<Rec>().swap(out[p]);
+  }
+  std::vector<Rec> recv(rtot / sizeof(Rec));
+  if (comm.on_device()) {
+    Buffer ds = ctx.alloc(std::max<size_t>(stot, 16)), dr = ctx.alloc(std::max<size_t>(rtot, 16));
+    hipStream_t st = ctx.comm_stream();
+    if (stot) OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send.data(), stot, hipMemcpyHostToDevice, st));
+    comm.alltoallv(ds.data(), sc, dr.data(), rc, DType::U8, st);
+    if (rtot)
+      OAP_HIP_CHECK(hipMemcpyAsync(recv.data(), dr.data(), rtot, hipMemcpyDeviceToHost, st));
+    comm.wait(st);
+  } else {
+    comm.alltoallv(send.data(), sc, recv.data(), rc, DType::U8, nullptr);
+  }
+  return recv;
+}
+
+// allgatherv of int32 ids (counts known on every rank), rank order.
+std::vector<int32_t> allgatherv_i32(Context& ctx, Comm& comm, const std::vector<int32_t>& mine,
+                                    const std::vector<int64_t>& counts) {
+  const int P = comm.size();
+  if (P == 1) return mine;
+  int64_t mx = 1;
+  for (int64_t c : counts) mx = std::max(mx, c);
+  std::vector<int64_t> pad(mx, 0);
+  for (size_t i = 0; i < mine.size(); ++i) pad[i] = mine[i];
+  const std::vector<int64_t> all = allgather_i64(ctx, comm, pad);
+  std::vector<int32_t> out;
+  for (int p = 0; p < P; ++p)
+    for (int64_t i = 0; i < counts[p]; ++i) out.push_back(int32_t(all[size_t(p) * mx + i]));
+  return out;
+}
+
+struct Csr {
+  std::vector<int64_t> ptr;
+  std::vector<int32_t> col;
+  std::vector<float> val;
+};
+
+// rows are a - row_base (must lie in [0, nrows)); sorted by (row, col), stable on input order
+Csr build_csr(std::vector<Rec>& recs, int64_t nrows, int64_t row_base) {
+  std::stable_sort(recs.begin(), recs.end(), [](const Rec& x, const Rec& y) {
+    return x.a != y.a ? x.a < y.a : x.b < y.b;
+  });
+  Csr c;
+  c.ptr.assign(nrows + 1, 0);
+  c.col.resize(recs.size());
+  c.val.resize(recs.size());
+  for (size_t k = 0; k < recs.size(); ++k) {
+    const int64_t row = int64_t(recs[k].a) - row_base;
+    OAP_CHECK(row >= 0 && row < nrows, "ALS CSR: row out of range");
+    c.ptr[row + 1]++;
+    c.col[k] = recs[k].b;
+    c.val[k] = recs[k].r;
+  }
+  for (int64_t i = 0; i < nrows; ++i) c.ptr[i + 1] += c.ptr[i];
+  return c;
+}
+
+struct Side {  // one factor matrix and the CSR of this rank's owned rows of it
+  int64_t n = 0;                 // global rows
+  std::vector<int64_t> cnt, off;  // per-rank owned counts / global offsets
+  std::vector<int32_t> ids;      // global index -> id
+  Csr csr;                       // owned rows; cols index the OTHER side
+};
+
+void init_factor_row(uint64_t seed, int32_t id, int r, int ld, float* out) {
+  double nrm = 0.0;
+  for (int f = 0; f < r; ++f) {
+    const double g = kern::als_init_gaussian(seed, id, f);
+    nrm += g * g;
+  }
+  nrm = std::sqrt(nrm);
+  for (int f = 0; f < ld; ++f)
+    out[f] = f < r ? float(kern::als_init_gaussian(seed, id, f) / nrm) : 0.f;
+}
+
+// fp64 Cholesky solve of the r x r SPD system (lower triangle of A used); false if not SPD.
+bool chol_solve(std::vector<double>& A, std::vector<double>& b, int r) {
+  for (int j = 0; j < r; ++j) {
+    double d = A[size_t(j) * r + j];
+    for (int k = 0; k < j; ++k) d -= A[size_t(j) * r + k] * A[size_t(j) * r + k];
+    if (!(d > 0.0)) return false;
+    d = std::sqrt(d);
+    A[size_t(j) * r + j] = d;
+    for (int i = j + 1; i < r; ++i) {
+      double s = A[size_t(i) * r + j];
+      for (int k = 0; k < j; ++k) s -= A[size_t(i) * r + k] * A[size_t(j) * r + k];
+      A[size_t(i) * r + j] = s / d;
+    }
+  }
+  for (int j = 0; j < r; ++j) {
+    double s = b[j];
+    for (int k = 0; k < j; ++k) s -= A[size_t(j) * r + k] * b[k];
+    b[j] = s / A[size_t(j) * r + j];
+  }
+  for (int j = r - 1; j >= 0; --j) {
+    double s = b[j];
+    for (int k = j + 1; k < r; ++k) s -= A[size_t(k) * r + j] * b[k];
+    b[j] = s / A[size_t(j) * r + j];
+  }
+  return true;
+}
+
+}  // namespace
+
+AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t* items,
+                  const float* ratings, int64_t n, const AlsParams& p) {
+  TraceRange tr_all(&ctx.metrics(), "als/fit");
+  OAP_CHECK(p.rank >= 1, "ALS rank must be >= 1");
+  OAP_CHECK(p.max_iter >= 0, "ALS maxIter must be >= 0");
+  const int P = comm.size(), me = comm.rank();
+  const int r = p.rank, ld = int(round_up(size_t(r), 16));
+  AlsResult res;
+  res.rank = r;
+  auto t_setup = std::chrono::steady_clock::now();
+
+  // ---- 1. ratings -> item owners; dense item indices --------------------------------------
+  Side U, I;
+  std::vector<Rec> recv1;
+  {
+    std::vector<std::vector<Rec>> out(P);
+    for (int64_t k = 0; k < n; ++k) out[owner_of(items[k], P)].push_back({users[k], items[k], ratings[k]});
+    recv1 = exchange(ctx, comm, out);
+  }
+  std::vector<int32_t> my_items;
+  for (const Rec& x : recv1) my_items.push_back(x.b);
+  std::sort(my_items.begin(), my_items.end());
+  my_items.erase(std::unique(my_items.begin(), my_items.end()), my_items.end());
+  I.cnt = allgather_i64(ctx, comm, {int64_t(my_items.size())});
+  I.off.assign(P + 1, 0);
+  for (int q = 0; q < P; ++q) I.off[q + 1] = I.off[q] + I.cnt[q];
+  I.n = I.off[P];
+  auto item_gidx = [&](int32_t id) {
+    return int32_t(I.off[me] + (std::lower_bound(my_items.begin(), my_items.end(), id) -
+                                my_items.begin()));
+  };
+  // ---- 2. -> user owners; dense user indices, user CSR (cols = global item index) ---------
+  std::vector<Rec> recv2;
+  {
+    std::vector<std::vector<Rec>> out(P);
+    for (const Rec& x : recv1) out[owner_of(x.a, P)].push_back({x.a, item_gidx(x.b), x.r});
+    std::vector<Rec>().swap(recv1);
+    recv2 = exchange(ctx, comm, out);
+  }
+  std::vector<int32_t> my_users;
+  for (const Rec& x : recv2) my_users.push_back(x.a);
+  std::sort(my_users.begin(), my_users.end());
+  my_users.erase(std::unique(my_users.begin(), my_users.end()), my_users.end());
+  U.cnt = allgather_i64(ctx, comm, {int64_t(my_users.size())});
+  U.off.assign(P + 1, 0);
+  for (int q = 0; q < P; ++q) U.off[q + 1] = U.off[q] + U.cnt[q];
+  U.n = U.off[P];
+  for (Rec& x : recv2)
+    x.a = int32_t(U.off[me] + (std::lower_bound(my_users.begin(), my_users.end(), x.a) -
+                               my_users.begin()));
+  // ---- 3. (global user, global item) -> item owners: item CSR (cols = global user index) --
+  std::vector<Rec> recv3;
+  {
+    std::vector<std::vector<Rec>> out(P);
+    for (const Rec& x : recv2) {
+      const int q = int(std::upper_bound(I.off.begin(), I.off.end(), int64_t(x.b)) - I.off.begin()) - 1;
+      out[q].push_back({x.b, x.a, x.r});
+    }
+    recv3 = exchange(ctx, comm, out);
+  }
+  U.csr = build_csr(recv2, U.cnt[me], U.off[me]);
+  I.csr = build_csr(recv3, I.cnt[me], I.off[me]);
+  std::vector<Rec>().swap(recv2);
+  std::vector<Rec>().swap(recv3);
+  U.ids = allgatherv_i32(ctx, comm, my_users, U.cnt);
+  I.ids = allgatherv_i32(ctx, comm, my_items, I.cnt);
+  {
+    int64_t nn = int64_t(U.csr.col.size());
+    res.nnz = int64_t(comm_allreduce_scalar(ctx, comm, double(nn), ReduceOp::Sum));
+  }
+  res.setup_ms = ms_since(t_setup);
+  ctx.metrics().add("als/setup", res.setup_ms * 1e3, res.nnz * int64_t(sizeof(Rec)) * 3);
+
+  std::vector<float> Xh, Yh;  // final factors (host, [n][ld])
+  auto t_train = std::chrono::steady_clock::now();
+  if (ctx.is_gpu()) {
+    OAP_CHECK(r <= kern::als_max_rank(), "GPU ALS supports rank <= " << kern::als_max_rank()
+                                                                      << " (use the CPU engine)");
+    ctx.activate();
+    hipStream_t s = ctx.compute();
+    const int cus = ctx.info().cu_count;
+    struct Dev {
+      Buffer f, ptr, col, val;
+    } dU, dI;
+    auto upload_side = [&](Side& S, Dev& D) {
+      D.f = ctx.alloc(std::max<size_t>(size_t(S.n) * ld * 4, 256));
+      D.ptr = ctx.alloc(S.csr.ptr.size() * 8);
+      D.col = ctx.alloc(std::max<size_t>(S.csr.col.size() * 4, 16));
+      D.val = ctx.alloc(std::max<size_t>(S.csr.val.size() * 4, 16));
+      ctx.copy_to_backend(D.ptr.data(), S.csr.ptr.data(), S.csr.ptr.size() * 8, s);
+      if (!S.csr.col.empty()) {
+        ctx.copy_to_backend(D.col.data(), S.csr.col.data(), S.csr.col.size() * 4, s);
+        ctx.copy_to_backend(D.val.data(), S.csr.val.data(), S.csr.val.size() * 4, s);
+      }
+      ctx.memset(D.f.data(), 0, size_t(S.n) * ld * 4);
+    };
+    upload_side(U, dU);
+    upload_side(I, dI);
+    {  // initial user factors from their ids (world-size independent)
+      Buffer ids = ctx.alloc(std::max<size_t>(U.ids.size() * 4, 16));
+      if (!U.ids.empty()) ctx.copy_to_backend(ids.data(), U.ids.data(), U.ids.size() * 4, s);
+      kern::als_init_factors(ids.as<int32_t>(), U.n, r, ld, p.seed, dU.f.as<float>(), s);
+      OAP_HIP_CHECK(hipStreamSynchronize(s));
+    }
+    Buffer ctr = ctx.alloc(16);
+    ctx.memset(ctr.data(), 0, 16);
+    Buffer gram64 = ctx.alloc((size_t(r) * r + r) * 8), gram32 = ctx.alloc(size_t(r) * r * 4);
+    Buffer zshift = ctx.alloc(size_t(ld + 128) * 4);
+    ctx.memset(zshift.data(), 0, size_t(ld + 128) * 4);
+    int64_t maxu = 0, maxi = 0;
+    for (int q = 0; q < P; ++q) {
+      maxu = std::max(maxu, U.cnt[q]);
+      maxi = std::max(maxi, I.cnt[q]);
+    }
+    const int64_t maxrows = std::max<int64_t>(1, std::max(maxu, maxi));
+    Buffer stage, gathered;
+    if (P > 1) {
+      stage = ctx.alloc(size_t(maxrows) * ld * 4);
+      gathered = ctx.alloc(size_t(maxrows) * ld * 4 * P);
+    }
+    // one half-iteration: dst rows of side D from source side S
+    auto half = [&](Side& Dst, Dev& dD, Side& Src, Dev& dS) {
+      Event e0, e1, e2, e3;
+      e0.record(s);
+      // Gramian of the source factors: owned slice -> allreduce
+      if (p.implicit) {
+        const int64_t cnt = Src.cnt[me];
+        const kern::PcaPlan plan = kern::pca_syrk_plan(cnt, r, cus);
+        Buffer part = ctx.alloc(plan.part_elems * 8), cpart = ctx.alloc(plan.cpart_elems * 8);
+        kern::pca_syrk(dS.f.as<float>() + Src.off[me] * ld, cnt, ld, r, zshift.as<float>(), plan,
+                       part.as<double>(), cpart.as<double>(), false, 4096, s);
+        kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), r, gram64.as<double>(),
+                         gram64.as<double>() + size_t(r) * r, s);
+        comm_allreduce(ctx, comm, gram64.data(), size_t(r) * r, DType::F64, ReduceOp::Sum, s);
+        kern::f64_to_f32(gram64.as<double>(), gram32.as<float>(), int64_t(r) * r, s);
+      }
+      e1.record(s);
+      kern::AlsSolveArgs a;
+      a.rowptr = dD.ptr.as<int64_t>();
+      a.cols = dD.col.as<int32_t>();
+      a.vals = dD.val.as<float>();
+      a.nrows = Dst.cnt[me];
+      a.src = dS.f.as<float>();
+      a.ld = ld;
+      a.r = r;
+      a.yty = p.implicit ? gram32.as<float>() : nullptr;
+      a.alpha = float(p.alpha);
+      a.lambda = float(p.reg);
+      a.implicit = p.implicit;
+      a.dst = P == 1 ? dD.f.as<float>() : stage.as<float>();
+      a.queue = ctr.as<unsigned long long>();
+      a.fail = ctr.as<unsigned long long>() + 1;
+      kern::als_solve(a, cus, s);
+      e2.record(s);
+      if (P > 1) {
+        comm_allgather(ctx, comm, stage.data(), gathered.data(), size_t(maxrows) * ld,
+                       DType::F32, s);
+        for (int q = 0; q < P; ++q)
+          if (Dst.cnt[q])
+            OAP_HIP_CHECK(hipMemcpyAsync(dD.f.as<float>() + Dst.off[q] * ld,
+                                         gathered.as<float>() + size_t(q) * maxrows * ld,
+                                         size_t(Dst.cnt[q]) * ld * 4, hipMemcpyDeviceToDevice, s));
+        if (comm.on_device()) comm.wait(s);
+      }
+      e3.record(s);
+      e3.sync();
+      res.gram_ms += Event::elapsed_ms(e0, e1);
+      res.solve_ms += Event::elapsed_ms(e1, e2);
+      res.comm_ms += Event::elapsed_ms(e2, e3);
+    };
+    for (int it = 0; it < p.max_iter; ++it) {
+      auto t0 = std::chrono::steady_clock::now();
+      {
+        TraceRange tr(&ctx.metrics(), "als/half_items");
+        half(I, dI, U, dU);
+      }
+      {
+        TraceRange tr(&ctx.metrics(), "als/half_users");
+        half(U, dU, I, dI);
+      }
+      res.iter_ms.push_back(ms_since(t0));
+      maybe_inject_fault(me, "als_iter", it);
+    }
+    unsigned long long fails = 0;
+    ctx.copy_to_host(&fails, ctr.as<unsigned long long>() + 1, 8);
+    res.failed_rows = int64_t(comm_allreduce_scalar(ctx, comm, double(fails), ReduceOp::Sum));
+    Xh.resize(size_t(U.n) * ld);
+    Yh.resize(size_t(I.n) * ld);
+    if (U.n) ctx.copy_to_host(Xh.data(), dU.f.data(), Xh.size() * 4);
+    if (I.n) ctx.copy_to_host(Yh.data(), dI.f.data(), Yh.size() * 4);
+  } else {
+    Xh.assign(size_t(U.n) * ld, 0.f);
+    Yh.assign(size_t(I.n) * ld, 0.f);
+    ctx.pool().parallel_for(U.n, [&](int, int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i) init_factor_row(p.seed, U.ids[i], r, ld, &Xh[size_t(i) * ld]);
+    });
+    int64_t fails = 0;
+    auto half = [&](Side& Dst, std::vector<float>& Fd, Side& Src, std::vector<float>& Fs) {
+      auto t0 = std::chrono::steady_clock::now();
+      std::vector<double> yty(size_t(r) * r, 0.0);
+      if (p.implicit) {
+        const int nt = ctx.pool().size();
+        std::vector<std::vector<double>> part(nt);
+        ctx.pool().parallel_for(Src.cnt[me], [&](int ci, int64_t b, int64_t e) {
+          std::vector<double>& G = part[ci];
+          G.assign(size_t(r) * r, 0.0);
+          for (int64_t k = b; k < e; ++k) {
+            const float* y = &Fs[size_t(Src.off[me] + k) * ld];
+            for (int i = 0; i < r; ++i)
+              for (int j = 0; j <= i; ++j) G[size_t(i) * r + j] += double(y[i]) * double(y[j]);
+          }
+        });
+        for (auto& G : part)
+          if (!G.empty())
+            for (size_t q = 0; q < yty.size(); ++q) yty[q] += G[q];
+        comm_allreduce_host(ctx, comm, yty.data(), yty.size(), DType::F64, ReduceOp::Sum);
+      }
+      auto t1 = std::chrono::steady_clock::now();
+      res.gram_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
+      const int64_t nloc = Dst.cnt[me];
+      std::vector<float> mine(size_t(std::max<int64_t>(nloc, 1)) * ld, 0.f);
+      std::vector<int64_t> fail_part(ctx.pool().size(), 0);
+      ctx.pool().parallel_for(nloc, [&](int ci, int64_t b, int64_t e) {
+        std::vector<double> A(size_t(r) * r), bv(r), y(r);
+        for (int64_t row = b; row < e; ++row) {
+          if (p.implicit)
+            A = yty;
+          else
+            std::fill(A.begin(), A.end(), 0.0);
+          std::fill(bv.begin(), bv.end(), 0.0);
+          int64_t nexp = 0;
+          for (int64_t q = Dst.csr.ptr[row]; q < Dst.csr.ptr[row + 1]; ++q) {
+            const float* ys = &Fs[size_t(Dst.csr.col[q]) * ld];
+            for (int f = 0; f < r; ++f) y[f] = ys[f];
+            const double rv = Dst.csr.val[q];
+            double ca, cb;
+            if (p.implicit) {
+              const double c1 = p.alpha * std::fabs(rv);
+              ca = c1;
+              cb = rv > 0.0 ? 1.0 + c1 : 0.0;
+              if (rv > 0.0) ++nexp;
+            } else {
+              ca = 1.0;
+              cb = rv;
+              ++nexp;
+            }
+            for (int i = 0; i < r; ++i) {
+              const double yi = ca * y[i];
+              for (int j = 0; j <= i; ++j) A[size_t(i) * r + j] += yi * y[j];
+              bv[i] += cb * y[i];
+            }
+          }
+          const double lam = p.reg * double(nexp);
+          for (int i = 0; i < r; ++i) A[size_t(i) * r + i] += lam;
+          float* out = &mine[size_t(row) * ld];
+          if (chol_solve(A, bv, r)) {
+            for (int f = 0; f < r; ++f) out[f] = float(bv[f]);
+          } else {
+            ++fail_part[ci];
+          }
+        }
+      });
+      for (int64_t f : fail_part) fails += f;
+      auto t2 = std::chrono::steady_clock::now();
+      res.solve_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
+      if (P == 1) {
+        std::copy(mine.begin(), mine.begin() + size_t(nloc) * ld, Fd.begin());
+      } else {
+        int64_t mx = 1;
+        for (int q = 0; q < P; ++q) mx = std::max(mx, Dst.cnt[q]);
+        mine.resize(size_t(mx) * ld, 0.f);
+        std::vector<float> all(size_t(mx) * ld * P);
+        comm_allgather(ctx, comm, mine.data(), all.data(), size_t(mx) * ld, DType::F32, nullptr);
+        for (int q = 0; q < P; ++q)
+          std::copy(all.begin() + size_t(q) * mx * ld,
+                    all.begin() + size_t(q) * mx * ld + size_t(Dst.cnt[q]) * ld,
+                    Fd.begin() + size_t(Dst.off[q]) * ld);
+      }
+      res.comm_ms += ms_since(t2);
+    };
+    for (int it = 0; it < p.max_iter; ++it) {
+      auto t0 = std::chrono::steady_clock::now();
+      half(I, Yh, U, Xh);
+      half(U, Xh, I, Yh);
+      res.iter_ms.push_back(ms_since(t0));
+      maybe_inject_fault(me, "als_iter", it);
+    }
+    res.failed_rows = int64_t(comm_allreduce_scalar(ctx, comm, double(fails), ReduceOp::Sum));
+  }
+  res.train_ms = ms_since(t_train);
+  res.user_ids = U.ids;
+  res.item_ids = I.ids;
+  res.user_factors.resize(size_t(U.n) * r);
+  res.item_factors.resize(size_t(I.n) * r);
+  for (int64_t i = 0; i < U.n; ++i)
+    std::copy(&Xh[size_t(i) * ld], &Xh[size_t(i) * ld] + r, &res.user_factors[size_t(i) * r]);
+  for (int64_t i = 0; i < I.n; ++i)
+    std::copy(&Yh[size_t(i) * ld], &Yh[size_t(i) * ld] + r, &res.item_factors[size_t(i) * r]);
+  if (me == 0 && Logger::instance().level() <= LogLevel::Info)
+    Logger::instance().log(LogLevel::Info, "als/fit",
+                           "\"nnz\":" + std::to_string(res.nnz) + ",\"users\":" +
+                               std::to_string(U.n) + ",\"items\":" + std::to_string(I.n) +
+                               ",\"rank\":" + std::to_string(r) + ",\"train_ms\":" +
+                               std::to_string(res.train_ms));
+  return res;
+}
+
+}  // namespace oap

@@ -1,0 +1,50 @@
+// Distributed implicit-feedback ALS driver.
+//
+// MI355X-native counterpart of the reference's ALS path: ratings shuffle (mllib-dal/src/main/
+// native/ALSShuffle.cpp:62-127), CSR build (scala/.../ALSDALImpl.scala:184-230) and oneDAL's
+// distributed implicit ALS (native/ALSDALImpl.cpp:216-438: 12 blocking collectives per
+// iteration through a root).  Here:
+//   * users and items are owned by rank id % P; a 3-step alltoallv gives every rank the CSR of
+//     its owned users (columns = global item index) and of its owned items (columns = global
+//     user index) — sparse and gapped IDs are handled by dense re-indexing;
+//   * factor matrices are replicated ([n_users | n_items] x r_pad, fp32 in HBM);
+//   * per half-iteration: Gramian of the owned source slice (MFMA SYRK) -> allreduce (r x r),
+//     per-row normal equations + Cholesky (kernels/als.hip) for the owned destination rows,
+//     then ONE allgather of the updated slices.
+// Iteration order and solve semantics follow Spark's implicit ALS (ALS.scala:1036-1062,
+// 1718-1800): items from users, then users from items.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "comm/comm.h"
+#include "runtime/context.h"
+
+namespace oap {
+
+struct AlsParams {
+  int rank = 10;
+  int max_iter = 10;
+  double reg = 0.1;
+  double alpha = 1.0;
+  bool implicit = true;
+  uint64_t seed = 0;
+};
+
+struct AlsResult {
+  int rank = 0;
+  std::vector<int32_t> user_ids, item_ids;      // global index order
+  std::vector<float> user_factors, item_factors;  // [n][rank] row-major
+  int64_t nnz = 0;                                // global ratings
+  double setup_ms = 0.0, train_ms = 0.0;
+  std::vector<double> iter_ms;                    // per iteration (both halves)
+  double solve_ms = 0.0, gram_ms = 0.0, comm_ms = 0.0;  // summed device/host phase times
+  int64_t failed_rows = 0;                        // rows whose system was not SPD
+};
+
+// users/items/ratings: this rank's share of the ratings (any partition).
+AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t* items,
+                  const float* ratings, int64_t n, const AlsParams& p);
+
+}  // namespace oap

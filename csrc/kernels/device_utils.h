@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "kernels/rng.h"
+
 namespace oap {
 namespace kern {
 
@@ -29,17 +31,6 @@ __device__ inline float wave_max_f32(float v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
   return v;
-}
-
-__host__ __device__ inline uint64_t splitmix64(uint64_t z) {
-  z += 0x9e3779b97f4a7c15ull;
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
-
-__host__ __device__ inline float u01_24(uint64_t h) {  // [0,1) with 24 random bits
-  return static_cast<float>(h >> 40) * (1.0f / 16777216.0f);
 }
 
 // x = hi + lo + O(2^-18 |x|): the 2-term bf16 split used by the "bf16x3" MFMA products.

@@ -118,6 +118,27 @@ PcaPlan pca_syrk_plan(int64_t n, int d, int num_cus);
 // part/cpart: fp64 slabs of p.part_elems / p.cpart_elems; shift: [p.shift_elems] zero padded.
 void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, const PcaPlan& p,
               double* part, double* cpart, bool four, int flush_rows, hipStream_t s);
+// ---- ALS (kernels/als.hip) -------------------------------------------------------------------
+struct AlsSolveArgs {
+  const int64_t* rowptr = nullptr;  // [nrows+1] CSR of the destination rows
+  const int32_t* cols = nullptr;    // source-row indices into src
+  const float* vals = nullptr;      // ratings
+  int64_t nrows = 0;
+  const float* src = nullptr;       // source factors [n_src][ld]
+  int ld = 0, r = 0;
+  const float* yty = nullptr;       // [r][r] Gramian of ALL source factors (implicit)
+  float alpha = 1.f, lambda = 0.f;
+  bool implicit = true;
+  float* dst = nullptr;             // [nrows][ld]
+  unsigned long long* queue = nullptr;  // device scratch counter
+  unsigned long long* fail = nullptr;   // device counter of non-SPD rows
+};
+int als_max_rank();
+void als_solve(const AlsSolveArgs& a, int num_cus, hipStream_t s);
+void als_init_factors(const int32_t* ids, int64_t n, int r, int ld, uint64_t seed, float* out,
+                      hipStream_t s);
+void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
+
 // out: d x d symmetric (both triangles written), colsum: [d]
 void pca_reduce(const PcaPlan& p, const double* part, const double* cpart, int d, double* out,
                 double* colsum, hipStream_t s);

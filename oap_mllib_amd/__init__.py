@@ -9,6 +9,7 @@ from .config import Config, get_config, set_config
 from .linalg import DenseMatrix, DenseVector, Matrices, SparseVector, Vectors
 from .models.clustering import KMeans, KMeansModel, KMeansSummary
 from .models.feature import PCA, PCAModel
+from .models.recommendation import ALS, ALSModel
 from .parallel.world import get_world, init_world, shutdown_world
 
 __version__ = "0.1.0"
@@ -16,5 +17,5 @@ __version__ = "0.1.0"
 _loader.require_on_gpu_hosts()
 
 __all__ = ["Config", "get_config", "set_config", "DenseMatrix", "DenseVector", "Matrices",
-           "SparseVector", "Vectors", "KMeans", "KMeansModel", "KMeansSummary", "PCA", "PCAModel", "get_world",
+           "SparseVector", "Vectors", "KMeans", "KMeansModel", "KMeansSummary", "PCA", "PCAModel", "ALS", "ALSModel", "get_world",
            "init_world", "shutdown_world", "__version__"]

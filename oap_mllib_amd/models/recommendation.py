@@ -1,0 +1,361 @@
+"""ALS estimator / model with the ``org.apache.spark.ml.recommendation`` contract.
+
+Mirrors the reference's shadow ``ALS`` (mllib-dal/src/main/scala/org/apache/spark-3.1.1/ml/
+recommendation/ALS.scala): Params and defaults (:241-245, blockSize :130), integer-id checks
+(``checkedCast``, :89-113), dispatch — accelerated iff ``implicitPrefs`` (:922-926; the
+reference's oneDAL path) — otherwise the vanilla Spark algorithm, ``ALSModel.transform`` with
+``coldStartStrategy`` nan/drop (:303-334), ``recommendForAll*`` / ``recommendFor*Subset``
+(:365-505) and persistence: metadata with an extra ``rank`` field plus ``userFactors`` /
+``itemFactors`` parquet of (id: int, features: array<float>) (:522-553).
+
+The native path (csrc/drivers/als.cpp) replaces ALSDALImpl.scala + ALSShuffle.cpp +
+ALSDALImpl.cpp: id-owner alltoallv shuffle with dense re-indexing, replicated fp32 factors in
+HBM, MFMA Gramian + allreduce, per-row normal equations + Cholesky on the GPU
+(kernels/als.hip), one allgather per half-iteration.
+
+Deviation (documented): ``implicitPrefs`` with ``nonnegative=True`` takes the vanilla NNLS path
+— the reference's oneDAL path silently ignored ``nonnegative``.
+"""
+from __future__ import annotations
+
+import time
+from typing import Any
+
+import numpy as np
+
+from .. import _loader
+from ..fallback import als_vanilla as vanilla
+from ..params import Param, gt_eq, in_array, to_bool, to_float, to_int, to_str
+from ..parallel.world import get_world
+from ..persistence import spark_format as sf
+from ..utils.logging import Instrumentation
+from .base import (DefaultParamsPersistence, Estimator, MLReadable, MLWritable, Model,
+                   choose_engine, java_string_hash)
+
+_INT_MAX = 2 ** 31 - 1
+
+
+def _lower(v):
+    return to_str(v).lower()
+
+
+class _ALSModelParams:
+    userCol = Param("userCol", "column name for user ids. Ids must be within the integer value "
+                    "range.", "user", converter=to_str)
+    itemCol = Param("itemCol", "column name for item ids. Ids must be within the integer value "
+                    "range.", "item", converter=to_str)
+    predictionCol = Param("predictionCol", "prediction column name", "prediction",
+                          converter=to_str)
+    coldStartStrategy = Param("coldStartStrategy", "strategy for dealing with unknown or new "
+                              "users/items at prediction time. Supported values: nan, drop.",
+                              "nan", in_array(["nan", "drop"]), _lower)
+    blockSize = Param("blockSize", "block size for stacking input data in matrices.", 4096,
+                      gt_eq(1), to_int)
+
+
+class _ALSParams(_ALSModelParams):
+    rank = Param("rank", "rank of the factorization", 10, gt_eq(1), to_int)
+    numUserBlocks = Param("numUserBlocks", "number of user blocks", 10, gt_eq(1), to_int)
+    numItemBlocks = Param("numItemBlocks", "number of item blocks", 10, gt_eq(1), to_int)
+    implicitPrefs = Param("implicitPrefs", "whether to use implicit preference", False,
+                          converter=to_bool)
+    alpha = Param("alpha", "alpha for implicit preference", 1.0, gt_eq(0), to_float)
+    ratingCol = Param("ratingCol", "column name for ratings", "rating", converter=to_str)
+    nonnegative = Param("nonnegative", "whether to use nonnegative constraint for least squares",
+                        False, converter=to_bool)
+    maxIter = Param("maxIter", "maximum number of iterations (>= 0)", 10, gt_eq(0), to_int)
+    regParam = Param("regParam", "regularization parameter (>= 0)", 0.1, gt_eq(0), to_float)
+    checkpointInterval = Param("checkpointInterval", "set checkpoint interval (>= 1) or disable "
+                               "checkpoint (-1)", 10, lambda v: v == -1 or v >= 1, to_int)
+    seed = Param("seed", "random seed",
+                 java_string_hash("org.apache.spark.ml.recommendation.ALS"), converter=to_int)
+    intermediateStorageLevel = Param("intermediateStorageLevel", "StorageLevel for intermediate "
+                                     "datasets. Cannot be 'NONE'.", "MEMORY_AND_DISK",
+                                     lambda v: v != "NONE", to_str)
+    finalStorageLevel = Param("finalStorageLevel", "StorageLevel for ALS model factors.",
+                              "MEMORY_AND_DISK", converter=to_str)
+
+
+def _frame(dataset: Any):
+    import pandas as pd
+
+    if isinstance(dataset, pd.DataFrame):
+        return dataset
+    if isinstance(dataset, dict):
+        return pd.DataFrame({k: list(v) if not isinstance(v, np.ndarray) else v
+                             for k, v in dataset.items()})
+    try:
+        import pyarrow as pa
+
+        if isinstance(dataset, pa.Table):
+            return dataset.to_pandas()
+    except ImportError:  # pragma: no cover
+        pass
+    if isinstance(dataset, np.ndarray) and dataset.dtype.names:
+        return pd.DataFrame({n: dataset[n] for n in dataset.dtype.names})
+    raise TypeError(f"unsupported dataset type {type(dataset).__name__}")
+
+
+def checked_cast(values, name: str) -> np.ndarray:
+    """Spark's checkedCast: integral values within the Int range, else an error."""
+    v = np.asarray(values)
+    if v.dtype.kind in "iu":
+        if len(v) and (v.min() < -_INT_MAX - 1 or v.max() > _INT_MAX):
+            raise ValueError(f"ALS only supports values in Integer range for column {name}")
+        return v.astype(np.int32)
+    if v.dtype.kind == "f":
+        if len(v) and (not np.all(np.isfinite(v)) or np.any(v != np.floor(v)) or
+                       v.min() < -_INT_MAX - 1 or v.max() > _INT_MAX):
+            raise ValueError(f"ALS only supports values in Integer range and without fractional "
+                             f"part for column {name}")
+        return v.astype(np.int32)
+    raise TypeError(f"Column {name} must be of numeric type, got {v.dtype}")
+
+
+class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
+    """Alternating least squares matrix factorisation (explicit or implicit feedback)."""
+
+    _uid_prefix = "als"
+    _spark_class = "org.apache.spark.ml.recommendation.ALS"
+
+    def __init__(self, **kwargs):
+        super().__init__(kwargs.pop("uid", None))
+        if kwargs:
+            self._set(**kwargs)
+
+    def setParams(self, **kwargs) -> "ALS":  # noqa: N802
+        return self._set(**kwargs)
+
+    def setNumBlocks(self, value: int) -> "ALS":  # noqa: N802
+        return self._set(numUserBlocks=value, numItemBlocks=value)
+
+    def _ratings(self, dataset):
+        df = _frame(dataset)
+        u = checked_cast(df[self.getOrDefault("userCol")].to_numpy(), self.getOrDefault("userCol"))
+        i = checked_cast(df[self.getOrDefault("itemCol")].to_numpy(), self.getOrDefault("itemCol"))
+        rc = self.getOrDefault("ratingCol")
+        r = (np.ones(len(u), dtype=np.float32) if rc == "" else
+             np.asarray(df[rc].to_numpy(), dtype=np.float32))
+        return u, i, r
+
+    def _fit(self, dataset: Any) -> "ALSModel":
+        instr = Instrumentation(self)
+        instr.logParams(self.extractParamMap())
+        w = get_world()
+        u, i, r = self._ratings(dataset)
+        rank = self.getOrDefault("rank")
+        implicit = self.getOrDefault("implicitPrefs")
+        native_ok = implicit and not self.getOrDefault("nonnegative")
+        engine = choose_engine(native_ok, w)
+        if engine == "gpu" and rank > _loader.load().als_max_rank():
+            engine = "vanilla"
+        seed = self.getOrDefault("seed") & 0xFFFFFFFFFFFFFFFF
+        t0 = time.time()
+        extra: dict = {"engine": engine}
+        if engine == "vanilla":
+            if w.distributed:  # the fallback is single-process: gather every rank's ratings
+                parts = w.allgather_obj((u, i, r))
+                u = np.concatenate([p[0] for p in parts])
+                i = np.concatenate([p[1] for p in parts])
+                r = np.concatenate([p[2] for p in parts])
+            res = vanilla.fit(u, i, r, rank, self.getOrDefault("maxIter"),
+                              self.getOrDefault("regParam"), implicit,
+                              self.getOrDefault("alpha"), self.getOrDefault("nonnegative"), seed)
+            uid, uf, iid, itf = res.user_ids, res.user_factors, res.item_ids, res.item_factors
+        else:
+            N = _loader.load()
+            out = N.als_fit(w.ctx, w.comm, u, i, r, rank, self.getOrDefault("maxIter"),
+                            self.getOrDefault("regParam"), self.getOrDefault("alpha"), implicit,
+                            seed)
+            uid, uf = np.asarray(out["user_ids"]), np.asarray(out["user_factors"])
+            iid, itf = np.asarray(out["item_ids"]), np.asarray(out["item_factors"])
+            extra.update({k: out[k] for k in ("nnz", "setup_ms", "train_ms", "iter_ms", "gram_ms",
+                                              "solve_ms", "comm_ms", "failed_rows")})
+        model = ALSModel(uid=self.uid, rank=rank, userFactors=_factor_frame(uid, uf),
+                         itemFactors=_factor_frame(iid, itf))
+        self._copyValues(model)
+        model.setParent(self)
+        model.fit_info = {"fit_seconds": time.time() - t0, **extra}
+        instr.logNamedValue("engine", engine)
+        instr.finish()
+        return model
+
+
+def _factor_frame(ids: np.ndarray, factors: np.ndarray):
+    import pandas as pd
+
+    order = np.argsort(ids, kind="stable")
+    f = np.asarray(factors, dtype=np.float32)[order]
+    return pd.DataFrame({"id": np.asarray(ids, dtype=np.int32)[order],
+                         "features": [row for row in f]})
+
+
+class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
+    _uid_prefix = "als"
+    _spark_class = "org.apache.spark.ml.recommendation.ALSModel"
+
+    def __init__(self, uid: str | None = None, rank: int = 0, userFactors=None,
+                 itemFactors=None):  # noqa: N803
+        super().__init__(uid)
+        self.rank = int(rank)
+        self.userFactors = userFactors if userFactors is not None else _factor_frame(
+            np.zeros(0, np.int32), np.zeros((0, rank), np.float32))
+        self.itemFactors = itemFactors if itemFactors is not None else _factor_frame(
+            np.zeros(0, np.int32), np.zeros((0, rank), np.float32))
+        self.fit_info: dict = {}
+
+    # ---- factor access -----------------------------------------------------------------
+    def _mat(self, which: str) -> tuple[np.ndarray, np.ndarray]:
+        df = self.userFactors if which == "user" else self.itemFactors
+        ids = df["id"].to_numpy().astype(np.int64)
+        F = (np.stack(df["features"].to_list()).astype(np.float32) if len(df)
+             else np.zeros((0, self.rank), np.float32))
+        return ids, F
+
+    def _lookup(self, which: str, keys: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        ids, F = self._mat(which)
+        pos = np.searchsorted(ids, keys)
+        pos = np.clip(pos, 0, max(len(ids) - 1, 0))
+        found = (len(ids) > 0) & (ids[pos] == keys) if len(ids) else np.zeros(len(keys), bool)
+        return found, (F[pos] if len(ids) else np.zeros((len(keys), self.rank), np.float32))
+
+    # ---- transform ---------------------------------------------------------------------
+    def _transform(self, dataset):
+        df = _frame(dataset).copy()
+        u = np.asarray(df[self.getOrDefault("userCol")].to_numpy(), dtype=np.float64)
+        it = np.asarray(df[self.getOrDefault("itemCol")].to_numpy(), dtype=np.float64)
+        ok_u = np.isfinite(u) & (u == np.floor(u)) & (np.abs(u) <= _INT_MAX)
+        ok_i = np.isfinite(it) & (it == np.floor(it)) & (np.abs(it) <= _INT_MAX)
+        fu, Fu = self._lookup("user", np.where(ok_u, u, -1).astype(np.int64))
+        fi, Fi = self._lookup("item", np.where(ok_i, it, -1).astype(np.int64))
+        pred = np.einsum("ij,ij->i", Fu.astype(np.float32), Fi.astype(np.float32),
+                         dtype=np.float32)
+        valid = fu & fi & ok_u & ok_i
+        pred = np.where(valid, pred, np.float32(np.nan)).astype(np.float32)
+        df[self.getOrDefault("predictionCol")] = pred
+        if self.getOrDefault("coldStartStrategy") == "drop":
+            df = df[~np.isnan(pred)].reset_index(drop=True)
+        return df
+
+    def predict(self, user: int, item: int) -> float:
+        fu, Fu = self._lookup("user", np.array([user]))
+        fi, Fi = self._lookup("item", np.array([item]))
+        return float(np.dot(Fu[0], Fi[0])) if fu[0] and fi[0] else float("nan")
+
+    # ---- recommendations ---------------------------------------------------------------
+    def _topk(self, src_ids, S, dst_ids, D, num: int, dst_col: str, src_col: str):
+        import pandas as pd
+
+        num = max(0, min(int(num), len(dst_ids)))
+        recs_idx, recs_val = _blocked_topk(S, D, num)
+        recs = [[{dst_col: int(dst_ids[j]), "rating": float(v)} for j, v in zip(ri, rv)]
+                for ri, rv in zip(recs_idx, recs_val)]
+        return pd.DataFrame({src_col: np.asarray(src_ids, dtype=np.int32),
+                             "recommendations": recs})
+
+    def recommendForAllUsers(self, numItems: int):  # noqa: N802,N803
+        uids, U = self._mat("user")
+        iids, I = self._mat("item")
+        return self._topk(uids, U, iids, I, numItems, self.getOrDefault("itemCol"),
+                          self.getOrDefault("userCol"))
+
+    def recommendForAllItems(self, numUsers: int):  # noqa: N802,N803
+        uids, U = self._mat("user")
+        iids, I = self._mat("item")
+        return self._topk(iids, I, uids, U, numUsers, self.getOrDefault("userCol"),
+                          self.getOrDefault("itemCol"))
+
+    def recommendForUserSubset(self, dataset, numItems: int):  # noqa: N802,N803
+        keys = np.unique(checked_cast(_frame(dataset)[self.getOrDefault("userCol")].to_numpy(),
+                                      self.getOrDefault("userCol")).astype(np.int64))
+        found, U = self._lookup("user", keys)
+        iids, I = self._mat("item")
+        return self._topk(keys[found], U[found], iids, I, numItems, self.getOrDefault("itemCol"),
+                          self.getOrDefault("userCol"))
+
+    def recommendForItemSubset(self, dataset, numUsers: int):  # noqa: N802,N803
+        keys = np.unique(checked_cast(_frame(dataset)[self.getOrDefault("itemCol")].to_numpy(),
+                                      self.getOrDefault("itemCol")).astype(np.int64))
+        found, I = self._lookup("item", keys)
+        uids, U = self._mat("user")
+        return self._topk(keys[found], I[found], uids, U, numUsers, self.getOrDefault("userCol"),
+                          self.getOrDefault("itemCol"))
+
+    def copy(self, extra: dict | None = None) -> "ALSModel":
+        m = super().copy(extra)
+        m.userFactors = self.userFactors.copy()
+        m.itemFactors = self.itemFactors.copy()
+        return m
+
+    # ---- persistence -------------------------------------------------------------------
+    def _save_impl(self, path: str, fmt: str) -> None:
+        import os
+
+        import pyarrow as pa
+
+        sf.write_metadata(path, self._spark_class, self.uid, self._paramMap,
+                          self.defaultParamMap(), extra={"rank": self.rank})
+        schema = pa.schema([pa.field("id", pa.int32(), nullable=False),
+                            pa.field("features", pa.list_(pa.field("element", pa.float32(),
+                                                                   nullable=False)))])
+        spark = sf.spark_schema([("id", "integer", False),
+                                 ("features", {"type": "array", "elementType": "float",
+                                               "containsNull": False}, True)])
+        for name, which in (("userFactors", "user"), ("itemFactors", "item")):
+            ids, F = self._mat(which)
+            t = pa.Table.from_pydict({"id": ids.astype(np.int32),
+                                      "features": [row.tolist() for row in F]}, schema=schema)
+            sf.write_parquet(os.path.join(path, name), t, spark)
+
+    @classmethod
+    def _load_impl(cls, path: str) -> "ALSModel":
+        import os
+
+        meta = sf.read_metadata(path, cls._spark_class)
+        frames = []
+        for name in ("userFactors", "itemFactors"):
+            t = sf.read_parquet_dir(os.path.join(path, name)).to_pydict()
+            frames.append(_factor_frame(np.asarray(t["id"], dtype=np.int32),
+                                        np.asarray(t["features"], dtype=np.float32).reshape(
+                                            len(t["id"]), int(meta["rank"]))))
+        m = cls(uid=meta["uid"], rank=int(meta["rank"]), userFactors=frames[0],
+                itemFactors=frames[1])
+        for k, v in meta.get("paramMap", {}).items():
+            if m.hasParam(k):
+                m._set(**{k: v})
+        return m
+
+
+def _blocked_topk(S: np.ndarray, D: np.ndarray, num: int, block: int = 4096):
+    """Top-`num` (index, score) per row of S @ D^T, descending; ties by lower index.
+
+    On a GPU world the scoring runs through torch on the MI355X (rocBLAS GEMM + topk); otherwise
+    numpy in row blocks.
+    """
+    n = len(S)
+    idx = np.zeros((n, num), dtype=np.int64)
+    val = np.zeros((n, num), dtype=np.float32)
+    if n == 0 or num == 0:
+        return idx, val
+    w = get_world()
+    if w.is_gpu:
+        import torch
+
+        dev = torch.device("cuda", w.device)
+        Dt = torch.from_numpy(np.ascontiguousarray(D, dtype=np.float32)).to(dev)
+        for b in range(0, n, block):
+            Sb = torch.from_numpy(np.ascontiguousarray(S[b:b + block], dtype=np.float32)).to(dev)
+            sc = Sb @ Dt.T
+            v, i = torch.topk(sc, num, dim=1, largest=True, sorted=True)
+            idx[b:b + block] = i.cpu().numpy()
+            val[b:b + block] = v.cpu().numpy()
+        return idx, val
+    for b in range(0, n, block):
+        sc = S[b:b + block].astype(np.float32) @ D.astype(np.float32).T
+        part = np.argpartition(-sc, num - 1, axis=1)[:, :num] if num < sc.shape[1] else \
+            np.tile(np.arange(sc.shape[1]), (len(sc), 1))
+        pv = np.take_along_axis(sc, part, axis=1)
+        order = np.lexsort((part, -pv), axis=1)
+        idx[b:b + block] = np.take_along_axis(part, order, axis=1)
+        val[b:b + block] = np.take_along_axis(pv, order, axis=1)
+    return idx, val

@@ -90,3 +90,18 @@ def pca_native(n=3000, d=12, k=4, seed=5, device="cpu", use_rccl=True):
            "ev": m.explainedVariance.toArray().tolist()}
     O.shutdown_world()
     return out
+
+
+def als_native(seed=3, device="cpu", use_rccl=True, rank=3):
+    import oap_mllib_amd as O
+    from test_als import gen_implicit
+
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl, device_id=0))
+    tr, _ = gen_implicit(30, 50, 2, 0.01, seed)
+    mine = {k: v[w.rank::w.size] for k, v in tr.items()}  # a strided (non-range) partition
+    m = O.ALS(rank=rank, maxIter=4, regParam=0.01, implicitPrefs=True, seed=0).fit(mine)
+    out = {"engine": m.fit_info["engine"], "uid": m.userFactors["id"].tolist(),
+           "uf": np.stack(m.userFactors["features"].to_list()).tolist(),
+           "if": np.stack(m.itemFactors["features"].to_list()).tolist()}
+    O.shutdown_world()
+    return out

@@ -27,6 +27,9 @@ for st in $STEPS; do
     pcabench)
       timeout -k 10 400 python benchmarks/bench_pca.py ${PCA_ARGS:-} > gpurun_out/bench_pca_$T.json 2> gpurun_out/bench_pca_$T.err
       rc=$?; echo pcabench_rc=$rc; cat gpurun_out/bench_pca_$T.json; tail -3 gpurun_out/bench_pca_$T.err; fatal $rc pcabench;;
+    alsbench)
+      timeout -k 10 600 python benchmarks/bench_als.py ${ALS_ARGS:-} > gpurun_out/bench_als_$T.json 2> gpurun_out/bench_als_$T.err
+      rc=$?; echo alsbench_rc=$rc; cat gpurun_out/bench_als_$T.json; tail -3 gpurun_out/bench_als_$T.err; fatal $rc alsbench;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- python3 $R/bench.py --rows 20000000 --steps 5 --warmup 1 --skip-fit > $R/gpurun_out/prof_$T.log 2>&1)
       rc=$?; echo prof_rc=$rc; fatal $rc prof;;
