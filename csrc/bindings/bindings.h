@@ -11,3 +11,4 @@ namespace py_bind {
 
 void register_pca(pybind11::module_& m);
 void register_als(pybind11::module_& m);
+void register_io(pybind11::module_& m);

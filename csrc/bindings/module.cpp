@@ -454,4 +454,5 @@ PYBIND11_MODULE(_native, m) {
 
   register_pca(m);
   register_als(m);
+  register_io(m);
 }

@@ -1,6 +1,8 @@
 #include "drivers/als.h"
 
 #include <algorithm>
+#include <atomic>
+#include <climits>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -106,25 +108,129 @@ struct Csr {
   std::vector<float> val;
 };
 
-// rows are a - row_base (must lie in [0, nrows)); sorted by (row, col), stable on input order
-Csr build_csr(std::vector<Rec>& recs, int64_t nrows, int64_t row_base) {
-  std::stable_sort(recs.begin(), recs.end(), [](const Rec& x, const Rec& y) {
-    return x.a != y.a ? x.a < y.a : x.b < y.b;
-  });
+// CSR by counting sort (rows are a - row_base, dense in [0, nrows)): atomic row histogram,
+// prefix sum, atomic scatter, then every row sorted by (col, value) — so the result does not
+// depend on the scatter order or the thread count.  O(nnz) + per-row sorts, all on the pool.
+Csr build_csr(ThreadPool& pool, std::vector<Rec>& recs, int64_t nrows, int64_t row_base) {
+  const int64_t nnz = int64_t(recs.size());
   Csr c;
+  std::vector<std::atomic<int64_t>> cnt(nrows + 1);
+  pool.parallel_for(nrows + 1, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) cnt[i].store(0, std::memory_order_relaxed);
+  });
+  std::atomic<bool> bad{false};
+  pool.parallel_for(nnz, [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const int64_t row = int64_t(recs[k].a) - row_base;
+      if (row < 0 || row >= nrows) {
+        bad = true;
+        continue;
+      }
+      cnt[row + 1].fetch_add(1, std::memory_order_relaxed);
+    }
+  });
+  OAP_CHECK(!bad, "ALS CSR: row out of range");
   c.ptr.assign(nrows + 1, 0);
-  c.col.resize(recs.size());
-  c.val.resize(recs.size());
-  for (size_t k = 0; k < recs.size(); ++k) {
-    const int64_t row = int64_t(recs[k].a) - row_base;
-    OAP_CHECK(row >= 0 && row < nrows, "ALS CSR: row out of range");
-    c.ptr[row + 1]++;
-    c.col[k] = recs[k].b;
-    c.val[k] = recs[k].r;
-  }
-  for (int64_t i = 0; i < nrows; ++i) c.ptr[i + 1] += c.ptr[i];
+  for (int64_t i = 0; i < nrows; ++i) c.ptr[i + 1] = c.ptr[i] + cnt[i + 1].load();
+  pool.parallel_for(nrows, [&](int, int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) cnt[i].store(c.ptr[i], std::memory_order_relaxed);
+  });
+  c.col.resize(nnz);
+  c.val.resize(nnz);
+  pool.parallel_for(nnz, [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const int64_t pos = cnt[int64_t(recs[k].a) - row_base].fetch_add(1, std::memory_order_relaxed);
+      c.col[pos] = recs[k].b;
+      c.val[pos] = recs[k].r;
+    }
+  });
+  pool.parallel_for(nrows, [&](int, int64_t b, int64_t e) {
+    std::vector<std::pair<int32_t, float>> tmp;
+    for (int64_t i = b; i < e; ++i) {
+      const int64_t p0 = c.ptr[i], p1 = c.ptr[i + 1];
+      if (p1 - p0 < 2) continue;
+      tmp.resize(p1 - p0);
+      for (int64_t q = p0; q < p1; ++q) tmp[q - p0] = {c.col[q], c.val[q]};
+      std::sort(tmp.begin(), tmp.end());
+      for (int64_t q = p0; q < p1; ++q) {
+        c.col[q] = tmp[q - p0].first;
+        c.val[q] = tmp[q - p0].second;
+      }
+    }
+  });
   return c;
 }
+
+// Sorted distinct ids with O(1) id -> rank lookup: a bitmap over [min, max] with per-word
+// popcount prefixes when the id range is moderate (the common case), else sort + binary search.
+struct IdIndex {
+  std::vector<int32_t> ids;  // sorted distinct
+  int64_t lo = 0;
+  std::vector<uint64_t> bits;
+  std::vector<int64_t> prefix;  // rank of the first id in each word
+  bool bitmap = false;
+
+  void build(ThreadPool& pool, const std::vector<Rec>& recs, bool use_a) {
+    const int64_t n = int64_t(recs.size());
+    ids.clear();
+    if (n == 0) return;
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (int64_t k = 0; k < n; ++k) {
+      const int64_t v = use_a ? recs[k].a : recs[k].b;
+      mn = std::min(mn, v);
+      mx = std::max(mx, v);
+    }
+    lo = mn;
+    const int64_t range = mx - mn + 1;
+    if (range <= (int64_t(1) << 31) && range <= 64 * n + (1 << 20)) {
+      bitmap = true;
+      const int64_t nw = (range + 63) / 64;
+      std::vector<std::atomic<uint64_t>> w(nw);
+      pool.parallel_for(nw, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) w[i].store(0, std::memory_order_relaxed);
+      });
+      pool.parallel_for(n, [&](int, int64_t b, int64_t e) {
+        for (int64_t k = b; k < e; ++k) {
+          const int64_t v = (use_a ? recs[k].a : recs[k].b) - lo;
+          w[v >> 6].fetch_or(uint64_t(1) << (v & 63), std::memory_order_relaxed);
+        }
+      });
+      bits.resize(nw);
+      prefix.resize(nw + 1);
+      prefix[0] = 0;
+      for (int64_t i = 0; i < nw; ++i) {
+        bits[i] = w[i].load();
+        prefix[i + 1] = prefix[i] + __builtin_popcountll(bits[i]);
+      }
+      ids.resize(prefix[nw]);
+      pool.parallel_for(nw, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) {
+          uint64_t x = bits[i];
+          int64_t o = prefix[i];
+          while (x) {
+            const int t = __builtin_ctzll(x);
+            ids[o++] = int32_t(lo + i * 64 + t);
+            x &= x - 1;
+          }
+        }
+      });
+    } else {
+      ids.resize(n);
+      for (int64_t k = 0; k < n; ++k) ids[k] = use_a ? recs[k].a : recs[k].b;
+      std::sort(ids.begin(), ids.end());
+      ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    }
+  }
+  int64_t rank(int32_t id) const {
+    if (bitmap) {
+      const int64_t v = int64_t(id) - lo;
+      const uint64_t word = bits[v >> 6];
+      const uint64_t below = (v & 63) ? (word & ((uint64_t(1) << (v & 63)) - 1)) : 0;
+      return prefix[v >> 6] + __builtin_popcountll(below);
+    }
+    return std::lower_bound(ids.begin(), ids.end(), id) - ids.begin();
+  }
+};
 
 struct Side {  // one factor matrix and the CSR of this rank's owned rows of it
   int64_t n = 0;                 // global rows
@@ -187,45 +293,55 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   // ---- 1. ratings -> item owners; dense item indices --------------------------------------
   Side U, I;
   std::vector<Rec> recv1;
-  {
+  if (P == 1) {
+    recv1.resize(n);
+    ctx.pool().parallel_for(n, [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) recv1[k] = {users[k], items[k], ratings[k]};
+    });
+  } else {
     std::vector<std::vector<Rec>> out(P);
     for (int64_t k = 0; k < n; ++k) out[owner_of(items[k], P)].push_back({users[k], items[k], ratings[k]});
     recv1 = exchange(ctx, comm, out);
   }
-  std::vector<int32_t> my_items;
-  for (const Rec& x : recv1) my_items.push_back(x.b);
-  std::sort(my_items.begin(), my_items.end());
-  my_items.erase(std::unique(my_items.begin(), my_items.end()), my_items.end());
+  IdIndex item_idx;
+  item_idx.build(ctx.pool(), recv1, false);
+  const std::vector<int32_t>& my_items = item_idx.ids;
   I.cnt = allgather_i64(ctx, comm, {int64_t(my_items.size())});
   I.off.assign(P + 1, 0);
   for (int q = 0; q < P; ++q) I.off[q + 1] = I.off[q] + I.cnt[q];
   I.n = I.off[P];
-  auto item_gidx = [&](int32_t id) {
-    return int32_t(I.off[me] + (std::lower_bound(my_items.begin(), my_items.end(), id) -
-                                my_items.begin()));
-  };
   // ---- 2. -> user owners; dense user indices, user CSR (cols = global item index) ---------
   std::vector<Rec> recv2;
-  {
+  if (P == 1) {
+    ctx.pool().parallel_for(int64_t(recv1.size()), [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) recv1[k].b = int32_t(item_idx.rank(recv1[k].b));
+    });
+    recv2.swap(recv1);
+  } else {
     std::vector<std::vector<Rec>> out(P);
-    for (const Rec& x : recv1) out[owner_of(x.a, P)].push_back({x.a, item_gidx(x.b), x.r});
+    for (const Rec& x : recv1)
+      out[owner_of(x.a, P)].push_back({x.a, int32_t(I.off[me] + item_idx.rank(x.b)), x.r});
     std::vector<Rec>().swap(recv1);
     recv2 = exchange(ctx, comm, out);
   }
-  std::vector<int32_t> my_users;
-  for (const Rec& x : recv2) my_users.push_back(x.a);
-  std::sort(my_users.begin(), my_users.end());
-  my_users.erase(std::unique(my_users.begin(), my_users.end()), my_users.end());
+  IdIndex user_idx;
+  user_idx.build(ctx.pool(), recv2, true);
+  const std::vector<int32_t>& my_users = user_idx.ids;
   U.cnt = allgather_i64(ctx, comm, {int64_t(my_users.size())});
   U.off.assign(P + 1, 0);
   for (int q = 0; q < P; ++q) U.off[q + 1] = U.off[q] + U.cnt[q];
   U.n = U.off[P];
-  for (Rec& x : recv2)
-    x.a = int32_t(U.off[me] + (std::lower_bound(my_users.begin(), my_users.end(), x.a) -
-                               my_users.begin()));
+  ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) recv2[k].a = int32_t(U.off[me] + user_idx.rank(recv2[k].a));
+  });
   // ---- 3. (global user, global item) -> item owners: item CSR (cols = global user index) --
   std::vector<Rec> recv3;
-  {
+  if (P == 1) {
+    recv3.resize(recv2.size());
+    ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) recv3[k] = {recv2[k].b, recv2[k].a, recv2[k].r};
+    });
+  } else {
     std::vector<std::vector<Rec>> out(P);
     for (const Rec& x : recv2) {
       const int q = int(std::upper_bound(I.off.begin(), I.off.end(), int64_t(x.b)) - I.off.begin()) - 1;
@@ -233,8 +349,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     }
     recv3 = exchange(ctx, comm, out);
   }
-  U.csr = build_csr(recv2, U.cnt[me], U.off[me]);
-  I.csr = build_csr(recv3, I.cnt[me], I.off[me]);
+  U.csr = build_csr(ctx.pool(), recv2, U.cnt[me], U.off[me]);
+  I.csr = build_csr(ctx.pool(), recv3, I.cnt[me], I.off[me]);
   std::vector<Rec>().swap(recv2);
   std::vector<Rec>().swap(recv3);
   U.ids = allgatherv_i32(ctx, comm, my_users, U.cnt);
@@ -256,7 +372,11 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     const int cus = ctx.info().cu_count;
     struct Dev {
       Buffer f, ptr, col, val;
+      Buffer short_rows, long_rows, long_chunk_ptr, chunk_begin, chunk_end, partials;
+      int64_t n_short = 0, n_long = 0, n_chunks = 0;
     } dU, dI;
+    // rows longer than kLong ratings are split into kLong-sized chunks (partial Gramians)
+    constexpr int64_t kLong = 4096;
     auto upload_side = [&](Side& S, Dev& D) {
       D.f = ctx.alloc(std::max<size_t>(size_t(S.n) * ld * 4, 256));
       D.ptr = ctx.alloc(S.csr.ptr.size() * 8);
@@ -268,6 +388,42 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         ctx.copy_to_backend(D.val.data(), S.csr.val.data(), S.csr.val.size() * 4, s);
       }
       ctx.memset(D.f.data(), 0, size_t(S.n) * ld * 4);
+      std::vector<int32_t> sr, lr;
+      std::vector<int64_t> lcp{0}, cb, ce;
+      const int64_t nloc = int64_t(S.csr.ptr.size()) - 1;
+      // longest rows first: they start early and the short ones fill in behind them
+      std::vector<std::pair<int64_t, int32_t>> order;
+      order.reserve(nloc);
+      for (int64_t i = 0; i < nloc; ++i)
+        order.push_back({S.csr.ptr[i + 1] - S.csr.ptr[i], int32_t(i)});
+      std::stable_sort(order.begin(), order.end(),
+                       [](const auto& x, const auto& y) { return x.first > y.first; });
+      for (const auto& [len, i] : order) {
+        if (len > kLong) {
+          lr.push_back(i);
+          for (int64_t p0 = S.csr.ptr[i]; p0 < S.csr.ptr[i + 1]; p0 += kLong) {
+            cb.push_back(p0);
+            ce.push_back(std::min(p0 + kLong, S.csr.ptr[i + 1]));
+          }
+          lcp.push_back(int64_t(cb.size()));
+        } else {
+          sr.push_back(i);
+        }
+      }
+      auto up = [&](Buffer& b, const void* h, size_t bytes) {
+        b = ctx.alloc(std::max<size_t>(bytes, 16));
+        if (bytes) ctx.copy_to_backend(b.data(), h, bytes, s);
+      };
+      up(D.short_rows, sr.data(), sr.size() * 4);
+      up(D.long_rows, lr.data(), lr.size() * 4);
+      up(D.long_chunk_ptr, lcp.data(), lcp.size() * 8);
+      up(D.chunk_begin, cb.data(), cb.size() * 8);
+      up(D.chunk_end, ce.data(), ce.size() * 8);
+      D.n_short = int64_t(sr.size());
+      D.n_long = int64_t(lr.size());
+      D.n_chunks = int64_t(cb.size());
+      D.partials = ctx.alloc(std::max<size_t>(size_t(D.n_chunks) * kern::als_partial_floats(r) * 4, 16));
+      OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
     upload_side(U, dU);
     upload_side(I, dI);
@@ -277,8 +433,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       kern::als_init_factors(ids.as<int32_t>(), U.n, r, ld, p.seed, dU.f.as<float>(), s);
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     }
-    Buffer ctr = ctx.alloc(16);
-    ctx.memset(ctr.data(), 0, 16);
+    Buffer ctr = ctx.alloc(32);
+    ctx.memset(ctr.data(), 0, 32);
     Buffer gram64 = ctx.alloc((size_t(r) * r + r) * 8), gram32 = ctx.alloc(size_t(r) * r * 4);
     Buffer zshift = ctx.alloc(size_t(ld + 128) * 4);
     ctx.memset(zshift.data(), 0, size_t(ld + 128) * 4);
@@ -314,7 +470,15 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       a.rowptr = dD.ptr.as<int64_t>();
       a.cols = dD.col.as<int32_t>();
       a.vals = dD.val.as<float>();
-      a.nrows = Dst.cnt[me];
+      a.short_rows = dD.short_rows.as<int32_t>();
+      a.n_short = dD.n_short;
+      a.long_rows = dD.long_rows.as<int32_t>();
+      a.n_long = dD.n_long;
+      a.long_chunk_ptr = dD.long_chunk_ptr.as<int64_t>();
+      a.chunk_begin = dD.chunk_begin.as<int64_t>();
+      a.chunk_end = dD.chunk_end.as<int64_t>();
+      a.n_chunks = dD.n_chunks;
+      a.partials = dD.partials.as<float>();
       a.src = dS.f.as<float>();
       a.ld = ld;
       a.r = r;
@@ -324,7 +488,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       a.implicit = p.implicit;
       a.dst = P == 1 ? dD.f.as<float>() : stage.as<float>();
       a.queue = ctr.as<unsigned long long>();
-      a.fail = ctr.as<unsigned long long>() + 1;
+      a.fail = ctr.as<unsigned long long>() + 2;
       kern::als_solve(a, cus, s);
       e2.record(s);
       if (P > 1) {
@@ -357,7 +521,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       maybe_inject_fault(me, "als_iter", it);
     }
     unsigned long long fails = 0;
-    ctx.copy_to_host(&fails, ctr.as<unsigned long long>() + 1, 8);
+    ctx.copy_to_host(&fails, ctr.as<unsigned long long>() + 2, 8);
     res.failed_rows = int64_t(comm_allreduce_scalar(ctx, comm, double(fails), ReduceOp::Sum));
     Xh.resize(size_t(U.n) * ld);
     Yh.resize(size_t(I.n) * ld);

@@ -1,4 +1,4 @@
-// Implicit-feedback ALS: per-row normal equations + Cholesky solve, one wave per row.
+// Implicit-feedback ALS: per-row normal equations + blocked Cholesky solve, one wave per row.
 //
 // The numerical spec is Spark's computeFactors (mllib-dal/src/main/scala/org/apache/spark-3.1.1/
 // ml/recommendation/ALS.scala:1718-1800): for destination row u with ratings (i, r_ui)
@@ -7,12 +7,17 @@
 // solved by Cholesky (CholeskySolver, :757-788).  It replaces the reference's oneDAL
 // implicit_als step4Local (native/ALSDALImpl.cpp:301-316).
 //
-// MI355X mapping: a 64-thread workgroup takes rows from an atomic work queue (power-law row
-// lengths balance dynamically).  The rating-weighted Gramian sum_i c1 y_i y_i^T is a small SYRK
-// over the row's gathered factors and runs on v_mfma_f32_16x16x4_f32 (exact fp32 products) with
-// the lower-triangle 16x16 tiles resident in accumulator registers; b and n_u ride along on the
-// VALU.  The assembled matrix goes to LDS (packed lower triangle) for a wave-parallel
-// right-looking Cholesky and the two triangular solves.
+// MI355X mapping (one 64-thread workgroup = one wave per row, rows from an atomic work queue):
+//  * Gramian: sum_i c1 y_i y_i^T is a small SYRK over the row's gathered factors on
+//    v_mfma_f32_16x16x4_f32 (exact fp32 products), lower 16x16 tiles resident in accumulator
+//    registers; b and n_u ride along on the VALU.  Rows longer than `long_len` ratings are split
+//    into chunks whose partial (tiles, b, n_u) go to a scratch slab (oap_als_partial) and are
+//    summed in chunk order by the solve kernel — power-law rows neither serialise on one wave
+//    nor lose determinism.
+//  * Solve: the assembled matrix goes to LDS (row stride RP+4: conflict-free MFMA fragment
+//    reads) and is factored by a right-looking blocked Cholesky with 16-wide panels: the
+//    diagonal block in registers (lane-per-row, cross-lane broadcasts), the panel TRSM
+//    lane-per-row against broadcast LDS rows, and the trailing SYRK update on MFMA.
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
@@ -23,40 +28,124 @@ namespace kern {
 namespace {
 
 constexpr int kAlsThreads = 64;
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 struct SolveArgs {
   const int64_t* rowptr;
   const int32_t* cols;
   const float* vals;
-  int64_t nrows;
-  const float* src;  // [n_src][ld]
+  const int32_t* rows;       // row list for this launch
+  int64_t nrows;             // entries of `rows`
+  const int64_t* chunk_ptr;  // long-row mode: chunks [chunk_ptr[q], chunk_ptr[q+1]) of rows[q]
+  const float* partials;     // long-row mode: per chunk partial_floats<NB>() floats
+  const float* src;          // [n_src][ld]
   int ld, r;
-  const float* yty;  // [r][r] (implicit) or null
+  const float* yty;          // [r][r] (implicit) or null
   float alpha, lambda;
   int implicit;
-  float* dst;        // [nrows][ld]
-  unsigned long long* queue;  // work counter (zeroed before launch)
-  unsigned long long* fail;   // rows whose matrix was not positive definite
+  float* dst;                // [*][ld], indexed by row id
+  unsigned long long* queue;
+  unsigned long long* fail;
 };
 
-__device__ inline int tri(int i) { return i * (i + 1) / 2; }
+struct PartialArgs {
+  const int32_t* cols;
+  const float* vals;
+  const int64_t* chunk_begin;  // rating range of each chunk
+  const int64_t* chunk_end;
+  int64_t nchunks;
+  const float* src;
+  int ld;
+  float alpha;
+  int implicit;
+  float* partials;
+};
 
 template <int NB>
-__global__ __launch_bounds__(kAlsThreads) void oap_als_solve(SolveArgs a) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int partial_floats() {
+  return (NB * (NB + 1) / 2) * 256 + 64 * NB + 64;
+}
+
+// Gramian + b + n_u of ratings [p0, p1) of one row (lane layout of the 16x16x4 f32 MFMA).
+template <int NB>
+__device__ inline void accumulate(const int32_t* __restrict__ cols, const float* __restrict__ vals,
+                                  int64_t p0, int64_t p1, const float* __restrict__ src, int ld,
+                                  float alpha, bool implicit, f4 (&acc)[NB * (NB + 1) / 2],
+                                  float (&bacc)[NB], int& nexp) {
+  const int lane = threadIdx.x, kk = lane >> 4, c = lane & 15;
+  for (int64_t p = p0; p < p1; p += 4) {
+    const int64_t idx = p + kk;
+    const bool ok = idx < p1;
+    const int item = ok ? cols[idx] : 0;
+    const float rv = ok ? vals[idx] : 0.f;
+    float wa, wb;
+    if (implicit) {
+      const float c1 = alpha * fabsf(rv);
+      wa = c1;
+      wb = rv > 0.f ? 1.f + c1 : 0.f;
+      nexp += (ok && rv > 0.f && c == 0) ? 1 : 0;
+    } else {  // explicit: A += y y^T, b += r y
+      wa = ok ? 1.f : 0.f;
+      wb = rv;
+      nexp += (ok && c == 0) ? 1 : 0;
+    }
+    const float* yrow = src + static_cast<int64_t>(item) * ld + c;
+    float yv[NB], av[NB];
+#pragma unroll
+    for (int f = 0; f < NB; ++f) {
+      yv[f] = ok ? yrow[16 * f] : 0.f;
+      av[f] = wa * yv[f];
+      bacc[f] = fmaf(wb, yv[f], bacc[f]);
+    }
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = 0; bj <= bi; ++bj, ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bi], yv[bj], acc[t], 0, 0, 0);
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(kAlsThreads) void oap_als_partial(PartialArgs a) {
   constexpr int NT = NB * (NB + 1) / 2;
+  const int lane = threadIdx.x;
+  for (int64_t q = blockIdx.x; q < a.nchunks; q += gridDim.x) {
+    f4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    float bacc[NB];
+#pragma unroll
+    for (int f = 0; f < NB; ++f) bacc[f] = 0.f;
+    int nexp = 0;
+    accumulate<NB>(a.cols, a.vals, a.chunk_begin[q], a.chunk_end[q], a.src, a.ld, a.alpha,
+                   a.implicit != 0, acc, bacc, nexp);
+    float* out = a.partials + q * partial_floats<NB>();
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[t * 256 + e * 64 + lane] = acc[t][e];
+#pragma unroll
+    for (int f = 0; f < NB; ++f) out[NT * 256 + f * 64 + lane] = bacc[f];
+    out[NT * 256 + NB * 64 + lane] = static_cast<float>(nexp);
+  }
+}
+
+template <int NB, bool LONG>
+__global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
+  constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int RP = 16 * NB, S = RP + 4;
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* M = lds;            // RP x S, lower triangle used
+  float* bv = lds + RP * S;  // RP
   const int r = a.r, lane = threadIdx.x;
-  float* L = lds;                   // packed lower triangle, r(r+1)/2
-  float* bv = lds + tri(r - 1) + r; // r
-  const int kk = lane >> 4, c = lane & 15;
 
   while (true) {
-    unsigned long long row_u = 0;
-    if (lane == 0) row_u = atomicAdd(a.queue, 1ull);
-    const int64_t row = static_cast<int64_t>(__shfl(row_u, 0, 64));
-    if (row >= a.nrows) break;
-    const int64_t p0 = a.rowptr[row], p1 = a.rowptr[row + 1];
+    unsigned long long q_u = 0;
+    if (lane == 0) q_u = atomicAdd(a.queue, 1ull);
+    const int64_t q = static_cast<int64_t>(__shfl(q_u, 0, 64));
+    if (q >= a.nrows) break;
+    const int64_t row = a.rows[q];
 
     f4 acc[NT];
 #pragma unroll
@@ -65,38 +154,22 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_solve(SolveArgs a) {
 #pragma unroll
     for (int f = 0; f < NB; ++f) bacc[f] = 0.f;
     int nexp = 0;
-    for (int64_t p = p0; p < p1; p += 4) {
-      const int64_t idx = p + kk;
-      const bool ok = idx < p1;
-      const int item = ok ? a.cols[idx] : 0;
-      const float rv = ok ? a.vals[idx] : 0.f;
-      float wa, wb;
-      if (a.implicit) {
-        const float c1 = a.alpha * fabsf(rv);
-        wa = c1;
-        wb = rv > 0.f ? 1.f + c1 : 0.f;
-        nexp += (ok && rv > 0.f && c == 0) ? 1 : 0;
-      } else {  // explicit: A += y y^T, b += r y
-        wa = ok ? 1.f : 0.f;
-        wb = rv;
-        nexp += (ok && c == 0) ? 1 : 0;
+    if constexpr (LONG) {
+      // sum the row's chunk partials in chunk order (deterministic)
+      for (int64_t ch = a.chunk_ptr[q]; ch < a.chunk_ptr[q + 1]; ++ch) {
+        const float* pp = a.partials + ch * partial_floats<NB>();
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[t][e] += pp[t * 256 + e * 64 + lane];
+#pragma unroll
+        for (int f = 0; f < NB; ++f) bacc[f] += pp[NT * 256 + f * 64 + lane];
+        nexp += static_cast<int>(pp[NT * 256 + NB * 64 + lane]);
       }
-      const float* yrow = a.src + static_cast<int64_t>(item) * a.ld + c;
-      float yv[NB], av[NB];
-#pragma unroll
-      for (int f = 0; f < NB; ++f) {
-        yv[f] = ok ? yrow[16 * f] : 0.f;
-        av[f] = wa * yv[f];
-        bacc[f] = fmaf(wb, yv[f], bacc[f]);
-      }
-      int t = 0;
-#pragma unroll
-      for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-        for (int bj = 0; bj <= bi; ++bj, ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bi], yv[bj], acc[t], 0, 0, 0);
+    } else {
+      accumulate<NB>(a.cols, a.vals, a.rowptr[row], a.rowptr[row + 1], a.src, a.ld, a.alpha,
+                     a.implicit != 0, acc, bacc, nexp);
     }
-    // reduce b over the 4 rating groups; n_u over the wave
 #pragma unroll
     for (int f = 0; f < NB; ++f) {
       bacc[f] += __shfl_xor(bacc[f], 16, 64);
@@ -105,11 +178,9 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_solve(SolveArgs a) {
     for (int m = 32; m >= 1; m >>= 1) nexp += __shfl_xor(nexp, m, 64);
     const float lam = a.lambda * static_cast<float>(nexp);
 
-    // assemble A (lower) = Gram + YtY + lam I into LDS; tile element (i = 16bi + 4kk + e,
-    // j = 16bj + c).  The lane coordinates are laundered so the per-element addresses are not
-    // hoisted out of the row loop as hundreds of live registers.
+    // ---- assemble A = Gram + YtY + lam I (padding rows/cols -> identity) into LDS
     {
-      int lid = lane;
+      int lid = lane;  // laundered: keeps per-element addresses from being hoisted
       asm volatile("" : "+v"(lid));
       const int kk = lid >> 4, c = lid & 15;
       int t = 0;
@@ -120,44 +191,119 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_solve(SolveArgs a) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = 16 * bi + 4 * kk + e, j = 16 * bj + c;
-            if (i < r && j <= i) {
-              float v = acc[t][e];
+            float v;
+            if (i < r && j < r) {
+              v = acc[t][e];
               if (a.yty) v += a.yty[i * r + j];
               if (i == j) v += lam;
-              L[tri(i) + j] = v;
+            } else {
+              v = (i == j) ? 1.f : 0.f;
             }
+            M[i * S + j] = v;
           }
-    }
-    if (kk == 0) {
+      if (kk == 0) {
 #pragma unroll
-      for (int f = 0; f < NB; ++f)
-        if (16 * f + c < r) bv[16 * f + c] = bacc[f];
+        for (int f = 0; f < NB; ++f) bv[16 * f + c] = (16 * f + c < r) ? bacc[f] : 0.f;
+      }
     }
     __syncthreads();
 
-    // right-looking Cholesky on the packed lower triangle
+    // ---- blocked right-looking Cholesky, 16-wide panels
     bool spd = true;
-    for (int j = 0; j < r; ++j) {
-      const float djj = L[tri(j) + j];
-      if (!(djj > 0.f)) {
+    for (int jb = 0; jb < NB; ++jb) {
+      const int o = 16 * jb;
+      // (1) diagonal block: lanes 0..15 own its rows, in registers
+      float t[16];
+      {
+        const int rl = lane & 15;
+#pragma unroll
+        for (int m = 0; m < 16; m += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(&M[(o + rl) * S + o + m]);
+          t[m] = v.x;
+          t[m + 1] = v.y;
+          t[m + 2] = v.z;
+          t[m + 3] = v.w;
+        }
+      }
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float piv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), j));
+        ok = ok && (piv > 0.f);
+        const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = 1.f / dj;
+        t[j] = (lane > j) ? t[j] * inv : (lane == j ? dj : t[j]);
+        const float lij = (lane > j) ? t[j] : 0.f;
+#pragma unroll
+        for (int k = j + 1; k < 16; ++k) {
+          const float lkj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), k));
+          t[k] = fmaf(-lij, lkj, t[k]);
+        }
+      }
+      if (!ok) {
         spd = false;
         break;
       }
-      const float d = sqrtf(djj), inv = 1.f / d;
+      if (lane < 16) {
+#pragma unroll
+        for (int m = 0; m < 16; m += 4)
+          *reinterpret_cast<float4*>(&M[(o + lane) * S + o + m]) =
+              make_float4(t[m], t[m + 1], t[m + 2], t[m + 3]);
+      }
       __syncthreads();
-      for (int i = j + 1 + lane; i < r; i += 64) L[tri(i) + j] *= inv;
-      if (lane == 0) L[tri(j) + j] = d;
+      if (jb + 1 == NB) break;
+      // (2) panel TRSM: rows below solve x L_jj^T = a, lane-per-row, L_jj rows broadcast
+      for (int i = o + 16 + lane; i < RP; i += 64) {
+        float x[16];
+#pragma unroll
+        for (int m = 0; m < 16; m += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(&M[i * S + o + m]);
+          x[m] = v.x;
+          x[m + 1] = v.y;
+          x[m + 2] = v.z;
+          x[m + 3] = v.w;
+        }
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) {
+          float lrow[16];
+#pragma unroll
+          for (int m = 0; m < 16; m += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(&M[(o + cc) * S + o + m]);
+            lrow[m] = v.x;
+            lrow[m + 1] = v.y;
+            lrow[m + 2] = v.z;
+            lrow[m + 3] = v.w;
+          }
+          float s = x[cc];
+#pragma unroll
+          for (int m = 0; m < cc; ++m) s = fmaf(-x[m], lrow[m], s);
+          x[cc] = s / lrow[cc];
+        }
+#pragma unroll
+        for (int m = 0; m < 16; m += 4)
+          *reinterpret_cast<float4*>(&M[i * S + o + m]) =
+              make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
+      }
       __syncthreads();
-      const int m = r - j - 1;
-      const int cnt = tri(m - 1) + m;  // m(m+1)/2 trailing elements
-      for (int t = lane; t < cnt; t += 64) {
-        const int ii = static_cast<int>((sqrtf(8.f * t + 1.f) - 1.f) * 0.5f);
-        int i2 = ii;
-        if (tri(i2) > t) --i2;
-        if (tri(i2 + 1) <= t) ++i2;
-        const int k2 = t - tri(i2);
-        const int i = j + 1 + i2, k = j + 1 + k2;
-        L[tri(i) + k] -= L[tri(i) + j] * L[tri(k) + j];
+      // (3) trailing update T[ib][kb] -= P_ib P_kb^T on MFMA (fragments straight from LDS)
+      {
+        const int kk = lane >> 4, c = lane & 15;
+        for (int ib = jb + 1; ib < NB; ++ib) {
+          float pa[4];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[(16 * ib + c) * S + o + 4 * s4 + kk];
+          for (int kb = jb + 1; kb <= ib; ++kb) {
+            f4 cacc;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cacc[e] = M[(16 * ib + 4 * kk + e) * S + 16 * kb + c];
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+              const float pb = M[(16 * kb + c) * S + o + 4 * s4 + kk];
+              cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s4], pb, cacc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) M[(16 * ib + 4 * kk + e) * S + 16 * kb + c] = cacc[e];
+          }
+        }
       }
       __syncthreads();
     }
@@ -168,19 +314,19 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_solve(SolveArgs a) {
       __syncthreads();
       continue;
     }
-    // forward L z = b, backward L^T x = z (in place in bv)
+    // ---- forward L z = b, backward L^T x = z (in place in bv)
     for (int j = 0; j < r; ++j) {
-      const float z = bv[j] / L[tri(j) + j];
+      const float z = bv[j] / M[j * S + j];
       __syncthreads();
       if (lane == 0) bv[j] = z;
-      for (int i = j + 1 + lane; i < r; i += 64) bv[i] -= L[tri(i) + j] * z;
+      for (int i = j + 1 + lane; i < r; i += 64) bv[i] = fmaf(-M[i * S + j], z, bv[i]);
       __syncthreads();
     }
     for (int j = r - 1; j >= 0; --j) {
-      const float x = bv[j] / L[tri(j) + j];
+      const float x = bv[j] / M[j * S + j];
       __syncthreads();
       if (lane == 0) bv[j] = x;
-      for (int i = lane; i < j; i += 64) bv[i] -= L[tri(j) + i] * x;
+      for (int i = lane; i < j; i += 64) bv[i] = fmaf(-M[j * S + i], x, bv[i]);
       __syncthreads();
     }
     for (int i = lane; i < a.ld; i += 64) out[i] = i < r ? bv[i] : 0.f;
@@ -189,16 +335,71 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_solve(SolveArgs a) {
 }
 
 template <int NB>
+size_t solve_lds() {
+  return (size_t(16 * NB) * (16 * NB + 4) + 16 * NB) * sizeof(float);
+}
+
+template <int NB, bool LONG>
 void launch_solve(const SolveArgs& a, int grid, hipStream_t s) {
-  const size_t lds = (size_t(a.r) * (a.r + 1) / 2 + size_t(a.r)) * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_als_solve<NB>),
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_als_solve<NB, LONG>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL(oap_als_solve<NB>, dim3(grid), dim3(kAlsThreads), lds, s, a);
+  hipLaunchKernelGGL((oap_als_solve<NB, LONG>), dim3(grid), dim3(kAlsThreads), solve_lds<NB>(),
+                     s, a);
   OAP_HIP_CHECK(hipGetLastError());
+}
+
+template <int NB>
+void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
+  const size_t lds = solve_lds<NB>();
+  const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 512))));
+  SolveArgs a{};
+  a.rowptr = s.rowptr;
+  a.cols = s.cols;
+  a.vals = s.vals;
+  a.src = s.src;
+  a.ld = s.ld;
+  a.r = s.r;
+  a.yty = s.yty;
+  a.alpha = s.alpha;
+  a.lambda = s.lambda;
+  a.implicit = s.implicit ? 1 : 0;
+  a.dst = s.dst;
+  a.fail = s.fail;
+  if (s.n_short > 0) {
+    OAP_HIP_CHECK(hipMemsetAsync(s.queue, 0, sizeof(unsigned long long), st));
+    a.rows = s.short_rows;
+    a.nrows = s.n_short;
+    a.queue = s.queue;
+    launch_solve<NB, false>(a, int(std::min<int64_t>(s.n_short, int64_t(num_cus) * per_cu)), st);
+  }
+  if (s.n_long > 0) {
+    PartialArgs pa{};
+    pa.cols = s.cols;
+    pa.vals = s.vals;
+    pa.chunk_begin = s.chunk_begin;
+    pa.chunk_end = s.chunk_end;
+    pa.nchunks = s.n_chunks;
+    pa.src = s.src;
+    pa.ld = s.ld;
+    pa.alpha = s.alpha;
+    pa.implicit = s.implicit ? 1 : 0;
+    pa.partials = s.partials;
+    hipLaunchKernelGGL(oap_als_partial<NB>,
+                       dim3(int(std::min<int64_t>(s.n_chunks, int64_t(num_cus) * 8))),
+                       dim3(kAlsThreads), 0, st, pa);
+    OAP_HIP_CHECK(hipGetLastError());
+    OAP_HIP_CHECK(hipMemsetAsync(s.queue + 1, 0, sizeof(unsigned long long), st));
+    a.rows = s.long_rows;
+    a.nrows = s.n_long;
+    a.chunk_ptr = s.long_chunk_ptr;
+    a.partials = s.partials;
+    a.queue = s.queue + 1;
+    launch_solve<NB, true>(a, int(std::min<int64_t>(s.n_long, int64_t(num_cus) * per_cu)), st);
+  }
 }
 
 __global__ void oap_f64_to_f32(const double* in, float* out, int64_t n) {
@@ -227,38 +428,31 @@ __global__ void oap_als_init(const int32_t* ids, int64_t n, int r, int ld, uint6
 
 int als_max_rank() { return 128; }
 
+size_t als_partial_floats(int r) {
+  switch ((r + 15) / 16) {
+    case 1: return partial_floats<1>();
+    case 2: return partial_floats<2>();
+    case 3: return partial_floats<3>();
+    case 4: return partial_floats<4>();
+    case 5: return partial_floats<5>();
+    case 6: return partial_floats<6>();
+    case 7: return partial_floats<7>();
+    default: return partial_floats<8>();
+  }
+}
+
 void als_solve(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
   OAP_CHECK(s.r >= 1 && s.r <= als_max_rank(), "GPU ALS supports rank <= " << als_max_rank());
   OAP_CHECK(s.ld % 16 == 0 && s.ld >= s.r, "ALS factor stride must be a multiple of 16 >= rank");
-  if (s.nrows == 0) return;
-  SolveArgs a;
-  a.rowptr = s.rowptr;
-  a.cols = s.cols;
-  a.vals = s.vals;
-  a.nrows = s.nrows;
-  a.src = s.src;
-  a.ld = s.ld;
-  a.r = s.r;
-  a.yty = s.yty;
-  a.alpha = s.alpha;
-  a.lambda = s.lambda;
-  a.implicit = s.implicit ? 1 : 0;
-  a.dst = s.dst;
-  a.queue = s.queue;
-  a.fail = s.fail;
-  OAP_HIP_CHECK(hipMemsetAsync(s.queue, 0, sizeof(unsigned long long), st));
-  const size_t lds = (size_t(s.r) * (s.r + 1) / 2 + size_t(s.r)) * sizeof(float);
-  const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 1024))));
-  const int grid = static_cast<int>(std::min<int64_t>(s.nrows, int64_t(num_cus) * per_cu));
   switch ((s.r + 15) / 16) {
-    case 1: launch_solve<1>(a, grid, st); break;
-    case 2: launch_solve<2>(a, grid, st); break;
-    case 3: launch_solve<3>(a, grid, st); break;
-    case 4: launch_solve<4>(a, grid, st); break;
-    case 5: launch_solve<5>(a, grid, st); break;
-    case 6: launch_solve<6>(a, grid, st); break;
-    case 7: launch_solve<7>(a, grid, st); break;
-    default: launch_solve<8>(a, grid, st); break;
+    case 1: run<1>(s, num_cus, st); break;
+    case 2: run<2>(s, num_cus, st); break;
+    case 3: run<3>(s, num_cus, st); break;
+    case 4: run<4>(s, num_cus, st); break;
+    case 5: run<5>(s, num_cus, st); break;
+    case 6: run<6>(s, num_cus, st); break;
+    case 7: run<7>(s, num_cus, st); break;
+    default: run<8>(s, num_cus, st); break;
   }
 }
 

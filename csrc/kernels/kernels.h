@@ -123,16 +123,27 @@ struct AlsSolveArgs {
   const int64_t* rowptr = nullptr;  // [nrows+1] CSR of the destination rows
   const int32_t* cols = nullptr;    // source-row indices into src
   const float* vals = nullptr;      // ratings
-  int64_t nrows = 0;
+  // rows with at most the long-row threshold of ratings, solved directly
+  const int32_t* short_rows = nullptr;
+  int64_t n_short = 0;
+  // long rows: their ratings are split into chunks (partial Gramians, summed in chunk order)
+  const int32_t* long_rows = nullptr;
+  int64_t n_long = 0;
+  const int64_t* long_chunk_ptr = nullptr;  // [n_long+1] chunk ranges per long row
+  const int64_t* chunk_begin = nullptr;     // [n_chunks] rating ranges
+  const int64_t* chunk_end = nullptr;
+  int64_t n_chunks = 0;
+  float* partials = nullptr;                // [n_chunks][als_partial_floats(r)]
   const float* src = nullptr;       // source factors [n_src][ld]
   int ld = 0, r = 0;
   const float* yty = nullptr;       // [r][r] Gramian of ALL source factors (implicit)
   float alpha = 1.f, lambda = 0.f;
   bool implicit = true;
-  float* dst = nullptr;             // [nrows][ld]
-  unsigned long long* queue = nullptr;  // device scratch counter
+  float* dst = nullptr;             // [nrows][ld], indexed by destination row
+  unsigned long long* queue = nullptr;  // device scratch: 2 counters
   unsigned long long* fail = nullptr;   // device counter of non-SPD rows
 };
+size_t als_partial_floats(int r);
 int als_max_rank();
 void als_solve(const AlsSolveArgs& a, int num_cus, hipStream_t s);
 void als_init_factors(const int32_t* ids, int64_t n, int r, int ld, uint64_t seed, float* out,

@@ -169,7 +169,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       pl[c * sb + f] = lo;
     }
   }
-  for (int c = tid; c < kpad; c += kThreads) cn[c] = (c < k) ? a.cnorm[c] : INFINITY;
+  // padded centroids get a huge FINITE norm: their keys must never be NaN bit patterns
+  for (int c = tid; c < kpad; c += kThreads) cn[c] = (c < k) ? a.cnorm[c] : 1e30f;
   for (int f = tid; f < DP; f += kThreads)
     sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
   if (LDSACC && accumulate) {
@@ -193,10 +194,9 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   // ---- per-row epilogue: exact cost, outputs, fixed-point accumulation
   auto finish = [&](const float (&xv)[KS][8], const float (&cv)[KS][8], int b, int64_t row,
                     bool valid) {
-    float part = 0.f;
+    float part = 0.f;  // padded features are zero in both operands
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      if (16 * s < d)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float e = xv[s][j] - cv[s][j];
@@ -221,17 +221,22 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       if (h == 0) atomicAdd(&cnt_l[b], 1u);
       if (!a.sums_too) return;
       double* ap = acc_l + b * (d | 1) + 8 * h;
+      // k-steps below KS-1 are all real features (KS = ceil(d/16)): no per-element guards
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const int f0 = 16 * s + 8 * h;
-        if (16 * s + 16 <= d || f0 < d) {
-          const float4 s0 = *reinterpret_cast<const float4*>(sc_l + f0);
-          const float4 s1 = *reinterpret_cast<const float4*>(sc_l + f0 + 4);
-          const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float4 s0 = *reinterpret_cast<const float4*>(sc_l + f0);
+        const float4 s1 = *reinterpret_cast<const float4*>(sc_l + f0 + 4);
+        const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        if (s < KS - 1 || d == DP) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (16 * s + 16 <= d || f0 + j < d)
-              atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv[s][j] * scv[j])));
+            atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv[s][j] * scv[j])));
+        } else {
+          const int nv = d - f0;  // real features of this lane's half of the last k-step
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nv) atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv[s][j] * scv[j])));
         }
       }
     } else {
@@ -256,17 +261,22 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   const int64_t stride = int64_t(gridDim.x) * kWaves;
   int64_t t = int64_t(blockIdx.x) * kWaves + wave;
 
+  // Rows past n are clamped to row n-1 (their results are discarded, nothing needs zeroing);
+  // only the last k-step can reach past the row stride, and it is zero-filled there.
   auto load_tile = [&](int64_t tt, float (&dst)[KS][8]) {
-    const int64_t row = tt * 32 + r;
-    const bool ok = tt < ntiles && row < a.n;
-    const float* p = a.x + (ok ? row : 0) * a.ld + 8 * h;
+    int64_t row = tt * 32 + r;
+    row = row < a.n ? row : a.n - 1;
+    const float* p = a.x + row * a.ld + 8 * h;
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int f = 16 * s + 8 * h + 4 * q;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (ok && f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+        float4 v;
+        if (s < KS - 1 || f < a.ld)
+          v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+        else
+          v = make_float4(0.f, 0.f, 0.f, 0.f);
         dst[s][4 * q + 0] = v.x;
         dst[s][4 * q + 1] = v.y;
         dst[s][4 * q + 2] = v.z;
@@ -331,8 +341,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       int k1 = 0x7fffffff, k2 = 0x7fffffff;
       auto mfma_chunk = [&](int c0, f32x16& acc) {
         if constexpr (BIAS) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+          // (the first MFMA below takes a zero C operand)
         } else {
           // norms first: the first MFMA needs the seeded accumulator + fragment 0 only
 #pragma unroll
@@ -347,15 +356,26 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
         const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
         bf16x8 ah[KS], al[KS];
+        if (a.ablate & 32) {  // timing ablation: operands from registers, no LDS fragment reads
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
-          al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
+          for (int s = 0; s < KS; ++s) {
+            ah[s] = xl[s];
+            al[s] = xh[s];
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
+            al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
+          }
         }
         // KS = ceil(d/16): every k-step holds real features, so there is no runtime guard here
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], acc, 0, 0, 0);
+          if (BIAS && s == 0)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], f32x16{}, 0, 0, 0);
+          else
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xl[s], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], xh[s], acc, 0, 0, 0);
         }
@@ -363,19 +383,24 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       auto epilogue = [&](int c0, const f32x16& acc) {
         // chunk-local keys carry the in-chunk offset 8(e>>2)+(e&3) (an inline constant: one
         // v_bfi_b32 per candidate); the lane's chunk base c0+4h is OR-ed in once per chunk.
-        int q1 = 0x7fffffff, q2 = 0x7fffffff;
+        // Keys stay floats (the index only perturbs the low mantissa bits), so the top-2 update
+        // is v_min_f32 + v_med3_f32: 3 VALU per candidate.
+        float q1 = INFINITY, q2 = INFINITY;
+        if (a.ablate & 16) {  // timing ablation: keep the MFMAs live, drop the top-2 VALU
+          k1 = min(k1, __float_as_int(acc[0]) | c0);
+          return;
+        }
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int off = 8 * (e >> 2) + (e & 3);
-          const int key = (__float_as_int(acc[e]) & ~0x3ff) | (off & 0x3ff);
-          q2 = max(q1, min(q2, key));  // second smallest of {q1, q2, key} (q1 <= q2)
-          q1 = min(q1, key);
+          const float key = __int_as_float((__float_as_int(acc[e]) & ~0x3ff) | (off & 0x3ff));
+          q2 = __builtin_amdgcn_fmed3f(q1, q2, key);  // 2nd smallest of {q1, q2, key}, q1 <= q2
+          q1 = fminf(q1, key);
         }
         const int base = c0 + 4 * h;  // disjoint from every in-chunk offset's bits
-        q1 |= base;
-        q2 |= base;
-        k2 = min(max(k1, q1), min(k2, q2));
-        k1 = min(k1, q1);
+        const int i1 = __float_as_int(q1) | base, i2 = __float_as_int(q2) | base;
+        k2 = min(max(k1, i1), min(k2, i2));
+        k1 = min(k1, i1);
       };
       if (a.ablate & 8) {
         k1 = r % k;  // timing ablation: no distance work
@@ -407,7 +432,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
       // the gap must beat: split + accumulation error, seed rounding, key truncation
       const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
-      const bool unsure = valid && !(a.ablate & 8) && !(b2 - b1 > thr);
+      const bool unsure = valid && !(a.ablate & 56) && !(b2 - b1 > thr);
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);
