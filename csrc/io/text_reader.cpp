@@ -212,16 +212,15 @@ RatingsText read_ratings(const std::string& path, const std::string& sep, Thread
           double f[3];
           const char* q = s;
           int k = 0;
-          for (; k < 3 && q < le; ++k) {
+          while (k < 3) {
             bool ok;
-            f[k] = parse_num(q, le, ok);
+            const double v = parse_num(q, le, ok);
             if (!ok) break;
-            if (k < 2) {
-              if (size_t(le - q) >= sep.size() && std::memcmp(q, sep.data(), sep.size()) == 0)
-                q += sep.size();
-              else
-                break;
-            }
+            f[k++] = v;
+            if (size_t(le - q) >= sep.size() && std::memcmp(q, sep.data(), sep.size()) == 0)
+              q += sep.size();
+            else
+              break;
           }
           if (k < 2) {
             err[t] = "bad rating line in " + path;
