@@ -5,7 +5,7 @@
 #include <string>
 #include <vector>
 
-#include "runtime/context.h"
+#include "runtime/thread_pool.h"
 
 namespace oap {
 

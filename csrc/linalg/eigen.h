@@ -10,7 +10,7 @@
 #include <cstdint>
 #include <vector>
 
-#include "runtime/context.h"
+#include "runtime/thread_pool.h"
 
 namespace oap {
 

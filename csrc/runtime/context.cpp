@@ -30,65 +30,6 @@ float Event::elapsed_ms(const Event& a, const Event& b) {
   return ms;
 }
 
-// -------------------------------------------------------------------------------- ThreadPool
-ThreadPool::ThreadPool(int nthreads) {
-  if (nthreads < 1) nthreads = 1;
-  for (int i = 1; i < nthreads; ++i) workers_.emplace_back([this, i] { worker(i); });
-}
-
-ThreadPool::~ThreadPool() {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    stop_ = true;
-  }
-  cv_.notify_all();
-  for (auto& t : workers_) t.join();
-}
-
-void ThreadPool::worker(int idx) {
-  int64_t seen = 0;
-  for (;;) {
-    const std::function<void(int, int64_t, int64_t)>* job;
-    int64_t n;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || generation_ != seen; });
-      if (stop_) return;
-      seen = generation_;
-      job = job_;
-      n = job_n_;
-    }
-    int parts = size();
-    int64_t b = n * idx / parts, e = n * (idx + 1) / parts;
-    if (b < e) (*job)(idx, b, e);
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      if (--pending_ == 0) done_cv_.notify_all();
-    }
-  }
-}
-
-void ThreadPool::parallel_for(int64_t n, const std::function<void(int, int64_t, int64_t)>& fn) {
-  int parts = size();
-  if (parts == 1 || n < 2) {
-    if (n > 0) fn(0, 0, n);
-    return;
-  }
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    job_ = &fn;
-    job_n_ = n;
-    pending_ = parts - 1;
-    ++generation_;
-  }
-  cv_.notify_all();
-  int64_t e = n / parts;
-  if (e > 0) fn(0, 0, e);
-  std::unique_lock<std::mutex> lk(mu_);
-  done_cv_.wait(lk, [&] { return pending_ == 0; });
-  job_ = nullptr;
-}
-
 // -------------------------------------------------------------------------------- devices
 int visible_device_count() {
   int n = 0;

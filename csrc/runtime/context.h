@@ -15,6 +15,7 @@
 #include "runtime/common.h"
 #include "runtime/log.h"
 #include "runtime/memory.h"
+#include "runtime/thread_pool.h"
 
 namespace oap {
 
@@ -49,28 +50,6 @@ class Event {
 
  private:
   hipEvent_t e_ = nullptr;
-};
-
-// Static-partition thread pool for the CPU engine: deterministic chunking so results do not
-// depend on scheduling.
-class ThreadPool {
- public:
-  explicit ThreadPool(int nthreads);
-  ~ThreadPool();
-  int size() const { return static_cast<int>(workers_.size()) + 1; }
-  // Runs fn(chunk_index, begin, end) over [0, n) split into size() contiguous chunks.
-  void parallel_for(int64_t n, const std::function<void(int, int64_t, int64_t)>& fn);
-
- private:
-  void worker(int idx);
-  std::vector<std::thread> workers_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(int, int64_t, int64_t)>* job_ = nullptr;
-  int64_t job_n_ = 0;
-  int64_t generation_ = 0;
-  int pending_ = 0;
-  bool stop_ = false;
 };
 
 struct DeviceInfo {
