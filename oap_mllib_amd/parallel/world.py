@@ -101,7 +101,14 @@ def _choose_backend(cfg: Config) -> tuple[str, int]:
         raise RuntimeError("config.device='gpu' but no HIP device is visible")
     if dev in ("auto", "gpu") and n > 0:
         local = _env_int("LOCAL_RANK", 0)
-        return "gpu", (cfg.device_id if cfg.device_id >= 0 else local % n)
+        device = cfg.device_id if cfg.device_id >= 0 else local % n
+        from ..utils.platform import check_platform_compatibility
+
+        rep = check_platform_compatibility()
+        if rep.gpu_ok(device):
+            return "gpu", device
+        if dev == "gpu":
+            raise RuntimeError(f"config.device='gpu' but the platform check failed: {rep.reason}")
     return "cpu", -1
 
 
