@@ -22,7 +22,8 @@ void register_als(py::module_& m) {
          py::array_t<int32_t, py::array::c_style | py::array::forcecast> users,
          py::array_t<int32_t, py::array::c_style | py::array::forcecast> items,
          py::array_t<float, py::array::c_style | py::array::forcecast> ratings, int rank,
-         int max_iter, double reg, double alpha, bool implicit, uint64_t seed) {
+         int max_iter, double reg, double alpha, bool implicit, uint64_t seed,
+         py::object init_ids, py::object init_factors) {
         const int64_t n = users.size();
         if (items.size() != n || ratings.size() != n)
           throw ConfigError("users, items and ratings must have the same length");
@@ -33,6 +34,20 @@ void register_als(py::module_& m) {
         p.alpha = alpha;
         p.implicit = implicit;
         p.seed = seed;
+        py::array_t<int32_t, py::array::c_style | py::array::forcecast> iid;
+        py::array_t<float, py::array::c_style | py::array::forcecast> ifac;
+        if (!init_ids.is_none()) {
+          iid = init_ids;
+          ifac = init_factors;
+          if (ifac.ndim() != 2 || ifac.shape(0) != iid.size() || ifac.shape(1) != rank)
+            throw ConfigError("init_factors must be len(init_ids) x rank");
+          for (int64_t q = 1; q < iid.size(); ++q)
+            if (iid.data()[q - 1] >= iid.data()[q])
+              throw ConfigError("init_ids must be strictly ascending");
+          p.init_ids = iid.data();
+          p.init_factors = ifac.data();
+          p.n_init = iid.size();
+        }
         AlsResult r;
         {
           py::gil_scoped_release rel;
@@ -65,6 +80,7 @@ void register_als(py::module_& m) {
       },
       py::arg("ctx"), py::arg("comm"), py::arg("users"), py::arg("items"), py::arg("ratings"),
       py::arg("rank") = 10, py::arg("max_iter") = 10, py::arg("reg") = 0.1,
-      py::arg("alpha") = 1.0, py::arg("implicit") = true, py::arg("seed") = 0);
+      py::arg("alpha") = 1.0, py::arg("implicit") = true, py::arg("seed") = 0,
+      py::arg("init_ids") = py::none(), py::arg("init_factors") = py::none());
   m.def("als_max_rank", &kern::als_max_rank);
 }

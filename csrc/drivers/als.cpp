@@ -277,6 +277,19 @@ bool chol_solve(std::vector<double>& A, std::vector<double>& b, int r) {
   return true;
 }
 
+// Rows of X (global user order, stride ld) whose id appears in the caller's initial factors
+// (ids sorted ascending, rank columns) are overwritten with them — the resume path.
+void overlay_init(const std::vector<int32_t>& ids, int r, int ld, const AlsParams& p,
+                  float* X) {
+  if (p.init_ids == nullptr || p.n_init == 0) return;
+  for (size_t g = 0; g < ids.size(); ++g) {
+    const int32_t* it = std::lower_bound(p.init_ids, p.init_ids + p.n_init, ids[g]);
+    if (it == p.init_ids + p.n_init || *it != ids[g]) continue;
+    const float* src = p.init_factors + size_t(it - p.init_ids) * r;
+    for (int f = 0; f < r; ++f) X[g * size_t(ld) + f] = src[f];
+  }
+}
+
 }  // namespace
 
 AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t* items,
@@ -427,11 +440,18 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     };
     upload_side(U, dU);
     upload_side(I, dI);
-    {  // initial user factors from their ids (world-size independent)
+    {  // initial user factors from their ids (world-size independent), or the caller's
       Buffer ids = ctx.alloc(std::max<size_t>(U.ids.size() * 4, 16));
       if (!U.ids.empty()) ctx.copy_to_backend(ids.data(), U.ids.data(), U.ids.size() * 4, s);
       kern::als_init_factors(ids.as<int32_t>(), U.n, r, ld, p.seed, dU.f.as<float>(), s);
       OAP_HIP_CHECK(hipStreamSynchronize(s));
+      if (p.init_ids && p.n_init && U.n) {
+        std::vector<float> X0(size_t(U.n) * ld);
+        ctx.copy_to_host(X0.data(), dU.f.data(), X0.size() * 4);
+        overlay_init(U.ids, r, ld, p, X0.data());
+        ctx.copy_to_backend(dU.f.data(), X0.data(), X0.size() * 4, s);
+        OAP_HIP_CHECK(hipStreamSynchronize(s));
+      }
     }
     Buffer ctr = ctx.alloc(32);
     ctx.memset(ctr.data(), 0, 32);
@@ -533,6 +553,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     ctx.pool().parallel_for(U.n, [&](int, int64_t b, int64_t e) {
       for (int64_t i = b; i < e; ++i) init_factor_row(p.seed, U.ids[i], r, ld, &Xh[size_t(i) * ld]);
     });
+    overlay_init(U.ids, r, ld, p, Xh.data());
     int64_t fails = 0;
     auto half = [&](Side& Dst, std::vector<float>& Fd, Side& Src, std::vector<float>& Fs) {
       auto t0 = std::chrono::steady_clock::now();

@@ -30,6 +30,11 @@ struct AlsParams {
   double alpha = 1.0;
   bool implicit = true;
   uint64_t seed = 0;
+  // optional initial user factors (resume from a checkpoint): ids sorted ascending,
+  // factors [n_init][rank]; users not listed get the seeded random initialisation
+  const int32_t* init_ids = nullptr;
+  const float* init_factors = nullptr;
+  int64_t n_init = 0;
 };
 
 struct AlsResult {

@@ -46,6 +46,10 @@ class Config:
     ingest_chunk_rows: int = 1 << 18
     log_level: str = "warn"
     log_file: str = ""
+    #: directory for periodic training snapshots ("" = off; the sc.checkpointDir analogue)
+    checkpoint_dir: str = ""
+    #: K-Means iterations between snapshots (ALS uses its checkpointInterval param)
+    checkpoint_interval: int = 10
 
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)

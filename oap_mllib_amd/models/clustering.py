@@ -23,6 +23,7 @@ from ..linalg import DenseVector
 from ..params import (Param, gt, in_array, to_float, to_int, to_str)
 from ..parallel.world import get_world
 from ..persistence import spark_format as sf
+from ..utils import checkpoint
 from ..utils.logging import Instrumentation
 from .base import (Estimator, HasTrainingSummary, MLReadable, MLWritable, Model,
                    DefaultParamsPersistence, choose_engine, java_string_hash)
@@ -121,9 +122,15 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
         else:
             N = _loader.load()
             table = upload_table(w, X)
-            r = N.kmeans_fit(w.ctx, w.comm, table, None, k, max_iter, tol,
-                             self.getOrDefault("initMode"), self.getOrDefault("initSteps"), seed)
-            centers, cost, n_iter = r["centers"], r["cost"], r["num_iter"]
+            ck = checkpoint.for_fit(w, self, X.shape)
+            if ck is None:
+                r = N.kmeans_fit(w.ctx, w.comm, table, None, k, max_iter, tol,
+                                 self.getOrDefault("initMode"), self.getOrDefault("initSteps"),
+                                 seed)
+                centers, cost, n_iter = r["centers"], r["cost"], r["num_iter"]
+            else:
+                r, centers, cost, n_iter = self._fit_segmented(N, w, table, ck, k, max_iter, tol,
+                                                                seed)
             extra = {"engine": engine, "init_seconds": r["init_seconds"],
                      "iter_seconds": r["iter_seconds"], "global_rows": r["global_rows"]}
         model = KMeansModel(uid=self.uid, centers=np.asarray(centers), trainingCost=float(cost),
@@ -140,6 +147,35 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
         instr.logNamedValue("engine", extra["engine"])
         instr.finish()
         return model
+
+
+    def _fit_segmented(self, N, w, table, ck, k, max_iter, tol, seed):
+        """Lloyd in checkpoint_interval-sized segments, resuming from a saved state."""
+        interval = max(1, int(w.config.checkpoint_interval))
+        state = ck.load()
+        centers, done, cost = None, 0, 0.0
+        if state is not None:
+            meta, arrays = state
+            centers, done, cost = arrays["centers"], int(meta["num_iter"]), float(meta["cost"])
+            if meta.get("converged"):
+                return {"init_seconds": 0.0, "iter_seconds": 0.0,
+                        "global_rows": meta["global_rows"]}, centers, cost, done
+        r = {"init_seconds": 0.0, "iter_seconds": 0.0, "global_rows": 0}
+        while True:
+            seg = min(interval, max_iter - done)
+            if seg <= 0 and centers is not None:
+                break
+            r = N.kmeans_fit(w.ctx, w.comm, table, centers, k, max(seg, 0), tol,
+                             self.getOrDefault("initMode"), self.getOrDefault("initSteps"), seed)
+            centers, cost = np.asarray(r["centers"]), float(r["cost"])
+            done += int(r["num_iter"])
+            conv = bool(r["converged"]) or done >= max_iter
+            ck.save({"num_iter": done, "cost": cost, "converged": bool(r["converged"]),
+                     "global_rows": r["global_rows"]}, {"centers": centers})
+            if conv or seg == 0:
+                break
+            k = centers.shape[0]
+        return r, centers, cost, done
 
 
 def upload_table(w, X: np.ndarray, layout: str = "kmeans"):

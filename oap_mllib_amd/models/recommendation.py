@@ -28,6 +28,7 @@ from ..fallback import als_vanilla as vanilla
 from ..params import Param, gt_eq, in_array, to_bool, to_float, to_int, to_str
 from ..parallel.world import get_world
 from ..persistence import spark_format as sf
+from ..utils import checkpoint
 from ..utils.logging import Instrumentation
 from .base import (DefaultParamsPersistence, Estimator, MLReadable, MLWritable, Model,
                    choose_engine, java_string_hash)
@@ -164,9 +165,9 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
             uid, uf, iid, itf = res.user_ids, res.user_factors, res.item_ids, res.item_factors
         else:
             N = _loader.load()
-            out = N.als_fit(w.ctx, w.comm, u, i, r, rank, self.getOrDefault("maxIter"),
-                            self.getOrDefault("regParam"), self.getOrDefault("alpha"), implicit,
-                            seed)
+            ck = checkpoint.for_fit(w, self, (len(u),)) \
+                if self.getOrDefault("checkpointInterval") > 0 else None
+            out = self._fit_native(N, w, u, i, r, rank, implicit, seed, ck)
             uid, uf = np.asarray(out["user_ids"]), np.asarray(out["user_factors"])
             iid, itf = np.asarray(out["item_ids"]), np.asarray(out["item_factors"])
             extra.update({k: out[k] for k in ("nnz", "setup_ms", "train_ms", "iter_ms", "gram_ms",
@@ -179,6 +180,33 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
         instr.logNamedValue("engine", engine)
         instr.finish()
         return model
+
+
+    def _fit_native(self, N, w, u, i, r, rank, implicit, seed, ck):
+        """Native fit; with a checkpointer, in checkpointInterval-sized segments that save
+        (and resume from) the user factors."""
+        max_iter = self.getOrDefault("maxIter")
+        args = (self.getOrDefault("regParam"), self.getOrDefault("alpha"), implicit, seed)
+        if ck is None:
+            return N.als_fit(w.ctx, w.comm, u, i, r, rank, max_iter, *args)
+        interval = self.getOrDefault("checkpointInterval")
+        done, ids, fac = 0, None, None
+        state = ck.load()
+        if state is not None:
+            meta, arrays = state
+            done, ids, fac = int(meta["num_iter"]), arrays["user_ids"], arrays["user_factors"]
+        out = None
+        while out is None or done < max_iter:
+            seg = min(interval, max_iter - done)
+            out = N.als_fit(w.ctx, w.comm, u, i, r, rank, max(seg, 0), *args, ids, fac)
+            done += max(seg, 0)
+            ids = np.asarray(out["user_ids"])
+            order = np.argsort(ids, kind="stable")
+            ids, fac = ids[order], np.asarray(out["user_factors"])[order]
+            ck.save({"num_iter": done}, {"user_ids": ids, "user_factors": fac})
+            if seg <= 0:
+                break
+        return out
 
 
 def _factor_frame(ids: np.ndarray, factors: np.ndarray):
