@@ -74,6 +74,12 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
   return m;
 }
 
+__device__ inline int med3_i32(int a, int b, int c) {
+  int r;
+  asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // Exact fp32 argmin over kpad centroids for the lane's row (both halves get the result).
 template <int KS>
 __device__ inline void exact_argmin(const float* __restrict__ cbase, int stride,
@@ -356,18 +362,10 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
         const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
         bf16x8 ah[KS], al[KS];
-        if (a.ablate & 32) {  // timing ablation: operands from registers, no LDS fragment reads
 #pragma unroll
-          for (int s = 0; s < KS; ++s) {
-            ah[s] = xl[s];
-            al[s] = xh[s];
-          }
-        } else {
-#pragma unroll
-          for (int s = 0; s < KS; ++s) {
-            ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
-            al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
-          }
+        for (int s = 0; s < KS; ++s) {
+          ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
+          al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
         }
         // KS = ceil(d/16): every k-step holds real features, so there is no runtime guard here
 #pragma unroll
@@ -385,20 +383,35 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         // v_bfi_b32 per candidate); the lane's chunk base c0+4h is OR-ed in once per chunk.
         // Keys stay floats (the index only perturbs the low mantissa bits), so the top-2 update
         // is v_min_f32 + v_med3_f32: 3 VALU per candidate.
-        float q1 = INFINITY, q2 = INFINITY;
-        if (a.ablate & 16) {  // timing ablation: keep the MFMAs live, drop the top-2 VALU
-          k1 = min(k1, __float_as_int(acc[0]) | c0);
-          return;
-        }
+        // Keys are compared as signed ints (same order as the floats for the non-negative
+        // distances; a tiny negative from rounding only ever looks like a near tie, which the
+        // exact pass re-decides).  Integer min / med3 avoid the NaN canonicalisation that float
+        // min/max would add, so the top-2 update is 3 VALU per candidate.  Four independent
+        // trackers (candidates e mod 4) keep the dependency chains short.
+        int t1[4], t2[4];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int off = 8 * (e >> 2) + (e & 3);
-          const float key = __int_as_float((__float_as_int(acc[e]) & ~0x3ff) | (off & 0x3ff));
-          q2 = __builtin_amdgcn_fmed3f(q1, q2, key);  // 2nd smallest of {q1, q2, key}, q1 <= q2
-          q1 = fminf(q1, key);
+          const int key = (__float_as_int(acc[e]) & ~0x3ff) | (off & 0x3ff);
+          const int t = e & 3;
+          if (e < 4) {
+            t1[t] = key;
+            t2[t] = 0x7fffffff;
+          } else {
+            t2[t] = med3_i32(t1[t], t2[t], key);  // 2nd smallest of {t1, t2, key}, t1 <= t2
+            t1[t] = min(t1[t], key);
+          }
         }
+        auto merge2 = [](int& x1, int& x2, int y1, int y2) {
+          x2 = min(max(x1, y1), min(x2, y2));
+          x1 = min(x1, y1);
+        };
+        merge2(t1[0], t2[0], t1[1], t2[1]);
+        merge2(t1[2], t2[2], t1[3], t2[3]);
+        merge2(t1[0], t2[0], t1[2], t2[2]);
+        const int q1 = t1[0], q2 = t2[0];
         const int base = c0 + 4 * h;  // disjoint from every in-chunk offset's bits
-        const int i1 = __float_as_int(q1) | base, i2 = __float_as_int(q2) | base;
+        const int i1 = q1 | base, i2 = q2 | base;
         k2 = min(max(k1, i1), min(k2, i2));
         k1 = min(k1, i1);
       };
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
       // the gap must beat: split + accumulation error, seed rounding, key truncation
       const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
-      const bool unsure = valid && !(a.ablate & 56) && !(b2 - b1 > thr);
+      const bool unsure = valid && !(a.ablate & 8) && !(b2 - b1 > thr);
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);

@@ -16,8 +16,9 @@
 // only this workgroup owns (deterministic); a second kernel sums the slabs in split order.
 //
 // Workgroup = 4 waves on one 128x128 output tile (each wave 64x64 = 2x2 MFMA blocks); rows are
-// staged 32 at a time through LDS transposed to [feature][row] bf16 hi/lo planes (40 KB), so
-// A and B fragments are single 16-byte LDS reads.  Blocks are remapped so that all tiles of one
+// staged 32 at a time through LDS transposed to [feature][row] bf16 hi/lo planes (2 x 40 KB,
+// double buffered: chunk c+1 is loaded and converted while chunk c feeds the MFMAs, one barrier
+// per chunk), so A and B fragments are single 16-byte LDS reads.  Blocks are remapped so that all tiles of one
 // row split land on one XCD and share its L2.
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
@@ -57,7 +58,8 @@ __device__ inline void tile_coords(int tile, int nb, int& ti, int& tj) {
 
 template <bool FOUR>
 __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * kPlane];  // [side][plane hi/lo]
+  // two stages x [side][plane hi/lo]: chunk c+1 is staged while chunk c feeds the MFMAs
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 4 * kPlane];
   const int G = a.splits * a.tiles;
   const int per = gridDim.x / 8;  // gridDim.x is a multiple of 8
   const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -93,8 +95,9 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
     }
   };
   // centre, split, transpose into the planes; rows past r_end contribute exact zeros
-  auto stage = [&](int64_t r0, int side, const float4 (&v)[4], const float4 sh, bool sums) {
-    __bf16* hi = lds + (2 * side) * kPlane;
+  auto stage = [&](__bf16* buf, int64_t r0, int side, const float4 (&v)[4], const float4 sh,
+                   bool sums) {
+    __bf16* hi = buf + (2 * side) * kPlane;
     __bf16* lo = hi + kPlane;
     float c[4][4];
 #pragma unroll
@@ -155,15 +158,20 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
     zero();
   };
 
-  const __bf16* aH = lds + (64 * wi + r) * kPS + 8 * h;
-  const __bf16* bH = lds + (diag ? 0 : 2 * kPlane) + (64 * wj + r) * kPS + 8 * h;
-  int since = 0;
-  if (r_begin < r_end) load(r_begin);
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk) {
-    stage(r0, 0, vI, shI, diag);
-    if (!diag) stage(r0, 1, vJ, shJ, false);
+  const int aoff = (64 * wi + r) * kPS + 8 * h;
+  const int boff = (diag ? 0 : 2 * kPlane) + (64 * wj + r) * kPS + 8 * h;
+  int since = 0, cur = 0;
+  if (r_begin < r_end) {
+    load(r_begin);
+    stage(lds, r_begin, 0, vI, shI, diag);
+    if (!diag) stage(lds, r_begin, 1, vJ, shJ, false);
     __syncthreads();
-    if (r0 + kChunk < r_end) load(r0 + kChunk);  // in flight during the MFMAs
+  }
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk) {
+    const bool more = r0 + kChunk < r_end;
+    if (more) load(r0 + kChunk);  // global loads in flight during the MFMAs
+    const __bf16* aH = lds + cur * (4 * kPlane) + aoff;
+    const __bf16* bH = lds + cur * (4 * kPlane) + boff;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
@@ -185,7 +193,13 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
             acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
         }
     }
+    if (more) {  // the other buffer was last read before the previous barrier
+      __bf16* nb = lds + (cur ^ 1) * (4 * kPlane);
+      stage(nb, r0 + kChunk, 0, vI, shI, diag);
+      if (!diag) stage(nb, r0 + kChunk, 1, vJ, shJ, false);
+    }
     __syncthreads();
+    cur ^= 1;
     if (++since == a.flush_chunks) {
       flush();
       since = 0;

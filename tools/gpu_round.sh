@@ -30,6 +30,12 @@ for st in $STEPS; do
     alsbench)
       timeout -k 10 600 python benchmarks/bench_als.py ${ALS_ARGS:-} > gpurun_out/bench_als_$T.json 2> gpurun_out/bench_als_$T.err
       rc=$?; echo alsbench_rc=$rc; cat gpurun_out/bench_als_$T.json; tail -3 gpurun_out/bench_als_$T.err; fatal $rc alsbench;;
+    alsprof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/alsprof_$T -o run -- python3 $R/benchmarks/bench_als.py --ratings 20000000 --users 1000000 --items 100000 --iters 2 > $R/gpurun_out/alsprof_$T.log 2>&1)
+      rc=$?; echo alsprof_rc=$rc; fatal $rc alsprof;;
+    pcaprof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/pcaprof_$T -o run -- python3 $R/benchmarks/bench_pca.py --reps 2 > $R/gpurun_out/pcaprof_$T.log 2>&1)
+      rc=$?; echo pcaprof_rc=$rc; fatal $rc pcaprof;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- python3 $R/bench.py --rows 20000000 --steps 5 --warmup 1 --skip-fit > $R/gpurun_out/prof_$T.log 2>&1)
       rc=$?; echo prof_rc=$rc; fatal $rc prof;;

@@ -20,10 +20,7 @@ C = t.to_numpy(g, 0, k)
 out = {}
 for name, precise, ab in [("full", False, 0), ("no_accumulate", False, 1), ("no_cost", False, 2),
                           ("no_acc_no_cost", False, 3), ("no_distance", False, 8),
-                          ("loads_only", False, 11), ("no_epilogue", False, 16),
-                          ("no_epi_acc_cost", False, 19), ("no_lds_frag", False, 32),
-                          ("no_lds_no_epi", False, 48), ("mfma_only", False, 51),
-                          ("precise_full", True, 0),
+                          ("loads_only", False, 11), ("precise_full", True, 0),
                           ("precise_no_acc_no_cost", True, 3)]:
     if only and name not in only:
         continue
