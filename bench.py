@@ -9,6 +9,8 @@ local row + one RCCL allreduce of the fixed-point centroid statistics + the fina
 the convergence read-back) — nothing is skipped: tol=-1 disables the convergence exit, so exactly K full iterations run.
 Scaling is STRONG: the global dataset is 100M rows for every N, each rank generating its own
 contiguous shard directly in HBM (synthetic Gaussian blobs, identical values for any N).
+--config kmeans_bf16 is BASELINE config #5: k=1000, 1B x 100 bf16 (208 GB of rows on one GPU —
+the 288 GB HBM partition sizing case), same protocol.
 The timed region is bracketed by a barrier + device synchronize on both sides and the MAX over
 ranks is reported.  `value` is whole-job samples/s = global_rows * K / t.  The end-to-end fit()
 wall clock (k-means|| init + Lloyd to convergence, maxIter=20) is reported alongside.
@@ -43,9 +45,10 @@ def bench_kmeans(args, w):
     base, rem = divmod(rows_total, w.size)
     local = base + (1 if w.rank < rem else 0)
     row0 = w.rank * base + min(w.rank, rem)
-    ld = N.kmeans_ld(d)
+    st = args.dtype
+    ld = N.kmeans_ld(d, st)
     t_ing = time.time()
-    table = N.synth_blobs(w.ctx, local, d, ld, row0, k, 10.0, 1.0, 20240917)
+    table = N.synth_blobs(w.ctx, local, d, ld, row0, k, 10.0, 1.0, 20240917, st)
     table.set_global(row0, rows_total)
     _barrier_sync(w)
     ingest_s = time.time() - t_ing
@@ -81,8 +84,9 @@ def bench_kmeans(args, w):
         "metric": "kmeans_samples_per_sec", "value": samples, "unit": "samples/s",
         "n_gpus": w.size, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el_max / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic (gaussian blobs, on-device)",
-        "config": {"model": "kmeans k=200 d=50 (Lloyd, euclidean)", "global_batch": rows_total,
+        "vs_baseline": None, "dtype": "fp32" if st == "f32" else "bf16",
+        "data": "synthetic (gaussian blobs, on-device)",
+        "config": {"model": f"kmeans k={k} d={d} (Lloyd, euclidean)", "global_batch": rows_total,
                    "seq_len": d, "parallelism": f"dp{w.size}", "k": k,
                    "rows": rows_total, "dim": d},
         "extra": {"fit_wall_s_end_to_end": fit_s,
@@ -92,8 +96,11 @@ def bench_kmeans(args, w):
                   "allreduce_us": ar["total_us"] / max(ar["count"], 1),
                   "achieved_tflops": flops / (el_max / args.steps) / 1e12,
                   "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
+                  "storage": st,
                   "distance_path": "fp32-exact MFMA" if args.precise else
-                  "bf16-split MFMA + exact-fp32 refinement (assignments identical to fp32)",
+                  ("bf16-split MFMA + exact-fp32 refinement (assignments identical to fp32)"
+                   if st == "f32" else "bf16 rows x bf16-split centroids on MFMA + exact-fp32 "
+                   "refinement (assignments identical to exact fp32 on the bf16 data)"),
                   "cost": r["cost"]},
     }
     return out
@@ -105,14 +112,22 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="kmeans", choices=["kmeans"])
-    ap.add_argument("--rows", type=int, default=100_000_000)
-    ap.add_argument("--dim", type=int, default=50)
-    ap.add_argument("--k", type=int, default=200)
+    ap.add_argument("--config", default="kmeans", choices=["kmeans", "kmeans_bf16"],
+                    help="kmeans: k=200, 100M x 50 f32 (headline); kmeans_bf16: k=1000, "
+                    "1B x 100 bf16")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--dim", type=int, default=None)
+    ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--skip-fit", action="store_true")
     ap.add_argument("--precise", action="store_true",
                     help="exact-fp32 MFMA distances only (no bf16-split fast path)")
     args = ap.parse_args(argv)
+    preset = {"kmeans": (100_000_000, 50, 200, "f32"),
+              "kmeans_bf16": (1_000_000_000, 100, 1000, "bf16")}[args.config]
+    args.rows = args.rows or preset[0]
+    args.dim = args.dim or preset[1]
+    args.k = args.k or preset[2]
+    args.dtype = preset[3]
 
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and ws != args.gpus:

@@ -324,16 +324,17 @@ PYBIND11_MODULE(_native, m) {
   m.def(
       "synth_blobs",
       [](std::shared_ptr<Context> ctx, int64_t rows, int cols, int64_t ld, int64_t row0,
-         int ncenters, double box, double sigma, uint64_t seed) {
+         int ncenters, double box, double sigma, uint64_t seed, const std::string& storage) {
         auto t = std::make_shared<DenseTable>();
+        const DType st = parse_dtype(storage);
         py::gil_scoped_release r;
         *t = synth_blobs_table(*ctx, rows, cols, ld <= 0 ? cols : ld, row0, ncenters, box, sigma,
-                               seed);
+                               seed, st);
         return t;
       },
       py::arg("ctx"), py::arg("rows"), py::arg("cols"), py::arg("ld") = 0, py::arg("row0") = 0,
       py::arg("ncenters") = 8, py::arg("box") = 10.0, py::arg("sigma") = 1.0,
-      py::arg("seed") = 42);
+      py::arg("seed") = 42, py::arg("storage") = "f32");
   m.def("assign_global_offsets",
         [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t) {
           py::gil_scoped_release r;
@@ -341,7 +342,9 @@ PYBIND11_MODULE(_native, m) {
         });
 
   // ---------------------------------------------------------------- K-Means
-  m.def("kmeans_ld", &kern::kmeans_ld);
+  m.def(
+      "kmeans_ld", [](int d, const std::string& dtype) { return kern::kmeans_ld(d, dtype == "bf16"); },
+      py::arg("d"), py::arg("dtype") = "f32");
   m.def(
       "kmeans_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,

@@ -216,7 +216,8 @@ struct AssignReq {
 int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const AssignReq& req,
                hipStream_t s) {
   kern::KMeansAssignArgs a;
-  a.x = x.data.as<float>();
+  a.x = x.data.data();
+  a.xbf16 = x.dtype == DType::BF16;
   a.n = x.rows;
   a.ld = static_cast<int>(x.ld);
   a.d = x.cols;
@@ -254,8 +255,11 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   a.mindist = mind;
   a.accumulate = false;
   a.cost_slab = nullptr;
-  for (int c = 0; c < g.k; c += kmax) {
-    const int kc = std::min(kmax, g.k - c);
+  // balanced chunks: ceil(k / kmax) launches of equal 32-multiples (no thin last pass)
+  const int nchunks = (g.k + kmax - 1) / kmax;
+  const int csize = static_cast<int>(round_up((g.k + nchunks - 1) / nchunks, 32));
+  for (int c = 0; c < g.k; c += csize) {
+    const int kc = std::min(csize, g.k - c);
     a.centers = g.c32.as<float>() + size_t(c) * g.dp;
     a.cnorm = g.cnorm.as<float>() + c;
     a.k = kc;
@@ -265,18 +269,19 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     kern::kmeans_assign(a, ctx.info().cu_count, s);
   }
   if (req.accumulate)
-    kern::kmeans_accumulate(x.data.as<float>(), x.rows, static_cast<int>(x.ld), x.cols, labels,
-                            g.k, req.scale, req.sums_too ? req.sums : nullptr, req.counts, s);
+    kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
+                            static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
+                            req.sums_too ? req.sums : nullptr, req.counts, s);
   if (req.cost_slab) return kern::reduce_sum_f32(mind, x.rows, req.cost_slab, s);
   return 0;
 }
 
 void check_gpu_table(const DenseTable& x) {
-  OAP_CHECK(x.dtype == DType::F32, "GPU K-Means expects an f32 table");
-  OAP_CHECK(x.ld == kern::kmeans_ld(x.cols), "table row stride " << x.ld
-                                                                 << " does not match the K-Means "
-                                                                    "layout "
-                                                                 << kern::kmeans_ld(x.cols));
+  OAP_CHECK(x.dtype == DType::F32 || x.dtype == DType::BF16,
+            "GPU K-Means expects an f32 or bf16 table, got " << dtype_name(x.dtype));
+  const int want = kern::kmeans_ld(x.cols, x.dtype == DType::BF16);
+  OAP_CHECK(x.ld == want, "table row stride " << x.ld << " does not match the K-Means layout "
+                                              << want);
 }
 
 // Operations the initialisers need, on either backend.
@@ -364,7 +369,7 @@ class InitOps {
       Buffer di = ctx_.alloc(sizeof(int64_t) * local_idx.size());
       Buffer dv = ctx_.alloc(sizeof(float) * local_idx.size() * d);
       ctx_.copy_to_backend(di.data(), local_idx.data(), sizeof(int64_t) * local_idx.size());
-      kern::gather_rows(x_.data.as<float>(), x_.ld, d, di.as<int64_t>(),
+      kern::gather_rows(x_.data.data(), x_.dtype, x_.ld, d, di.as<int64_t>(),
                         int64_t(local_idx.size()), dv.as<float>(), ctx_.compute());
       std::vector<float> h(local_idx.size() * d);
       ctx_.copy_to_host(h.data(), dv.data(), sizeof(float) * h.size());
@@ -776,7 +781,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     roctx_pop();
     float ms_assign = Event::elapsed_ms(e0, e1), ms_comm = Event::elapsed_ms(e1, e2),
           ms_all = Event::elapsed_ms(e0, e3);
-    M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.rows) * x.ld * 4);
+    M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.bytes()));
     M.add("kmeans/allreduce", ms_comm * 1e3, int64_t(kd + k) * 8 + 8);
     M.add("kmeans/iteration", ms_all * 1e3);
     auto* fl = flags_h.as<kern::KMeansFlags>();
@@ -854,7 +859,8 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
   Buffer stats = ctx.alloc(sizeof(u64) * (size_t(k) * d + k));
   Buffer slab = ctx.alloc(sizeof(double) * kern::kmeans_cost_slab_size(ctx.info().cu_count));
   kern::KMeansAssignArgs a;
-  a.x = x.data.as<float>();
+  a.x = x.data.data();
+  a.xbf16 = x.dtype == DType::BF16;
   a.n = x.rows;
   a.ld = static_cast<int>(x.ld);
   a.d = d;

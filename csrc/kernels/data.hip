@@ -70,16 +70,45 @@ __global__ __launch_bounds__(256) void oap_column_absmax4(const float4* x, int64
   }
 }
 
-__global__ void oap_column_absmax(const float* x, int64_t rows, int cols, int64_t ld,
-                                  float* out) {
+// bf16 rows with ld % 8 == 0: the same flat-stream scheme with 16-byte groups of 8 columns.
+__global__ __launch_bounds__(256) void oap_column_absmax8_bf16(const bf16x8* x, int64_t rows,
+                                                               int ld8, int cols, float* out) {
+  __shared__ float part[256 * 8];
+  const int per_block = (256 / ld8) * ld8;
+  const int t = threadIdx.x;
+  float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (t < per_block) {
+    const int cg = t % ld8;
+    const int64_t rstride = int64_t(gridDim.x) * (per_block / ld8);
+    for (int64_t r = int64_t(blockIdx.x) * (per_block / ld8) + t / ld8; r < rows; r += rstride) {
+      const bf16x8 v = x[r * ld8 + cg];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], fabsf(static_cast<float>(v[j])));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) part[t * 8 + j] = m[j];
+  __syncthreads();
+  for (int c = t; c < ld8 * 8 && c < cols; c += blockDim.x) {
+    float mm = 0.f;
+    const int cg = c / 8, lane = c % 8;
+    for (int i = cg; i < per_block; i += ld8) mm = fmaxf(mm, part[i * 8 + lane]);
+    atomicMax(reinterpret_cast<int*>(out) + c, __float_as_int(mm));  // mm >= 0: int order
+  }
+}
+
+template <typename T>
+__global__ void oap_column_absmax(const T* x, int64_t rows, int cols, int64_t ld, float* out) {
   for (int c = threadIdx.x; c < cols; c += blockDim.x) {
     float m = 0.f;
-    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) m = fmaxf(m, fabsf(x[r * ld + c]));
+    for (int64_t r = blockIdx.x; r < rows; r += gridDim.x)
+      m = fmaxf(m, fabsf(static_cast<float>(x[r * ld + c])));
     atomicMax(reinterpret_cast<int*>(out) + c, __float_as_int(m));  // m >= 0: int order == float
   }
 }
 
-__global__ void oap_synth_blobs(float* x, int64_t rows, int cols, int64_t ld, int64_t row0,
+template <typename T>
+__global__ void oap_synth_blobs(T* x, int64_t rows, int cols, int64_t ld, int64_t row0,
                                 int ncenters, float box, float sigma, uint64_t seed) {
   const int64_t total = rows * ld;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
@@ -87,7 +116,7 @@ __global__ void oap_synth_blobs(float* x, int64_t rows, int cols, int64_t ld, in
     int64_t r = i / ld;
     int c = static_cast<int>(i - r * ld);
     if (c >= cols) {
-      x[i] = 0.f;
+      x[i] = static_cast<T>(0.f);
       continue;
     }
     int64_t grow = row0 + r;
@@ -98,7 +127,7 @@ __global__ void oap_synth_blobs(float* x, int64_t rows, int cols, int64_t ld, in
     uint64_t h2 = splitmix64(h1);
     float u1 = fmaxf(u01_24(h1), 1e-7f), u2 = u01_24(h2);
     float gauss = sqrtf(-2.f * logf(u1)) * cosf(6.2831853f * u2);
-    x[i] = center + sigma * gauss;
+    x[i] = static_cast<T>(center + sigma * gauss);
   }
 }
 
@@ -138,14 +167,15 @@ __global__ void oap_sum_f64(const double* in, int m, double* out) {
   if (threadIdx.x == 0) out[0] = v;
 }
 
-__global__ void oap_gather_rows(const float* x, int64_t ld, int cols, const int64_t* idx,
+template <typename T>
+__global__ void oap_gather_rows(const T* x, int64_t ld, int cols, const int64_t* idx,
                                 int64_t m, float* out) {
   const int64_t total = m * cols;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
        i += int64_t(gridDim.x) * blockDim.x) {
     int64_t r = i / cols;
     int c = static_cast<int>(i - r * cols);
-    out[i] = x[idx[r] * ld + c];
+    out[i] = static_cast<float>(x[idx[r] * ld + c]);
   }
 }
 
@@ -187,26 +217,48 @@ void convert_pad(const void* src, DType src_t, int64_t rows, int cols, int64_t s
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-void column_absmax(const float* x, int64_t rows, int cols, int64_t ld, float* out,
+void column_absmax(const void* xv, DType t, int64_t rows, int cols, int64_t ld, float* out,
                    hipStream_t s) {
   if (rows == 0) return;
-  if (ld % 4 == 0 && ld / 4 <= 256 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+  OAP_CHECK(t == DType::F32 || t == DType::BF16, "column_absmax: f32 or bf16 rows");
+  const bool aligned = (reinterpret_cast<uintptr_t>(xv) & 15) == 0;
+  const int grid = static_cast<int>(rows < 2048 ? rows : 2048);
+  if (t == DType::BF16) {
+    if (ld % 8 == 0 && ld / 8 <= 256 && aligned) {
+      hipLaunchKernelGGL(oap_column_absmax8_bf16, dim3(2048), dim3(256), 0, s,
+                         static_cast<const bf16x8*>(xv), rows, static_cast<int>(ld / 8), cols,
+                         out);
+    } else {
+      hipLaunchKernelGGL(oap_column_absmax<__bf16>, dim3(grid), dim3(256), 0, s,
+                         static_cast<const __bf16*>(xv), rows, cols, ld, out);
+    }
+    OAP_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const float* x = static_cast<const float*>(xv);
+  if (ld % 4 == 0 && ld / 4 <= 256 && aligned) {
     hipLaunchKernelGGL(oap_column_absmax4, dim3(2048), dim3(256), 0, s,
                        reinterpret_cast<const float4*>(x), rows, static_cast<int>(ld / 4), cols,
                        out);
     OAP_HIP_CHECK(hipGetLastError());
     return;
   }
-  int grid = static_cast<int>(rows < 2048 ? rows : 2048);
-  hipLaunchKernelGGL(oap_column_absmax, dim3(grid), dim3(256), 0, s, x, rows, cols, ld, out);
+  hipLaunchKernelGGL(oap_column_absmax<float>, dim3(grid), dim3(256), 0, s, x, rows, cols, ld,
+                     out);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-void synth_blobs(float* x, int64_t rows, int cols, int64_t ld, int64_t row0, int ncenters,
+void synth_blobs(void* x, DType t, int64_t rows, int cols, int64_t ld, int64_t row0, int ncenters,
                  float box, float sigma, uint64_t seed, hipStream_t s) {
   if (rows == 0) return;
-  hipLaunchKernelGGL(oap_synth_blobs, dim3(grid_for(rows * ld, 256)), dim3(256), 0, s, x, rows,
-                     cols, ld, row0, ncenters, box, sigma, seed);
+  OAP_CHECK(t == DType::F32 || t == DType::BF16, "synth_blobs: f32 or bf16 rows");
+  const dim3 grid(grid_for(rows * ld, 256));
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(oap_synth_blobs<__bf16>, grid, dim3(256), 0, s, static_cast<__bf16*>(x),
+                       rows, cols, ld, row0, ncenters, box, sigma, seed);
+  else
+    hipLaunchKernelGGL(oap_synth_blobs<float>, grid, dim3(256), 0, s, static_cast<float*>(x),
+                       rows, cols, ld, row0, ncenters, box, sigma, seed);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
@@ -236,11 +288,16 @@ void sum_f64(const double* in, int m, double* out, hipStream_t s) {
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-void gather_rows(const float* x, int64_t ld, int cols, const int64_t* idx, int64_t m, float* out,
-                 hipStream_t s) {
+void gather_rows(const void* x, DType t, int64_t ld, int cols, const int64_t* idx, int64_t m,
+                 float* out, hipStream_t s) {
   if (m == 0) return;
-  hipLaunchKernelGGL(oap_gather_rows, dim3(grid_for(m * cols, 256)), dim3(256), 0, s, x, ld,
-                     cols, idx, m, out);
+  const dim3 grid(grid_for(m * cols, 256));
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(oap_gather_rows<__bf16>, grid, dim3(256), 0, s,
+                       static_cast<const __bf16*>(x), ld, cols, idx, m, out);
+  else
+    hipLaunchKernelGGL(oap_gather_rows<float>, grid, dim3(256), 0, s,
+                       static_cast<const float*>(x), ld, cols, idx, m, out);
   OAP_HIP_CHECK(hipGetLastError());
 }
 

@@ -10,28 +10,32 @@ namespace oap {
 namespace kern {
 
 // ----------------------------------------------------------------------------- data layout
-// Row stride (elements) of the dense f32 tables the K-Means kernels read (multiple of 4, zero
-// padded) and the padded feature count of the centroid layout (multiple of 16 when d <= 128).
-int kmeans_ld(int d);
+// Row stride (elements) of the dense tables the K-Means kernels read (16-byte rows, zero padded:
+// a multiple of 4 for f32, of 8 for bf16) and the padded feature count of the centroid layout
+// (multiple of 16 when d <= 128).
+int kmeans_ld(int d, bool bf16 = false);
 int kmeans_dp(int d);
 // Dense ingestion: src rows (f64 or f32, row stride src_ld) -> dst rows (f32 / bf16 / f64, row
 // stride dst_ld, zero padded).  Both pointers are device pointers.
 void convert_pad(const void* src, DType src_t, int64_t rows, int cols, int64_t src_ld, void* dst,
                  DType dst_t, int64_t dst_ld, hipStream_t s);
 // Per-column max |x| over rows (atomicMax on the float bit pattern), out[cols] must be zeroed.
-void column_absmax(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s);
+// x is f32 or bf16 (t).
+void column_absmax(const void* x, DType t, int64_t rows, int cols, int64_t ld, float* out,
+                   hipStream_t s);
 // Deterministic synthetic Gaussian blobs (hash RNG): rows [row0, row0+rows) of a global dataset,
-// x = center[label] + sigma * N(0,1) with centers uniform in [-box, box]^cols.
-void synth_blobs(float* x, int64_t rows, int cols, int64_t ld, int64_t row0, int ncenters,
+// x = center[label] + sigma * N(0,1) with centers uniform in [-box, box]^cols, stored as f32 or
+// bf16 (t; bf16 = the f32 value rounded to nearest even).
+void synth_blobs(void* x, DType t, int64_t rows, int cols, int64_t ld, int64_t row0, int ncenters,
                  float box, float sigma, uint64_t seed, hipStream_t s);
 
 // Deterministic float sum: per-block partials into slab (returns #partials, <= 256).
 int reduce_sum_f32(const float* v, int64_t n, double* slab, hipStream_t s);
 // Sums in[0..m) in a fixed order into out[0].
 void sum_f64(const double* in, int m, double* out, hipStream_t s);
-// out[i][0..cols) = x[idx[i]][0..cols)
-void gather_rows(const float* x, int64_t ld, int cols, const int64_t* idx, int64_t m, float* out,
-                 hipStream_t s);
+// out[i][0..cols) = x[idx[i]][0..cols)   (x f32 or bf16)
+void gather_rows(const void* x, DType t, int64_t ld, int cols, const int64_t* idx, int64_t m,
+                 float* out, hipStream_t s);
 // Appends i to out_idx for every flag[i] != 0 (unordered; *counter zeroed by the caller).
 void compact_flags(const int32_t* flag, int64_t n, int64_t* out_idx, unsigned long long* counter,
                    hipStream_t s);
@@ -42,7 +46,8 @@ void bernoulli_select(const float* cost, int64_t n, int64_t row0, double factor,
 
 // ----------------------------------------------------------------------------- K-Means
 struct KMeansAssignArgs {
-  const float* x = nullptr;  // [n][ld] f32, ld = kmeans_ld(d)
+  const void* x = nullptr;  // [n][ld] f32 or bf16 (xbf16), ld = kmeans_ld(d, xbf16)
+  bool xbf16 = false;
   int64_t n = 0;
   int ld = 0;
   int d = 0;
@@ -73,10 +78,12 @@ int kmeans_lds_kmax(int d, bool precise);
 // Returns the number of blocks used (== entries written to cost_slab).
 int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s);
 int kmeans_cost_slab_size(int num_cus);
-// sums/counts += rows grouped by labels (fixed point; used after chunked assignment).
-void kmeans_accumulate(const float* x, int64_t n, int ld, int d, const int32_t* labels, int k,
-                       const float* scale, unsigned long long* sums, unsigned long long* counts,
-                       hipStream_t s);
+// sums/counts += rows grouped by labels (fixed point; used after chunked assignment).  Cluster
+// ranges are owned by workgroup groups that each keep their slice of the sums in LDS, so every
+// row element costs one LDS atomic instead of a global one (sums == nullptr: counts only).
+void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
+                       const int32_t* labels, int k, const float* scale,
+                       unsigned long long* sums, unsigned long long* counts, hipStream_t s);
 
 struct KMeansFinalizeArgs {
   const unsigned long long* sums = nullptr;  // global (allreduced) fixed-point sums [k][d]

@@ -7,9 +7,13 @@
 //   spark-3.1.1/mllib/clustering/KMeans.scala:306-330) and the tolerance test Σ(Δc)² <= tol²,
 //   evaluated redundantly on every rank — the reference needs a root merge plus a `converged`
 //   broadcast for this (KMeansDALImpl.cpp:101-130, :207-214).
-// * oap_kmeans_accumulate — label-driven fixed-point accumulation for the chunked large-k path.
+// * oap_kmeans_accumulate_owned — label-driven fixed-point accumulation for the chunked large-k
+//   path (cluster ranges owned by workgroup groups, sums in LDS).
 #include <hip/hip_runtime.h>
 
+#include <hip/hip_bf16.h>
+
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 
@@ -22,19 +26,21 @@ namespace kern {
 namespace {
 
 // Generic fallback (d > 128): one thread per row, VALU distances, global integer atomics.
+template <typename T>
 __global__ __launch_bounds__(256) void oap_kmeans_assign_generic(KMeansAssignArgs a, int dp) {
+  const T* x = static_cast<const T*>(a.x);
   __shared__ double wsum[4];
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   double my_cost = 0.0;
   for (int64_t row = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; row < a.n; row += stride) {
-    const float* xr = a.x + row * a.ld;
+    const T* xr = x + row * a.ld;
     float best = INFINITY;
     int bidx = 0;
     for (int c = 0; c < a.k; ++c) {
       const float* cr = a.centers + size_t(c) * dp;
       float acc = 0.f;
       for (int f = 0; f < a.d; ++f) {
-        const float df = xr[f] - cr[f];
+        const float df = static_cast<float>(xr[f]) - cr[f];
         acc = fmaf(df, df, acc);
       }
       if (acc < best) {
@@ -55,7 +61,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_assign_generic(KMeansAssignArg
     if (a.accumulate && !a.merge) {
       atomicAdd(&a.counts[bidx], 1ull);
       for (int f = 0; a.sums_too && f < a.d; ++f) {
-        const long long q = static_cast<long long>(rintf(xr[f] * a.scale[f]));
+        const long long q = static_cast<long long>(rintf(static_cast<float>(xr[f]) * a.scale[f]));
         atomicAdd(&a.sums[size_t(bidx) * a.d + f], static_cast<u64>(q));
       }
     }
@@ -70,9 +76,11 @@ __global__ __launch_bounds__(256) void oap_kmeans_assign_generic(KMeansAssignArg
   }
 }
 
-__global__ void oap_kmeans_accumulate(const float* x, int64_t n, int ld, int d,
-                                      const int32_t* labels, int k, const float* scale, u64* sums,
-                                      u64* counts) {
+// Label-driven accumulation, global-atomic fallback (rows wider than 64 x 16 bytes).
+template <typename T>
+__global__ void oap_kmeans_accumulate_global(const T* x, int64_t n, int ld, int d,
+                                             const int32_t* labels, int k, const float* scale,
+                                             u64* sums, u64* counts) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n * d; i += stride) {
     const int64_t row = i / d;
@@ -81,9 +89,107 @@ __global__ void oap_kmeans_accumulate(const float* x, int64_t n, int ld, int d,
     if (b < 0 || b >= k) continue;
     if (f == 0) atomicAdd(&counts[b], 1ull);
     if (!sums) continue;
-    const long long q = static_cast<long long>(rintf(x[row * ld + f] * scale[f]));
+    const long long q = static_cast<long long>(rintf(static_cast<float>(x[row * ld + f]) * scale[f]));
     atomicAdd(&sums[size_t(b) * d + f], static_cast<u64>(q));
   }
+}
+
+// Label-driven accumulation for the chunked (large-k) path, deterministic and LDS-resident.
+// The k clusters are split into G ranges of kg; block i serves range i % G over row slice i / G
+// (256 slices, so per-block partial sums obey the fixed-point bound of
+// kmeans_rows_per_block_bound).  A wave reads 64 labels, compacts the rows of its range into a
+// wave-private LDS list (ballot + popcount), then gathers those rows 16 bytes per lane — SEG
+// lanes cover one padded row, 64 / SEG rows per load instruction, U load groups in flight — and
+// adds rint(x * 2^e) into the range's fp64 LDS table (exact integers, so the atomic order cannot
+// change a bit).  Table layout: cluster stride `rs` (odd), segment stride EPS + 1 doubles, so
+// the SEG lanes of one row hit distinct banks.  One global int64 atomic per (cluster, feature)
+// per block at the end.  Replaces a global atomic per row element.
+constexpr int kAccThreads = 512;
+constexpr int kAccU = 4;
+template <typename T>
+__global__ __launch_bounds__(kAccThreads) void oap_kmeans_accumulate_owned(
+    const T* x, int64_t n, int ld, int d, const int32_t* labels, int k, int kg, int G, int rs,
+    const float* scale, u64* sums, u64* counts) {
+  constexpr int EPS = 16 / sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int g = blockIdx.x % G, b = blockIdx.x / G, B = gridDim.x / G;
+  const int c0 = g * kg, nk = min(k, c0 + kg) - c0;
+  double* acc = reinterpret_cast<double*>(smem);
+  const size_t acc_bytes = (size_t(kg) * rs * 8 + 15) / 16 * 16;
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + acc_bytes);
+  int* lists = reinterpret_cast<int*>(smem + acc_bytes + (size_t(kg) * 4 + 15) / 16 * 16);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < nk * rs; i += kAccThreads) acc[i] = 0.0;
+  for (int i = tid; i < nk; i += kAccThreads) cnt[i] = 0u;
+  __syncthreads();
+  const int SEG = ld * int(sizeof(T)) / 16, rpi = 64 / SEG;
+  const int slot = lane / SEG, seg = lane - slot * SEG;
+  const bool lane_ok = slot < rpi;
+  float sc[EPS];
+#pragma unroll
+  for (int j = 0; j < EPS; ++j) {
+    const int f = seg * EPS + j;
+    sc[j] = (sums && lane_ok && f < d) ? scale[f] : 0.f;
+  }
+  int* rows_l = lists + wave * 128;
+  int* cls_l = rows_l + 64;
+  const int64_t r0 = n * b / B, r1 = n * (b + 1) / B;
+  for (int64_t base = r0 + int64_t(wave) * 64; base < r1; base += int64_t(kAccThreads)) {
+    const int64_t row = base + lane;
+    int cl = -1;
+    if (row < r1) {
+      const int lab = labels[row];
+      if (static_cast<unsigned>(lab - c0) < static_cast<unsigned>(nk)) cl = lab - c0;
+    }
+    const u64 mask = __ballot(cl >= 0);
+    if (mask == 0) continue;
+    if (cl >= 0) {
+      const int pos = __popcll(mask & ((1ull << lane) - 1ull));
+      rows_l[pos] = lane;
+      cls_l[pos] = cl;
+      atomicAdd(&cnt[cl], 1u);
+    }
+    if (!sums) continue;
+    __builtin_amdgcn_wave_barrier();  // the list is written and read by this wave only
+    const int m = __popcll(mask);
+    for (int q0 = 0; q0 < m; q0 += rpi * kAccU) {
+      T v[kAccU][EPS];
+      int clq[kAccU];
+      bool ok[kAccU];
+#pragma unroll
+      for (int u = 0; u < kAccU; ++u) {
+        const int qi = q0 + u * rpi + slot;
+        ok[u] = lane_ok && qi < m;
+        clq[u] = 0;
+        if (ok[u]) {
+          clq[u] = cls_l[qi];
+          const T* p = x + (base + rows_l[qi]) * ld + seg * EPS;
+          const uint4 raw = *reinterpret_cast<const uint4*>(p);
+          __builtin_memcpy(&v[u][0], &raw, 16);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kAccU; ++u) {
+        if (!ok[u]) continue;
+        double* ap = acc + clq[u] * rs + seg * (EPS + 1);
+#pragma unroll
+        for (int j = 0; j < EPS; ++j)
+          if (seg * EPS + j < d)
+            atomicAdd(ap + j, static_cast<double>(rintf(static_cast<float>(v[u][j]) * sc[j])));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // list reads done before the next batch overwrites it
+  }
+  __syncthreads();
+  if (sums)
+    for (int i = tid; i < nk * d; i += kAccThreads) {
+      const int c = i / d, f = i - c * d;
+      const double v = acc[c * rs + (f / EPS) * (EPS + 1) + f % EPS];  // exact, |v| < 2^53
+      if (v != 0.0)
+        atomicAdd(&sums[size_t(c0 + c) * d + f], static_cast<u64>(static_cast<long long>(v)));
+    }
+  for (int i = tid; i < nk; i += kAccThreads)
+    if (cnt[i]) atomicAdd(&counts[c0 + i], static_cast<u64>(cnt[i]));
 }
 
 __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a) {
@@ -171,7 +277,7 @@ __global__ void oap_kmeans_prepare_centers(const double* c64, int k, int d, int 
 }  // namespace
 
 // --------------------------------------------------------------------------- host wrappers
-int kmeans_ld(int d) { return (d + 3) / 4 * 4; }
+int kmeans_ld(int d, bool bf16) { return bf16 ? (d + 7) / 8 * 8 : (d + 3) / 4 * 4; }
 int kmeans_dp(int d) { return d <= 128 ? (d + 15) / 16 * 16 : d; }
 int kmeans_cost_slab_size(int num_cus) { return num_cus > 8192 ? num_cus : 8192; }
 int kmeans_lds_kmax(int d, bool precise) { return kmeans_mfma_kmax(d, precise); }
@@ -184,14 +290,18 @@ int64_t kmeans_rows_per_block_bound(int64_t n) {
 
 int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s) {
   OAP_CHECK(a.kpad % 32 == 0 && a.kpad >= a.k, "kpad must be a multiple of 32 >= k");
-  OAP_CHECK(a.ld == kmeans_ld(a.d), "row stride " << a.ld << " != kmeans_ld(" << a.d << ")");
+  OAP_CHECK(a.ld == kmeans_ld(a.d, a.xbf16),
+            "row stride " << a.ld << " != kmeans_ld(" << a.d << ", " << a.xbf16 << ")");
   OAP_CHECK(!a.merge || (a.labels && a.mindist), "merge mode needs labels and mindist");
   if (a.n == 0) return 0;
   const int dp = kmeans_dp(a.d);
   const bool generic = a.d > 128 || a.kpad > kmeans_mfma_kmax(a.d, a.precise);
   if (generic) {
     const int grid = grid_for(a.n, 256, 4096);
-    hipLaunchKernelGGL(oap_kmeans_assign_generic, dim3(grid), dim3(256), 0, s, a, dp);
+    if (a.xbf16)
+      hipLaunchKernelGGL(oap_kmeans_assign_generic<__bf16>, dim3(grid), dim3(256), 0, s, a, dp);
+    else
+      hipLaunchKernelGGL(oap_kmeans_assign_generic<float>, dim3(grid), dim3(256), 0, s, a, dp);
     OAP_HIP_CHECK(hipGetLastError());
     return grid;
   }
@@ -200,12 +310,62 @@ int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s) {
   return grid;
 }
 
-void kmeans_accumulate(const float* x, int64_t n, int ld, int d, const int32_t* labels, int k,
-                       const float* scale, unsigned long long* sums, unsigned long long* counts,
-                       hipStream_t s) {
+void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
+                       const int32_t* labels, int k, const float* scale,
+                       unsigned long long* sums, unsigned long long* counts, hipStream_t s) {
   if (n == 0) return;
-  hipLaunchKernelGGL(oap_kmeans_accumulate, dim3(grid_for(n * d, 256)), dim3(256), 0, s, x, n, ld,
-                     d, labels, k, scale, sums, counts);
+  const int es = xbf16 ? 2 : 4, eps = 16 / es;
+  const int seg = ld * es / 16;
+  OAP_CHECK(ld * es % 16 == 0, "kmeans_accumulate: rows must be 16-byte multiples");
+  // LDS plan: [kg x rs] fp64 sums | [kg] counts | 8 waves x 128 ints of compaction lists
+  const size_t fixed = size_t(kAccThreads / 64) * 128 * 4 + 32;
+  int rs = 0, kg = k;
+  if (sums) {
+    rs = (seg * (eps + 1)) | 1;
+    kg = static_cast<int>((kLdsLimit - fixed) / (size_t(rs) * 8 + 4));
+  } else {
+    kg = static_cast<int>(std::min<size_t>(size_t(k), (kLdsLimit - fixed) / 4));
+  }
+  if (seg > 64 || kg < 1) {  // very wide rows: global atomics
+    const dim3 grid(grid_for(n * d, 256));
+    if (xbf16)
+      hipLaunchKernelGGL(oap_kmeans_accumulate_global<__bf16>, grid, dim3(256), 0, s,
+                         static_cast<const __bf16*>(x), n, ld, d, labels, k, scale, sums, counts);
+    else
+      hipLaunchKernelGGL(oap_kmeans_accumulate_global<float>, grid, dim3(256), 0, s,
+                         static_cast<const float*>(x), n, ld, d, labels, k, scale, sums, counts);
+    OAP_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const int G = (k + kg - 1) / kg;
+  kg = (k + G - 1) / G;
+  const size_t lds = (size_t(kg) * rs * 8 + 15) / 16 * 16 + (size_t(kg) * 4 + 15) / 16 * 16 +
+                     size_t(kAccThreads / 64) * 128 * 4;
+  OAP_CHECK(lds <= kLdsLimit, "kmeans_accumulate: LDS plan " << lds);
+  const dim3 grid(256 * G);  // 256 row slices per cluster range (fixed-point bound)
+  if (xbf16) {
+    static bool set = false;
+    if (!set) {
+      OAP_HIP_CHECK(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&oap_kmeans_accumulate_owned<__bf16>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
+      set = true;
+    }
+    hipLaunchKernelGGL(oap_kmeans_accumulate_owned<__bf16>, grid, dim3(kAccThreads), lds, s,
+                       static_cast<const __bf16*>(x), n, ld, d, labels, k, kg, G, rs, scale, sums,
+                       counts);
+  } else {
+    static bool set = false;
+    if (!set) {
+      OAP_HIP_CHECK(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&oap_kmeans_accumulate_owned<float>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
+      set = true;
+    }
+    hipLaunchKernelGGL(oap_kmeans_accumulate_owned<float>, grid, dim3(kAccThreads), lds, s,
+                       static_cast<const float*>(x), n, ld, d, labels, k, kg, G, rs, scale, sums,
+                       counts);
+  }
   OAP_HIP_CHECK(hipGetLastError());
 }
 

@@ -25,7 +25,8 @@
 //   bit.  The flush converts to int64 and adds across workgroups, ranks (RCCL) in integer
 //   arithmetic: results are bitwise identical for any schedule and any world size.
 // * Persistent grid (>= 256 workgroups of 512 threads, one per CU: 2 waves per SIMD so one wave's
-//   VALU epilogue overlaps the other's MFMAs), register prefetch of the next tile.
+//   VALU epilogue overlaps the other's MFMAs), register prefetch two tiles ahead.
+// * f32 or bf16 row storage (bf16: half the HBM bytes, 2 MFMAs per k-step, exact operands).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -80,11 +81,27 @@ __device__ inline int med3_i32(int a, int b, int c) {
   return r;
 }
 
-// Exact fp32 argmin over kpad centroids for the lane's row (both halves get the result).
+// The lane's slice of one 32-row tile: features f = 16s + 8h + j (s < KS, j < 8) of row r.
+// f32 tables keep the fp32 values; bf16 tables keep the raw bf16 vectors, which are already
+// the MFMA B operand (and exact: bf16 -> fp32 is a shift).
+template <int KS, bool XB>
+struct Frag;
 template <int KS>
-__device__ inline void exact_argmin(const float* __restrict__ cbase, int stride,
-                                    const float (&x)[KS][8], const float* __restrict__ cn,
-                                    int kpad, int d, int r, int h, int& bidx) {
+struct Frag<KS, false> {
+  float v[KS][8];
+  __device__ float at(int s, int j) const { return v[s][j]; }
+};
+template <int KS>
+struct Frag<KS, true> {
+  bf16x8 v[KS];
+  __device__ float at(int s, int j) const { return static_cast<float>(v[s][j]); }
+};
+
+// Exact fp32 argmin over kpad centroids for the lane's row (both halves get the result).
+template <int KS, class F>
+__device__ inline void exact_argmin(const float* __restrict__ cbase, int stride, const F& x,
+                                    const float* __restrict__ cn, int kpad, int d, int r, int h,
+                                    int& bidx) {
   float best = INFINITY;
   bidx = 0x7fffffff;
   for (int c0 = 0; c0 < kpad; c0 += 32) {
@@ -96,10 +113,10 @@ __device__ inline void exact_argmin(const float* __restrict__ cbase, int stride,
       for (int q = 0; q < 2; ++q) {
         if (16 * s + 4 * q < d) {  // wave-uniform: skip all-padding groups
           float4 a4 = *reinterpret_cast<const float4*>(cp + 16 * s + 4 * q);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, x[s][4 * q + 0], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, x[s][4 * q + 1], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, x[s][4 * q + 2], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, x[s][4 * q + 3], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, x.at(s, 4 * q + 0), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, x.at(s, 4 * q + 1), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, x.at(s, 4 * q + 2), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, x.at(s, 4 * q + 3), acc, 0, 0, 0);
         }
       }
     }
@@ -137,12 +154,23 @@ __device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8
     }
 }
 
-// BIAS (fast path, d + 2 <= 16*KS): two padding features carry the norms through the MFMAs —
-// x' = [x, 1, |x|^2], c' = [-2c, |c|^2, 1] — so accumulators start at zero and the chunk loop
-// reads only the operand fragments from LDS (no norm loads / seeding VALU).
-template <int KS, bool PRECISE, bool LDSACC, bool BIAS>
+// BIAS (fast path): padding features carry the norms through the MFMAs so accumulators start at
+// zero and the chunk loop reads only the operand fragments from LDS (no norm loads / seeding
+// VALU).  f32 rows: x' = [x, 1, |x|^2], c' = [-2c, |c|^2, 1] (d + 2 <= 16*KS; |x|^2 is split
+// hi/lo like every other feature).  bf16 rows: x' = [x, 1, hi(|x|^2), lo(|x|^2)],
+// c' = [-2c, |c|^2, 1, 1] (d + 3 <= 16*KS) — x is exact in bf16, so each k-step needs only the
+// two products x c_hi + x c_lo.
+//
+// XB (bf16 storage): rows are bf16 (row stride a.ld elements, multiple of 8).  Half the HBM
+// bytes of f32 and 2 instead of 3 MFMAs per k-step; the refinement bound of the f32 split still
+// holds (the bf16 products have strictly less error), so assignments equal an exact fp32
+// evaluation of the bf16 data.
+template <int KS, bool PRECISE, bool LDSACC, bool BIAS, bool XB>
 __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
+  // Register budget: three rotating tiles (prefetch two ahead) when they fit, else two.
+  constexpr bool DEEP = XB || KS <= 4;
+  using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
   const Smem L = smem_plan(DP, kpad, k, d, PRECISE, LDSACC, a.sums_too);
@@ -170,6 +198,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       float w = -2.f * v;  // exact scaling: split(-2c) == -2 split(c)
       if (BIAS && f == d) w = (c < k) ? a.cnorm[c] : 1e30f;
       if (BIAS && f == d + 1) w = 1.f;
+      if (BIAS && XB && f == d + 2) w = 1.f;
       bf16_split(w, hi, lo);
       ph[c * sb + f] = hi;
       pl[c * sb + f] = lo;
@@ -198,14 +227,13 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   double my_cost = 0.0;
 
   // ---- per-row epilogue: exact cost, outputs, fixed-point accumulation
-  auto finish = [&](const float (&xv)[KS][8], const float (&cv)[KS][8], int b, int64_t row,
-                    bool valid) {
+  auto finish = [&](const F& xv, const float (&cv)[KS][8], int b, int64_t row, bool valid) {
     float part = 0.f;  // padded features are zero in both operands
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float e = xv[s][j] - cv[s][j];
+          const float e = xv.at(s, j) - cv[s][j];
           part = fmaf(e, e, part);
         }
     const float rowcost = part + __shfl_xor(part, 32, 64);
@@ -237,12 +265,13 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         if (s < KS - 1 || d == DP) {
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv[s][j] * scv[j])));
+            atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv.at(s, j) * scv[j])));
         } else {
           const int nv = d - f0;  // real features of this lane's half of the last k-step
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (j < nv) atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv[s][j] * scv[j])));
+            if (j < nv)
+              atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv.at(s, j) * scv[j])));
         }
       }
     } else {
@@ -255,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
           for (int j = 0; j < 8; ++j) {
             const int f = 16 * s + 8 * h + j;
             if (f < d) {
-              const long long qv = static_cast<long long>(rintf(xv[s][j] * sc_l[f]));
+              const long long qv = static_cast<long long>(rintf(xv.at(s, j) * sc_l[f]));
               atomicAdd(gp + f, static_cast<u64>(qv));
             }
           }
@@ -269,35 +298,50 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 
   // Rows past n are clamped to row n-1 (their results are discarded, nothing needs zeroing);
   // only the last k-step can reach past the row stride, and it is zero-filled there.
-  auto load_tile = [&](int64_t tt, float (&dst)[KS][8]) {
+  auto load_tile = [&](int64_t tt, F& dst) {
     int64_t row = tt * 32 + r;
     row = row < a.n ? row : a.n - 1;
-    const float* p = a.x + row * a.ld + 8 * h;
+    if constexpr (XB) {
+      const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int f = 16 * s + 8 * h + 4 * q;
-        float4 v;
+      for (int s = 0; s < KS; ++s) {
+        const int f = 16 * s + 8 * h;
         if (s < KS - 1 || f < a.ld)
-          v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+          dst.v[s] = *reinterpret_cast<const bf16x8*>(p + 16 * s);
         else
-          v = make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[s][4 * q + 0] = v.x;
-        dst[s][4 * q + 1] = v.y;
-        dst[s][4 * q + 2] = v.z;
-        dst[s][4 * q + 3] = v.w;
+          dst.v[s] = bf16x8{};
       }
+    } else {
+      const float* p = static_cast<const float*>(a.x) + row * a.ld + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int f = 16 * s + 8 * h + 4 * q;
+          float4 v;
+          if (s < KS - 1 || f < a.ld)
+            v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+          else
+            v = make_float4(0.f, 0.f, 0.f, 0.f);
+          dst.v[s][4 * q + 0] = v.x;
+          dst.v[s][4 * q + 1] = v.y;
+          dst.v[s][4 * q + 2] = v.z;
+          dst.v[s][4 * q + 3] = v.w;
+        }
+    }
   };
 
-  // One tile: `x` holds its rows (loaded one tile earlier), `xn` receives the next tile's prefetch.
-  // The loop below alternates two named buffers, so no register copies are needed.
-  auto process = [&](const int64_t t, float (&x)[KS][8], float (&xn)[KS][8]) {
+  // One tile: `x` holds its rows, `xn` receives the prefetch of tile `pf`.  DEEP: pf is two
+  // tiles ahead and issued AFTER this tile's c_best loads — vmcnt retires in issue order, so
+  // waiting for c_best never waits for the freshly issued prefetch, and each prefetch has about
+  // two tile-times to land.  Otherwise pf is the next tile, issued before the MFMAs.  The loops
+  // below rotate named buffers, so no register copies are needed.
+  auto process = [&](const int64_t t, F& x, F& xn, const int64_t pf) {
     const int64_t row = t * 32 + r;
     const bool valid = row < a.n;
     int bidx;
     if constexpr (PRECISE) {
-      load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
+      load_tile(pf, xn);  // prefetch, hidden behind this tile's MFMAs
       if (a.ablate & 8)
         bidx = r % k;  // timing ablation: no distance work
       else
@@ -314,30 +358,48 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       }
       finish(x, cb, bidx, row, valid);
     } else {
-      // split the row into bf16 hi/lo MFMA operands (the fp32 copy stays live for the epilogue)
-      bf16x8 xh[KS], xl[KS];
+      // MFMA B operands: f32 rows are split into bf16 hi/lo (the fp32 copy stays live for the
+      // epilogue); bf16 rows are used as they are.
+      bf16x8 xh[KS], xl[XB ? 1 : KS];
       float nx2 = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) nx2 = fmaf(x[s][j], x[s][j], nx2);
+        for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += __shfl_xor(nx2, 32, 64);
       const int jb = d - 16 * (KS - 1) - 8 * h;  // lane-local slot of bias feature d (if in range)
+      if constexpr (XB) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
+        for (int s = 0; s < KS - 1; ++s) xh[s] = x.v[s];
+        bf16x8 last = x.v[KS - 1];
+        if constexpr (BIAS) {
+          __bf16 nh, nl;
+          bf16_split(nx2, nh, nl);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float v = x[s][j];
-          if (BIAS && s == KS - 1) {
-            v = (j == jb) ? 1.f : v;
-            v = (j == jb + 1) ? nx2 : v;
+          for (int j = 0; j < 8; ++j) {
+            last[j] = (j == jb) ? static_cast<__bf16>(1.f) : last[j];
+            last[j] = (j == jb + 1) ? nh : last[j];
+            last[j] = (j == jb + 2) ? nl : last[j];
           }
-          __bf16 hi, lo;
-          bf16_split(v, hi, lo);
-          xh[s][j] = hi;
-          xl[s][j] = lo;
         }
-      load_tile(t + stride, xn);  // prefetch, hidden behind this tile's MFMAs
+        xh[KS - 1] = last;
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            float v = x.v[s][j];
+            if (BIAS && s == KS - 1) {
+              v = (j == jb) ? 1.f : v;
+              v = (j == jb + 1) ? nx2 : v;
+            }
+            __bf16 hi, lo;
+            bf16_split(v, hi, lo);
+            xh[s][j] = hi;
+            xl[s][j] = lo;
+          }
+      }
+      if constexpr (!DEEP) load_tile(pf, xn);  // prefetch, hidden behind this tile's MFMAs
 
       // Accumulators are seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
       // ends at |x - c|^2.  Top-2 tracking runs on integer KEYS: the float's bits with the low 10
@@ -374,15 +436,14 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], f32x16{}, 0, 0, 0);
           else
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xl[s], acc, 0, 0, 0);
+          if constexpr (!XB)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xl[s], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], xh[s], acc, 0, 0, 0);
         }
       };
       auto epilogue = [&](int c0, const f32x16& acc) {
         // chunk-local keys carry the in-chunk offset 8(e>>2)+(e&3) (an inline constant: one
-        // v_bfi_b32 per candidate); the lane's chunk base c0+4h is OR-ed in once per chunk.
-        // Keys stay floats (the index only perturbs the low mantissa bits), so the top-2 update
-        // is v_min_f32 + v_med3_f32: 3 VALU per candidate.
+        // v_and_or_b32 per candidate); the lane's chunk base c0+4h is OR-ed in once per chunk.
         // Keys are compared as signed ints (same order as the floats for the non-negative
         // distances; a tiny negative from rounding only ever looks like a near tie, which the
         // exact pass re-decides).  Integer min / med3 avoid the NaN canonicalisation that float
@@ -461,16 +522,30 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
           for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
       }
+      if constexpr (DEEP) load_tile(pf, xn);  // younger than the c_best loads (see above)
       finish(x, cb, bidx, row, valid);
     }
   };
 
-  float xa[KS][8], xb[KS][8];
-  load_tile(t, xa);
-  for (; t < ntiles; t += 2 * stride) {  // t is wave-uniform: both branches stay uniform
-    process(t, xa, xb);
-    if (t + stride >= ntiles) break;
-    process(t + stride, xb, xa);
+  if constexpr (DEEP) {
+    F xa, xb, xc;
+    load_tile(t, xa);
+    load_tile(t + stride, xb);
+    for (; t < ntiles; t += 3 * stride) {  // t is wave-uniform: every branch stays uniform
+      process(t, xa, xc, t + 2 * stride);
+      if (t + stride >= ntiles) break;
+      process(t + stride, xb, xa, t + 3 * stride);
+      if (t + 2 * stride >= ntiles) break;
+      process(t + 2 * stride, xc, xb, t + 4 * stride);
+    }
+  } else {
+    F xa, xb;
+    load_tile(t, xa);
+    for (; t < ntiles; t += 2 * stride) {
+      process(t, xa, xb, t + stride);
+      if (t + stride >= ntiles) break;
+      process(t + stride, xb, xa, t + 2 * stride);
+    }
   }
 
   // ---- deterministic per-block cost: fixed shuffle tree, waves in index order
@@ -495,32 +570,48 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   }
 }
 
-template <int KS, bool P, bool LA, bool B>
+template <int KS, bool P, bool LA, bool B, bool XB>
 void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA, a.sums_too);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA, B>),
+        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA, B, XB>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA, B>), dim3(grid), dim3(kThreads), L.total, s,
-                     a);
+  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA, B, XB>), dim3(grid), dim3(kThreads),
+                     L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-template <int KS>
+template <int KS, bool XB>
 void launch_ks(const KMeansAssignArgs& a, int grid, hipStream_t s, bool lds_acc) {
   if (a.precise) {
-    if (lds_acc) launch3<KS, true, true, false>(a, grid, s);
-    else launch3<KS, true, false, false>(a, grid, s);
-  } else if (a.d + 2 <= 16 * KS) {
-    if (lds_acc) launch3<KS, false, true, true>(a, grid, s);
-    else launch3<KS, false, false, true>(a, grid, s);
+    if (lds_acc) launch3<KS, true, true, false, XB>(a, grid, s);
+    else launch3<KS, true, false, false, XB>(a, grid, s);
+  } else if (a.d + (XB ? 3 : 2) <= 16 * KS) {
+    if (lds_acc) launch3<KS, false, true, true, XB>(a, grid, s);
+    else launch3<KS, false, false, true, XB>(a, grid, s);
   } else {
-    if (lds_acc) launch3<KS, false, true, false>(a, grid, s);
-    else launch3<KS, false, false, false>(a, grid, s);
+    if (lds_acc) launch3<KS, false, true, false, XB>(a, grid, s);
+    else launch3<KS, false, false, false, XB>(a, grid, s);
+  }
+}
+
+template <bool XB>
+void launch_xb(const KMeansAssignArgs& a, int grid, hipStream_t s, bool lds_acc) {
+  const int dp = (a.d + 15) / 16 * 16;
+  switch (dp / 16) {
+    case 1: launch_ks<1, XB>(a, grid, s, lds_acc); break;
+    case 2: launch_ks<2, XB>(a, grid, s, lds_acc); break;
+    case 3: launch_ks<3, XB>(a, grid, s, lds_acc); break;
+    case 4: launch_ks<4, XB>(a, grid, s, lds_acc); break;
+    case 5: launch_ks<5, XB>(a, grid, s, lds_acc); break;
+    case 6: launch_ks<6, XB>(a, grid, s, lds_acc); break;
+    case 7: launch_ks<7, XB>(a, grid, s, lds_acc); break;
+    case 8: launch_ks<8, XB>(a, grid, s, lds_acc); break;
+    default: OAP_THROW(ConfigError, "kmeans_assign: unsupported d=" << a.d);
   }
 }
 
@@ -547,17 +638,10 @@ void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t 
   const bool acc = a.accumulate && !a.merge;
   const bool lds_acc =
       acc && smem_plan(dp, a.kpad, a.k, a.d, a.precise, true, a.sums_too).total <= kLdsLimit;
-  switch (dp / 16) {
-    case 1: launch_ks<1>(a, grid, s, lds_acc); break;
-    case 2: launch_ks<2>(a, grid, s, lds_acc); break;
-    case 3: launch_ks<3>(a, grid, s, lds_acc); break;
-    case 4: launch_ks<4>(a, grid, s, lds_acc); break;
-    case 5: launch_ks<5>(a, grid, s, lds_acc); break;
-    case 6: launch_ks<6>(a, grid, s, lds_acc); break;
-    case 7: launch_ks<7>(a, grid, s, lds_acc); break;
-    case 8: launch_ks<8>(a, grid, s, lds_acc); break;
-    default: OAP_THROW(ConfigError, "kmeans_assign: unsupported d=" << a.d);
-  }
+  if (a.xbf16)
+    launch_xb<true>(a, grid, s, lds_acc);
+  else
+    launch_xb<false>(a, grid, s, lds_acc);
 }
 
 }  // namespace kern

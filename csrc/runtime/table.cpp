@@ -23,6 +23,16 @@ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 float u01(uint64_t h) { return static_cast<float>(h >> 40) * (1.0f / 16777216.0f); }
+// float -> nearest-even bf16 -> float (the device's __bf16 conversion for finite values)
+float bf16_round(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  u &= 0xffff0000u;
+  float o;
+  std::memcpy(&o, &u, 4);
+  return o;
+}
 }  // namespace
 
 DenseTable upload_dense(Context& ctx, const void* host, DType src_t, int64_t rows, int cols,
@@ -93,18 +103,21 @@ DenseTable upload_dense(Context& ctx, const void* host, DType src_t, int64_t row
 }
 
 DenseTable synth_blobs_table(Context& ctx, int64_t rows, int cols, int64_t ld, int64_t row0,
-                             int ncenters, double box, double sigma, uint64_t seed) {
+                             int ncenters, double box, double sigma, uint64_t seed,
+                             DType storage) {
+  OAP_CHECK(storage == DType::F32 || storage == DType::BF16,
+            "synth_blobs: storage must be f32 or bf16");
   DenseTable t;
   t.rows = rows;
   t.cols = cols;
   t.ld = ld;
   t.backend = ctx.backend();
-  TraceRange tr(&ctx.metrics(), "ingest/synth_blobs", int64_t(rows) * ld * 4);
+  TraceRange tr(&ctx.metrics(), "ingest/synth_blobs", int64_t(rows) * ld * dtype_size(storage));
   if (ctx.is_gpu()) {
-    t.dtype = DType::F32;
+    t.dtype = storage;
     ctx.activate();
     t.data = ctx.alloc(t.bytes() == 0 ? 256 : t.bytes());
-    kern::synth_blobs(t.data.as<float>(), rows, cols, ld, row0, ncenters, float(box),
+    kern::synth_blobs(t.data.data(), storage, rows, cols, ld, row0, ncenters, float(box),
                       float(sigma), seed, ctx.compute());
     OAP_HIP_CHECK(hipStreamSynchronize(ctx.compute()));
     return t;
@@ -129,7 +142,8 @@ DenseTable synth_blobs_table(Context& ctx, int64_t rows, int cols, int64_t ld, i
         uint64_t h2 = splitmix64(h1);
         float u1 = std::fmax(u01(h1), 1e-7f), u2 = u01(h2);
         float g = std::sqrt(-2.f * std::log(u1)) * std::cos(6.2831853f * u2);
-        x[size_t(r) * ld + c] = double(center + float(sigma) * g);
+        const float v = center + float(sigma) * g;
+        x[size_t(r) * ld + c] = storage == DType::BF16 ? double(bf16_round(v)) : double(v);
       }
     }
   });
@@ -152,10 +166,10 @@ std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t
   if (!t.local_absmax.empty()) {
     mx = t.local_absmax;
   } else if (ctx.is_gpu()) {
-    OAP_CHECK(t.dtype == DType::F32, "column_absmax expects an f32 table");
     Buffer d = ctx.alloc(sizeof(float) * t.cols);
     ctx.memset(d.data(), 0, sizeof(float) * t.cols);
-    kern::column_absmax(t.data.as<float>(), t.rows, t.cols, t.ld, d.as<float>(), ctx.compute());
+    kern::column_absmax(t.data.data(), t.dtype, t.rows, t.cols, t.ld, d.as<float>(),
+                        ctx.compute());
     std::vector<float> h(t.cols);
     ctx.copy_to_host(h.data(), d.data(), sizeof(float) * t.cols);
     for (int c = 0; c < t.cols; ++c) mx[c] = h[c];

@@ -34,9 +34,11 @@ DenseTable upload_dense(Context& ctx, const void* host, DType src_t, int64_t row
                         int64_t src_ld, DType storage, int64_t ld, int64_t chunk_rows = 1 << 18);
 
 // Deterministic synthetic Gaussian blobs generated directly on the backend (rows
-// [row0, row0+rows) of a global dataset; identical values for any sharding).
+// [row0, row0+rows) of a global dataset; identical values for any sharding).  `storage` F32 or
+// BF16 (GPU: the table's dtype; CPU: f64 storage of the same f32 / bf16-rounded values).
 DenseTable synth_blobs_table(Context& ctx, int64_t rows, int cols, int64_t ld, int64_t row0,
-                             int ncenters, double box, double sigma, uint64_t seed);
+                             int ncenters, double box, double sigma, uint64_t seed,
+                             DType storage = DType::F32);
 
 // Fills global_offset / global_rows with an allgather of local row counts.
 void assign_global_offsets(Context& ctx, Comm& comm, DenseTable& t);

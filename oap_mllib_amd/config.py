@@ -32,7 +32,8 @@ class Config:
     hbm_fraction: float = 0.92
     #: host threads of the native CPU engine (0 = min(cores, 16))
     cpu_threads: int = 0
-    #: storage dtype for dense GPU tables: "f32" or "bf16"
+    #: storage dtype of GPU K-Means tables: "f32" or "bf16" (bf16 halves HBM bytes and uses 2
+    #: instead of 3 MFMA products; assignments stay exact for the bf16 values)
     storage_dtype: str = "f32"
     #: collective watchdog (seconds); <= 0 disables
     comm_timeout_s: float = 600.0

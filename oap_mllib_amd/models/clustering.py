@@ -183,10 +183,13 @@ def upload_table(w, X: np.ndarray, layout: str = "kmeans"):
     N = _loader.load()
     d = X.shape[1]
     if w.is_gpu:
-        ld = N.kmeans_ld(d) if layout == "kmeans" else d
+        st = w.config.storage_dtype
+        if layout == "kmeans":
+            ld = N.kmeans_ld(d, st)
+        else:
+            st, ld = "f32", d  # PCA reads f32 rows
         src = X if X.dtype in (np.float32, np.float64) else X.astype(np.float64)
-        return N.upload_dense(w.ctx, np.ascontiguousarray(src), w.config.storage_dtype
-                              if layout != "kmeans" else "f32", ld)
+        return N.upload_dense(w.ctx, np.ascontiguousarray(src), st, ld)
     return N.upload_dense(w.ctx, np.ascontiguousarray(X, dtype=np.float64), "f64", d)
 
 

@@ -159,3 +159,74 @@ def test_many_centroids_chunked_path(gpu_world, native):
     rc = native.kmeans_fit(c, native.LocalComm(False), tc, C, k, 2, 0.0)
     assert r["last_counts"] == rc["last_counts"]
     assert np.array_equal(r["centers"], rc["centers"])
+
+
+def bf16_round(X):
+    """Round-to-nearest-even to bf16, returned as float64 (what a bf16 table stores)."""
+    u = np.ascontiguousarray(X, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+@pytest.mark.parametrize("d,k", [(50, 200), (100, 1000), (13, 9), (128, 40), (100, 64)])
+def test_bf16_table_fit_bitwise_equals_cpu_engine(native, d, k):
+    """bf16 storage: exact fp32 assignments of the bf16 values => the CPU engine's integers.
+    Covers the LDS-resident path, the chunked large-k path (k=1000: balanced centroid chunks +
+    cluster-range-owned LDS accumulation) and the non-bias / wide-row variants."""
+    rng = np.random.default_rng(3 * d + k)
+    C = rng.uniform(-10, 10, size=(k, d))
+    n = 30000
+    X = bf16_round(C[rng.integers(0, k, n)] + rng.normal(0, 0.3, size=(n, d)))
+    init = bf16_round(C + rng.normal(0, 0.05, size=C.shape))
+    g, c = native.Context(0, 0.5, 0), native.Context(-1)
+    tg = native.upload_dense(g, X, "bf16", native.kmeans_ld(d, "bf16"))
+    np.testing.assert_array_equal(tg.to_numpy(g, 0, 64), X[:64])  # rounding == device cast
+    tc = native.upload_dense(c, X, "f64", d)
+    rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, 4, 0.0)
+    rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, 4, 0.0)
+    assert rg["last_counts"] == rc["last_counts"]
+    assert np.array_equal(rg["centers"], rc["centers"])
+    np.testing.assert_allclose(rg["cost"], rc["cost"], rtol=1e-5)
+    lab, dist = native.kmeans_predict(g, tg, rg["centers"])
+    ref_lab, ref_d = vanilla.find_closest(X, rg["centers"])
+    assert (lab == ref_lab).mean() > 0.9999
+    np.testing.assert_allclose(dist[lab == ref_lab], ref_d[lab == ref_lab], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("d,k", [(50, 200), (100, 60)])
+def test_bf16_fast_path_bitwise_equals_precise(native, d, k):
+    X = bf16_round(f32_blobs(60000, d, k, seed=d + 3 * k, sigma=3.0, box=4.0))
+    init = X[np.random.default_rng(6).choice(len(X), k, replace=False)]
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X, "bf16", native.kmeans_ld(d, "bf16"))
+    rf = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 3, 0.0, precise=False)
+    rp = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 3, 0.0, precise=True)
+    assert rf["last_counts"] == rp["last_counts"]
+    assert np.array_equal(rf["centers"], rp["centers"])
+
+
+def test_bf16_synth_matches_cpu_generator(native):
+    g, c = native.Context(0, 0.5, 0), native.Context(-1)
+    tg = native.synth_blobs(g, 3000, 100, native.kmeans_ld(100, "bf16"), 500, 11, 10.0, 1.0, 9,
+                            "bf16")
+    tc = native.synth_blobs(c, 3000, 100, 100, 500, 11, 10.0, 1.0, 9, "bf16")
+    a, b = tg.to_numpy(g), tc.to_numpy(c)
+    assert np.array_equal(bf16_round(a), a)
+    # device and host libm may differ in the last float ulp before rounding to bf16
+    assert np.mean(a == b) > 0.999
+    np.testing.assert_allclose(a, b, rtol=1e-2, atol=1e-2)
+
+
+def test_api_bf16_storage():
+    """KMeans estimator with bf16 storage through the public API."""
+    X = f32_blobs(20000, 24, 8, seed=12)
+    O.shutdown_world()
+    O.init_world(O.get_config().replace(device="gpu", device_id=0, storage_dtype="bf16"), rank=0,
+                 size=1, local_rank=0)
+    try:
+        m = O.KMeans(k=8, seed=2).fit(X)
+        assert m.fit_info["engine"] == "gpu"
+        ref = vanilla.fit(bf16_round(X), 8, 20, 1e-4, init_centers=None, seed=2)
+        assert abs(m.summary.trainingCost - ref.cost) / ref.cost < 1e-3
+    finally:
+        O.shutdown_world()

@@ -16,7 +16,10 @@ reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 d, k = 50, 200
 g = N.Context(0, 0.9, 0)
 t = N.synth_blobs(g, rows, d, N.kmeans_ld(d), 0, k, 10.0, 1.0, 20240917)
-C = t.to_numpy(g, 0, k)
+# centers as in the benchmark: k-means|| init + 2 Lloyd iterations (the fast path's refinement
+# rate depends on them; raw data rows as centers would force near ties)
+comm = N.LocalComm()
+C = N.kmeans_fit(g, comm, t, None, k, 2, -1.0, "k-means||", 2, 7)["centers"]
 out = {}
 for name, precise, ab in [("full", False, 0), ("no_accumulate", False, 1), ("no_cost", False, 2),
                           ("no_acc_no_cost", False, 3), ("no_distance", False, 8),
