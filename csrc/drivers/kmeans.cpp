@@ -210,6 +210,9 @@ struct AssignReq {
   float* mindist = nullptr;   // device, optional
   double* cost_slab = nullptr;
   u64* refine_tiles = nullptr;
+  // chunked path: `labels` already holds the previous assignment (a Lloyd iteration > 0), so
+  // the merge passes start from its exact distance
+  bool labels_valid = false;
 };
 
 // Returns the number of cost partials written to req.cost_slab.
@@ -255,6 +258,15 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   a.mindist = mind;
   a.accumulate = false;
   a.cost_slab = nullptr;
+  // Every chunk runs in merge mode against the row's best exact (cost, index) so far: seeded
+  // with the previous assignment's distance when there is one (most rows keep their label, so
+  // chunks that cannot win skip the exact re-decision of their own near ties), else +huge.
+  if (req.labels_valid && req.labels) {
+    kern::kmeans_seed_mindist(a, s);
+  } else {
+    OAP_HIP_CHECK(hipMemsetAsync(mind, 0x7f, sizeof(float) * x.rows, s));  // 3.4e38, finite
+    OAP_HIP_CHECK(hipMemsetAsync(labels, 0, sizeof(int32_t) * x.rows, s));
+  }
   // balanced chunks: ceil(k / kmax) launches of equal 32-multiples (no thin last pass)
   const int nchunks = (g.k + kmax - 1) / kmax;
   const int csize = static_cast<int>(round_up((g.k + nchunks - 1) / nchunks, 32));
@@ -265,7 +277,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.k = kc;
     a.kpad = static_cast<int>(round_up(kc, 32));
     a.base = c;
-    a.merge = c > 0;
+    a.merge = true;
     kern::kmeans_assign(a, ctx.info().cu_count, s);
   }
   if (req.accumulate)
@@ -729,6 +741,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   req.counts = counts;
   req.cost_slab = slab.as<double>();
   req.refine_tiles = refine_d.as<u64>();
+  // chunked (large-k) path: labels/mindist persist across iterations to seed the merge passes
+  Buffer lab_keep, mind_keep;
+  if (x.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x.cols, p.precise) && x.rows > 0) {
+    lab_keep = ctx.alloc(sizeof(int32_t) * x.rows);
+    mind_keep = ctx.alloc(sizeof(float) * x.rows);
+    req.labels = lab_keep.as<int32_t>();
+    req.mindist = mind_keep.as<float>();
+  }
 
   kern::KMeansFinalizeArgs fa;
   fa.sums = sums;
@@ -753,6 +773,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     roctx_push("kmeans/iteration");
     e0.record(s);
     OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
+    req.labels_valid = it > 0;
     int nb = gpu_assign(ctx, x, g, req, s);
     if (nb > 0)
       kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);

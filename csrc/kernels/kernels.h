@@ -77,6 +77,9 @@ int64_t kmeans_rows_per_block_bound(int64_t n);
 int kmeans_lds_kmax(int d, bool precise);
 // Returns the number of blocks used (== entries written to cost_slab).
 int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s);
+// Chunked path (d <= 128): mindist[i] = |x_i - centers[labels[i]]|^2, bitwise as the assign
+// kernel computes it, so later merge passes can skip chunks that cannot beat it.
+void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s);
 int kmeans_cost_slab_size(int num_cus);
 // sums/counts += rows grouped by labels (fixed point; used after chunked assignment).  Cluster
 // ranges are owned by workgroup groups that each keep their slice of the sums in LDS, so every

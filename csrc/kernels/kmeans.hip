@@ -310,6 +310,10 @@ int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s) {
   return grid;
 }
 
+void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
+  launch_kmeans_seed_mindist(a, s);
+}
+
 void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
                        const int32_t* labels, int k, const float* scale,
                        unsigned long long* sums, unsigned long long* counts, hipStream_t s) {

@@ -240,7 +240,9 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     if (!valid) return;
     if (h == 0) {
       if (a.merge) {
-        if (rowcost < a.mindist[row]) {
+        // (cost, index) order: lowest index wins exact ties whatever the chunk order / seed
+        const float md = a.mindist[row];
+        if (rowcost < md || (rowcost == md && a.base + b < a.labels[row])) {
           a.mindist[row] = rowcost;
           a.labels[row] = a.base + b;
         }
@@ -358,6 +360,10 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       }
       finish(x, cb, bidx, row, valid);
     } else {
+      // merge mode: the row's best exact cost so far (earlier chunks / previous label), fetched
+      // now so it has landed by the refinement decision
+      float md_prev = INFINITY;
+      if (a.merge && valid) md_prev = a.mindist[row];
       // MFMA B operands: f32 rows are split into bf16 hi/lo (the fp32 copy stays live for the
       // epilogue); bf16 rows are used as they are.
       bf16x8 xh[KS], xl[XB ? 1 : KS];
@@ -506,7 +512,11 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
       // the gap must beat: split + accumulation error, seed rounding, key truncation
       const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
-      const bool unsure = valid && !(a.ablate & 8) && !(b2 - b1 > thr);
+      // A near tie inside this chunk only matters if the chunk can still win: in merge mode a
+      // row whose chunk-best is provably worse than its best exact cost so far needs no exact
+      // re-decision (thr bounds one candidate's error with room to spare).
+      const bool unsure =
+          valid && !(a.ablate & 8) && !(b2 - b1 > thr) && !(a.merge && b1 - thr > md_prev);
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);
@@ -570,6 +580,86 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   }
 }
 
+// mindist[row] = |x_row - c_{labels[row]}|^2 with exactly the assign kernel's lane layout and
+// fp32 summation order (so a later chunk that picks the same center computes the bitwise same
+// value).  Seeds the chunked large-k passes with the previous iteration's labels.
+template <int KS, bool XB>
+__global__ __launch_bounds__(256) void oap_kmeans_seed_mindist(KMeansAssignArgs a) {
+  constexpr int DP = 16 * KS;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ntiles = (a.n + 31) / 32;
+  for (int64_t t = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64; t < ntiles;
+       t += int64_t(gridDim.x) * blockDim.x / 64) {
+    const int64_t row = t * 32 + r;
+    const bool valid = row < a.n;
+    const int64_t rr = valid ? row : a.n - 1;
+    int b = a.labels[rr];
+    if (b < 0 || b >= a.k) b = 0;
+    const float* cp = a.centers + size_t(b) * DP + 8 * h;
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float xv[8];
+      const int f = 16 * s + 8 * h;
+      if constexpr (XB) {
+        bf16x8 v = bf16x8{};
+        if (s < KS - 1 || f < a.ld)
+          v = *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(a.x) + rr * a.ld + f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = static_cast<float>(v[j]);
+      } else {
+        const float* p = static_cast<const float*>(a.x) + rr * a.ld + f;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (s < KS - 1 || f + 4 * q < a.ld) v = *reinterpret_cast<const float4*>(p + 4 * q);
+          xv[4 * q + 0] = v.x;
+          xv[4 * q + 1] = v.y;
+          xv[4 * q + 2] = v.z;
+          xv[4 * q + 3] = v.w;
+        }
+      }
+      const float4 c0 = *reinterpret_cast<const float4*>(cp + 16 * s);
+      const float4 c1 = *reinterpret_cast<const float4*>(cp + 16 * s + 4);
+      const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = xv[j] - cv[j];
+        part = fmaf(e, e, part);
+      }
+    }
+    const float rowcost = part + __shfl_xor(part, 32, 64);
+    if (valid && h == 0) {
+      a.mindist[row] = rowcost;
+      a.labels[row] = b;
+    }
+  }
+}
+
+template <int KS, bool XB>
+void launch_seed(const KMeansAssignArgs& a, hipStream_t s) {
+  const int64_t tiles = (a.n + 31) / 32;
+  const int grid = static_cast<int>(tiles / 4 + 1 < 8192 ? tiles / 4 + 1 : 8192);
+  hipLaunchKernelGGL((oap_kmeans_seed_mindist<KS, XB>), dim3(grid), dim3(256), 0, s, a);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+template <bool XB>
+void seed_xb(const KMeansAssignArgs& a, hipStream_t s) {
+  switch ((a.d + 15) / 16) {
+    case 1: launch_seed<1, XB>(a, s); break;
+    case 2: launch_seed<2, XB>(a, s); break;
+    case 3: launch_seed<3, XB>(a, s); break;
+    case 4: launch_seed<4, XB>(a, s); break;
+    case 5: launch_seed<5, XB>(a, s); break;
+    case 6: launch_seed<6, XB>(a, s); break;
+    case 7: launch_seed<7, XB>(a, s); break;
+    case 8: launch_seed<8, XB>(a, s); break;
+    default: OAP_THROW(ConfigError, "kmeans_seed_mindist: unsupported d=" << a.d);
+  }
+}
+
 template <int KS, bool P, bool LA, bool B, bool XB>
 void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA, a.sums_too);
@@ -616,6 +706,15 @@ void launch_xb(const KMeansAssignArgs& a, int grid, hipStream_t s, bool lds_acc)
 }
 
 }  // namespace
+
+void launch_kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
+  if (a.n == 0) return;
+  OAP_CHECK(a.d <= 128 && a.labels && a.mindist, "kmeans_seed_mindist: bad arguments");
+  if (a.xbf16)
+    seed_xb<true>(a, s);
+  else
+    seed_xb<false>(a, s);
+}
 
 int kmeans_mfma_kmax(int d, bool precise) {
   if (d > 128) return 0;

@@ -11,6 +11,8 @@ constexpr size_t kLdsLimit = 160 * 1024;
 
 // Launches the MFMA assign kernel (d <= 128, centroids fit the LDS plan).  `grid` blocks.
 void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s);
+// mindist/labels of the chunked path seeded from labels (the previous assignment).
+void launch_kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s);
 // Largest kpad (multiple of 32) whose centroid planes fit LDS for d features.
 int kmeans_mfma_kmax(int d, bool precise);
 // Grid the MFMA assign kernel uses for n rows (>= 256 blocks once there is work for them, so the
