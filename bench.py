@@ -92,6 +92,8 @@ def bench_kmeans(args, w):
         "extra": {"fit_wall_s_end_to_end": fit_s,
                   "fit_iters": fit_iters if fit_s is not None else None,
                   "init_kmeans_parallel_s": init_s, "ingest_synth_s": ingest_s,
+                  "init_phases_ms": {kk.split("/")[-1]: round(vv["total_us"] / 1e3, 1)
+                                     for kk, vv in m.items() if kk.startswith("kmeans/init/")},
                   "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
                   "allreduce_us": ar["total_us"] / max(ar["count"], 1),
                   "achieved_tflops": flops / (el_max / args.steps) / 1e12,

@@ -4,6 +4,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <map>
 #include <random>
@@ -213,6 +214,9 @@ struct AssignReq {
   // chunked path: `labels` already holds the previous assignment (a Lloyd iteration > 0), so
   // the merge passes start from its exact distance
   bool labels_valid = false;
+  // chunked path: `mindist` already holds an upper bound that only a strictly closer center may
+  // replace (k-means|| cost updates: the merge passes then compute min(old, new) in place)
+  bool mindist_seeded = false;
 };
 
 // Returns the number of cost partials written to req.cost_slab.
@@ -263,6 +267,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   // chunks that cannot win skip the exact re-decision of their own near ties), else +huge.
   if (req.labels_valid && req.labels) {
     kern::kmeans_seed_mindist(a, s);
+  } else if (req.mindist_seeded && req.mindist) {
+    OAP_HIP_CHECK(hipMemsetAsync(labels, 0, sizeof(int32_t) * x.rows, s));
   } else {
     OAP_HIP_CHECK(hipMemsetAsync(mind, 0x7f, sizeof(float) * x.rows, s));  // 3.4e38, finite
     OAP_HIP_CHECK(hipMemsetAsync(labels, 0, sizeof(int32_t) * x.rows, s));
@@ -317,9 +323,17 @@ class InitOps {
     if (ctx_.is_gpu()) {
       GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
       AssignReq req;
-      req.mindist = tmp_.as<float>();
-      gpu_assign(ctx_, x_, g, req, ctx_.compute());
-      kern::elementwise_min(costs_.as<float>(), tmp_.as<float>(), x_.rows, ctx_.compute());
+      if (x_.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x_.cols, false)) {
+        // chunked: merge straight into the running costs (chunks that cannot lower a row's cost
+        // skip their exact re-decisions)
+        req.mindist = costs_.as<float>();
+        req.mindist_seeded = true;
+        gpu_assign(ctx_, x_, g, req, ctx_.compute());
+      } else {
+        req.mindist = tmp_.as<float>();
+        gpu_assign(ctx_, x_, g, req, ctx_.compute());
+        kern::elementwise_min(costs_.as<float>(), tmp_.as<float>(), x_.rows, ctx_.compute());
+      }
       OAP_HIP_CHECK(hipStreamSynchronize(ctx_.compute()));
     } else {
       std::vector<double> d2(x_.rows);
@@ -474,10 +488,21 @@ std::vector<int64_t> sample_without_replacement(int64_t n, int64_t m, uint64_t s
 
 // ------------------------------------------------------------------------ local k-means++
 namespace {
+// Elementwise loops over the candidate points run on the pool; every reduction over points is
+// sequential in point order, so results are identical for any pool size (and to the serial code).
+void for_points(ThreadPool* pool, size_t n, const std::function<void(size_t, size_t)>& fn) {
+  if (!pool || pool->size() <= 1 || n < 256) {
+    fn(0, n);
+    return;
+  }
+  pool->parallel_for(int64_t(n), [&](int, int64_t b, int64_t e) { fn(size_t(b), size_t(e)); });
+}
+
 // One greedy k-means++ seeding (2 + ln k candidate draws per step, keep the one that lowers the
 // weighted potential most) followed by weighted Lloyd; returns the weighted cost.
 double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>& w, int d, int k,
-                      int max_iter, std::mt19937_64& rng, std::vector<double>& centers) {
+                      int max_iter, std::mt19937_64& rng, std::vector<double>& centers,
+                      ThreadPool* pool) {
   const size_t n = pts.size() / d;
   std::uniform_real_distribution<double> U(0.0, 1.0);
   auto dist2 = [&](size_t i, const double* c) {
@@ -501,47 +526,56 @@ double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>&
     std::copy(pts.begin() + i * d, pts.begin() + (i + 1) * d, centers.begin() + size_t(c) * d);
   };
   set_center(0, pick(w));
-  std::vector<double> cost(n), mass(n), trial(n);
-  for (size_t i = 0; i < n; ++i) cost[i] = dist2(i, centers.data());
+  std::vector<double> cost(n), mass(n);
+  for_points(pool, n, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) cost[i] = dist2(i, centers.data());
+  });
   const int trials = 2 + static_cast<int>(std::log(double(k)));
+  std::vector<size_t> cand(trials);
+  std::vector<std::vector<double>> trial(trials, std::vector<double>(n));
   for (int c = 1; c < k; ++c) {
     for (size_t i = 0; i < n; ++i) mass[i] = w[i] * cost[i];
-    size_t best_i = 0;
-    double best_pot = std::numeric_limits<double>::infinity();
-    std::vector<double> best_cost;
-    for (int t = 0; t < trials; ++t) {
-      size_t cand = pick(mass);
-      double pot = 0.0;
-      const double* cc = pts.data() + cand * d;
-      for (size_t i = 0; i < n; ++i) {
-        trial[i] = std::min(cost[i], dist2(i, cc));
-        pot += w[i] * trial[i];
+    for (int t = 0; t < trials; ++t) cand[t] = pick(mass);  // same RNG order as drawing per trial
+    for_points(pool, n, [&](size_t b, size_t e) {
+      for (int t = 0; t < trials; ++t) {
+        const double* cc = pts.data() + cand[t] * d;
+        for (size_t i = b; i < e; ++i) trial[t][i] = std::min(cost[i], dist2(i, cc));
       }
+    });
+    int best_t = 0;
+    double best_pot = std::numeric_limits<double>::infinity();
+    for (int t = 0; t < trials; ++t) {
+      double pot = 0.0;
+      for (size_t i = 0; i < n; ++i) pot += w[i] * trial[t][i];
       if (pot < best_pot) {
         best_pot = pot;
-        best_i = cand;
-        best_cost = trial;
+        best_t = t;
       }
     }
-    set_center(c, best_i);
-    cost = best_cost;
+    set_center(c, cand[best_t]);
+    cost.swap(trial[best_t]);
   }
-  std::vector<int> old(n, -1);
-  std::vector<int> lab(n, 0);
+  std::vector<int> old(n, -1), lab(n, 0);
   bool moved = true;
   for (int it = 0; moved && it < max_iter; ++it) {
     moved = false;
+    for_points(pool, n, [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; ++i) {
+        int best = 0;
+        double bd = std::numeric_limits<double>::infinity();
+        for (int c = 0; c < k; ++c) {
+          double v = dist2(i, centers.data() + size_t(c) * d);
+          if (v < bd) {
+            bd = v;
+            best = c;
+          }
+        }
+        lab[i] = best;
+      }
+    });
     std::vector<double> cnt(k, 0.0), sums(size_t(k) * d, 0.0);
     for (size_t i = 0; i < n; ++i) {
-      int best = 0;
-      double bd = std::numeric_limits<double>::infinity();
-      for (int c = 0; c < k; ++c) {
-        double v = dist2(i, centers.data() + size_t(c) * d);
-        if (v < bd) {
-          bd = v;
-          best = c;
-        }
-      }
+      const int best = lab[i];
       for (int f = 0; f < d; ++f) sums[size_t(best) * d + f] += w[i] * pts[i * d + f];
       cnt[best] += w[i];
       if (best != old[i]) {
@@ -558,28 +592,33 @@ double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>&
       }
     }
   }
+  std::vector<double> bdist(n);
+  for_points(pool, n, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; ++i) {
+      double bd = std::numeric_limits<double>::infinity();
+      for (int c = 0; c < k; ++c) bd = std::min(bd, dist2(i, centers.data() + size_t(c) * d));
+      bdist[i] = bd;
+    }
+  });
   double total = 0.0;
-  for (size_t i = 0; i < n; ++i) {
-    double bd = std::numeric_limits<double>::infinity();
-    for (int c = 0; c < k; ++c) bd = std::min(bd, dist2(i, centers.data() + size_t(c) * d));
-    total += w[i] * bd;
-  }
+  for (size_t i = 0; i < n; ++i) total += w[i] * bdist[i];
   return total;
 }
 }  // namespace
 
 // Spark's LocalKMeans.kMeansPlusPlus runs ONE plain k-means++ seeding + Lloyd; here the seeding
 // is greedy (sklearn-style local trials) and the best of 3 restarts by weighted cost is kept —
-// a strictly better local optimum for the same candidate set (deterministic given the seed).
+// a strictly better local optimum for the same candidate set (deterministic given the seed, for
+// any pool size).
 std::vector<double> local_kmeans_pp(const std::vector<double>& pts, const std::vector<double>& w,
-                                    int d, int k, int max_iter, uint64_t seed) {
+                                    int d, int k, int max_iter, uint64_t seed, ThreadPool* pool) {
   const size_t n = d ? pts.size() / d : 0;
   OAP_CHECK(n > 0 && w.size() == n, "local_kmeans_pp: bad inputs");
   std::mt19937_64 rng(mix64(seed));
   std::vector<double> best, cur;
   double best_cost = std::numeric_limits<double>::infinity();
   for (int r = 0; r < 3; ++r) {
-    double c = kmeans_pp_once(pts, w, d, k, max_iter, rng, cur);
+    double c = kmeans_pp_once(pts, w, d, k, max_iter, rng, cur, pool);
     if (c < best_cost) {
       best_cost = c;
       best = cur;
@@ -607,9 +646,13 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
     std::vector<double> cand = fetch_global_rows(ctx, comm, x, ops, first);
     std::vector<double> newc = cand;
     for (int step = 0; step < p.init_steps; ++step) {
-      ops.update_costs(newc, static_cast<int>(newc.size() / d));
+      {
+        TraceRange tu(&ctx.metrics(), "kmeans/init/update_costs");
+        ops.update_costs(newc, static_cast<int>(newc.size() / d));
+      }
       double sum = comm_allreduce_scalar(ctx, comm, ops.local_cost_sum(), ReduceOp::Sum);
       if (!(sum > 0.0)) break;  // every point already a center
+      TraceRange ts(&ctx.metrics(), "kmeans/init/sample");
       auto local = ops.select(2.0 * p.k / sum, seed, step);
       newc = host_allgatherv_rows(ctx, comm, ops.rows(local), d);
       cand.insert(cand.end(), newc.begin(), newc.end());
@@ -618,10 +661,15 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
     centers = distinct_rows(cand, d);
     int m = static_cast<int>(centers.size() / d);
     if (m > p.k) {
-      auto cnt = ops.count_closest(centers, m);
-      host_allreduce(ctx, comm, cnt.data(), cnt.size(), DType::I64, ReduceOp::Sum);
+      std::vector<int64_t> cnt;
+      {
+        TraceRange tc(&ctx.metrics(), "kmeans/init/count_closest");
+        cnt = ops.count_closest(centers, m);
+        host_allreduce(ctx, comm, cnt.data(), cnt.size(), DType::I64, ReduceOp::Sum);
+      }
       std::vector<double> w(cnt.begin(), cnt.end());
-      centers = local_kmeans_pp(centers, w, d, p.k, 30, seed ^ 0x1234567ull);
+      TraceRange tl(&ctx.metrics(), "kmeans/init/local_kmeans_pp");
+      centers = local_kmeans_pp(centers, w, d, p.k, 30, seed ^ 0x1234567ull, &ctx.pool());
     }
   }
   *k_eff = static_cast<int>(centers.size() / d);

@@ -66,9 +66,11 @@ void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>
 double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
                             int k, int reps, bool precise, int ablate);
 
-// k-means++ over weighted candidates, then up to max_iter weighted Lloyd iterations (host).
+// k-means++ over weighted candidates, then up to max_iter weighted Lloyd iterations (host,
+// elementwise loops on `pool` when given; identical results for any pool size).
 // Mirrors the semantics of Spark's LocalKMeans.kMeansPlusPlus (RNG stream is our own).
 std::vector<double> local_kmeans_pp(const std::vector<double>& pts, const std::vector<double>& w,
-                                    int d, int k, int max_iter, uint64_t seed);
+                                    int d, int k, int max_iter, uint64_t seed,
+                                    ThreadPool* pool = nullptr);
 
 }  // namespace oap
