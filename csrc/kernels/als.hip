@@ -314,22 +314,95 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       __syncthreads();
       continue;
     }
-    // ---- forward L z = b, backward L^T x = z (in place in bv)
-    for (int j = 0; j < r; ++j) {
-      const float z = bv[j] / M[j * S + j];
-      __syncthreads();
-      if (lane == 0) bv[j] = z;
-      for (int i = j + 1 + lane; i < r; i += 64) bv[i] = fmaf(-M[i * S + j], z, bv[i]);
-      __syncthreads();
+    // ---- blocked triangular solves, right-hand side in registers: lane l holds rows l and
+    // l + 64 (v0, v1).  Per 16-row block: the diagonal solve runs in registers (16 sequential
+    // steps, readlane broadcasts), the off-diagonal part is one lane-parallel update — instead
+    // of r sequential LDS round trips per direction.
+    float v0 = bv[lane], v1 = (lane + 64 < RP) ? bv[lane + 64] : 0.f;
+    // forward: L z = b
+#pragma unroll
+    for (int jb = 0; jb < NB; ++jb) {
+      const int o = 16 * jb, base = o & 63, rl = lane - base;
+      const bool mine = rl >= 0 && rl < 16;
+      const int rr = mine ? rl : 0;
+      float t[16];
+#pragma unroll
+      for (int m = 0; m < 16; m += 4) {
+        const float4 q = *reinterpret_cast<const float4*>(&M[(o + rr) * S + o + m]);
+        t[m] = q.x;
+        t[m + 1] = q.y;
+        t[m + 2] = q.z;
+        t[m + 3] = q.w;
+      }
+      float vd = (o < 64) ? v0 : v1;
+      float z[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const float zl = vd / t[j];  // meaningful at lane base + j (t[j] = L_jj there)
+        z[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), base + j));
+        if (rl == j) vd = z[j];
+        else if (mine && rl > j) vd = fmaf(-t[j], z[j], vd);
+      }
+      if (o < 64) v0 = vd;
+      else v1 = vd;
+      if (jb + 1 < NB) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int i = lane + 64 * h;
+          if (i >= o + 16 && i < RP) {
+            float acc2 = 0.f;
+#pragma unroll
+            for (int m = 0; m < 16; m += 4) {
+              const float4 q = *reinterpret_cast<const float4*>(&M[i * S + o + m]);
+              acc2 = fmaf(q.x, z[m], acc2);
+              acc2 = fmaf(q.y, z[m + 1], acc2);
+              acc2 = fmaf(q.z, z[m + 2], acc2);
+              acc2 = fmaf(q.w, z[m + 3], acc2);
+            }
+            if (h == 0) v0 -= acc2;
+            else v1 -= acc2;
+          }
+        }
+      }
     }
-    for (int j = r - 1; j >= 0; --j) {
-      const float x = bv[j] / M[j * S + j];
-      __syncthreads();
-      if (lane == 0) bv[j] = x;
-      for (int i = lane; i < j; i += 64) bv[i] = fmaf(-M[j * S + i], x, bv[i]);
-      __syncthreads();
+    // backward: L^T x = z
+#pragma unroll
+    for (int jb = NB - 1; jb >= 0; --jb) {
+      const int o = 16 * jb, base = o & 63, rl = lane - base;
+      const bool mine = rl >= 0 && rl < 16;
+      float vd = (o < 64) ? v0 : v1;
+      if (jb + 1 < NB) {
+        // z_{o+m} -= sum_{i >= o+16} L[i][o+m] x_i: x staged in LDS, 4 row groups per column
+        bv[lane] = v0;
+        if (lane + 64 < RP) bv[lane + 64] = v1;
+        __syncthreads();
+        const int m = lane & 15, g = lane >> 4;
+        float part = 0.f;
+        for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[i * S + o + m], bv[i], part);
+        part += __shfl_xor(part, 16, 64);
+        part += __shfl_xor(part, 32, 64);
+        const float sub = __shfl(part, (lane - base) & 15, 64);
+        if (mine) vd -= sub;
+        __syncthreads();
+      }
+      // diagonal block: lane base + p holds column p of L_jj
+      float c[16];
+      const int cp = mine ? rl : 0;
+#pragma unroll
+      for (int mm = 0; mm < 16; ++mm) c[mm] = M[(o + mm) * S + o + cp];
+#pragma unroll
+      for (int j = 15; j >= 0; --j) {
+        const float xl = vd / c[j];  // meaningful at lane base + j
+        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), base + j));
+        if (rl == j) vd = xj;
+        else if (mine && rl < j) vd = fmaf(-c[j], xj, vd);
+      }
+      if (o < 64) v0 = vd;
+      else v1 = vd;
     }
-    for (int i = lane; i < a.ld; i += 64) out[i] = i < r ? bv[i] : 0.f;
+    if (lane < a.ld) out[lane] = lane < r ? v0 : 0.f;
+    if (lane + 64 < a.ld) out[lane + 64] = lane + 64 < r ? v1 : 0.f;
+    for (int i = lane + 128; i < a.ld; i += 64) out[i] = 0.f;
     __syncthreads();
   }
 }
