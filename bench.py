@@ -78,6 +78,7 @@ def bench_kmeans(args, w):
     m = w.ctx.metrics()["phases"]
     ak = m.get("kmeans/assign_kernel", {"total_us": 0, "count": 1})
     ar = m.get("kmeans/allreduce", {"total_us": 0, "count": 1})
+    itr = m.get("kmeans/iteration", {"total_us": 0, "count": 1})
     samples = rows_total * args.steps / el_max
     flops = 2.0 * rows_total * k * d
     out = {
@@ -96,6 +97,11 @@ def bench_kmeans(args, w):
                                      for kk, vv in m.items() if kk.startswith("kmeans/init/")},
                   "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
                   "allreduce_us": ar["total_us"] / max(ar["count"], 1),
+                  # device time of one whole iteration minus assign and allreduce: finalize,
+                  # the flag/count read-back and launch gaps
+                  "iteration_rest_us": (itr["total_us"] / max(itr["count"], 1)
+                                        - ak["total_us"] / max(ak["count"], 1)
+                                        - ar["total_us"] / max(ar["count"], 1)),
                   "achieved_tflops": flops / (el_max / args.steps) / 1e12,
                   "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
                   "storage": st,

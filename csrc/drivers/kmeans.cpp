@@ -812,6 +812,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   fa.tol = p.tol;
   fa.cost_in = cost_d.as<double>();
   fa.flags = flags_d.data();
+  Buffer fin_scratch = ctx.alloc(sizeof(double) * 2 * std::max(k, 1));
+  fa.scratch = fin_scratch.as<double>();
 
   RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
   Event e0, e1, e2, e3;

@@ -68,7 +68,8 @@ struct KMeansAssignArgs {
   bool precise = false;                  // exact-fp32 MFMA only (no bf16x3 fast path)
   bool merge = false;                    // keep labels/mindist from earlier chunks unless beaten
   unsigned long long* refine_tiles = nullptr;  // optional: tiles that took the exact pass
-  int ablate = 0;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work
+  int ablate = 0;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work,
+                   // 16 prefetch two tiles ahead instead of one
 };
 // Upper bound on rows one assign workgroup processes for n local rows (device independent); the
 // fixed-point scale keeps per-workgroup LDS partial sums below 2^53 with it.
@@ -102,6 +103,7 @@ struct KMeansFinalizeArgs {
   double tol = 0.0;
   const double* cost_in = nullptr;  // allreduced cost (1 value)
   void* flags = nullptr;            // KMeansFlags out
+  double* scratch = nullptr;        // [2k]: enables the multi-block finalize (else 1 block)
 };
 struct KMeansFlags {
   int converged;

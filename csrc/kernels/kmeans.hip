@@ -246,6 +246,89 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
   }
 }
 
+// Multi-block finalize (one wave per cluster): new centers + per-cluster shift / norm into
+// scratch; oap_kmeans_finalize_flags reduces them.  The fp64 sums keep the single-block
+// kernel's sequential feature order (lane 0), so results are bitwise unchanged.
+__global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinalizeArgs a) {
+  __shared__ double s_df[4][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + w;
+  if (c >= a.k) return;
+  const long long cntv = static_cast<long long>(a.counts[c]);
+  double* c64 = a.centers64 + size_t(c) * a.d;
+  for (int f0 = 0; f0 < a.d; f0 += 256) {
+    const int nf = min(256, a.d - f0);
+    for (int f = lane; f < nf; f += 64) {
+      double df = 0.0;
+      if (cntv > 0) {
+        const long long sv = static_cast<long long>(a.sums[size_t(c) * a.d + f0 + f]);
+        const double nv = double(sv) * a.inv_scale[f0 + f] / double(cntv);  // == CPU formula
+        df = nv - c64[f0 + f];
+        c64[f0 + f] = nv;
+      }
+      const float v = static_cast<float>(c64[f0 + f]);
+      a.centers32[size_t(c) * a.dp + f0 + f] = v;
+      s_df[w][f] = df;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      double sh = f0 == 0 ? 0.0 : a.scratch[c];
+      for (int f = 0; f < nf; ++f) sh += s_df[w][f] * s_df[w][f];
+      a.scratch[c] = sh;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0) {
+    double nrm = 0.0;
+    for (int f = 0; f < a.d; ++f) {
+      const double v = double(static_cast<float>(c64[f]));
+      nrm += v * v;
+    }
+    a.cnorm[c] = static_cast<float>(nrm);
+    a.scratch[a.k + c] = double(sqrtf(static_cast<float>(nrm)));
+    if (cntv <= 0) a.scratch[c] = -1.0;  // empty: keeps its center, not part of the test
+  }
+}
+
+__global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeArgs a) {
+  __shared__ double s_shift[256];
+  __shared__ float s_norm[256];
+  __shared__ int s_conv, s_nonempty;
+  if (threadIdx.x == 0) {
+    s_conv = 1;
+    s_nonempty = 0;
+  }
+  __syncthreads();
+  double my_max = 0.0;
+  float my_nmax = 0.f;
+  for (int c = threadIdx.x; c < a.k; c += blockDim.x) {
+    const double sh = a.scratch[c];
+    if (sh >= 0.0) {
+      atomicAdd(&s_nonempty, 1);
+      if (sh > a.tol * a.tol) atomicAnd(&s_conv, 0);
+      my_max = fmax(my_max, sh);
+    }
+    my_nmax = fmaxf(my_nmax, static_cast<float>(a.scratch[a.k + c]));
+  }
+  s_shift[threadIdx.x] = my_max;
+  s_norm[threadIdx.x] = my_nmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mx = 0.0;
+    float nm = 0.f;
+    for (int i = 0; i < int(blockDim.x); ++i) {
+      mx = fmax(mx, s_shift[i]);
+      nm = fmaxf(nm, s_norm[i]);
+    }
+    KMeansFlags* fl = static_cast<KMeansFlags*>(a.flags);
+    fl->converged = s_conv;
+    fl->nonempty = s_nonempty;
+    fl->cost = a.cost_in ? a.cost_in[0] : 0.0;
+    fl->max_shift2 = mx;
+    if (a.cstat) a.cstat[0] = nm * 1.0000001f;
+  }
+}
+
 __global__ void oap_kmeans_prepare_centers(const double* c64, int k, int d, int dp, float* c32,
                                            float* cnorm, float* cstat, int kpad) {
   __shared__ float s_norm[256];
@@ -374,7 +457,13 @@ void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
 }
 
 void kmeans_finalize(const KMeansFinalizeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(oap_kmeans_finalize, dim3(1), dim3(256), 0, s, a);
+  if (a.scratch) {
+    hipLaunchKernelGGL(oap_kmeans_finalize_clusters, dim3((a.k + 3) / 4), dim3(256), 0, s, a);
+    OAP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(oap_kmeans_finalize_flags, dim3(1), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(oap_kmeans_finalize, dim3(1), dim3(256), 0, s, a);
+  }
   OAP_HIP_CHECK(hipGetLastError());
 }
 

@@ -165,11 +165,10 @@ __device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8
 // bytes of f32 and 2 instead of 3 MFMAs per k-step; the refinement bound of the f32 split still
 // holds (the bf16 products have strictly less error), so assignments equal an exact fp32
 // evaluation of the bf16 data.
-template <int KS, bool PRECISE, bool LDSACC, bool BIAS, bool XB>
+template <int KS, bool PRECISE, bool LDSACC, bool BIAS, bool XB, bool DEEP>
 __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
-  // Register budget: three rotating tiles (prefetch two ahead) when they fit, else two.
-  constexpr bool DEEP = XB || KS <= 4;
+  // DEEP: three rotating tiles (prefetch two ahead); else two (prefetch one ahead).
   using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
@@ -660,19 +659,32 @@ void seed_xb(const KMeansAssignArgs& a, hipStream_t s) {
   }
 }
 
-template <int KS, bool P, bool LA, bool B, bool XB>
-void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+template <int KS, bool P, bool LA, bool B, bool XB, bool DEEP>
+void launch4(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   const Smem L = smem_plan(16 * KS, a.kpad, a.k, a.d, P, LA, a.sums_too);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA, B, XB>),
+        reinterpret_cast<const void*>(&oap_kmeans_assign_mfma<KS, P, LA, B, XB, DEEP>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA, B, XB>), dim3(grid), dim3(kThreads),
-                     L.total, s, a);
+  hipLaunchKernelGGL((oap_kmeans_assign_mfma<KS, P, LA, B, XB, DEEP>), dim3(grid),
+                     dim3(kThreads), L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
+}
+
+// Prefetch depth (measured, profiles/ablate_kmeans_r24.json): one tile ahead for f32 and bf16
+// rows (10.2 vs 10.4 and 8.1 vs 8.4 ms per 100M rows) — the third buffer costs more in
+// register pressure than it hides.  The ablation bit 16 selects two-ahead (tuning A/B only).
+template <int KS, bool P, bool LA, bool B, bool XB>
+void launch3(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  constexpr bool kDeepOk = XB || KS <= 4;
+  const bool deep = kDeepOk && (a.ablate & 16) != 0;
+  if (deep)
+    launch4<KS, P, LA, B, XB, kDeepOk>(a, grid, s);
+  else
+    launch4<KS, P, LA, B, XB, false>(a, grid, s);
 }
 
 template <int KS, bool XB>
