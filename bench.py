@@ -104,9 +104,11 @@ def bench_kmeans(args, w):
                                         - ar["total_us"] / max(ar["count"], 1)),
                   "achieved_tflops": flops / (el_max / args.steps) / 1e12,
                   "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
+                  "tier3_tiles_per_iter": r["tier3_tiles"] / max(args.steps, 1),
                   "storage": st,
                   "distance_path": "fp32-exact MFMA" if args.precise else
-                  ("bf16-split MFMA + exact-fp32 refinement (assignments identical to fp32)"
+                  ("tiered bf16 MFMA (1 product, then bf16x3 split where unsure) + exact-fp32 "
+                   "refinement (assignments identical to fp32)"
                    if st == "f32" else "bf16 rows x bf16-split centroids on MFMA + exact-fp32 "
                    "refinement (assignments identical to exact fp32 on the bf16 data)"),
                   "cost": r["cost"]},

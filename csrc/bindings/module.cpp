@@ -387,6 +387,7 @@ PYBIND11_MODULE(_native, m) {
         out["iter_seconds"] = r.iter_seconds;
         out["global_rows"] = r.global_rows;
         out["refine_tiles"] = r.refine_tiles;
+        out["tier3_tiles"] = r.tier3_tiles;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

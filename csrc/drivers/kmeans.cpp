@@ -217,6 +217,8 @@ struct AssignReq {
   // chunked path: `mindist` already holds an upper bound that only a strictly closer center may
   // replace (k-means|| cost updates: the merge passes then compute min(old, new) in place)
   bool mindist_seeded = false;
+  // start at the 1-product tier (the fit turns it off when tier-3 re-runs get frequent)
+  bool fast1 = true;
 };
 
 // Returns the number of cost partials written to req.cost_slab.
@@ -243,6 +245,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   a.sums_too = req.sums_too;
   a.precise = req.precise;
   a.refine_tiles = req.refine_tiles;
+  a.fast1 = req.fast1 && !req.precise;
   const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
   if (x.cols > 128 || g.kpad <= kmax || kmax == 0)
     return kern::kmeans_assign(a, ctx.info().cu_count, s);
@@ -766,12 +769,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer scale = ctx.alloc(sizeof(float) * (round_up(d, 4) + 4));
   Buffer inv_scale = ctx.alloc(sizeof(double) * d);
   Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags));
-  Buffer refine_d = ctx.alloc(sizeof(u64));
+  Buffer refine_d = ctx.alloc(2 * sizeof(u64));  // [exact re-decisions, tier-3 re-runs]
   Buffer flags_h = ctx.alloc_pinned(sizeof(kern::KMeansFlags));
   Buffer counts_h = ctx.alloc_pinned(sizeof(u64) * k);
-  Buffer refine_h = ctx.alloc_pinned(sizeof(u64));
+  Buffer refine_h = ctx.alloc_pinned(2 * sizeof(u64));
   ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4), s);
-  ctx.memset(refine_d.data(), 0, sizeof(u64), s);
+  ctx.memset(refine_d.data(), 0, 2 * sizeof(u64), s);
   ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * kd, s);
   ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d, s);
   ctx.copy_to_backend(inv_scale.data(), fp.inv_scale.data(), sizeof(double) * d, s);
@@ -815,6 +818,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer fin_scratch = ctx.alloc(sizeof(double) * 2 * std::max(k, 1));
   fa.scratch = fin_scratch.as<double>();
 
+  u64 tier2_seen = 0;
   RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
   Event e0, e1, e2, e3;
   const int64_t flops_per_iter = 2 * int64_t(x.rows) * k * d;
@@ -847,6 +851,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                  hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(
         hipMemcpyAsync(counts_h.data(), counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
+    OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
+                                 hipMemcpyDeviceToHost, s));
     e3.record(s);
     comm.wait(s);
     roctx_pop();
@@ -866,6 +872,16 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     res.cost = fl->cost;
     res.cost_history.push_back(fl->cost);
     res.num_iter = it + 1;
+    {  // adaptive tier: tier-1 first pays off only while tier-3 re-runs stay rare
+      const u64 t2 = refine_h.as<u64>()[1];
+      const double tiles = double((x.rows + 31) / 32);
+      if (req.fast1 && tiles > 0 && double(t2 - tier2_seen) > 0.02 * tiles) {
+        req.fast1 = false;
+        Logger::instance().log(LogLevel::Info, "kmeans/tier1_off",
+                               "\"iter\":" + std::to_string(it));
+      }
+      tier2_seen = t2;
+    }
     if (fl->converged && p.tol >= 0) {  // tol < 0: run exactly max_iter iterations
       res.converged = true;
       break;
@@ -874,8 +890,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);
   res.centers.resize(kd);
   ctx.copy_to_host(res.centers.data(), c64.data(), sizeof(double) * kd, s);
-  ctx.copy_to_host(refine_h.data(), refine_d.data(), sizeof(u64), s);
-  res.refine_tiles = static_cast<int64_t>(*refine_h.as<u64>());
+  ctx.copy_to_host(refine_h.data(), refine_d.data(), 2 * sizeof(u64), s);
+  res.refine_tiles = static_cast<int64_t>(refine_h.as<u64>()[0]);
+  res.tier3_tiles = static_cast<int64_t>(refine_h.as<u64>()[1]);
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
   M.set_value("kmeans/refine_tiles", double(res.refine_tiles));
@@ -945,6 +962,7 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
   a.counts = stats.as<u64>() + size_t(k) * d;
   a.cost_slab = slab.as<double>();
   a.precise = precise;
+  a.fast1 = !precise && !(ablate & 32);
   a.ablate = ablate;
   hipStream_t s = ctx.compute();
   Event e0, e1;

@@ -46,6 +46,7 @@ struct KMeansResult {
   double iter_seconds = 0.0;
   int64_t global_rows = 0;
   int64_t refine_tiles = 0;  // 32-row tiles re-decided by the exact pass (GPU fast path)
+  int64_t tier3_tiles = 0;   // 32-row tiles whose tier-1 (one bf16 product) answer was unsure
 };
 
 // Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for

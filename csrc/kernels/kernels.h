@@ -67,9 +67,11 @@ struct KMeansAssignArgs {
   bool sums_too = true;
   bool precise = false;                  // exact-fp32 MFMA only (no bf16x3 fast path)
   bool merge = false;                    // keep labels/mindist from earlier chunks unless beaten
-  unsigned long long* refine_tiles = nullptr;  // optional: tiles that took the exact pass
+  // optional [2]: tiles that took the exact pass, tiles that took the 3-product tier (fast1)
+  unsigned long long* refine_tiles = nullptr;
+  bool fast1 = false;  // start at the 1-product tier (see kmeans_assign.hip)
   int ablate = 0;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work,
-                   // 16 prefetch two tiles ahead instead of one
+                   // 16 prefetch two tiles ahead instead of one, 32 no tier-1 first pass
 };
 // Upper bound on rows one assign workgroup processes for n local rows (device independent); the
 // fixed-point scale keeps per-workgroup LDS partial sums below 2^53 with it.

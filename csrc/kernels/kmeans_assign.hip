@@ -31,6 +31,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "kernels/device_utils.h"
 #include "kernels/kmeans_internal.h"
@@ -216,9 +217,9 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  float thr1 = 0.f, thr0 = 0.f;
+  float thr1 = 0.f, thr0 = 0.f, cmax = 0.f;
   if constexpr (!PRECISE) {
-    const float cmax = a.cstat ? a.cstat[0] : 0.f;
+    cmax = a.cstat ? a.cstat[0] : 0.f;
     thr1 = 1.25e-4f * cmax;  // 2 candidates x (bf16 split + accumulation) + fp32-path bound
     // bias feature: |c|^2 enters as a bf16 hi/lo pair (error <= 2^-18 |c|^2 per candidate)
     thr0 = (BIAS ? 1e-5f : 2e-6f) * cmax * cmax + 1e-30f;
@@ -363,8 +364,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       // now so it has landed by the refinement decision
       float md_prev = INFINITY;
       if (a.merge && valid) md_prev = a.mindist[row];
-      // MFMA B operands: f32 rows are split into bf16 hi/lo (the fp32 copy stays live for the
-      // epilogue); bf16 rows are used as they are.
+      // MFMA B operands: xh = the row's bf16 hi part (bf16 rows: the row itself); the lo part of
+      // f32 rows is built only when the 3-product tier runs.
       bf16x8 xh[KS], xl[XB ? 1 : KS];
       float nx2 = 0.f;
 #pragma unroll
@@ -398,12 +399,24 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
               v = (j == jb) ? 1.f : v;
               v = (j == jb + 1) ? nx2 : v;
             }
-            __bf16 hi, lo;
-            bf16_split(v, hi, lo);
-            xh[s][j] = hi;
-            xl[s][j] = lo;
+            xh[s][j] = static_cast<__bf16>(v);
           }
       }
+      auto build_lo = [&]() {
+        if constexpr (!XB) {
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              float v = x.v[s][j];
+              if (BIAS && s == KS - 1) {
+                v = (j == jb) ? 1.f : v;
+                v = (j == jb + 1) ? nx2 : v;
+              }
+              xl[s][j] = static_cast<__bf16>(v - static_cast<float>(xh[s][j]));
+            }
+        }
+      };
       if constexpr (!DEEP) load_tile(pf, xn);  // prefetch, hidden behind this tile's MFMAs
 
       // Accumulators are seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
@@ -411,11 +424,16 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       // mantissa bits replaced by the centroid index (kpad <= 1024) — int min/max give value
       // order plus lowest-index tie-break in 4 VALU ops per candidate.  Two accumulators let chunk
       // c's key epilogue (VALU) interleave with chunk c+1's MFMAs.
+      //
+      // Tiers (TERMS): 1 = hi x hi only (one MFMA per k-step; bound ~0.8% of |x||c|), 3 = the
+      // bf16x3 split (x_hi c_hi + x_hi c_lo + x_lo c_hi; bf16 rows: x c_hi + x c_lo; bound
+      // ~1e-4).  With a.fast1 the tile starts at tier 1 and only tiles holding a row whose top-2
+      // gap is inside tier 1's bound run tier 3; rows still unsure after tier 3 are re-decided in
+      // exact fp32.  Every tier's bound is rigorous, so the assignments never change.
       int k1 = 0x7fffffff, k2 = 0x7fffffff;
-      auto mfma_chunk = [&](int c0, f32x16& acc) {
-        if constexpr (BIAS) {
-          // (the first MFMA below takes a zero C operand)
-        } else {
+      auto mfma_chunk = [&](auto tag, int c0, f32x16& acc) {
+        constexpr int T = decltype(tag)::value;
+        if constexpr (!BIAS) {
           // norms first: the first MFMA needs the seeded accumulator + fragment 0 only
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
@@ -428,11 +446,11 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         }
         const __bf16* ah_p = ph + size_t(c0 + r) * sb + 8 * h;
         const __bf16* al_p = pl + size_t(c0 + r) * sb + 8 * h;
-        bf16x8 ah[KS], al[KS];
+        bf16x8 ah[KS], al[T == 1 ? 1 : KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
           ah[s] = *reinterpret_cast<const bf16x8*>(ah_p + 16 * s);
-          al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
+          if constexpr (T != 1) al[s] = *reinterpret_cast<const bf16x8*>(al_p + 16 * s);
         }
         // KS = ceil(d/16): every k-step holds real features, so there is no runtime guard here
 #pragma unroll
@@ -441,9 +459,11 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], f32x16{}, 0, 0, 0);
           else
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xh[s], acc, 0, 0, 0);
-          if constexpr (!XB)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xl[s], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], xh[s], acc, 0, 0, 0);
+          if constexpr (T != 1) {
+            if constexpr (!XB)
+              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], xl[s], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], xh[s], acc, 0, 0, 0);
+          }
         }
       };
       auto epilogue = [&](int c0, const f32x16& acc) {
@@ -481,41 +501,66 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         k2 = min(max(k1, i1), min(k2, i2));
         k1 = min(k1, i1);
       };
-      if (a.ablate & 8) {
-        k1 = r % k;  // timing ablation: no distance work
+      auto run_tier = [&](auto tag) {
+        k1 = 0x7fffffff;
         k2 = 0x7fffffff;
-      } else {
-        f32x16 accA, accB;
-        mfma_chunk(0, accA);
-        int c0 = 32;
-        for (; c0 + 32 < kpad; c0 += 64) {  // branch-free body: chunk pairs
-          mfma_chunk(c0, accB);
-          epilogue(c0 - 32, accA);
-          mfma_chunk(c0 + 32, accA);
-          epilogue(c0, accB);
-        }
-        if (c0 < kpad) {  // one chunk left (wave-uniform)
-          mfma_chunk(c0, accB);
-          epilogue(c0 - 32, accA);
-          epilogue(c0, accB);
+        if (a.ablate & 8) {
+          k1 = r % k;  // timing ablation: no distance work
         } else {
-          epilogue(c0 - 32, accA);
+          f32x16 accA, accB;
+          mfma_chunk(tag, 0, accA);
+          int c0 = 32;
+          for (; c0 + 32 < kpad; c0 += 64) {  // branch-free body: chunk pairs
+            mfma_chunk(tag, c0, accB);
+            epilogue(c0 - 32, accA);
+            mfma_chunk(tag, c0 + 32, accA);
+            epilogue(c0, accB);
+          }
+          if (c0 < kpad) {  // one chunk left (wave-uniform)
+            mfma_chunk(tag, c0, accB);
+            epilogue(c0 - 32, accA);
+            epilogue(c0, accB);
+          } else {
+            epilogue(c0 - 32, accA);
+          }
         }
-      }
-      {  // merge the two halves' top-2 keys
+        // merge the two halves' top-2 keys
         const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
         k2 = min(max(k1, o1), min(k2, o2));
         k1 = min(k1, o1);
-      }
-      bidx = k1 & 0x3ff;
-      const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
-      // the gap must beat: split + accumulation error, seed rounding, key truncation
-      const float thr = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2 + 2.5e-4f * fabsf(b2);
+      };
       // A near tie inside this chunk only matters if the chunk can still win: in merge mode a
       // row whose chunk-best is provably worse than its best exact cost so far needs no exact
-      // re-decision (thr bounds one candidate's error with room to spare).
-      const bool unsure =
-          valid && !(a.ablate & 8) && !(b2 - b1 > thr) && !(a.merge && b1 - thr > md_prev);
+      // re-decision (every threshold bounds one candidate's error with room to spare).
+      auto unsure_at = [&](float thr) {
+        const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
+        const float t = thr + 2.5e-4f * fabsf(b2);  // + key truncation
+        return valid && !(a.ablate & 8) && !(b2 - b1 > t) && !(a.merge && b1 - t > md_prev);
+      };
+      // tier-3 bound: split + accumulation error, seed rounding
+      const float thr3 = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2;
+      bool unsure;
+      if (a.fast1) {
+        run_tier(std::integral_constant<int, 1>{});
+        // tier-1 bound, two candidates: cross term 2 x 2(2^-8 + 2^-18)|c||x|, |c|^2 bias
+        // 2 x 2^-9 cmax^2, |x|^2 bias 2^-9 nx2 (cancels in the gap, not in the merge test),
+        // fp32 accumulation 4e-5 (cmax^2 + nx2)
+        const float cm = cmax;
+        const float thrA = 0.0157f * cm * sqrtf(nx2) + 0.004f * cm * cm + 0.002f * nx2 +
+                           4e-5f * (cm * cm + nx2) + 1e-30f;
+        unsure = unsure_at(thrA);
+        if (__any(unsure)) {
+          build_lo();
+          run_tier(std::integral_constant<int, 3>{});
+          unsure = unsure_at(thr3);
+          if (lane == 0 && a.refine_tiles) atomicAdd(a.refine_tiles + 1, 1ull);
+        }
+      } else {
+        build_lo();
+        run_tier(std::integral_constant<int, 3>{});
+        unsure = unsure_at(thr3);
+      }
+      bidx = k1 & 0x3ff;
       if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);

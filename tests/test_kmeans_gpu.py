@@ -118,6 +118,7 @@ def test_fast_path_bitwise_equals_precise(native, d, k):
     t = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
     rf = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 4, 0.0, precise=False)
     rp = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 4, 0.0, precise=True)
+    assert rf["tier3_tiles"] > 0  # overlapping data: tier 1 escalates (then switches itself off)
     assert rf["last_counts"] == rp["last_counts"]
     assert np.array_equal(rf["centers"], rp["centers"])
     assert rf["cost"] == rp["cost"]
