@@ -1,0 +1,237 @@
+// C ABI over the native drivers (see oap_capi.h).  Exceptions never cross the boundary: every
+// entry point catches, stores the message in a thread-local buffer and returns a negative code.
+#include "capi/oap_capi.h"
+
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "comm/comm.h"
+#include "drivers/als.h"
+#include "drivers/kmeans.h"
+#include "drivers/pca.h"
+#include "kernels/kernels.h"
+#include "runtime/context.h"
+#include "runtime/table.h"
+
+struct oap_ctx {
+  std::unique_ptr<oap::Context> ctx;
+  std::shared_ptr<oap::Comm> comm;
+};
+
+struct oap_als_result {
+  oap::AlsResult r;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    g_last_error.clear();
+    f();
+    return 0;
+  } catch (const oap::CommError& e) {
+    g_last_error = std::string("CommError: ") + e.what();
+    return -3;
+  } catch (const oap::ConfigError& e) {
+    g_last_error = std::string("ConfigError: ") + e.what();
+    return -2;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  } catch (...) {
+    g_last_error = "unknown native error";
+    return -1;
+  }
+}
+
+// Rank-local rows -> the backend's K-Means / PCA table layout.
+oap::DenseTable upload(oap_ctx* c, const double* x, int64_t rows, int cols, bool kmeans_layout,
+                       bool bf16) {
+  OAP_CHECK(c && c->ctx, "null context");
+  OAP_CHECK(rows >= 0 && cols > 0, "bad shape " << rows << "x" << cols);
+  OAP_CHECK(x || rows == 0, "null row buffer");
+  oap::Context& ctx = *c->ctx;
+  if (!ctx.is_gpu())
+    return oap::upload_dense(ctx, x, oap::DType::F64, rows, cols, cols, oap::DType::F64, cols);
+  const oap::DType st = bf16 ? oap::DType::BF16 : oap::DType::F32;
+  const int64_t ld = kmeans_layout ? oap::kern::kmeans_ld(cols, bf16) : cols;
+  return oap::upload_dense(ctx, x, oap::DType::F64, rows, cols, cols,
+                           kmeans_layout ? st : oap::DType::F32, ld);
+}
+
+}  // namespace
+
+extern "C" {
+
+int oap_capi_version(void) { return OAP_CAPI_VERSION; }
+
+const char* oap_last_error(void) { return g_last_error.c_str(); }
+
+int oap_device_count(void) { return oap::visible_device_count(); }
+
+int oap_check_platform(int device) {
+  int ok = 0;
+  const int rc = guarded([&] {
+    if (device < 0 || device >= oap::visible_device_count()) return;
+    const oap::DeviceInfo d = oap::query_device(device);
+    ok = d.arch.rfind("gfx950", 0) == 0 ? 1 : 0;
+  });
+  return rc < 0 ? rc : ok;
+}
+
+oap_ctx* oap_ctx_create(int device, double hbm_fraction, int cpu_threads) {
+  oap_ctx* out = nullptr;
+  guarded([&] {
+    auto c = std::make_unique<oap_ctx>();
+    c->ctx = std::make_unique<oap::Context>(device, hbm_fraction, cpu_threads);
+    c->comm = std::make_shared<oap::LocalComm>(device >= 0);
+    out = c.release();
+  });
+  return out;
+}
+
+void oap_ctx_destroy(oap_ctx* ctx) {
+  guarded([&] {
+    if (!ctx) return;
+    ctx->comm.reset();
+    delete ctx;
+  });
+}
+
+int oap_rccl_unique_id(unsigned char out[OAP_UNIQUE_ID_BYTES]) {
+  return guarded([&] {
+    const std::string id = oap::rccl_unique_id();
+    OAP_CHECK(id.size() <= OAP_UNIQUE_ID_BYTES, "unique id of " << id.size() << " bytes");
+    std::memset(out, 0, OAP_UNIQUE_ID_BYTES);
+    std::memcpy(out, id.data(), id.size());
+  });
+}
+
+int oap_ctx_join(oap_ctx* c, const unsigned char id[OAP_UNIQUE_ID_BYTES], int world, int rank,
+                 double timeout_s) {
+  return guarded([&] {
+    OAP_CHECK(c && c->ctx, "null context");
+    OAP_CHECK(c->ctx->is_gpu(), "RCCL communicators need a GPU context");
+    OAP_CHECK(world >= 1 && rank >= 0 && rank < world, "bad world/rank " << world << "/" << rank);
+    if (world == 1) {
+      c->comm = std::make_shared<oap::LocalComm>(true);
+      return;
+    }
+    std::string uid(reinterpret_cast<const char*>(id), OAP_UNIQUE_ID_BYTES);
+    c->comm = std::make_shared<oap::RcclComm>(uid, world, rank, c->ctx->device(), timeout_s);
+  });
+}
+
+int oap_ctx_world_size(const oap_ctx* c) { return c && c->comm ? c->comm->size() : -1; }
+int oap_ctx_rank(const oap_ctx* c) { return c && c->comm ? c->comm->rank() : -1; }
+
+int oap_kmeans_fit(oap_ctx* c, const double* x, int64_t rows, int cols,
+                   const double* init_centers, int k, int max_iter, double tol, int storage_bf16,
+                   double* out_centers, double* out_cost, int* out_iters) {
+  return guarded([&] {
+    OAP_CHECK(init_centers && k >= 1, "initial centers required (k >= 1)");
+    oap::DenseTable t = upload(c, x, rows, cols, true, storage_bf16 != 0);
+    oap::KMeansParams p;
+    p.k = k;
+    p.max_iter = max_iter;
+    p.tol = tol;
+    p.init = oap::KMeansInit::Given;
+    std::vector<double> init(init_centers, init_centers + size_t(k) * cols);
+    oap::KMeansResult r = oap::kmeans_fit(*c->ctx, *c->comm, t, init, p);
+    if (out_centers) std::memcpy(out_centers, r.centers.data(), r.centers.size() * sizeof(double));
+    if (out_cost) *out_cost = r.cost;
+    if (out_iters) *out_iters = r.num_iter;
+  });
+}
+
+int oap_kmeans_init(oap_ctx* c, const double* x, int64_t rows, int cols, int k, const char* mode,
+                    int init_steps, uint64_t seed, double* out_centers, int* out_k) {
+  return guarded([&] {
+    oap::DenseTable t = upload(c, x, rows, cols, true, false);
+    oap::KMeansParams p;
+    p.k = k;
+    p.init_steps = init_steps;
+    p.seed = seed;
+    const std::string m = mode ? mode : "k-means||";
+    OAP_CHECK(m == "random" || m == "k-means||", "unknown init mode '" << m << "'");
+    p.init = m == "random" ? oap::KMeansInit::Random : oap::KMeansInit::Parallel;
+    int keff = 0;
+    std::vector<double> cs = oap::kmeans_init_centers(*c->ctx, *c->comm, t, p, &keff);
+    if (out_centers) std::memcpy(out_centers, cs.data(), cs.size() * sizeof(double));
+    if (out_k) *out_k = keff;
+  });
+}
+
+int oap_kmeans_predict(oap_ctx* c, const double* x, int64_t rows, int cols, const double* centers,
+                       int k, int32_t* labels, double* dist2) {
+  return guarded([&] {
+    OAP_CHECK(centers && k >= 1, "centers required");
+    oap::DenseTable t = upload(c, x, rows, cols, true, false);
+    std::vector<double> cs(centers, centers + size_t(k) * cols);
+    std::vector<int32_t> lab(rows);
+    std::vector<double> d2(rows);
+    oap::kmeans_predict(*c->ctx, t, cs, k, lab.data(), d2.data());
+    if (labels) std::memcpy(labels, lab.data(), lab.size() * sizeof(int32_t));
+    if (dist2) std::memcpy(dist2, d2.data(), d2.size() * sizeof(double));
+  });
+}
+
+int oap_pca_fit(oap_ctx* c, const double* x, int64_t rows, int cols, int k, double* out_pc,
+                double* out_explained) {
+  return guarded([&] {
+    OAP_CHECK(k >= 1 && k <= cols, "k must be in [1, cols]");
+    oap::DenseTable t = upload(c, x, rows, cols, false, false);
+    oap::PcaParams p;
+    p.k = k;
+    oap::PcaResult r = oap::pca_fit(*c->ctx, *c->comm, t, p);
+    if (out_pc) std::memcpy(out_pc, r.pc.data(), r.pc.size() * sizeof(double));
+    if (out_explained)
+      std::memcpy(out_explained, r.explained.data(), r.explained.size() * sizeof(double));
+  });
+}
+
+int oap_als_fit(oap_ctx* c, const int32_t* users, const int32_t* items, const float* ratings,
+                int64_t n, int rank, int max_iter, double reg, double alpha, int implicit,
+                uint64_t seed, oap_als_result** out) {
+  return guarded([&] {
+    OAP_CHECK(c && c->ctx && out, "null argument");
+    OAP_CHECK(n == 0 || (users && items && ratings), "null rating buffers");
+    oap::AlsParams p;
+    p.rank = rank;
+    p.max_iter = max_iter;
+    p.reg = reg;
+    p.alpha = alpha;
+    p.implicit = implicit != 0;
+    p.seed = seed;
+    auto res = std::make_unique<oap_als_result>();
+    res->r = oap::als_fit(*c->ctx, *c->comm, users, items, ratings, n, p);
+    *out = res.release();
+  });
+}
+
+int64_t oap_als_result_count(const oap_als_result* res, int which) {
+  if (!res) return -1;
+  return static_cast<int64_t>(which == 0 ? res->r.user_ids.size() : res->r.item_ids.size());
+}
+
+int oap_als_result_rank(const oap_als_result* res) { return res ? res->r.rank : -1; }
+
+const int32_t* oap_als_result_ids(const oap_als_result* res, int which) {
+  if (!res) return nullptr;
+  return which == 0 ? res->r.user_ids.data() : res->r.item_ids.data();
+}
+
+const float* oap_als_result_factors(const oap_als_result* res, int which) {
+  if (!res) return nullptr;
+  return which == 0 ? res->r.user_factors.data() : res->r.item_factors.data();
+}
+
+void oap_als_result_free(oap_als_result* res) { delete res; }
+
+}  // extern "C"

@@ -31,10 +31,18 @@ def ext_path() -> Path:
     return PKG / ("_native" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
+def capi_path() -> Path:
+    return PKG / "liboap_mllib.so"
+
+
 def _includes() -> list[str]:
     import pybind11
 
-    return [f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    inc = [f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    jh = os.environ.get("JAVA_HOME")
+    if jh:  # JNI shim headers
+        inc += [f"-I{jh}/include", f"-I{jh}/include/linux"]
+    return inc
 
 
 def _sources() -> list[Path]:
@@ -122,6 +130,18 @@ def build(jobs: int | None = None, clean: bool = False, debug: bool = False,
             raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"[oap build] linked {out.relative_to(ROOT)}", flush=True)
+    # liboap_mllib.so: the same native core without the Python bindings, exporting the C ABI
+    # (csrc/capi/oap_capi.h) and, when a JDK was found, the JNI shim (csrc/jni/).
+    lib = capi_path()
+    cobjs = [o for o, s in zip(objs, srcs) if "bindings" not in s.relative_to(CSRC).parts]
+    if todo or not lib.exists() or any(o.stat().st_mtime > lib.stat().st_mtime for o in cobjs):
+        cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}"] + [str(o) for o in cobjs] + [
+            "-o", str(lib), "-lrccl", "-ldl", "-lpthread", "-Wl,-rpath,/opt/rocm/lib"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print(f"[oap build] linked {lib.relative_to(ROOT)}", flush=True)
     return out
 
 
