@@ -30,6 +30,16 @@ namespace {
 constexpr int kAlsThreads = 64;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// LDS image of the row's matrix: only the lower 16x16 blocks, packed (block (bi, bj), bi >= bj, at
+// bi (bi + 1) / 2 + bj), row stride 20 floats (odd 16-byte slots: lane-per-row 16-byte reads are
+// conflict-free) and a 16-byte pad per block (consecutive blocks start on different banks).
+// 28 blocks at rank 100 = 36 KB per row instead of 52 KB for the full square: 4 rows per CU.
+constexpr int kBS = 20, kBlkF = 16 * kBS + 4;
+__device__ inline int mi(int i, int j) {
+  const int bi = i >> 4, bj = j >> 4;
+  return (bi * (bi + 1) / 2 + bj) * kBlkF + (i & 15) * kBS + (j & 15);
+}
+
 struct SolveArgs {
   const int64_t* rowptr;
   const int32_t* cols;
@@ -134,10 +144,10 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_partial(PartialArgs a) {
 template <int NB, bool LONG>
 __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
   constexpr int NT = NB * (NB + 1) / 2;
-  constexpr int RP = 16 * NB, S = RP + 4;
+  constexpr int RP = 16 * NB;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* M = lds;            // RP x S, lower triangle used
-  float* bv = lds + RP * S;  // RP
+  float* M = lds;  // lower 16x16 blocks, packed (mi)
+  float* bv = lds + NB * (NB + 1) / 2 * kBlkF;  // RP
   const int r = a.r, lane = threadIdx.x;
 
   while (true) {
@@ -199,7 +209,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
             } else {
               v = (i == j) ? 1.f : 0.f;
             }
-            M[i * S + j] = v;
+            M[mi(i, j)] = v;
           }
       if (kk == 0) {
 #pragma unroll
@@ -218,7 +228,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         const int rl = lane & 15;
 #pragma unroll
         for (int m = 0; m < 16; m += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(&M[(o + rl) * S + o + m]);
+          const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + rl, o + m)]);
           t[m] = v.x;
           t[m + 1] = v.y;
           t[m + 2] = v.z;
@@ -246,7 +256,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       if (lane < 16) {
 #pragma unroll
         for (int m = 0; m < 16; m += 4)
-          *reinterpret_cast<float4*>(&M[(o + lane) * S + o + m]) =
+          *reinterpret_cast<float4*>(&M[mi(o + lane, o + m)]) =
               make_float4(t[m], t[m + 1], t[m + 2], t[m + 3]);
       }
       __syncthreads();
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         float x[16];
 #pragma unroll
         for (int m = 0; m < 16; m += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(&M[i * S + o + m]);
+          const float4 v = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
           x[m] = v.x;
           x[m + 1] = v.y;
           x[m + 2] = v.z;
@@ -267,7 +277,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
           float lrow[16];
 #pragma unroll
           for (int m = 0; m < 16; m += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(&M[(o + cc) * S + o + m]);
+            const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + cc, o + m)]);
             lrow[m] = v.x;
             lrow[m + 1] = v.y;
             lrow[m + 2] = v.z;
@@ -280,7 +290,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         }
 #pragma unroll
         for (int m = 0; m < 16; m += 4)
-          *reinterpret_cast<float4*>(&M[i * S + o + m]) =
+          *reinterpret_cast<float4*>(&M[mi(i, o + m)]) =
               make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
       }
       __syncthreads();
@@ -290,18 +300,18 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         for (int ib = jb + 1; ib < NB; ++ib) {
           float pa[4];
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[(16 * ib + c) * S + o + 4 * s4 + kk];
+          for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[mi(16 * ib + c, o + 4 * s4 + kk)];
           for (int kb = jb + 1; kb <= ib; ++kb) {
             f4 cacc;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) cacc[e] = M[(16 * ib + 4 * kk + e) * S + 16 * kb + c];
+            for (int e = 0; e < 4; ++e) cacc[e] = M[mi(16 * ib + 4 * kk + e, 16 * kb + c)];
 #pragma unroll
             for (int s4 = 0; s4 < 4; ++s4) {
-              const float pb = M[(16 * kb + c) * S + o + 4 * s4 + kk];
+              const float pb = M[mi(16 * kb + c, o + 4 * s4 + kk)];
               cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s4], pb, cacc, 0, 0, 0);
             }
 #pragma unroll
-            for (int e = 0; e < 4; ++e) M[(16 * ib + 4 * kk + e) * S + 16 * kb + c] = cacc[e];
+            for (int e = 0; e < 4; ++e) M[mi(16 * ib + 4 * kk + e, 16 * kb + c)] = cacc[e];
           }
         }
       }
@@ -328,7 +338,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       float t[16];
 #pragma unroll
       for (int m = 0; m < 16; m += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(&M[(o + rr) * S + o + m]);
+        const float4 q = *reinterpret_cast<const float4*>(&M[mi(o + rr, o + m)]);
         t[m] = q.x;
         t[m + 1] = q.y;
         t[m + 2] = q.z;
@@ -353,7 +363,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
             float acc2 = 0.f;
 #pragma unroll
             for (int m = 0; m < 16; m += 4) {
-              const float4 q = *reinterpret_cast<const float4*>(&M[i * S + o + m]);
+              const float4 q = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
               acc2 = fmaf(q.x, z[m], acc2);
               acc2 = fmaf(q.y, z[m + 1], acc2);
               acc2 = fmaf(q.z, z[m + 2], acc2);
@@ -378,7 +388,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         __syncthreads();
         const int m = lane & 15, g = lane >> 4;
         float part = 0.f;
-        for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[i * S + o + m], bv[i], part);
+        for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[mi(i, o + m)], bv[i], part);
         part += __shfl_xor(part, 16, 64);
         part += __shfl_xor(part, 32, 64);
         const float sub = __shfl(part, (lane - base) & 15, 64);
@@ -389,7 +399,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       float c[16];
       const int cp = mine ? rl : 0;
 #pragma unroll
-      for (int mm = 0; mm < 16; ++mm) c[mm] = M[(o + mm) * S + o + cp];
+      for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi(o + mm, o + cp)];
 #pragma unroll
       for (int j = 15; j >= 0; --j) {
         const float xl = vd / c[j];  // meaningful at lane base + j
@@ -409,7 +419,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
 
 template <int NB>
 size_t solve_lds() {
-  return (size_t(16 * NB) * (16 * NB + 4) + 16 * NB) * sizeof(float);
+  return (size_t(NB * (NB + 1) / 2) * kBlkF + 16 * NB) * sizeof(float);
 }
 
 template <int NB, bool LONG>
