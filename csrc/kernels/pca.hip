@@ -57,7 +57,7 @@ __device__ inline void tile_coords(int tile, int nb, int& ti, int& tj) {
 }
 
 template <bool FOUR>
-__global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
+__global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
   // two stages x [side][plane hi/lo]: chunk c+1 is staged while chunk c feeds the MFMAs
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 4 * kPlane];
   const int G = a.splits * a.tiles;
@@ -81,9 +81,11 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
   const float4 shI = *reinterpret_cast<const float4*>(a.shift + fi);
   const float4 shJ = *reinterpret_cast<const float4*>(a.shift + fj);
 
-  float4 vI[4], vJ[4];
+  // two register stages: the rows of chunk c+2 are in flight while chunk c feeds the MFMAs and
+  // chunk c+1 (loaded one chunk earlier) is converted into the other LDS buffer
+  float4 vIa[4], vJa[4], vIb[4], vJb[4];
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
-  auto load = [&](int64_t r0) {
+  auto load = [&](int64_t r0, float4 (&vI)[4], float4 (&vJ)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t row = r0 + 4 * lg + i;
@@ -162,14 +164,18 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
   const int boff = (diag ? 0 : 2 * kPlane) + (64 * wj + r) * kPS + 8 * h;
   int since = 0, cur = 0;
   if (r_begin < r_end) {
-    load(r_begin);
-    stage(lds, r_begin, 0, vI, shI, diag);
-    if (!diag) stage(lds, r_begin, 1, vJ, shJ, false);
+    load(r_begin, vIa, vJa);
+    stage(lds, r_begin, 0, vIa, shI, diag);
+    if (!diag) stage(lds, r_begin, 1, vJa, shJ, false);
+    if (r_begin + kChunk < r_end) load(r_begin + kChunk, vIb, vJb);
     __syncthreads();
   }
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk) {
+  // one chunk: MFMAs on LDS buffer `cur`; rows of chunk r0 + 2 kChunk -> (nI, nJ) (the set that
+  // held chunk r0, already staged); chunk r0 + kChunk from (sI, sJ) -> the other LDS buffer
+  auto step = [&](int64_t r0, float4 (&sI)[4], float4 (&sJ)[4], float4 (&nI)[4],
+                  float4 (&nJ)[4]) {
     const bool more = r0 + kChunk < r_end;
-    if (more) load(r0 + kChunk);  // global loads in flight during the MFMAs
+    if (r0 + 2 * kChunk < r_end) load(r0 + 2 * kChunk, nI, nJ);  // in flight for 2 chunks
     const __bf16* aH = lds + cur * (4 * kPlane) + aoff;
     const __bf16* bH = lds + cur * (4 * kPlane) + boff;
 #pragma unroll
@@ -195,8 +201,8 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
     }
     if (more) {  // the other buffer was last read before the previous barrier
       __bf16* nb = lds + (cur ^ 1) * (4 * kPlane);
-      stage(nb, r0 + kChunk, 0, vI, shI, diag);
-      if (!diag) stage(nb, r0 + kChunk, 1, vJ, shJ, false);
+      stage(nb, r0 + kChunk, 0, sI, shI, diag);
+      if (!diag) stage(nb, r0 + kChunk, 1, sJ, shJ, false);
     }
     __syncthreads();
     cur ^= 1;
@@ -204,6 +210,11 @@ __global__ __launch_bounds__(kSyrkThreads) void oap_pca_syrk(SyrkArgs a) {
       flush();
       since = 0;
     }
+  };
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += 2 * kChunk) {
+    step(r0, vIb, vJb, vIa, vJa);
+    if (r0 + kChunk >= r_end) break;
+    step(r0 + kChunk, vIa, vJa, vIb, vJb);
   }
   if (first || since > 0) flush();
   if (diag) {  // column sums: the 8 loader lanes of one feature group are adjacent
