@@ -85,15 +85,16 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
   // chunk c+1 (loaded one chunk earlier) is converted into the other LDS buffer
   float4 vIa[4], vJa[4], vIb[4], vJb[4];
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
+  // Loads are unconditional (row clamped to r_end - 1, feature group clamped to 0): no
+  // per-row branches; stage() zeroes what lies outside the matrix.
+  const int fiL = okI ? fi : 0, fjL = okJ ? fj : 0;
   auto load = [&](int64_t r0, float4 (&vI)[4], float4 (&vJ)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int64_t row = r0 + 4 * lg + i;
-      const bool ok = row < r_end;
-      const float* p = a.x + (ok ? row : 0) * a.ld;
-      vI[i] = (ok && okI) ? *reinterpret_cast<const float4*>(p + fi) : make_float4(0, 0, 0, 0);
-      if (!diag)
-        vJ[i] = (ok && okJ) ? *reinterpret_cast<const float4*>(p + fj) : make_float4(0, 0, 0, 0);
+      const int64_t row = min(r0 + 4 * lg + i, r_end - 1);
+      const float* p = a.x + row * a.ld;
+      vI[i] = *reinterpret_cast<const float4*>(p + fiL);
+      if (!diag) vJ[i] = *reinterpret_cast<const float4*>(p + fjL);
     }
   };
   // centre, split, transpose into the planes; rows past r_end contribute exact zeros
@@ -101,14 +102,20 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
                    bool sums) {
     __bf16* hi = buf + (2 * side) * kPlane;
     __bf16* lo = hi + kPlane;
+    const bool okF = side == 0 ? okI : okJ;
     float c[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const bool ok = r0 + 4 * lg + i < r_end;
+      const bool ok = okF && r0 + 4 * lg + i < r_end;
       c[0][i] = ok ? v[i].x - sh.x : 0.f;
       c[1][i] = ok ? v[i].y - sh.y : 0.f;
       c[2][i] = ok ? v[i].z - sh.z : 0.f;
       c[3][i] = ok ? v[i].w - sh.w : 0.f;
+    }
+    if (sums) {  // column sums: 4 rows in fp32, then fp64 across chunks
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        cs[f] += static_cast<double>((c[f][0] + c[f][1]) + (c[f][2] + c[f][3]));
     }
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
@@ -120,7 +127,6 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
         bf16_split(c[f][i], a_, b_);
         ph[i] = a_;
         pl[i] = b_;
-        if (sums) cs[f] += static_cast<double>(c[f][i]);
       }
       const int off = (4 * lq + f) * kPS + 4 * lg;
       *reinterpret_cast<bf16x4*>(hi + off) = ph;
