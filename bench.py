@@ -32,6 +32,8 @@ def _barrier_sync(w):
 
     if w.size > 1:
         w.barrier()
+    if w.device >= 0:
+        torch.cuda.set_device(w.device)  # sync (and create torch's context on) OUR GPU only
     torch.cuda.synchronize()
     if w.ctx is not None:
         w.ctx.sync()
