@@ -770,7 +770,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer inv_scale = ctx.alloc(sizeof(double) * d);
   Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags));
   Buffer refine_d = ctx.alloc(2 * sizeof(u64));  // [exact re-decisions, tier-3 re-runs]
-  Buffer flags_h = ctx.alloc_pinned(sizeof(kern::KMeansFlags));
   Buffer counts_h = ctx.alloc_pinned(sizeof(u64) * k);
   Buffer refine_h = ctx.alloc_pinned(2 * sizeof(u64));
   ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4), s);
@@ -820,71 +819,93 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
 
   u64 tier2_seen = 0;
   RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
-  Event e0, e1, e2, e3;
   const int64_t flops_per_iter = 2 * int64_t(x.rows) * k * d;
-  for (int it = 0; it < p.max_iter; ++it) {
-    maybe_inject_fault(comm.rank(), "kmeans_iter", it);
-    roctx_push("kmeans/iteration");
-    e0.record(s);
-    OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
-    req.labels_valid = it > 0;
-    int nb = gpu_assign(ctx, x, g, req, s);
-    if (nb > 0)
-      kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
-    else
-      OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
-    e1.record(s);
-    if (comm.size() > 1) {
-      if (comm.on_device()) {
-        if (rccl) rccl->group_start();
-        comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
-        comm.allreduce(cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
-        if (rccl) rccl->group_end();
-      } else {
-        comm_allreduce(ctx, comm, stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
-        comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+  // With a tolerance the host must see each iteration's convergence flag before deciding to
+  // launch the next one (batch of 1).  tol < 0 means "exactly max_iter iterations": then up to
+  // kBatch iterations are enqueued back to back (kernels + collective, no host round trip in
+  // between) and their flags / timings are read once per batch — the host re-checks the
+  // adaptive distance tier at every batch boundary.
+  constexpr int kBatch = 8;
+  const int B = p.tol < 0 ? kBatch : 1;
+  struct IterEvents {
+    Event e0, e1, e2, e3;
+  };
+  std::vector<IterEvents> ev(B);
+  Buffer flags_hb = ctx.alloc_pinned(sizeof(kern::KMeansFlags) * B);
+  auto* flh = flags_hb.as<kern::KMeansFlags>();
+  bool stop = false;
+  for (int it0 = 0; it0 < p.max_iter && !stop; it0 += B) {
+    const int nb_it = std::min(B, p.max_iter - it0);
+    for (int b = 0; b < nb_it; ++b) {
+      const int it = it0 + b;
+      maybe_inject_fault(comm.rank(), "kmeans_iter", it);
+      roctx_push("kmeans/iteration");
+      ev[b].e0.record(s);
+      OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
+      req.labels_valid = it > 0;
+      int nb = gpu_assign(ctx, x, g, req, s);
+      if (nb > 0)
+        kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
+      else
+        OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+      ev[b].e1.record(s);
+      if (comm.size() > 1) {
+        if (comm.on_device()) {
+          if (rccl) rccl->group_start();
+          comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
+          comm.allreduce(cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+          if (rccl) rccl->group_end();
+        } else {
+          comm_allreduce(ctx, comm, stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
+          comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+        }
       }
+      ev[b].e2.record(s);
+      kern::kmeans_finalize(fa, s);
+      OAP_HIP_CHECK(hipMemcpyAsync(flh + b, flags_d.data(), sizeof(kern::KMeansFlags),
+                                   hipMemcpyDeviceToHost, s));
+      ev[b].e3.record(s);
+      roctx_pop();
     }
-    e2.record(s);
-    kern::kmeans_finalize(fa, s);
-    OAP_HIP_CHECK(hipMemcpyAsync(flags_h.data(), flags_d.data(), sizeof(kern::KMeansFlags),
-                                 hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(
         hipMemcpyAsync(counts_h.data(), counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
-    e3.record(s);
     comm.wait(s);
-    roctx_pop();
-    float ms_assign = Event::elapsed_ms(e0, e1), ms_comm = Event::elapsed_ms(e1, e2),
-          ms_all = Event::elapsed_ms(e0, e3);
-    M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.bytes()));
-    M.add("kmeans/allreduce", ms_comm * 1e3, int64_t(kd + k) * 8 + 8);
-    M.add("kmeans/iteration", ms_all * 1e3);
-    auto* fl = flags_h.as<kern::KMeansFlags>();
-    if (Logger::instance().level() <= LogLevel::Info) {
-      std::ostringstream os;
-      os << "\"iter\":" << it << ",\"cost\":" << fl->cost << ",\"assign_us\":" << ms_assign * 1e3
-         << ",\"allreduce_us\":" << ms_comm * 1e3 << ",\"tflops\":"
-         << (ms_assign > 0 ? double(flops_per_iter) / (ms_assign * 1e-3) / 1e12 : 0.0);
-      Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
+    for (int b = 0; b < nb_it; ++b) {
+      const int it = it0 + b;
+      const float ms_assign = Event::elapsed_ms(ev[b].e0, ev[b].e1),
+                  ms_comm = Event::elapsed_ms(ev[b].e1, ev[b].e2),
+                  ms_all = Event::elapsed_ms(ev[b].e0, ev[b].e3);
+      M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.bytes()));
+      M.add("kmeans/allreduce", ms_comm * 1e3, int64_t(kd + k) * 8 + 8);
+      M.add("kmeans/iteration", ms_all * 1e3);
+      const kern::KMeansFlags& fl = flh[b];
+      if (Logger::instance().level() <= LogLevel::Info) {
+        std::ostringstream os;
+        os << "\"iter\":" << it << ",\"cost\":" << fl.cost << ",\"assign_us\":" << ms_assign * 1e3
+           << ",\"allreduce_us\":" << ms_comm * 1e3 << ",\"tflops\":"
+           << (ms_assign > 0 ? double(flops_per_iter) / (ms_assign * 1e-3) / 1e12 : 0.0);
+        Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
+      }
+      res.cost = fl.cost;
+      res.cost_history.push_back(fl.cost);
+      res.num_iter = it + 1;
+      if (fl.converged && p.tol >= 0) {  // (B == 1 here: nothing was enqueued past it)
+        res.converged = true;
+        stop = true;
+        break;
+      }
     }
-    res.cost = fl->cost;
-    res.cost_history.push_back(fl->cost);
-    res.num_iter = it + 1;
     {  // adaptive tier: tier-1 first pays off only while tier-3 re-runs stay rare
       const u64 t2 = refine_h.as<u64>()[1];
-      const double tiles = double((x.rows + 31) / 32);
+      const double tiles = double((x.rows + 31) / 32) * nb_it;
       if (req.fast1 && tiles > 0 && double(t2 - tier2_seen) > 0.02 * tiles) {
         req.fast1 = false;
         Logger::instance().log(LogLevel::Info, "kmeans/tier1_off",
-                               "\"iter\":" + std::to_string(it));
+                               "\"iter\":" + std::to_string(res.num_iter - 1));
       }
       tier2_seen = t2;
-    }
-    if (fl->converged && p.tol >= 0) {  // tol < 0: run exactly max_iter iterations
-      res.converged = true;
-      break;
     }
   }
   res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);

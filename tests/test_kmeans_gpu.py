@@ -231,3 +231,18 @@ def test_api_bf16_storage():
         assert abs(m.summary.trainingCost - ref.cost) / ref.cost < 1e-3
     finally:
         O.shutdown_world()
+
+
+def test_batched_iterations_match_stepwise(native):
+    """tol < 0 enqueues iterations in batches without host round trips: same result and cost
+    history as the step-by-step loop (tol = 0 here never converges within 5 iterations)."""
+    X = f32_blobs(40000, 20, 16, seed=21, sigma=1.5)
+    init = X[:16]
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X, "f32", native.kmeans_ld(20))
+    a = native.kmeans_fit(g, native.LocalComm(True), t, init, 16, 11, -1.0)
+    b = native.kmeans_fit(g, native.LocalComm(True), t, init, 16, 11, 0.0)
+    assert a["num_iter"] == 11 and b["num_iter"] == 11
+    assert np.array_equal(a["centers"], b["centers"])
+    assert a["cost_history"] == b["cost_history"]
+    assert a["last_counts"] == b["last_counts"]
