@@ -78,42 +78,71 @@ constexpr int partial_floats() {
 }
 
 // Gramian + b + n_u of ratings [p0, p1) of one row (lane layout of the 16x16x4 f32 MFMA).
+// Ratings go kSteps x 4 at a time: lanes fetch the block's (item, rating) pairs with one load
+// each (the next block's pairs are prefetched), then all k-steps' factor rows (kSteps x NB loads
+// per lane) are issued before the first MFMA — more rows in flight per wave, and the
+// item-index -> factor-row dependency is paid once per block.  Loads are unconditional
+// (out-of-range ratings read row 0 with zero weights).  kSteps = 2 keeps the rank-100 solve
+// kernel free of register spills (4 spills).
 template <int NB>
 __device__ inline void accumulate(const int32_t* __restrict__ cols, const float* __restrict__ vals,
                                   int64_t p0, int64_t p1, const float* __restrict__ src, int ld,
                                   float alpha, bool implicit, f4 (&acc)[NB * (NB + 1) / 2],
                                   float (&bacc)[NB], int& nexp) {
+  constexpr int kSteps = 2, kBlock = 4 * kSteps;
   const int lane = threadIdx.x, kk = lane >> 4, c = lane & 15;
-  for (int64_t p = p0; p < p1; p += 4) {
-    const int64_t idx = p + kk;
-    const bool ok = idx < p1;
-    const int item = ok ? cols[idx] : 0;
-    const float rv = ok ? vals[idx] : 0.f;
-    float wa, wb;
-    if (implicit) {
-      const float c1 = alpha * fabsf(rv);
-      wa = c1;
-      wb = rv > 0.f ? 1.f + c1 : 0.f;
-      nexp += (ok && rv > 0.f && c == 0) ? 1 : 0;
-    } else {  // explicit: A += y y^T, b += r y
-      wa = ok ? 1.f : 0.f;
-      wb = rv;
-      nexp += (ok && c == 0) ? 1 : 0;
+  auto fetch = [&](int64_t p, int& it, float& rv) {
+    const int64_t q = p + (c & (kBlock - 1));
+    const bool ok = q < p1;
+    it = ok ? cols[q] : -1;
+    rv = ok ? vals[q] : 0.f;
+  };
+  int it_n = -1;
+  float rv_n = 0.f;
+  if (p0 < p1) fetch(p0, it_n, rv_n);
+  for (int64_t p = p0; p < p1; p += kBlock) {
+    const int it_l = it_n;
+    const float rv_l = rv_n;
+    if (p + kBlock < p1) fetch(p + kBlock, it_n, rv_n);  // next block's pairs in flight
+    float yv[kSteps][NB], rvs[kSteps];
+    bool oks[kSteps];
+#pragma unroll
+    for (int s4 = 0; s4 < kSteps; ++s4) {
+      const int item = __shfl(it_l, 4 * s4 + kk, 64);
+      rvs[s4] = __shfl(rv_l, 4 * s4 + kk, 64);
+      oks[s4] = item >= 0;
+      const float* yrow = src + static_cast<int64_t>(oks[s4] ? item : 0) * ld + c;
+#pragma unroll
+      for (int f = 0; f < NB; ++f) yv[s4][f] = yrow[16 * f];
     }
-    const float* yrow = src + static_cast<int64_t>(item) * ld + c;
-    float yv[NB], av[NB];
 #pragma unroll
-    for (int f = 0; f < NB; ++f) {
-      yv[f] = ok ? yrow[16 * f] : 0.f;
-      av[f] = wa * yv[f];
-      bacc[f] = fmaf(wb, yv[f], bacc[f]);
+    for (int s4 = 0; s4 < kSteps; ++s4) {
+      const bool ok = oks[s4];
+      const float rv = rvs[s4];
+      float wa, wb;
+      if (implicit) {
+        const float c1 = alpha * fabsf(rv);
+        wa = ok ? c1 : 0.f;
+        wb = (ok && rv > 0.f) ? 1.f + c1 : 0.f;
+        nexp += (ok && rv > 0.f && c == 0) ? 1 : 0;
+      } else {  // explicit: A += y y^T, b += r y
+        wa = ok ? 1.f : 0.f;
+        wb = ok ? rv : 0.f;
+        nexp += (ok && c == 0) ? 1 : 0;
+      }
+      float av[NB];
+#pragma unroll
+      for (int f = 0; f < NB; ++f) {
+        av[f] = wa * yv[s4][f];
+        bacc[f] = fmaf(wb, yv[s4][f], bacc[f]);
+      }
+      int t = 0;
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+        for (int bj = 0; bj <= bi; ++bj, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bi], yv[s4][bj], acc[t], 0, 0, 0);
     }
-    int t = 0;
-#pragma unroll
-    for (int bi = 0; bi < NB; ++bi)
-#pragma unroll
-      for (int bj = 0; bj <= bi; ++bj, ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bi], yv[bj], acc[t], 0, 0, 0);
   }
 }
 
