@@ -121,7 +121,8 @@ void kmeans_prepare_centers(const double* centers64, int k, int d, int dp, float
 
 // ---- PCA (kernels/pca.hip) ------------------------------------------------------------------
 struct PcaPlan {
-  int nb = 0;      // 128-feature blocks
+  int tw = 128;    // output tile width (128 or 256)
+  int nb = 0;      // tw-feature blocks
   int tiles = 0;   // upper-triangular 128x128 tiles
   int splits = 0;  // row splits (one fp64 slab each)
   int64_t rows_per_split = 0;

@@ -235,9 +235,172 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
   }
 }
 
+// 256 x 256 output tile per workgroup (d > 128): 8 waves in a 2 x 4 grid, each 128 x 64
+// (4 x 2 MFMA blocks, 128 accumulator registers).  Per staged row the tile does twice the MFMA
+// work of the 128-wide kernel, so the per-row staging VALU, the LDS writes, the barriers and the
+// L2 / HBM traffic per flop all halve.  One LDS stage (82 KB): rows of chunk c+1 are loaded into
+// registers while chunk c feeds the MFMAs; two barriers per chunk.
+constexpr int kTile2 = 256;
+constexpr int kPlane2 = kTile2 * kPS;
+constexpr int kSyrk2Threads = 512;
+
+template <bool FOUR>
+__global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * kPlane2];  // [side][hi|lo][feat][row]
+  const int G = a.splits * a.tiles;
+  const int per = gridDim.x / 8;
+  const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= G) return;
+  const int split = L / a.tiles, tile = L - split * a.tiles;
+  int ti, tj;
+  tile_coords(tile, a.nb, ti, tj);
+  const bool diag = ti == tj;
+  const int64_t r_begin = int64_t(split) * a.rows_per_split;
+  const int64_t r_end = min(a.n, r_begin + a.rows_per_split);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wi = wave >> 2, wj = wave & 3;
+  // loader: rows 4*lg .. 4*lg+3 of the chunk, features 4*lq .. 4*lq+3 of each side
+  const int lg = tid & 7, lq = tid >> 3;
+  const int fi = ti * kTile2 + 4 * lq, fj = tj * kTile2 + 4 * lq;
+  const bool okI = fi < a.ld, okJ = fj < a.ld;
+  const int fiL = okI ? fi : 0, fjL = okJ ? fj : 0;
+  const float4 shI = *reinterpret_cast<const float4*>(a.shift + fi);
+  const float4 shJ = *reinterpret_cast<const float4*>(a.shift + fj);
+
+  float4 vI[4], vJ[4];
+  double cs[4] = {0.0, 0.0, 0.0, 0.0};
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t row = min(r0 + 4 * lg + i, r_end - 1);
+      const float* p = a.x + row * a.ld;
+      vI[i] = *reinterpret_cast<const float4*>(p + fiL);
+      if (!diag) vJ[i] = *reinterpret_cast<const float4*>(p + fjL);
+    }
+  };
+  auto stage = [&](int64_t r0, int side, const float4 (&v)[4], const float4 sh, bool sums) {
+    __bf16* hi = lds + (2 * side) * kPlane2;
+    __bf16* lo = hi + kPlane2;
+    const bool okF = side == 0 ? okI : okJ;
+    float c[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool ok = okF && r0 + 4 * lg + i < r_end;
+      c[0][i] = ok ? v[i].x - sh.x : 0.f;
+      c[1][i] = ok ? v[i].y - sh.y : 0.f;
+      c[2][i] = ok ? v[i].z - sh.z : 0.f;
+      c[3][i] = ok ? v[i].w - sh.w : 0.f;
+    }
+    if (sums) {
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        cs[f] += static_cast<double>((c[f][0] + c[f][1]) + (c[f][2] + c[f][3]));
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      bf16x4 ph, pl;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        __bf16 a_, b_;
+        bf16_split(c[f][i], a_, b_);
+        ph[i] = a_;
+        pl[i] = b_;
+      }
+      const int off = (4 * lq + f) * kPS + 4 * lg;
+      *reinterpret_cast<bf16x4*>(hi + off) = ph;
+      *reinterpret_cast<bf16x4*>(lo + off) = pl;
+    }
+  };
+
+  f32x16 acc[4][2];
+  auto zero = [&]() {
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.f;
+  };
+  zero();
+  double* slab = a.part + (size_t(split) * a.tiles + tile) * (size_t(kTile2) * kTile2);
+  bool first = true;
+  auto flush = [&]() {
+    double* base = slab + (128 * wi + 4 * h) * kTile2 + 64 * wj + r;
+    asm volatile("" : "+v"(base));
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          double* p = base + (32 * x + (e & 3) + 8 * (e >> 2)) * kTile2 + 32 * y;
+          const double v = static_cast<double>(acc[x][y][e]);
+          *p = first ? v : *p + v;
+          if ((e & 3) == 3) asm volatile("" ::: "memory");
+        }
+    first = false;
+    zero();
+  };
+
+  const int aoff = (128 * wi + r) * kPS + 8 * h;
+  const int boff = (diag ? 0 : 2 * kPlane2) + (64 * wj + r) * kPS + 8 * h;
+  int since = 0;
+  if (r_begin < r_end) load(r_begin);
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk) {
+    stage(r0, 0, vI, shI, diag);
+    if (!diag) stage(r0, 1, vJ, shJ, false);
+    __syncthreads();
+    if (r0 + kChunk < r_end) load(r0 + kChunk);  // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ah[4], al[4], bh[2], bl[2];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        ah[x] = *reinterpret_cast<const bf16x8*>(lds + aoff + 32 * x * kPS + 16 * ks);
+        al[x] = *reinterpret_cast<const bf16x8*>(lds + kPlane2 + aoff + 32 * x * kPS + 16 * ks);
+      }
+#pragma unroll
+      for (int y = 0; y < 2; ++y) {
+        bh[y] = *reinterpret_cast<const bf16x8*>(lds + boff + 32 * y * kPS + 16 * ks);
+        bl[y] = *reinterpret_cast<const bf16x8*>(lds + kPlane2 + boff + 32 * y * kPS + 16 * ks);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bl[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bh[y], acc[x][y], 0, 0, 0);
+          if (FOUR)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
+        }
+    }
+    __syncthreads();  // every wave is done reading before the next stage overwrites
+    if (++since == a.flush_chunks) {
+      flush();
+      since = 0;
+    }
+  }
+  if (first || since > 0) flush();
+  if (diag) {
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      double v = cs[f];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (lg == 0) a.cpart[(size_t(split) * a.nb + ti) * kTile2 + 4 * lq + f] = v;
+    }
+  }
+}
+
 __global__ void oap_pca_reduce(const double* __restrict__ part, const double* __restrict__ cpart,
-                               int splits, int tiles, int nb, int d, double* __restrict__ out,
-                               double* __restrict__ colsum) {
+                               int splits, int tiles, int nb, int d, int tw,
+                               double* __restrict__ out, double* __restrict__ colsum) {
+  const int kTile = tw;  // 128 or 256
   const int64_t total = int64_t(tiles) * kTile * kTile;
   for (int64_t idx = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; idx < total;
        idx += int64_t(gridDim.x) * blockDim.x) {
@@ -265,21 +428,25 @@ __global__ void oap_pca_reduce(const double* __restrict__ part, const double* __
 
 PcaPlan pca_syrk_plan(int64_t n, int d, int num_cus) {
   PcaPlan p;
-  p.nb = (d + kTile - 1) / kTile;
+  // 256-wide tiles (one 512-thread workgroup per CU) once there are at least two 128-wide column
+  // blocks; 128-wide tiles (two 256-thread workgroups per CU) for d <= 128
+  p.tw = d > kTile ? kTile2 : kTile;
+  p.nb = (d + p.tw - 1) / p.tw;
   p.tiles = p.nb * (p.nb + 1) / 2;
-  const int64_t want = int64_t(std::max(num_cus, 64)) * 6;  // ~2 resident workgroups per CU x 3
+  const int per_cu = p.tw == kTile2 ? 3 : 6;  // resident workgroups per CU x ~3 waves of them
+  const int64_t want = int64_t(std::max(num_cus, 64)) * per_cu;
   int64_t s = (want + p.tiles - 1) / p.tiles;
   const int64_t max_s = std::max<int64_t>(1, (n + 4 * kChunk - 1) / (4 * kChunk));
   s = std::max<int64_t>(1, std::min(s, max_s));
-  // bound the fp64 slab (splits x tiles x 128 KB) to 1 GiB unless one split already exceeds it
-  const int64_t slab_tile = int64_t(kTile) * kTile * 8;
+  // bound the fp64 slab (splits x tiles x tw^2 doubles) to 1 GiB unless one split exceeds it
+  const int64_t slab_tile = int64_t(p.tw) * p.tw * 8;
   while (s > 1 && s * p.tiles * slab_tile > (int64_t(1) << 30)) --s;
   p.splits = static_cast<int>(s);
   p.rows_per_split = round_up((n + s - 1) / s, kChunk);
   if (p.rows_per_split == 0) p.rows_per_split = kChunk;
-  p.part_elems = size_t(p.splits) * p.tiles * kTile * kTile;
-  p.cpart_elems = size_t(p.splits) * p.nb * kTile;
-  p.shift_elems = size_t(p.nb) * kTile;
+  p.part_elems = size_t(p.splits) * p.tiles * p.tw * p.tw;
+  p.cpart_elems = size_t(p.splits) * p.nb * p.tw;
+  p.shift_elems = size_t(p.nb) * p.tw;
   const int64_t g = int64_t(p.splits) * p.tiles;
   p.grid = static_cast<int>(round_up(g, 8));
   return p;
@@ -302,18 +469,24 @@ void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, 
   a.rows_per_split = p.rows_per_split;
   a.part = part;
   a.cpart = cpart;
-  if (four)
+  if (p.tw == kTile2) {
+    if (four)
+      hipLaunchKernelGGL(oap_pca_syrk_w256<true>, dim3(p.grid), dim3(kSyrk2Threads), 0, s, a);
+    else
+      hipLaunchKernelGGL(oap_pca_syrk_w256<false>, dim3(p.grid), dim3(kSyrk2Threads), 0, s, a);
+  } else if (four) {
     hipLaunchKernelGGL(oap_pca_syrk<true>, dim3(p.grid), dim3(kSyrkThreads), 0, s, a);
-  else
+  } else {
     hipLaunchKernelGGL(oap_pca_syrk<false>, dim3(p.grid), dim3(kSyrkThreads), 0, s, a);
+  }
   OAP_HIP_CHECK(hipGetLastError());
 }
 
 void pca_reduce(const PcaPlan& p, const double* part, const double* cpart, int d, double* out,
                 double* colsum, hipStream_t s) {
-  const int64_t total = int64_t(p.tiles) * kTile * kTile;
+  const int64_t total = int64_t(p.tiles) * p.tw * p.tw;
   hipLaunchKernelGGL(oap_pca_reduce, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s, part,
-                     cpart, p.splits, p.tiles, p.nb, d, out, colsum);
+                     cpart, p.splits, p.tiles, p.nb, d, p.tw, out, colsum);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
