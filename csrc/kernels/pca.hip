@@ -238,15 +238,18 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
 // 256 x 256 output tile per workgroup (d > 128): 8 waves in a 2 x 4 grid, each 128 x 64
 // (4 x 2 MFMA blocks, 128 accumulator registers).  Per staged row the tile does twice the MFMA
 // work of the 128-wide kernel, so the per-row staging VALU, the LDS writes, the barriers and the
-// L2 / HBM traffic per flop all halve.  One LDS stage (82 KB): rows of chunk c+1 are loaded into
-// registers while chunk c feeds the MFMAs; two barriers per chunk.
+// L2 / HBM traffic per flop all halve.  16-row chunks, two LDS stages (96 KB): chunk c+1 is
+// converted into the other stage while chunk c feeds the MFMAs (one barrier per chunk), and the
+// rows of chunk c+2 are in flight in registers.
 constexpr int kTile2 = 256;
-constexpr int kPlane2 = kTile2 * kPS;
+constexpr int kChunk2 = 16;
+constexpr int kPS2 = kChunk2 + 8;        // 48 B per feature row: odd 16-byte slots
+constexpr int kPlane2 = kTile2 * kPS2;
 constexpr int kSyrk2Threads = 512;
 
 template <bool FOUR>
 __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[4 * kPlane2];  // [side][hi|lo][feat][row]
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 4 * kPlane2];  // [stage][side][hi|lo]
   const int G = a.splits * a.tiles;
   const int per = gridDim.x / 8;
   const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int wi = wave >> 2, wj = wave & 3;
-  // loader: rows 4*lg .. 4*lg+3 of the chunk, features 4*lq .. 4*lq+3 of each side
+  // loader: rows 2*lg, 2*lg+1 of the chunk, features 4*lq .. 4*lq+3 of each side
   const int lg = tid & 7, lq = tid >> 3;
   const int fi = ti * kTile2 + 4 * lq, fj = tj * kTile2 + 4 * lq;
   const bool okI = fi < a.ld, okJ = fj < a.ld;
@@ -269,25 +272,26 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   const float4 shI = *reinterpret_cast<const float4*>(a.shift + fi);
   const float4 shJ = *reinterpret_cast<const float4*>(a.shift + fj);
 
-  float4 vI[4], vJ[4];
+  float4 vI[2], vJ[2];
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
   auto load = [&](int64_t r0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t row = min(r0 + 4 * lg + i, r_end - 1);
+    for (int i = 0; i < 2; ++i) {
+      const int64_t row = min(r0 + 2 * lg + i, r_end - 1);
       const float* p = a.x + row * a.ld;
       vI[i] = *reinterpret_cast<const float4*>(p + fiL);
       if (!diag) vJ[i] = *reinterpret_cast<const float4*>(p + fjL);
     }
   };
-  auto stage = [&](int64_t r0, int side, const float4 (&v)[4], const float4 sh, bool sums) {
-    __bf16* hi = lds + (2 * side) * kPlane2;
+  auto stage = [&](__bf16* buf, int64_t r0, int side, const float4 (&v)[2], const float4 sh,
+                   bool sums) {
+    __bf16* hi = buf + (2 * side) * kPlane2;
     __bf16* lo = hi + kPlane2;
     const bool okF = side == 0 ? okI : okJ;
-    float c[4][4];
+    float c[4][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const bool ok = okF && r0 + 4 * lg + i < r_end;
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = okF && r0 + 2 * lg + i < r_end;
       c[0][i] = ok ? v[i].x - sh.x : 0.f;
       c[1][i] = ok ? v[i].y - sh.y : 0.f;
       c[2][i] = ok ? v[i].z - sh.z : 0.f;
@@ -295,23 +299,22 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
     }
     if (sums) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f)
-        cs[f] += static_cast<double>((c[f][0] + c[f][1]) + (c[f][2] + c[f][3]));
+      for (int f = 0; f < 4; ++f) cs[f] += static_cast<double>(c[f][0] + c[f][1]);
     }
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-      bf16x4 ph, pl;
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      bf16x2 ph, pl;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 2; ++i) {
         __bf16 a_, b_;
         bf16_split(c[f][i], a_, b_);
         ph[i] = a_;
         pl[i] = b_;
       }
-      const int off = (4 * lq + f) * kPS + 4 * lg;
-      *reinterpret_cast<bf16x4*>(hi + off) = ph;
-      *reinterpret_cast<bf16x4*>(lo + off) = pl;
+      const int off = (4 * lq + f) * kPS2 + 2 * lg;
+      *reinterpret_cast<bf16x2*>(hi + off) = ph;
+      *reinterpret_cast<bf16x2*>(lo + off) = pl;
     }
   };
 
@@ -345,47 +348,55 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
     zero();
   };
 
-  const int aoff = (128 * wi + r) * kPS + 8 * h;
-  const int boff = (diag ? 0 : 2 * kPlane2) + (64 * wj + r) * kPS + 8 * h;
-  int since = 0;
-  if (r_begin < r_end) load(r_begin);
-  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk) {
-    stage(r0, 0, vI, shI, diag);
-    if (!diag) stage(r0, 1, vJ, shJ, false);
+  const int aoff = (128 * wi + r) * kPS2 + 8 * h;
+  const int boff = (diag ? 0 : 2 * kPlane2) + (64 * wj + r) * kPS2 + 8 * h;
+  const int flush_every = a.flush_chunks * (kChunk / kChunk2);  // same rows per flush
+  int since = 0, cur = 0;
+  if (r_begin < r_end) {
+    load(r_begin);
+    stage(lds, r_begin, 0, vI, shI, diag);
+    if (!diag) stage(lds, r_begin, 1, vJ, shJ, false);
+    if (r_begin + kChunk2 < r_end) load(r_begin + kChunk2);
     __syncthreads();
-    if (r0 + kChunk < r_end) load(r0 + kChunk);  // in flight during the MFMAs
+  }
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk2) {
+    const __bf16* buf = lds + cur * (4 * kPlane2);
+    bf16x8 ah[4], al[4], bh[2], bl[2];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 ah[4], al[4], bh[2], bl[2];
+    for (int x = 0; x < 4; ++x) {
+      ah[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + 32 * x * kPS2);
+      al[x] = *reinterpret_cast<const bf16x8*>(buf + kPlane2 + aoff + 32 * x * kPS2);
+    }
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        ah[x] = *reinterpret_cast<const bf16x8*>(lds + aoff + 32 * x * kPS + 16 * ks);
-        al[x] = *reinterpret_cast<const bf16x8*>(lds + kPlane2 + aoff + 32 * x * kPS + 16 * ks);
-      }
+    for (int y = 0; y < 2; ++y) {
+      bh[y] = *reinterpret_cast<const bf16x8*>(buf + boff + 32 * y * kPS2);
+      bl[y] = *reinterpret_cast<const bf16x8*>(buf + kPlane2 + boff + 32 * y * kPS2);
+    }
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) {
-        bh[y] = *reinterpret_cast<const bf16x8*>(lds + boff + 32 * y * kPS + 16 * ks);
-        bl[y] = *reinterpret_cast<const bf16x8*>(lds + kPlane2 + boff + 32 * y * kPS + 16 * ks);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bl[y], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bh[y], acc[x][y], 0, 0, 0);
+        if (FOUR)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
       }
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) {
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bl[y], acc[x][y], 0, 0, 0);
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bh[y], acc[x][y], 0, 0, 0);
-          if (FOUR)
-            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
-        }
+    if (r0 + kChunk2 < r_end) {  // the other stage was last read before the previous barrier
+      __bf16* nb = lds + (cur ^ 1) * (4 * kPlane2);
+      stage(nb, r0 + kChunk2, 0, vI, shI, diag);
+      if (!diag) stage(nb, r0 + kChunk2, 1, vJ, shJ, false);
+      if (r0 + 2 * kChunk2 < r_end) load(r0 + 2 * kChunk2);
     }
-    __syncthreads();  // every wave is done reading before the next stage overwrites
-    if (++since == a.flush_chunks) {
+    __syncthreads();
+    cur ^= 1;
+    if (++since == flush_every) {
       flush();
       since = 0;
     }
   }
   if (first || since > 0) flush();
-  if (diag) {
+  if (diag) {  // column sums: the 8 loader lanes of one feature group are adjacent
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
       double v = cs[f];
@@ -442,7 +453,7 @@ PcaPlan pca_syrk_plan(int64_t n, int d, int num_cus) {
   const int64_t slab_tile = int64_t(p.tw) * p.tw * 8;
   while (s > 1 && s * p.tiles * slab_tile > (int64_t(1) << 30)) --s;
   p.splits = static_cast<int>(s);
-  p.rows_per_split = round_up((n + s - 1) / s, kChunk);
+  p.rows_per_split = round_up((n + s - 1) / s, kChunk);  // a multiple of both chunk sizes
   if (p.rows_per_split == 0) p.rows_per_split = kChunk;
   p.part_elems = size_t(p.splits) * p.tiles * p.tw * p.tw;
   p.cpart_elems = size_t(p.splits) * p.nb * p.tw;
