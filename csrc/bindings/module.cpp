@@ -297,6 +297,42 @@ PYBIND11_MODULE(_native, m) {
       });
 
   m.def(
+      "table_view",
+      [](std::shared_ptr<Context> ctx, uintptr_t ptr, int64_t rows, int cols, int64_t ld,
+         const std::string& dtype) {
+        // Zero-copy view of memory owned elsewhere (a torch tensor's storage, ptr =
+        // tensor.data_ptr()); the caller keeps the owner alive while the view is used.
+        const DType dt = parse_dtype(dtype);
+        OAP_CHECK(rows >= 0 && cols > 0 && ld >= cols, "bad view shape");
+        OAP_CHECK(ptr != 0 || rows == 0, "null view pointer");
+        OAP_CHECK(ptr % 16 == 0, "view rows must be 16-byte aligned");
+        auto t = std::make_shared<DenseTable>();
+        t->rows = rows;
+        t->cols = cols;
+        t->ld = ld;
+        t->dtype = dt;
+        t->backend = ctx->backend();
+        t->data = Buffer::view(reinterpret_cast<void*>(ptr), size_t(rows) * ld * dtype_size(dt));
+        return t;
+      },
+      py::arg("ctx"), py::arg("ptr"), py::arg("rows"), py::arg("cols"), py::arg("ld"),
+      py::arg("dtype") = "f32");
+  m.def(
+      "kmeans_predict_device",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> centers,
+         uintptr_t labels_ptr, uintptr_t dist_ptr) {
+        auto c = py::array_t<double, py::array::c_style | py::array::forcecast>(centers);
+        if (c.ndim() != 2 || c.shape(1) != t->cols)
+          throw ConfigError("centers must be k x d with d == table cols");
+        std::vector<double> cv(c.data(), c.data() + c.size());
+        const int k = static_cast<int>(c.shape(0));
+        py::gil_scoped_release rel;
+        kmeans_predict_device(*ctx, *t, cv, k, reinterpret_cast<int32_t*>(labels_ptr),
+                              reinterpret_cast<float*>(dist_ptr));
+      },
+      py::arg("ctx"), py::arg("table"), py::arg("centers"), py::arg("labels_ptr"),
+      py::arg("dist_ptr"));
+  m.def(
       "upload_dense",
       [](std::shared_ptr<Context> ctx, py::array arr, const std::string& storage, int64_t ld) {
         py::buffer_info bi = arr.request();

@@ -922,6 +922,23 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   return res;
 }
 
+void kmeans_predict_device(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
+                           int k, int32_t* labels, float* dist2) {
+  OAP_CHECK(ctx.is_gpu(), "kmeans_predict_device needs a GPU context");
+  OAP_CHECK(centers.size() == size_t(k) * x.cols, "centers must be k x d");
+  OAP_CHECK(labels && dist2, "device output pointers required");
+  check_gpu_table(x);
+  ctx.activate();
+  if (x.rows == 0) return;
+  TraceRange tr(&ctx.metrics(), "kmeans/predict_device");
+  GpuCenters g = upload_centers(ctx, centers, k, x.cols);
+  AssignReq req;
+  req.labels = labels;
+  req.mindist = dist2;
+  gpu_assign(ctx, x, g, req, ctx.compute());
+  OAP_HIP_CHECK(hipStreamSynchronize(ctx.compute()));
+}
+
 void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>& centers, int k,
                     int32_t* labels, double* dist2) {
   OAP_CHECK(centers.size() == size_t(k) * x.cols, "centers must be k x d");

@@ -62,6 +62,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
 void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>& centers, int k,
                     int32_t* labels, double* dist2);
 
+// Same on device-resident outputs (e.g. torch tensors): labels[rows] int32, dist2[rows] f32.
+void kmeans_predict_device(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
+                           int k, int32_t* labels, float* dist2);
+
 // Average device time (ms) of the fused assign kernel over `reps` launches with optional timing
 // ablations (kern::KMeansAssignArgs::ablate) — the per-phase cost breakdown used for tuning.
 double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,

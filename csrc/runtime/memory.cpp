@@ -169,9 +169,18 @@ Buffer Buffer::device(const std::shared_ptr<DeviceArena>& arena, size_t bytes) {
   return b;
 }
 
+Buffer Buffer::view(void* p, size_t bytes) {
+  Buffer b;
+  b.ptr_ = p;
+  b.bytes_ = bytes;
+  b.kind_ = MemKind::View;
+  return b;
+}
+
 void Buffer::reset() {
   if (!ptr_) return;
   switch (kind_) {
+    case MemKind::View: break;
     case MemKind::Host: std::free(ptr_); break;
     case MemKind::Pinned: (void)hipHostFree(ptr_); break;
     case MemKind::Device:

@@ -64,7 +64,7 @@ class DeviceArena {
   std::map<void*, Block> live_;
 };
 
-enum class MemKind : int { Host = 0, Device = 1, Pinned = 2 };
+enum class MemKind : int { Host = 0, Device = 1, Pinned = 2, View = 3 };
 
 // Owning, typed-agnostic buffer.  Device buffers come from an arena; host buffers are 64-byte
 // aligned malloc; pinned buffers are hipHostMalloc (for async H2D/D2H).
@@ -74,6 +74,9 @@ class Buffer {
   static Buffer host(size_t bytes);
   static Buffer pinned(size_t bytes);
   static Buffer device(const std::shared_ptr<DeviceArena>& arena, size_t bytes);
+  // Non-owning view of memory someone else manages (e.g. a torch tensor's device storage);
+  // the owner must outlive the view.
+  static Buffer view(void* p, size_t bytes);
   ~Buffer();
   Buffer(Buffer&& o) noexcept;
   Buffer& operator=(Buffer&& o) noexcept;
