@@ -63,11 +63,22 @@ def bench_kmeans(args, w):
         N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, -1.0)
     _barrier_sync(w)
     t0 = time.perf_counter()
-    r = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, -1.0, precise=args.precise)
+    r = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, -1.0, precise=args.precise,
+                     prune=not args.no_prune)
     _barrier_sync(w)
     el = time.perf_counter() - t0
     el_max = float(w.allreduce_np(np.array([el]), "max")[0])
     assert r["num_iter"] == args.steps, r["num_iter"]
+    # the same timed run with every distance evaluated (no bound-based pruning), for reference
+    ms_unpruned = None
+    if not args.no_prune and not args.precise and not args.skip_unpruned:
+        _barrier_sync(w)
+        t2 = time.perf_counter()
+        ru = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, -1.0, prune=False)
+        _barrier_sync(w)
+        el_u = float(w.allreduce_np(np.array([time.perf_counter() - t2]), "max")[0])
+        ms_unpruned = el_u / args.steps * 1e3
+        assert np.array_equal(ru["centers"], r["centers"]), "pruning changed the result"
     # end-to-end fit(): init + Lloyd to convergence (maxIter 20, tol 1e-4)
     fit_s = None
     if not args.skip_fit:
@@ -107,6 +118,11 @@ def bench_kmeans(args, w):
                   "achieved_tflops": flops / (el_max / args.steps) / 1e12,
                   "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
                   "tier3_tiles_per_iter": r["tier3_tiles"] / max(args.steps, 1),
+                  # 32-row tile passes whose distance work the exact bounds skipped (pruning:
+                  # labels provably unchanged; cost, outputs and sums still computed per row)
+                  "pruned_tiles_per_iter": r.get("pruned_tiles", 0) / max(args.steps, 1),
+                  "tiles_per_pass": (rows_total + 31) // 32,
+                  "ms_per_step_unpruned": ms_unpruned,
                   "storage": st,
                   "distance_path": "fp32-exact MFMA" if args.precise else
                   ("tiered bf16 MFMA (1 product, then bf16x3 split where unsure) + exact-fp32 "
@@ -131,6 +147,10 @@ def main(argv=None):
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
     ap.add_argument("--skip-fit", action="store_true")
+    ap.add_argument("--no-prune", action="store_true",
+                    help="evaluate every distance (disable the exact bound-based pruning)")
+    ap.add_argument("--skip-unpruned", action="store_true",
+                    help="do not repeat the timed run without pruning for reference")
     ap.add_argument("--precise", action="store_true",
                     help="exact-fp32 MFMA distances only (no bf16-split fast path)")
     args = ap.parse_args(argv)

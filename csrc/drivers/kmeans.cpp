@@ -219,6 +219,15 @@ struct AssignReq {
   bool mindist_seeded = false;
   // start at the 1-product tier (the fit turns it off when tier-3 re-runs get frequent)
   bool fast1 = true;
+  // pruning state (kmeans_assign.hip "Pruning"): bounds [rows] float2 pairs; drift / drift_max
+  // only when bounds and `labels` hold the previous iteration's values
+  float* bounds = nullptr;
+  const float* drift = nullptr;
+  const float* drift_max = nullptr;
+  u64* pruned_tiles = nullptr;
+  // chunked path with pruning: [ceil(rows/32)] active-tile list + its counter
+  int32_t* tile_list = nullptr;
+  unsigned* tile_count = nullptr;
 };
 
 // Returns the number of cost partials written to req.cost_slab.
@@ -246,6 +255,12 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   a.precise = req.precise;
   a.refine_tiles = req.refine_tiles;
   a.fast1 = req.fast1 && !req.precise;
+  a.bounds = req.bounds;
+  a.drift = req.drift;
+  a.drift_max = req.drift_max;
+  a.pruned_tiles = req.pruned_tiles;
+  OAP_CHECK(!req.bounds || (x.cols <= 128 && !req.precise && req.labels),
+            "kmeans pruning needs the fast path (d <= 128) and persistent labels");
   const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
   if (x.cols > 128 || g.kpad <= kmax || kmax == 0)
     return kern::kmeans_assign(a, ctx.info().cu_count, s);
@@ -269,7 +284,23 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   // with the previous assignment's distance when there is one (most rows keep their label, so
   // chunks that cannot win skip the exact re-decision of their own near ties), else +huge.
   if (req.labels_valid && req.labels) {
+    if (req.bounds && req.drift && req.tile_list) {
+      OAP_HIP_CHECK(hipMemsetAsync(req.tile_count, 0, sizeof(unsigned), s));
+      a.tile_list = req.tile_list;
+      a.tile_count = req.tile_count;
+    }
     kern::kmeans_seed_mindist(a, s);
+    if (a.tile_list && req.pruned_tiles) {
+      // pruned tile passes = (tiles - listed tiles) per chunk: counted on the device
+      kern::kmeans_count_pruned(a.tile_count, (x.rows + 31) / 32,
+                                (g.k + kmax - 1) / kmax, req.pruned_tiles, s);
+    }
+  } else if (req.bounds) {
+    // no previous assignment: every row is processed; the merge passes build its bound from
+    // scratch, the seed verdict reads as "recompute" (0xbf bytes: negative floats)
+    OAP_HIP_CHECK(hipMemsetAsync(mind, 0x7f, sizeof(float) * x.rows, s));
+    OAP_HIP_CHECK(hipMemsetAsync(labels, 0, sizeof(int32_t) * x.rows, s));
+    OAP_HIP_CHECK(hipMemsetAsync(req.bounds, 0xbf, sizeof(float) * 2 * x.rows, s));
   } else if (req.mindist_seeded && req.mindist) {
     OAP_HIP_CHECK(hipMemsetAsync(labels, 0, sizeof(int32_t) * x.rows, s));
   } else {
@@ -793,11 +824,33 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   req.refine_tiles = refine_d.as<u64>();
   // chunked (large-k) path: labels/mindist persist across iterations to seed the merge passes
   Buffer lab_keep, mind_keep;
-  if (x.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x.cols, p.precise) && x.rows > 0) {
+  const bool chunked = x.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x.cols, p.precise);
+  if (chunked && x.rows > 0) {
     lab_keep = ctx.alloc(sizeof(int32_t) * x.rows);
     mind_keep = ctx.alloc(sizeof(float) * x.rows);
     req.labels = lab_keep.as<int32_t>();
     req.mindist = mind_keep.as<float>();
+  }
+  // pruning: per-row bounds (+ labels) persist across iterations, finalize reports the drift
+  const bool prune = p.prune && !p.precise && x.cols <= 128 && x.rows > 0;
+  Buffer bounds_b, drift_b, pruned_d, tiles_b;
+  if (prune) {
+    bounds_b = ctx.alloc(sizeof(float) * 2 * x.rows);
+    drift_b = ctx.alloc(sizeof(float) * (k + 1));
+    pruned_d = ctx.alloc(sizeof(u64));
+    ctx.memset(pruned_d.data(), 0, sizeof(u64), s);
+    if (!req.labels) {
+      lab_keep = ctx.alloc(sizeof(int32_t) * x.rows);
+      req.labels = lab_keep.as<int32_t>();
+    }
+    req.bounds = bounds_b.as<float>();
+    req.pruned_tiles = pruned_d.as<u64>();
+    if (chunked) {
+      tiles_b = ctx.alloc(sizeof(int32_t) * ((x.rows + 31) / 32) + 64);
+      req.tile_list = tiles_b.as<int32_t>();
+      req.tile_count = reinterpret_cast<unsigned*>(tiles_b.as<char>() +
+                                                   sizeof(int32_t) * ((x.rows + 31) / 32));
+    }
   }
 
   kern::KMeansFinalizeArgs fa;
@@ -816,6 +869,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   fa.flags = flags_d.data();
   Buffer fin_scratch = ctx.alloc(sizeof(double) * 2 * std::max(k, 1));
   fa.scratch = fin_scratch.as<double>();
+  if (prune) fa.drift = drift_b.as<float>();
 
   u64 tier2_seen = 0;
   RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
@@ -843,6 +897,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       ev[b].e0.record(s);
       OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
       req.labels_valid = it > 0;
+      if (prune) {
+        req.drift = it > 0 ? drift_b.as<float>() : nullptr;
+        req.drift_max = it > 0 ? drift_b.as<float>() + k : nullptr;
+      }
       int nb = gpu_assign(ctx, x, g, req, s);
       if (nb > 0)
         kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
@@ -914,6 +972,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   ctx.copy_to_host(refine_h.data(), refine_d.data(), 2 * sizeof(u64), s);
   res.refine_tiles = static_cast<int64_t>(refine_h.as<u64>()[0]);
   res.tier3_tiles = static_cast<int64_t>(refine_h.as<u64>()[1]);
+  if (prune) {
+    u64 pt = 0;
+    ctx.copy_to_host(&pt, pruned_d.data(), sizeof(u64), s);
+    res.pruned_tiles = static_cast<int64_t>(pt);
+  }
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
   M.set_value("kmeans/refine_tiles", double(res.refine_tiles));

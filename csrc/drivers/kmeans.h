@@ -31,6 +31,9 @@ struct KMeansParams {
   // exact-fp32 MFMA distances only (default: bf16-split fast path + exact refinement, which
   // yields the same assignments)
   bool precise = false;
+  // bound-based pruning of the distance work in Lloyd iterations after the first (GPU fast
+  // path, d <= 128); exact: assignments, centers and costs are bitwise those without it
+  bool prune = true;
 };
 
 struct KMeansResult {
@@ -47,6 +50,7 @@ struct KMeansResult {
   int64_t global_rows = 0;
   int64_t refine_tiles = 0;  // 32-row tiles re-decided by the exact pass (GPU fast path)
   int64_t tier3_tiles = 0;   // 32-row tiles whose tier-1 (one bf16 product) answer was unsure
+  int64_t pruned_tiles = 0;  // 32-row tile passes whose distance work the bounds skipped
 };
 
 // Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for

@@ -72,6 +72,22 @@ struct KMeansAssignArgs {
   bool fast1 = false;  // start at the 1-product tier (see kmeans_assign.hip)
   int ablate = 0;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work,
                    // 16 prefetch two tiles ahead instead of one, 32 no tier-1 first pass
+  // Bound-based pruning (fast path, d <= 128; see kmeans_assign.hip "Pruning").  bounds [n]:
+  // single launch: {upper bound on |x - c_label|, lower bound on the distance to every other
+  // center}; chunked (merge) passes: {running lower bound (squared) on the non-best candidates,
+  // row-skippable flag/lower bound written by the seed pass}.  drift / drift_max (set only when
+  // bounds and labels hold the previous iteration's values): per-center movement of the fp32
+  // centers since then (global index) and its maximum.
+  float* bounds = nullptr;  // float2 pairs
+  const float* drift = nullptr;
+  const float* drift_max = nullptr;
+  // optional counter of 32-row tiles whose distance work the bounds skipped
+  unsigned long long* pruned_tiles = nullptr;
+  // chunked passes after a pruning seed: the seed appends every tile holding a row that may
+  // change its label to tile_list (count in *tile_count, zeroed before the seed); the passes
+  // then visit only those tiles, so pruned tiles cost no row reads at all
+  int32_t* tile_list = nullptr;
+  unsigned* tile_count = nullptr;
 };
 // Upper bound on rows one assign workgroup processes for n local rows (device independent); the
 // fixed-point scale keeps per-workgroup LDS partial sums below 2^53 with it.
@@ -83,6 +99,9 @@ int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s);
 // Chunked path (d <= 128): mindist[i] = |x_i - centers[labels[i]]|^2, bitwise as the assign
 // kernel computes it, so later merge passes can skip chunks that cannot beat it.
 void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s);
+// *pruned += (ntiles - *listed) * passes (device side: no host round trip)
+void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
+                         unsigned long long* pruned, hipStream_t s);
 int kmeans_cost_slab_size(int num_cus);
 // sums/counts += rows grouped by labels (fixed point; used after chunked assignment).  Cluster
 // ranges are owned by workgroup groups that each keep their slice of the sums in LDS, so every
@@ -106,6 +125,8 @@ struct KMeansFinalizeArgs {
   const double* cost_in = nullptr;  // allreduced cost (1 value)
   void* flags = nullptr;            // KMeansFlags out
   double* scratch = nullptr;        // [2k]: enables the multi-block finalize (else 1 block)
+  // optional [k + 1] out: |centers32_new - centers32_old| per center (rounded up), [k] = max
+  float* drift = nullptr;
 };
 struct KMeansFlags {
   int converged;

@@ -195,29 +195,36 @@ __global__ __launch_bounds__(kAccThreads) void oap_kmeans_accumulate_owned(
 __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a) {
   __shared__ int s_conv, s_nonempty;
   __shared__ double s_shift[256];
-  __shared__ float s_norm[256];
+  __shared__ float s_norm[256], s_drift[256];
   if (threadIdx.x == 0) {
     s_conv = 1;
     s_nonempty = 0;
   }
   __syncthreads();
   double my_max = 0.0;
-  float my_nmax = 0.f;
+  float my_nmax = 0.f, my_drift = 0.f;
   for (int c = threadIdx.x; c < a.k; c += blockDim.x) {
     const long long cntv = static_cast<long long>(a.counts[c]);
     double* c64 = a.centers64 + size_t(c) * a.d;
-    double shift2 = 0.0, nrm = 0.0;
+    double shift2 = 0.0, nrm = 0.0, dr2 = 0.0;
     if (cntv > 0) {
       atomicAdd(&s_nonempty, 1);
       for (int f = 0; f < a.d; ++f) {
         const long long sv = static_cast<long long>(a.sums[size_t(c) * a.d + f]);
         const double nv = double(sv) * a.inv_scale[f] / double(cntv);  // == CPU engine formula
         const double df = nv - c64[f];
+        const double dv = double(static_cast<float>(nv) - static_cast<float>(c64[f]));
         shift2 += df * df;
+        dr2 += dv * dv;
         c64[f] = nv;
       }
       if (shift2 > a.tol * a.tol) atomicAnd(&s_conv, 0);
       if (shift2 > my_max) my_max = shift2;
+    }
+    if (a.drift) {
+      const float dr = static_cast<float>(sqrt(dr2) * (1.0 + 1e-6));  // rounded up
+      a.drift[c] = dr;
+      my_drift = fmaxf(my_drift, dr);
     }
     for (int f = 0; f < a.d; ++f) {
       const float v = static_cast<float>(c64[f]);
@@ -229,13 +236,15 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
   }
   s_shift[threadIdx.x] = my_max;
   s_norm[threadIdx.x] = my_nmax;
+  s_drift[threadIdx.x] = my_drift;
   __syncthreads();
   if (threadIdx.x == 0) {
     double mx = 0.0;
-    float nm = 0.f;
+    float nm = 0.f, dm = 0.f;
     for (int i = 0; i < int(blockDim.x); ++i) {
       mx = fmax(mx, s_shift[i]);
       nm = fmaxf(nm, s_norm[i]);
+      dm = fmaxf(dm, s_drift[i]);
     }
     KMeansFlags* fl = static_cast<KMeansFlags*>(a.flags);
     fl->converged = s_conv;
@@ -243,6 +252,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
     fl->cost = a.cost_in ? a.cost_in[0] : 0.0;
     fl->max_shift2 = mx;
     if (a.cstat) a.cstat[0] = nm * 1.0000001f;
+    if (a.drift) a.drift[a.k] = dm;
   }
 }
 
@@ -251,33 +261,42 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
 // kernel's sequential feature order (lane 0), so results are bitwise unchanged.
 __global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinalizeArgs a) {
   __shared__ double s_df[4][256];
+  __shared__ float s_dv[4][256];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + w;
   if (c >= a.k) return;
   const long long cntv = static_cast<long long>(a.counts[c]);
   double* c64 = a.centers64 + size_t(c) * a.d;
+  double dr2 = 0.0;  // lane 0: squared movement of the fp32 center
   for (int f0 = 0; f0 < a.d; f0 += 256) {
     const int nf = min(256, a.d - f0);
     for (int f = lane; f < nf; f += 64) {
       double df = 0.0;
+      float dv = 0.f;
       if (cntv > 0) {
         const long long sv = static_cast<long long>(a.sums[size_t(c) * a.d + f0 + f]);
         const double nv = double(sv) * a.inv_scale[f0 + f] / double(cntv);  // == CPU formula
         df = nv - c64[f0 + f];
+        dv = static_cast<float>(nv) - static_cast<float>(c64[f0 + f]);
         c64[f0 + f] = nv;
       }
       const float v = static_cast<float>(c64[f0 + f]);
       a.centers32[size_t(c) * a.dp + f0 + f] = v;
       s_df[w][f] = df;
+      s_dv[w][f] = dv;
     }
     __builtin_amdgcn_wave_barrier();
     if (lane == 0) {
       double sh = f0 == 0 ? 0.0 : a.scratch[c];
-      for (int f = 0; f < nf; ++f) sh += s_df[w][f] * s_df[w][f];
+      for (int f = 0; f < nf; ++f) {
+        sh += s_df[w][f] * s_df[w][f];
+        dr2 += double(s_dv[w][f]) * double(s_dv[w][f]);
+      }
       a.scratch[c] = sh;
     }
     __builtin_amdgcn_wave_barrier();
   }
+  if (lane == 0 && a.drift) a.drift[c] = static_cast<float>(sqrt(dr2) * (1.0 + 1e-6));
   if (lane == 0) {
     double nrm = 0.0;
     for (int f = 0; f < a.d; ++f) {
@@ -292,7 +311,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinali
 
 __global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeArgs a) {
   __shared__ double s_shift[256];
-  __shared__ float s_norm[256];
+  __shared__ float s_norm[256], s_drift[256];
   __shared__ int s_conv, s_nonempty;
   if (threadIdx.x == 0) {
     s_conv = 1;
@@ -300,7 +319,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeA
   }
   __syncthreads();
   double my_max = 0.0;
-  float my_nmax = 0.f;
+  float my_nmax = 0.f, my_drift = 0.f;
   for (int c = threadIdx.x; c < a.k; c += blockDim.x) {
     const double sh = a.scratch[c];
     if (sh >= 0.0) {
@@ -309,17 +328,21 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeA
       my_max = fmax(my_max, sh);
     }
     my_nmax = fmaxf(my_nmax, static_cast<float>(a.scratch[a.k + c]));
+    if (a.drift) my_drift = fmaxf(my_drift, a.drift[c]);
   }
   s_shift[threadIdx.x] = my_max;
   s_norm[threadIdx.x] = my_nmax;
+  s_drift[threadIdx.x] = my_drift;
   __syncthreads();
   if (threadIdx.x == 0) {
     double mx = 0.0;
-    float nm = 0.f;
+    float nm = 0.f, dm = 0.f;
     for (int i = 0; i < int(blockDim.x); ++i) {
       mx = fmax(mx, s_shift[i]);
       nm = fmaxf(nm, s_norm[i]);
+      dm = fmaxf(dm, s_drift[i]);
     }
+    if (a.drift) a.drift[a.k] = dm;
     KMeansFlags* fl = static_cast<KMeansFlags*>(a.flags);
     fl->converged = s_conv;
     fl->nonempty = s_nonempty;
@@ -395,6 +418,19 @@ int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s) {
 
 void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
   launch_kmeans_seed_mindist(a, s);
+}
+
+__global__ void oap_kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
+                                        unsigned long long* pruned) {
+  if (threadIdx.x == 0)
+    *pruned += static_cast<unsigned long long>(ntiles - int64_t(*listed)) * passes;
+}
+
+void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
+                         unsigned long long* pruned, hipStream_t s) {
+  hipLaunchKernelGGL(oap_kmeans_count_pruned, dim3(1), dim3(64), 0, s, listed, ntiles, passes,
+                     pruned);
+  OAP_HIP_CHECK(hipGetLastError());
 }
 
 void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,

@@ -27,6 +27,16 @@
 // * Persistent grid (>= 256 workgroups of 512 threads, one per CU: 2 waves per SIMD so one wave's
 //   VALU epilogue overlaps the other's MFMAs), register prefetch two tiles ahead.
 // * f32 or bf16 row storage (bf16: half the HBM bytes, 2 MFMAs per k-step, exact operands).
+// * Pruning (Hamerly-style bounds, exact): each row keeps an upper bound u on its distance to its
+//   center and a lower bound l on its distance to every other center.  When the centers move,
+//   u grows by its center's drift and l shrinks by the largest drift (triangle inequality, fp32
+//   rounding folded into rounded-up drifts and a margin wider than two candidates' fp32
+//   evaluation error).  A tile whose rows all keep l^2 - u^2 > margin provably keeps every label
+//   — the exact-fp32 argmin cannot change — so it skips the MFMA distance work and goes straight
+//   to the exact cost and the accumulation.  Bounds are refreshed from the top-2 keys of every
+//   tile that does run.  Chunked (large-k) passes: the seed pass computes the exact distance to
+//   the old label and writes the per-row verdict; passes skip tiles whose rows all passed and
+//   merge a running lower bound over the non-best candidates for the rest.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -49,7 +59,7 @@ __host__ __device__ inline int stride_bf16(int dp) { return dp + 8; }  // (dp+8)
 __host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)/4 odd slots
 
 struct Smem {
-  size_t planes, cn, sc, acc, cnt, wcost, total;
+  size_t planes, cn, dr, sc, acc, cnt, wcost, total;
 };
 // lds_acc: LDS counters (+ the fp64 fixed-point sum accumulator when lds_sums).
 __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool precise,
@@ -60,6 +70,8 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
   off += precise ? size_t(kpad) * stride_f32(dp) * 4 : size_t(2) * kpad * stride_bf16(dp) * 2;
   off = round16(off);
   m.cn = off;
+  off = round16(off + size_t(kpad) * 4);
+  m.dr = off;  // per-center drift (pruning)
   off = round16(off + size_t(kpad) * 4);
   m.sc = off;
   off = round16(off + size_t(dp) * 4);
@@ -179,6 +191,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   __bf16* pl = ph + size_t(kpad) * sb;
   float* p32 = reinterpret_cast<float*>(smem + L.planes);
   float* cn = reinterpret_cast<float*>(smem + L.cn);
+  float* dr_l = reinterpret_cast<float*>(smem + L.dr);
   float* sc_l = reinterpret_cast<float*>(smem + L.sc);
   double* acc_l = reinterpret_cast<double*>(smem + L.acc);
   unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
@@ -206,6 +219,13 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   }
   // padded centroids get a huge FINITE norm: their keys must never be NaN bit patterns
   for (int c = tid; c < kpad; c += kThreads) cn[c] = (c < k) ? a.cnorm[c] : 1e30f;
+  // Pruning (see the header): single launches test each row's bounds against the drift of its
+  // own center; chunked passes only read the seed pass's per-row verdict.
+  const bool prune_single = !PRECISE && a.bounds && a.drift && !a.merge;
+  const bool prune_merge = !PRECISE && a.bounds && a.drift && a.merge;
+  const bool need_meta = !PRECISE && a.bounds && (a.drift || a.merge);
+  if (prune_single)
+    for (int c = tid; c < kpad; c += kThreads) dr_l[c] = (c < k) ? a.drift[a.base + c] : 0.f;
   for (int f = tid; f < DP; f += kThreads)
     sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
   if (LDSACC && accumulate) {
@@ -224,10 +244,25 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     // bias feature: |c|^2 enters as a bf16 hi/lo pair (error <= 2^-18 |c|^2 per candidate)
     thr0 = (BIAS ? 1e-5f : 2e-6f) * cmax * cmax + 1e-30f;
   }
+  const float dmax = prune_single ? a.drift_max[0] : 0.f;
+  // fp32 evaluation error of two candidates' distances, relative to |x|^2 + cmax^2 (+ rounding
+  // of the bound arithmetic): a bound gap wider than this decides the exact-fp32 argmin too
+  const float mrel = 4e-7f * float(d + 8);
+  const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);  // direct-form |x - c|^2 rounding
+  unsigned long long n_pruned = 0;
   double my_cost = 0.0;
 
+  // Bounds update carried into finish(): single launch: l = the row's new lower bound (distance);
+  // merge: l / lo = lower bounds (squared) on the chunk's candidates / on those other than the
+  // chunk's pick, lin = running bound from earlier chunks, yin = the seed's verdict (kept).
+  struct BUpd {
+    float l = 0.f, lo = 0.f, lin = INFINITY, yin = -1.f;
+    bool same = false;  // pruned row: its stored label is already right
+  };
+
   // ---- per-row epilogue: exact cost, outputs, fixed-point accumulation
-  auto finish = [&](const F& xv, const float (&cv)[KS][8], int b, int64_t row, bool valid) {
+  auto finish = [&](const F& xv, const float (&cv)[KS][8], int b, int64_t row, bool valid,
+                    const BUpd& bu) {
     float part = 0.f;  // padded features are zero in both operands
 #pragma unroll
     for (int s = 0; s < KS; ++s)
@@ -242,13 +277,22 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       if (a.merge) {
         // (cost, index) order: lowest index wins exact ties whatever the chunk order / seed
         const float md = a.mindist[row];
-        if (rowcost < md || (rowcost == md && a.base + b < a.labels[row])) {
+        const bool take = rowcost < md || (rowcost == md && a.base + b < a.labels[row]);
+        if (take) {
           a.mindist[row] = rowcost;
           a.labels[row] = a.base + b;
         }
+        if (!PRECISE && a.bounds) {
+          // the displaced best (exact md) joins the non-best candidates when this chunk wins
+          const float lo = take ? fminf(bu.lin, fminf(md, bu.lo)) : fminf(bu.lin, bu.l);
+          reinterpret_cast<float2*>(a.bounds)[row] = make_float2(lo, bu.yin);
+        }
       } else {
-        if (a.labels) a.labels[row] = a.base + b;
+        if (a.labels && !bu.same) a.labels[row] = a.base + b;
         if (a.mindist) a.mindist[row] = rowcost;
+        if (!PRECISE && a.bounds)
+          reinterpret_cast<float2*>(a.bounds)[row] =
+              make_float2(sqrtf(rowcost) * ueps + 1e-30f, bu.l);
       }
       my_cost += double(rowcost);
     }
@@ -294,9 +338,15 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     }
   };
 
-  const int64_t ntiles = (a.n + 31) / 32;
+  const int64_t ntiles_all = (a.n + 31) / 32;
+  // positions walk either every tile or the seed's list of active tiles (chunked + pruning)
+  const int64_t ntiles = a.tile_list ? int64_t(*a.tile_count) : ntiles_all;
   const int64_t stride = int64_t(gridDim.x) * kWaves;
   int64_t t = int64_t(blockIdx.x) * kWaves + wave;
+  auto tile_of = [&](int64_t q) -> int64_t {
+    if (!a.tile_list) return q;  // (past the end: load_tile clamps the rows)
+    return q < ntiles ? int64_t(a.tile_list[q]) : ntiles_all - 1;
+  };
 
   // Rows past n are clamped to row n-1 (their results are discarded, nothing needs zeroing);
   // only the last k-step can reach past the row stride, and it is zero-filled there.
@@ -333,12 +383,27 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     }
   };
 
+  // Per-row pruning state of a tile (prefetched with the rows).
+  struct Meta {
+    int lab = 0;
+    float bx = 0.f, by = -1.f;
+  };
+  auto load_meta = [&](int64_t tt, Meta& m) {
+    if (!need_meta) return;
+    int64_t row = tt * 32 + r;
+    row = row < a.n ? row : a.n - 1;
+    const float2 b = reinterpret_cast<const float2*>(a.bounds)[row];
+    m.bx = b.x;
+    m.by = b.y;
+    if (prune_single) m.lab = a.labels[row];
+  };
+
   // One tile: `x` holds its rows, `xn` receives the prefetch of tile `pf`.  DEEP: pf is two
   // tiles ahead and issued AFTER this tile's c_best loads — vmcnt retires in issue order, so
   // waiting for c_best never waits for the freshly issued prefetch, and each prefetch has about
   // two tile-times to land.  Otherwise pf is the next tile, issued before the MFMAs.  The loops
   // below rotate named buffers, so no register copies are needed.
-  auto process = [&](const int64_t t, F& x, F& xn, const int64_t pf) {
+  auto process = [&](const int64_t t, F& x, F& xn, const Meta& m, Meta& mn, const int64_t pf) {
     const int64_t row = t * 32 + r;
     const bool valid = row < a.n;
     int bidx;
@@ -358,7 +423,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
           for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
       }
-      finish(x, cb, bidx, row, valid);
+      finish(x, cb, bidx, row, valid, BUpd{});
     } else {
       // merge mode: the row's best exact cost so far (earlier chunks / previous label), fetched
       // now so it has landed by the refinement decision
@@ -373,6 +438,34 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += __shfl_xor(nx2, 32, 64);
+      const float marg = mrel * (nx2 + cmax * cmax);
+      // Pruning: a tile whose rows all keep their center provably (bounds) skips the distance
+      // work; its rows still get the exact cost, outputs and accumulation from their label.
+      if (prune_single || prune_merge) {
+        float lk = 0.f;
+        bool ok;
+        if (prune_merge) {
+          ok = m.by >= 0.f;  // the seed pass's verdict for this iteration
+        } else {
+          const float u = m.bx + dr_l[min(max(m.lab, 0), k - 1)];
+          lk = m.by - dmax;
+          ok = lk > 0.f && (lk - u) * (lk + u) > marg;
+        }
+        if (__all(!valid || ok)) {
+          load_tile(pf, xn);
+          load_meta(pf, mn);
+          ++n_pruned;
+          if (prune_merge) return;  // labels / mindist already hold the seed's exact answer
+          const int b = min(max(m.lab, 0), k - 1);
+          float cb[KS][8];
+          load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cb);
+          BUpd bu;
+          bu.l = lk;
+          bu.same = true;
+          finish(x, cb, b, row, valid, bu);
+          return;
+        }
+      }
       const int jb = d - 16 * (KS - 1) - 8 * h;  // lane-local slot of bias feature d (if in range)
       if constexpr (XB) {
 #pragma unroll
@@ -417,7 +510,10 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
             }
         }
       };
-      if constexpr (!DEEP) load_tile(pf, xn);  // prefetch, hidden behind this tile's MFMAs
+      if constexpr (!DEEP) {  // prefetch, hidden behind this tile's MFMAs
+        load_tile(pf, xn);
+        load_meta(pf, mn);
+      }
 
       // Accumulators are seeded with |c|^2 + |x|^2 and the planes hold -2c, so each MFMA chain
       // ends at |x - c|^2.  Top-2 tracking runs on integer KEYS: the float's bits with the low 10
@@ -540,6 +636,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       // tier-3 bound: split + accumulation error, seed rounding
       const float thr3 = fmaf(thr1, sqrtf(nx2), thr0) + 2e-6f * nx2;
       bool unsure;
+      float thr_used = thr3;  // bound of the tier that produced k1 / k2
       if (a.fast1) {
         run_tier(std::integral_constant<int, 1>{});
         // tier-1 bound, two candidates: cross term 2 x 2(2^-8 + 2^-18)|c||x|, |c|^2 bias
@@ -549,7 +646,9 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         const float thrA = 0.0157f * cm * sqrtf(nx2) + 0.004f * cm * cm + 0.002f * nx2 +
                            4e-5f * (cm * cm + nx2) + 1e-30f;
         unsure = unsure_at(thrA);
+        thr_used = thrA;
         if (__any(unsure)) {
+          thr_used = thr3;
           build_lo();
           run_tier(std::integral_constant<int, 3>{});
           unsure = unsure_at(thr3);
@@ -576,31 +675,56 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
           for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
       }
-      if constexpr (DEEP) load_tile(pf, xn);  // younger than the c_best loads (see above)
-      finish(x, cb, bidx, row, valid);
+      if constexpr (DEEP) {  // younger than the c_best loads (see above)
+        load_tile(pf, xn);
+        load_meta(pf, mn);
+      }
+      BUpd bu;
+      if (a.bounds) {
+        // every candidate's true distance is >= its key - tt; the pick's rivals are the other
+        // keys (the second key, or the first when the exact pass picked another center)
+        const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
+        const float tt = thr_used + 2.5e-4f * fabsf(b2) + marg;
+        const float lo = ((bidx == (k1 & 0x3ff)) ? b2 : b1) - tt;
+        if (a.merge) {
+          bu.l = b1 - tt;
+          bu.lo = lo;
+          bu.lin = (a.base == 0) ? INFINITY : m.bx;  // the first chunk starts the bound afresh
+          bu.yin = m.by;
+        } else {
+          bu.l = sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f);  // NaN (no second key) -> 0
+        }
+      }
+      finish(x, cb, bidx, row, valid, bu);
     }
   };
 
   if constexpr (DEEP) {
     F xa, xb, xc;
-    load_tile(t, xa);
-    load_tile(t + stride, xb);
+    Meta ma, mb, mc;
+    load_tile(tile_of(t), xa);
+    load_meta(tile_of(t), ma);
+    load_tile(tile_of(t + stride), xb);
+    load_meta(tile_of(t + stride), mb);
     for (; t < ntiles; t += 3 * stride) {  // t is wave-uniform: every branch stays uniform
-      process(t, xa, xc, t + 2 * stride);
+      process(tile_of(t), xa, xc, ma, mc, tile_of(t + 2 * stride));
       if (t + stride >= ntiles) break;
-      process(t + stride, xb, xa, t + 3 * stride);
+      process(tile_of(t + stride), xb, xa, mb, ma, tile_of(t + 3 * stride));
       if (t + 2 * stride >= ntiles) break;
-      process(t + 2 * stride, xc, xb, t + 4 * stride);
+      process(tile_of(t + 2 * stride), xc, xb, mc, mb, tile_of(t + 4 * stride));
     }
   } else {
     F xa, xb;
-    load_tile(t, xa);
+    Meta ma, mb;
+    load_tile(tile_of(t), xa);
+    load_meta(tile_of(t), ma);
     for (; t < ntiles; t += 2 * stride) {
-      process(t, xa, xb, t + stride);
+      process(tile_of(t), xa, xb, ma, mb, tile_of(t + stride));
       if (t + stride >= ntiles) break;
-      process(t + stride, xb, xa, t + 2 * stride);
+      process(tile_of(t + stride), xb, xa, mb, ma, tile_of(t + 2 * stride));
     }
   }
+  if (lane == 0 && n_pruned && a.pruned_tiles) atomicAdd(a.pruned_tiles, n_pruned);
 
   // ---- deterministic per-block cost: fixed shuffle tree, waves in index order
   const double wsum = wave_sum_f64(my_cost);
@@ -627,12 +751,23 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 // mindist[row] = |x_row - c_{labels[row]}|^2 with exactly the assign kernel's lane layout and
 // fp32 summation order (so a later chunk that picks the same center computes the bitwise same
 // value).  Seeds the chunked large-k passes with the previous iteration's labels.
+//
+// With bounds + drift it also decides pruning for the iteration's chunk passes: the row's lower
+// bound on the non-label centers (the merged chunk bound of the last iteration, or the seed's own
+// decayed bound for rows whose tile was skipped) minus the largest drift, against the exact
+// distance just computed.  Writes bounds[row] = {unset (>= 3e38), l if the row provably keeps its
+// label else -1}.
 template <int KS, bool XB>
 __global__ __launch_bounds__(256) void oap_kmeans_seed_mindist(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const int64_t ntiles = (a.n + 31) / 32;
+  const bool prune = a.bounds && a.drift;
+  const float dmax = prune ? a.drift_max[0] : 0.f;
+  const float cmax = a.cstat ? a.cstat[0] : 0.f;
+  const float mrel = 4e-7f * float(a.d + 8);
+  const float ueps2 = 1.f + 2e-6f + 1.2e-7f * float(a.d + 4);
   for (int64_t t = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64; t < ntiles;
        t += int64_t(gridDim.x) * blockDim.x / 64) {
     const int64_t row = t * 32 + r;
@@ -641,7 +776,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_seed_mindist(KMeansAssignArgs 
     int b = a.labels[rr];
     if (b < 0 || b >= a.k) b = 0;
     const float* cp = a.centers + size_t(b) * DP + 8 * h;
-    float part = 0.f;
+    float part = 0.f, px = 0.f;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       float xv[8];
@@ -671,13 +806,28 @@ __global__ __launch_bounds__(256) void oap_kmeans_seed_mindist(KMeansAssignArgs 
       for (int j = 0; j < 8; ++j) {
         const float e = xv[j] - cv[j];
         part = fmaf(e, e, part);
+        px = fmaf(xv[j], xv[j], px);
       }
     }
     const float rowcost = part + __shfl_xor(part, 32, 64);
+    const float nx2 = px + __shfl_xor(px, 32, 64);
+    float2 bnew = make_float2(3.4e38f, -1.f);
+    if (a.bounds) {
+      const float2 bo = reinterpret_cast<const float2*>(a.bounds)[rr];
+      if (prune) {
+        const float lp =
+            bo.x >= 3e38f ? bo.y : fmaxf(sqrtf(fmaxf(bo.x, 0.f)) * (1.f - 1e-6f), bo.y);
+        const float l = lp - dmax;
+        if (l > 0.f && l * l - rowcost * ueps2 > mrel * (nx2 + cmax * cmax)) bnew.y = l;
+      }
+    }
     if (valid && h == 0) {
       a.mindist[row] = rowcost;
       a.labels[row] = b;
+      if (a.bounds) reinterpret_cast<float2*>(a.bounds)[row] = bnew;
     }
+    if (a.tile_list && __any(valid && bnew.y < 0.f) && lane == 0)
+      a.tile_list[atomicAdd(a.tile_count, 1u)] = static_cast<int32_t>(t);
   }
 }
 

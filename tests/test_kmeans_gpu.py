@@ -246,3 +246,28 @@ def test_batched_iterations_match_stepwise(native):
     assert np.array_equal(a["centers"], b["centers"])
     assert a["cost_history"] == b["cost_history"]
     assert a["last_counts"] == b["last_counts"]
+
+
+@pytest.mark.parametrize("d,k,dtype,n", [(50, 200, "f32", 200000), (20, 16, "f32", 100000),
+                                         (50, 1500, "f32", 60000), (100, 1000, "bf16", 60000),
+                                         (100, 60, "bf16", 100000), (128, 40, "f32", 50000)])
+def test_pruning_is_exact(native, d, k, dtype, n):
+    """Bound-based pruning skips distance work but never changes a label: centers, cost history
+    and counts are bitwise those of the unpruned fit (single-launch and chunked large-k paths)."""
+    rng = np.random.default_rng(d * 7 + k)
+    C = rng.uniform(-10, 10, size=(k, d))
+    X = C[rng.integers(0, k, n)] + rng.normal(0, 1.0, size=(n, d))
+    X = bf16_round(X) if dtype == "bf16" else X.astype(np.float32).astype(np.float64)
+    # start near the truth with a few centers misplaced: centers still move (and the largest
+    # move shrinks as they settle), so pruning ramps up over the iterations
+    init = C + rng.normal(0, 0.3, size=C.shape)
+    init[:2] = X[rng.choice(n, 2, replace=False)]
+    init = bf16_round(init) if dtype == "bf16" else init.astype(np.float32).astype(np.float64)
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X, dtype, native.kmeans_ld(d, dtype))
+    rp = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
+    ru = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=False)
+    assert ru["pruned_tiles"] == 0 and rp["pruned_tiles"] > 0
+    assert rp["last_counts"] == ru["last_counts"]
+    assert np.array_equal(rp["centers"], ru["centers"])
+    assert rp["cost_history"] == ru["cost_history"]
