@@ -228,6 +228,10 @@ struct AssignReq {
   // chunked path with pruning: [ceil(rows/32)] active-tile list + its counter
   int32_t* tile_list = nullptr;
   unsigned* tile_count = nullptr;
+  // chunked path: defer in-chunk near ties to a re-run after the last chunk (pays off when the
+  // centers are distinct cluster centers — Lloyd / predict; k-means|| candidate sets hold
+  // several near-identical points per cluster, whose ties are genuine, so init passes opt out)
+  bool defer = true;
 };
 
 // Returns the number of cost partials written to req.cost_slab.
@@ -310,16 +314,50 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   // balanced chunks: ceil(k / kmax) launches of equal 32-multiples (no thin last pass)
   const int nchunks = (g.k + kmax - 1) / kmax;
   const int csize = static_cast<int>(round_up((g.k + nchunks - 1) / nchunks, 32));
-  for (int c = 0; c < g.k; c += csize) {
+  // Near ties inside a chunk that could still win are deferred (KMeansAssignArgs::defer_list):
+  // after the last chunk each chunk re-runs on its deferred tiles against the row's final best,
+  // which rules most of them out without the 3-product / exact re-decision (an unseeded first
+  // chunk would otherwise escalate nearly every tile).
+  int dgrid = 0;
+  int64_t dcap = 0;
+  kern::kmeans_defer_layout(x.rows, ctx.info().cu_count, &dgrid, &dcap);
+  const size_t per_chunk = size_t(dgrid) * size_t(dcap);  // list entries of one chunk
+  const size_t cnt_stride = round_up(size_t(dgrid), 16);
+  Buffer defer = ctx.alloc(sizeof(int32_t) * per_chunk * nchunks +
+                           sizeof(unsigned) * cnt_stride * nchunks);
+  auto dlist = [&](int ci) { return defer.as<int32_t>() + per_chunk * ci; };
+  auto dcount = [&](int ci) {
+    return reinterpret_cast<unsigned*>(defer.as<int32_t>() + per_chunk * nchunks) +
+           cnt_stride * ci;
+  };
+  OAP_HIP_CHECK(hipMemsetAsync(dcount(0), 0, sizeof(unsigned) * cnt_stride * nchunks, s));
+  auto run_chunk = [&](int ci, bool main_pass) {
+    const int c = ci * csize;
     const int kc = std::min(csize, g.k - c);
-    a.centers = g.c32.as<float>() + size_t(c) * g.dp;
-    a.cnorm = g.cnorm.as<float>() + c;
-    a.k = kc;
-    a.kpad = static_cast<int>(round_up(kc, 32));
-    a.base = c;
-    a.merge = true;
-    kern::kmeans_assign(a, ctx.info().cu_count, s);
-  }
+    kern::KMeansAssignArgs b = a;
+    b.centers = g.c32.as<float>() + size_t(c) * g.dp;
+    b.cnorm = g.cnorm.as<float>() + c;
+    b.k = kc;
+    b.kpad = static_cast<int>(round_up(kc, 32));
+    b.base = c;
+    b.merge = true;
+    b.fresh_bound = main_pass && ci == 0;
+    if (main_pass) {
+      if (req.defer) {
+        b.defer_list = dlist(ci);
+        b.defer_count = dcount(ci);
+      }
+    } else {
+      b.tile_list = dlist(ci);
+      b.tile_count = dcount(ci);
+      b.seg_list = true;
+      b.pruned_tiles = nullptr;
+    }
+    kern::kmeans_assign(b, ctx.info().cu_count, s);
+  };
+  for (int ci = 0; ci * csize < g.k; ++ci) run_chunk(ci, true);
+  if (req.defer)
+    for (int ci = 0; ci * csize < g.k; ++ci) run_chunk(ci, false);
   if (req.accumulate)
     kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
                             static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
@@ -361,6 +399,7 @@ class InitOps {
         // chunked: merge straight into the running costs (chunks that cannot lower a row's cost
         // skip their exact re-decisions)
         req.mindist = costs_.as<float>();
+        req.defer = false;
         req.mindist_seeded = true;
         gpu_assign(ctx_, x_, g, req, ctx_.compute());
       } else {
@@ -451,6 +490,7 @@ class InitOps {
       AssignReq req;
       req.accumulate = true;
       req.sums_too = false;
+      req.defer = false;
       req.counts = dc.as<u64>();
       gpu_assign(ctx_, x_, g, req, ctx_.compute());
       ctx_.copy_to_host(cnt.data(), dc.data(), sizeof(u64) * m);

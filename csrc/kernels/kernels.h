@@ -88,6 +88,15 @@ struct KMeansAssignArgs {
   // then visit only those tiles, so pruned tiles cost no row reads at all
   int32_t* tile_list = nullptr;
   unsigned* tile_count = nullptr;
+  // merge passes: a tile holding a row whose pick inside this chunk is a near tie that could
+  // still win is not escalated here but appended to defer_list; the driver re-runs the chunk on
+  // those tiles after the last chunk, when the row's best-so-far usually rules the chunk out.
+  // Segmented per workgroup: [grid][kmeans_defer_segment(n)] tiles, defer_count [grid] (zeroed);
+  // the re-run passes the same arrays as tile_list / tile_count with seg_list set.
+  int32_t* defer_list = nullptr;
+  unsigned* defer_count = nullptr;
+  bool seg_list = false;
+  bool fresh_bound = true;  // merge + bounds: this pass starts the row's running bound afresh
 };
 // Upper bound on rows one assign workgroup processes for n local rows (device independent); the
 // fixed-point scale keeps per-workgroup LDS partial sums below 2^53 with it.
@@ -103,6 +112,8 @@ void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s);
 void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
                          unsigned long long* pruned, hipStream_t s);
 int kmeans_cost_slab_size(int num_cus);
+// Deferral list layout of one merge pass over n rows: workgroups x per-workgroup capacity.
+void kmeans_defer_layout(int64_t n, int num_cus, int* grid, int64_t* seg_cap);
 // sums/counts += rows grouped by labels (fixed point; used after chunked assignment).  Cluster
 // ranges are owned by workgroup groups that each keep their slice of the sums in LDS, so every
 // row element costs one LDS atomic instead of a global one (sums == nullptr: counts only).

@@ -88,6 +88,13 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
   return m;
 }
 
+// Capacity of one workgroup's deferral segment: the most tiles a workgroup of the persistent
+// grid visits.
+__host__ __device__ inline int64_t defer_segment(int64_t ntiles, int64_t grid) {
+  const int64_t stride = grid * kWaves;
+  return (ntiles + stride - 1) / stride * kWaves;
+}
+
 __device__ inline int med3_i32(int a, int b, int c) {
   int r;
   asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -253,10 +260,12 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   double my_cost = 0.0;
 
   // Bounds update carried into finish(): single launch: l = the row's new lower bound (distance);
-  // merge: l / lo = lower bounds (squared) on the chunk's candidates / on those other than the
-  // chunk's pick, lin = running bound from earlier chunks, yin = the seed's verdict (kept).
+  // merge: l / lo = lower bounds (squared) on every candidate of the chunk / on all but the
+  // first key's (launch-local index i1), lin = running bound from earlier passes, yin = the seed's
+  // verdict (kept).
   struct BUpd {
     float l = 0.f, lo = 0.f, lin = INFINITY, yin = -1.f;
+    int i1 = -1;
     bool same = false;  // pruned row: its stored label is already right
   };
 
@@ -277,14 +286,19 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       if (a.merge) {
         // (cost, index) order: lowest index wins exact ties whatever the chunk order / seed
         const float md = a.mindist[row];
-        const bool take = rowcost < md || (rowcost == md && a.base + b < a.labels[row]);
+        const int lab = a.labels[row];
+        const bool take = rowcost < md || (rowcost == md && a.base + b < lab);
         if (take) {
           a.mindist[row] = rowcost;
           a.labels[row] = a.base + b;
         }
         if (!PRECISE && a.bounds) {
-          // the displaced best (exact md) joins the non-best candidates when this chunk wins
-          const float lo = take ? fminf(bu.lin, fminf(md, bu.lo)) : fminf(bu.lin, bu.l);
+          // running bound over every candidate except the row's best: when this chunk wins, the
+          // displaced best (exact md) joins and the pick leaves; otherwise the best may itself
+          // sit in this chunk (seeded label, a deferred re-run) and must be left out
+          const int best = take ? b : lab - a.base;
+          const float ch = (best == bu.i1) ? bu.lo : bu.l;
+          const float lo = take ? fminf(bu.lin, fminf(md, ch)) : fminf(bu.lin, ch);
           reinterpret_cast<float2*>(a.bounds)[row] = make_float2(lo, bu.yin);
         }
       } else {
@@ -339,13 +353,25 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   };
 
   const int64_t ntiles_all = (a.n + 31) / 32;
-  // positions walk either every tile or the seed's list of active tiles (chunked + pruning)
-  const int64_t ntiles = a.tile_list ? int64_t(*a.tile_count) : ntiles_all;
-  const int64_t stride = int64_t(gridDim.x) * kWaves;
-  int64_t t = int64_t(blockIdx.x) * kWaves + wave;
+  // Positions walk every tile, the seed's list of active tiles (one list, grid-strided), or —
+  // seg_list — this workgroup's own segment of a deferral list (see defer_list below).
+  const int64_t seg_cap = defer_segment(ntiles_all, gridDim.x);
+  const int32_t* list = a.tile_list ? a.tile_list + (a.seg_list ? blockIdx.x * seg_cap : 0) : nullptr;
+  const int64_t ntiles = !a.tile_list  ? ntiles_all
+                         : a.seg_list ? int64_t(a.tile_count[blockIdx.x])
+                                      : int64_t(*a.tile_count);
+  const int64_t stride = a.seg_list ? int64_t(kWaves) : int64_t(gridDim.x) * kWaves;
+  int64_t t = a.seg_list ? int64_t(wave) : int64_t(blockIdx.x) * kWaves + wave;
   auto tile_of = [&](int64_t q) -> int64_t {
-    if (!a.tile_list) return q;  // (past the end: load_tile clamps the rows)
-    return q < ntiles ? int64_t(a.tile_list[q]) : ntiles_all - 1;
+    if (!list) return q;  // (past the end: load_tile clamps the rows)
+    return q < ntiles ? int64_t(list[q]) : ntiles_all - 1;
+  };
+  // deferral: one list segment + counter per workgroup (no single hot counter)
+  auto defer_tile = [&](int64_t tile) {
+    if (lane == 0) {
+      const unsigned i = atomicAdd(a.defer_count + blockIdx.x, 1u);
+      a.defer_list[blockIdx.x * seg_cap + i] = static_cast<int32_t>(tile);
+    }
   };
 
   // Rows past n are clamped to row n-1 (their results are discarded, nothing needs zeroing);
@@ -647,6 +673,10 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
                            4e-5f * (cm * cm + nx2) + 1e-30f;
         unsure = unsure_at(thrA);
         thr_used = thrA;
+        if (a.defer_list && __any(unsure)) {
+          defer_tile(t);
+          unsure = false;  // decided after the last chunk (see KMeansAssignArgs::defer_list)
+        }
         if (__any(unsure)) {
           thr_used = thr3;
           build_lo();
@@ -658,6 +688,10 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         build_lo();
         run_tier(std::integral_constant<int, 3>{});
         unsure = unsure_at(thr3);
+        if (a.defer_list && __any(unsure)) {
+          defer_tile(t);
+          unsure = false;
+        }
       }
       bidx = k1 & 0x3ff;
       if (__any(unsure)) {
@@ -688,8 +722,9 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         const float lo = ((bidx == (k1 & 0x3ff)) ? b2 : b1) - tt;
         if (a.merge) {
           bu.l = b1 - tt;
-          bu.lo = lo;
-          bu.lin = (a.base == 0) ? INFINITY : m.bx;  // the first chunk starts the bound afresh
+          bu.lo = b2 - tt;  // NaN (no second key) is ignored by fminf
+          bu.i1 = k1 & 0x3ff;
+          bu.lin = a.fresh_bound ? INFINITY : m.bx;  // the first chunk starts the bound afresh
           bu.yin = m.by;
         } else {
           bu.l = sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f);  // NaN (no second key) -> 0
@@ -937,6 +972,11 @@ int kmeans_mfma_grid(int64_t n, int num_cus) {
   const int64_t want = (tiles + kWaves - 1) / kWaves;
   const int64_t cap = num_cus > 256 ? num_cus : 256;
   return static_cast<int>(want < cap ? (want < 1 ? 1 : want) : cap);
+}
+
+void kmeans_defer_layout(int64_t n, int num_cus, int* grid, int64_t* seg_cap) {
+  *grid = kmeans_mfma_grid(n, num_cus);
+  *seg_cap = defer_segment((n + 31) / 32, *grid);
 }
 
 void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s) {
