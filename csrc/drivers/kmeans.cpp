@@ -343,7 +343,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.merge = true;
     b.fresh_bound = main_pass && ci == 0;
     if (main_pass) {
-      if (req.defer) {
+      if (req.defer && c + csize < g.k) {  // the last chunk already sees the final best
         b.defer_list = dlist(ci);
         b.defer_count = dcount(ci);
       }
@@ -357,11 +357,17 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   };
   for (int ci = 0; ci * csize < g.k; ++ci) run_chunk(ci, true);
   if (req.defer)
-    for (int ci = 0; ci * csize < g.k; ++ci) run_chunk(ci, false);
-  if (req.accumulate)
-    kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
-                            static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
-                            req.sums_too ? req.sums : nullptr, req.counts, s);
+    for (int ci = 0; (ci + 1) * csize < g.k; ++ci) run_chunk(ci, false);
+  if (req.accumulate) {
+    Buffer bins = ctx.alloc(kern::kmeans_bin_scratch_bytes(x.rows, g.k));
+    if (!kern::kmeans_accumulate_binned(x.data.data(), x.dtype == DType::BF16, x.rows,
+                                        static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
+                                        req.sums_too ? req.sums : nullptr, req.counts,
+                                        bins.data(), s))
+      kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
+                              static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
+                              req.sums_too ? req.sums : nullptr, req.counts, s);
+  }
   if (req.cost_slab) return kern::reduce_sum_f32(mind, x.rows, req.cost_slab, s);
   return 0;
 }

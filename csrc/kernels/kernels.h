@@ -121,6 +121,15 @@ void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
                        const int32_t* labels, int k, const float* scale,
                        unsigned long long* sums, unsigned long long* counts, hipStream_t s);
 
+// Same result via rows binned by cluster range first (every accumulation lane works on a row
+// of its range).  scratch: kmeans_bin_scratch_bytes(n, k).  Returns false (nothing launched)
+// when the layout does not apply; the caller then uses kmeans_accumulate.
+size_t kmeans_bin_scratch_bytes(int64_t n, int k);
+bool kmeans_accumulate_binned(const void* x, bool xbf16, int64_t n, int ld, int d,
+                              const int32_t* labels, int k, const float* scale,
+                              unsigned long long* sums, unsigned long long* counts, void* scratch,
+                              hipStream_t s);
+
 struct KMeansFinalizeArgs {
   const unsigned long long* sums = nullptr;  // global (allreduced) fixed-point sums [k][d]
   const unsigned long long* counts = nullptr;

@@ -192,6 +192,176 @@ __global__ __launch_bounds__(kAccThreads) void oap_kmeans_accumulate_owned(
     if (cnt[i]) atomicAdd(&counts[c0 + i], static_cast<u64>(cnt[i]));
 }
 
+// ---- binned accumulation: rows grouped by cluster range first (two cheap passes over the
+// labels), so every lane of the accumulation kernel works on a row of its range — the scan
+// variant above reads every label in every range and keeps a dependent load chain per 64 rows.
+constexpr int kBinThreads = 256;
+constexpr int kBinRows = 4096;  // rows per bin block chunk
+__global__ __launch_bounds__(kBinThreads) void oap_kmeans_bin_count(const int32_t* labels,
+                                                                     int64_t n, int kg, int G,
+                                                                     unsigned* gcount) {
+  extern __shared__ unsigned hist[];
+  for (int i = threadIdx.x; i < G; i += kBinThreads) hist[i] = 0u;
+  __syncthreads();
+  for (int64_t r = int64_t(blockIdx.x) * kBinThreads + threadIdx.x; r < n;
+       r += int64_t(gridDim.x) * kBinThreads) {
+    const int g = labels[r] / kg;
+    atomicAdd(&hist[min(max(g, 0), G - 1)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G; i += kBinThreads)
+    if (hist[i]) atomicAdd(&gcount[i], hist[i]);
+}
+
+// gcount [G] -> goff [G+1] exclusive offsets; gfill [G] = goff (scatter cursors)
+__global__ void oap_kmeans_bin_offsets(const unsigned* gcount, int G, unsigned* goff,
+                                       unsigned* gfill) {
+  if (threadIdx.x != 0) return;
+  unsigned acc = 0;
+  for (int g = 0; g < G; ++g) {
+    goff[g] = acc;
+    gfill[g] = acc;
+    acc += gcount[g];
+  }
+  goff[G] = acc;
+}
+
+// One chunk of kBinRows rows per block iteration: LDS ranks per range, one global reservation
+// per (chunk, range), then the (row, label) entries land in their range's region.
+__global__ __launch_bounds__(kBinThreads) void oap_kmeans_bin_scatter(const int32_t* labels,
+                                                                       int64_t n, int kg, int G,
+                                                                       unsigned* gfill,
+                                                                       int2* bins) {
+  extern __shared__ unsigned sm[];
+  unsigned* cnt = sm;       // [G]
+  unsigned* base = sm + G;  // [G]
+  constexpr int kPer = kBinRows / kBinThreads;
+  for (int64_t c0 = int64_t(blockIdx.x) * kBinRows; c0 < n; c0 += int64_t(gridDim.x) * kBinRows) {
+    for (int i = threadIdx.x; i < G; i += kBinThreads) cnt[i] = 0u;
+    __syncthreads();
+    int lab[kPer];
+    unsigned pos[kPer];
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t r = c0 + j * kBinThreads + threadIdx.x;
+      lab[j] = r < n ? labels[r] : -1;
+      pos[j] = 0u;
+      if (r < n) pos[j] = atomicAdd(&cnt[min(max(lab[j] / kg, 0), G - 1)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G; i += kBinThreads)
+      base[i] = cnt[i] ? atomicAdd(&gfill[i], cnt[i]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      const int64_t r = c0 + j * kBinThreads + threadIdx.x;
+      if (r < n) {
+        const int g = min(max(lab[j] / kg, 0), G - 1);
+        bins[base[g] + pos[j]] = make_int2(static_cast<int>(r), lab[j]);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Accumulation over the binned entries of range g = blockIdx % G: block slice b of the range's
+// entries (256 slices: the fixed-point per-block bound holds as in the scan variant).  Entries
+// are fetched two batches ahead and rows one batch ahead of the LDS atomics, so the dependent
+// entry -> row load chain overlaps the previous batch's atomics.
+template <typename T>
+__global__ __launch_bounds__(kAccThreads) void oap_kmeans_accumulate_binned(
+    const T* x, int ld, int d, const int2* bins, const unsigned* goff, int k, int kg, int G,
+    int rs, const float* scale, u64* sums, u64* counts) {
+  constexpr int EPS = 16 / sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int g = blockIdx.x % G, b = blockIdx.x / G, B = gridDim.x / G;
+  const int c0 = g * kg, nk = min(k, c0 + kg) - c0;
+  double* acc = reinterpret_cast<double*>(smem);
+  const size_t acc_bytes = (size_t(kg) * rs * 8 + 15) / 16 * 16;
+  unsigned* cnt = reinterpret_cast<unsigned*>(smem + acc_bytes);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < nk * rs; i += kAccThreads) acc[i] = 0.0;
+  for (int i = tid; i < nk; i += kAccThreads) cnt[i] = 0u;
+  __syncthreads();
+  const int SEG = ld * int(sizeof(T)) / 16, rpi = 64 / SEG;
+  const int slot = lane / SEG, seg = lane - slot * SEG;
+  const bool lane_ok = slot < rpi;
+  float sc[EPS];
+#pragma unroll
+  for (int j = 0; j < EPS; ++j) {
+    const int f = seg * EPS + j;
+    sc[j] = (sums && lane_ok && f < d) ? scale[f] : 0.f;
+  }
+  const int64_t tot = int64_t(goff[g + 1]) - goff[g];
+  const int64_t e0 = goff[g] + tot * b / B, e1 = goff[g] + tot * (b + 1) / B;
+  const int per = rpi * kAccU;                       // entries per wave batch
+  const int64_t step = int64_t(kAccThreads / 64) * per;  // entries per block batch
+  struct Batch {
+    int2 en[kAccU];
+    T v[kAccU][EPS];
+  };
+  auto load_entries = [&](int64_t q0, Batch& bt) {
+#pragma unroll
+    for (int u = 0; u < kAccU; ++u) {
+      const int64_t qi = q0 + u * rpi + slot;
+      bt.en[u] = (lane_ok && qi < e1) ? bins[qi] : make_int2(-1, -1);
+    }
+  };
+  auto load_rows = [&](Batch& bt) {
+#pragma unroll
+    for (int u = 0; u < kAccU; ++u)
+      if (bt.en[u].x >= 0) {
+        const T* p = x + int64_t(bt.en[u].x) * ld + seg * EPS;
+        const uint4 raw = *reinterpret_cast<const uint4*>(p);
+        __builtin_memcpy(&bt.v[u][0], &raw, 16);
+      }
+  };
+  auto consume = [&](const Batch& bt) {
+#pragma unroll
+    for (int u = 0; u < kAccU; ++u) {
+      if (bt.en[u].x < 0) continue;
+      const int cl = bt.en[u].y - c0;
+      if (seg == 0) atomicAdd(&cnt[cl], 1u);
+      if (!sums) continue;
+      double* ap = acc + cl * rs + seg * (EPS + 1);
+#pragma unroll
+      for (int j = 0; j < EPS; ++j)
+        if (seg * EPS + j < d)
+          atomicAdd(ap + j, static_cast<double>(rintf(static_cast<float>(bt.v[u][j]) * sc[j])));
+    }
+  };
+  // three rotating batches: at the top of each step X0 holds batch q (rows in flight) and X1
+  // the entries of batch q + step
+  int64_t q = e0 + int64_t(wave) * per;
+  Batch X0, X1, X2;
+  load_entries(q, X0);
+  load_rows(X0);
+  load_entries(q + step, X1);
+  for (; q < e1; q += 3 * step) {
+    load_rows(X1);
+    load_entries(q + 2 * step, X2);
+    consume(X0);
+    if (q + step >= e1) break;
+    load_rows(X2);
+    load_entries(q + 3 * step, X0);
+    consume(X1);
+    if (q + 2 * step >= e1) break;
+    load_rows(X0);
+    load_entries(q + 4 * step, X1);
+    consume(X2);
+  }
+  __syncthreads();
+  if (sums)
+    for (int i = tid; i < nk * d; i += kAccThreads) {
+      const int c = i / d, f = i - c * d;
+      const double v = acc[c * rs + (f / EPS) * (EPS + 1) + f % EPS];  // exact, |v| < 2^53
+      if (v != 0.0)
+        atomicAdd(&sums[size_t(c0 + c) * d + f], static_cast<u64>(static_cast<long long>(v)));
+    }
+  for (int i = tid; i < nk; i += kAccThreads)
+    if (cnt[i]) atomicAdd(&counts[c0 + i], static_cast<u64>(cnt[i]));
+}
+
 __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a) {
   __shared__ int s_conv, s_nonempty;
   __shared__ double s_shift[256];
@@ -490,6 +660,70 @@ void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
                        counts);
   }
   OAP_HIP_CHECK(hipGetLastError());
+}
+
+size_t kmeans_bin_scratch_bytes(int64_t n, int k) {
+  return sizeof(int2) * size_t(std::max<int64_t>(n, 1)) + sizeof(unsigned) * (3 * size_t(k) + 8);
+}
+
+bool kmeans_accumulate_binned(const void* x, bool xbf16, int64_t n, int ld, int d,
+                              const int32_t* labels, int k, const float* scale,
+                              unsigned long long* sums, unsigned long long* counts, void* scratch,
+                              hipStream_t s) {
+  if (n == 0) return true;
+  const int es = xbf16 ? 2 : 4, eps = 16 / es;
+  const int seg = ld * es / 16;
+  if (ld * es % 16 != 0 || seg > 64 || n >= (int64_t(1) << 31)) return false;
+  int rs = 0, kg = k;
+  if (sums) {
+    rs = (seg * (eps + 1)) | 1;
+    kg = static_cast<int>((kLdsLimit - 64) / (size_t(rs) * 8 + 4));
+  } else {
+    kg = static_cast<int>(std::min<size_t>(size_t(k), (kLdsLimit - 64) / 4));
+  }
+  if (kg < 1) return false;
+  const int G = (k + kg - 1) / kg;
+  kg = (k + G - 1) / G;
+  const size_t lds = (size_t(kg) * rs * 8 + 15) / 16 * 16 + (size_t(kg) * 4 + 15) / 16 * 16;
+  if (lds > kLdsLimit) return false;
+  int2* bins = static_cast<int2*>(scratch);
+  unsigned* gcount = reinterpret_cast<unsigned*>(bins + n);
+  unsigned* goff = gcount + G;  // [G + 1]
+  unsigned* gfill = goff + G + 1;
+  OAP_HIP_CHECK(hipMemsetAsync(gcount, 0, sizeof(unsigned) * G, s));
+  const int bgrid = static_cast<int>(std::min<int64_t>((n + kBinRows - 1) / kBinRows, 4096));
+  hipLaunchKernelGGL(oap_kmeans_bin_count, dim3(bgrid), dim3(kBinThreads), sizeof(unsigned) * G,
+                     s, labels, n, kg, G, gcount);
+  hipLaunchKernelGGL(oap_kmeans_bin_offsets, dim3(1), dim3(64), 0, s, gcount, G, goff, gfill);
+  hipLaunchKernelGGL(oap_kmeans_bin_scatter, dim3(bgrid), dim3(kBinThreads),
+                     sizeof(unsigned) * 2 * G, s, labels, n, kg, G, gfill, bins);
+  OAP_HIP_CHECK(hipGetLastError());
+  const dim3 grid(256 * G);  // 256 slices per cluster range (fixed-point bound)
+  if (xbf16) {
+    static bool set = false;
+    if (!set) {
+      OAP_HIP_CHECK(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&oap_kmeans_accumulate_binned<__bf16>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
+      set = true;
+    }
+    hipLaunchKernelGGL(oap_kmeans_accumulate_binned<__bf16>, grid, dim3(kAccThreads), lds, s,
+                       static_cast<const __bf16*>(x), ld, d, bins, goff, k, kg, G, rs, scale, sums,
+                       counts);
+  } else {
+    static bool set = false;
+    if (!set) {
+      OAP_HIP_CHECK(hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&oap_kmeans_accumulate_binned<float>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
+      set = true;
+    }
+    hipLaunchKernelGGL(oap_kmeans_accumulate_binned<float>, grid, dim3(kAccThreads), lds, s,
+                       static_cast<const float*>(x), ld, d, bins, goff, k, kg, G, rs, scale, sums,
+                       counts);
+  }
+  OAP_HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 void kmeans_finalize(const KMeansFinalizeArgs& a, hipStream_t s) {

@@ -795,6 +795,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 template <int KS, bool XB>
 __global__ __launch_bounds__(256) void oap_kmeans_seed_mindist(KMeansAssignArgs a) {
   constexpr int DP = 16 * KS;
+  using F = Frag<KS, XB>;
   const int lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const int64_t ntiles = (a.n + 31) / 32;
@@ -803,66 +804,87 @@ __global__ __launch_bounds__(256) void oap_kmeans_seed_mindist(KMeansAssignArgs 
   const float cmax = a.cstat ? a.cstat[0] : 0.f;
   const float mrel = 4e-7f * float(a.d + 8);
   const float ueps2 = 1.f + 2e-6f + 1.2e-7f * float(a.d + 4);
-  for (int64_t t = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64; t < ntiles;
-       t += int64_t(gridDim.x) * blockDim.x / 64) {
-    const int64_t row = t * 32 + r;
-    const bool valid = row < a.n;
-    const int64_t rr = valid ? row : a.n - 1;
-    int b = a.labels[rr];
-    if (b < 0 || b >= a.k) b = 0;
-    const float* cp = a.centers + size_t(b) * DP + 8 * h;
-    float part = 0.f, px = 0.f;
+  // one tile per wave step; the next tile's label, bounds and rows are prefetched while this
+  // tile's center rows (L2) are fetched — issued first, so waiting for them (vmcnt retires in
+  // order) never waits for the younger prefetch
+  struct T {
+    F x;
+    int lab = 0;
+    float2 bo = make_float2(0.f, -1.f);
+  };
+  auto load = [&](int64_t tt, T& d) {
+    int64_t row = tt * 32 + r;
+    row = row < a.n ? row : a.n - 1;
+    d.lab = a.labels[row];
+    if (a.bounds) d.bo = reinterpret_cast<const float2*>(a.bounds)[row];
+    if constexpr (XB) {
+      const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      float xv[8];
-      const int f = 16 * s + 8 * h;
-      if constexpr (XB) {
-        bf16x8 v = bf16x8{};
-        if (s < KS - 1 || f < a.ld)
-          v = *reinterpret_cast<const bf16x8*>(static_cast<const __bf16*>(a.x) + rr * a.ld + f);
+      for (int s = 0; s < KS; ++s) {
+        const int f = 16 * s + 8 * h;
+        d.x.v[s] = (s < KS - 1 || f < a.ld) ? *reinterpret_cast<const bf16x8*>(p + 16 * s)
+                                            : bf16x8{};
+      }
+    } else {
+      const float* p = static_cast<const float*>(a.x) + row * a.ld + 8 * h;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = static_cast<float>(v[j]);
-      } else {
-        const float* p = static_cast<const float*>(a.x) + rr * a.ld + f;
+      for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
+          const int f = 16 * s + 8 * h + 4 * q;
           float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (s < KS - 1 || f + 4 * q < a.ld) v = *reinterpret_cast<const float4*>(p + 4 * q);
-          xv[4 * q + 0] = v.x;
-          xv[4 * q + 1] = v.y;
-          xv[4 * q + 2] = v.z;
-          xv[4 * q + 3] = v.w;
+          if (s < KS - 1 || f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+          d.x.v[s][4 * q + 0] = v.x;
+          d.x.v[s][4 * q + 1] = v.y;
+          d.x.v[s][4 * q + 2] = v.z;
+          d.x.v[s][4 * q + 3] = v.w;
         }
-      }
-      const float4 c0 = *reinterpret_cast<const float4*>(cp + 16 * s);
-      const float4 c1 = *reinterpret_cast<const float4*>(cp + 16 * s + 4);
-      const float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    }
+  };
+  auto step = [&](int64_t t, const T& c, T& nx, int64_t tn) {
+    const int64_t row = t * 32 + r;
+    const bool valid = row < a.n;
+    int b = c.lab;
+    if (b < 0 || b >= a.k) b = 0;
+    float cv[KS][8];
+    load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cv);
+    load(tn, nx);
+    float part = 0.f, px = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float e = xv[j] - cv[j];
+        const float xv = c.x.at(s, j);
+        const float e = xv - cv[s][j];
         part = fmaf(e, e, part);
-        px = fmaf(xv[j], xv[j], px);
+        px = fmaf(xv, xv, px);
       }
-    }
     const float rowcost = part + __shfl_xor(part, 32, 64);
     const float nx2 = px + __shfl_xor(px, 32, 64);
     float2 bnew = make_float2(3.4e38f, -1.f);
-    if (a.bounds) {
-      const float2 bo = reinterpret_cast<const float2*>(a.bounds)[rr];
-      if (prune) {
-        const float lp =
-            bo.x >= 3e38f ? bo.y : fmaxf(sqrtf(fmaxf(bo.x, 0.f)) * (1.f - 1e-6f), bo.y);
-        const float l = lp - dmax;
-        if (l > 0.f && l * l - rowcost * ueps2 > mrel * (nx2 + cmax * cmax)) bnew.y = l;
-      }
+    if (prune) {
+      const float2 bo = c.bo;
+      const float lp =
+          bo.x >= 3e38f ? bo.y : fmaxf(sqrtf(fmaxf(bo.x, 0.f)) * (1.f - 1e-6f), bo.y);
+      const float l = lp - dmax;
+      if (l > 0.f && l * l - rowcost * ueps2 > mrel * (nx2 + cmax * cmax)) bnew.y = l;
     }
     if (valid && h == 0) {
       a.mindist[row] = rowcost;
-      a.labels[row] = b;
+      if (b != c.lab) a.labels[row] = b;  // labels stay (only an out-of-range one is reset)
       if (a.bounds) reinterpret_cast<float2*>(a.bounds)[row] = bnew;
     }
     if (a.tile_list && __any(valid && bnew.y < 0.f) && lane == 0)
       a.tile_list[atomicAdd(a.tile_count, 1u)] = static_cast<int32_t>(t);
+  };
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x / 64;
+  int64_t t = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) / 64;
+  T ta, tb;
+  load(t, ta);
+  for (; t < ntiles; t += 2 * stride) {  // wave-uniform trip count
+    step(t, ta, tb, t + stride);
+    if (t + stride >= ntiles) break;
+    step(t + stride, tb, ta, t + 2 * stride);
   }
 }
 
