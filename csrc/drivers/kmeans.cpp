@@ -406,10 +406,12 @@ class InitOps {
         // skip their exact re-decisions)
         req.mindist = costs_.as<float>();
         req.defer = false;
+        req.fast1 = false;  // candidate sets: near ties are the rule (see count_closest)
         req.mindist_seeded = true;
         gpu_assign(ctx_, x_, g, req, ctx_.compute());
       } else {
         req.mindist = tmp_.as<float>();
+        req.fast1 = false;
         gpu_assign(ctx_, x_, g, req, ctx_.compute());
         kern::elementwise_min(costs_.as<float>(), tmp_.as<float>(), x_.rows, ctx_.compute());
       }
@@ -497,6 +499,9 @@ class InitOps {
       req.accumulate = true;
       req.sums_too = false;
       req.defer = false;
+      // k-means|| candidates sit several per cluster, so the 1-product tier's bound (~0.8%)
+      // almost never separates a row's top two: start at the bf16x3 tier (same answers)
+      req.fast1 = false;
       req.counts = dc.as<u64>();
       gpu_assign(ctx_, x_, g, req, ctx_.compute());
       ctx_.copy_to_host(cnt.data(), dc.data(), sizeof(u64) * m);

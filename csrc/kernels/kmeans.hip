@@ -192,6 +192,35 @@ __global__ __launch_bounds__(kAccThreads) void oap_kmeans_accumulate_owned(
     if (cnt[i]) atomicAdd(&counts[c0 + i], static_cast<u64>(cnt[i]));
 }
 
+// ---- counts only (k-means|| candidate weights): a label histogram, the rows are never read.
+// Per-block LDS histogram of all k clusters, one global atomic per non-empty (block, cluster).
+constexpr int kCntThreads = 256;
+__global__ __launch_bounds__(kCntThreads) void oap_kmeans_count_labels(const int32_t* labels,
+                                                                        int64_t n, int k,
+                                                                        u64* counts) {
+  extern __shared__ unsigned hist[];
+  for (int i = threadIdx.x; i < k; i += kCntThreads) hist[i] = 0u;
+  __syncthreads();
+  const int64_t n4 = n / 4;
+  const int4* l4 = reinterpret_cast<const int4*>(labels);
+  for (int64_t q = int64_t(blockIdx.x) * kCntThreads + threadIdx.x; q < n4;
+       q += int64_t(gridDim.x) * kCntThreads) {
+    const int4 v = l4[q];
+    if (unsigned(v.x) < unsigned(k)) atomicAdd(&hist[v.x], 1u);
+    if (unsigned(v.y) < unsigned(k)) atomicAdd(&hist[v.y], 1u);
+    if (unsigned(v.z) < unsigned(k)) atomicAdd(&hist[v.z], 1u);
+    if (unsigned(v.w) < unsigned(k)) atomicAdd(&hist[v.w], 1u);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t r = n4 * 4 + threadIdx.x; r < n; r += kCntThreads) {
+      const int v = labels[r];
+      if (unsigned(v) < unsigned(k)) atomicAdd(&hist[v], 1u);
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k; i += kCntThreads)
+    if (hist[i]) atomicAdd(&counts[i], static_cast<u64>(hist[i]));
+}
+
 // ---- binned accumulation: rows grouped by cluster range first (two cheap passes over the
 // labels), so every lane of the accumulation kernel works on a row of its range — the scan
 // variant above reads every label in every range and keeps a dependent load chain per 64 rows.
@@ -603,10 +632,32 @@ void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
   OAP_HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+// counts without sums: label histogram (labels must be 16-byte aligned, as device buffers are)
+bool count_labels(const int32_t* labels, int64_t n, int k, unsigned long long* counts,
+                  hipStream_t s) {
+  if (size_t(k) * 4 > kLdsLimit - 64 || (reinterpret_cast<uintptr_t>(labels) & 15)) return false;
+  const int grid = static_cast<int>(std::max<int64_t>(
+      1, std::min<int64_t>((n / 4 + kCntThreads - 1) / kCntThreads, 2048)));
+  static bool set = false;
+  if (!set) {
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_kmeans_count_labels),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(kLdsLimit)));
+    set = true;
+  }
+  hipLaunchKernelGGL(oap_kmeans_count_labels, dim3(grid), dim3(kCntThreads), size_t(k) * 4, s,
+                     labels, n, k, counts);
+  OAP_HIP_CHECK(hipGetLastError());
+  return true;
+}
+}  // namespace
+
 void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
                        const int32_t* labels, int k, const float* scale,
                        unsigned long long* sums, unsigned long long* counts, hipStream_t s) {
   if (n == 0) return;
+  if (!sums && count_labels(labels, n, k, counts, s)) return;
   const int es = xbf16 ? 2 : 4, eps = 16 / es;
   const int seg = ld * es / 16;
   OAP_CHECK(ld * es % 16 == 0, "kmeans_accumulate: rows must be 16-byte multiples");
@@ -671,6 +722,7 @@ bool kmeans_accumulate_binned(const void* x, bool xbf16, int64_t n, int ld, int 
                               unsigned long long* sums, unsigned long long* counts, void* scratch,
                               hipStream_t s) {
   if (n == 0) return true;
+  if (!sums) return count_labels(labels, n, k, counts, s);
   const int es = xbf16 ? 2 : 4, eps = 16 / es;
   const int seg = ld * es / 16;
   if (ld * es % 16 != 0 || seg > 64 || n >= (int64_t(1) << 31)) return false;
