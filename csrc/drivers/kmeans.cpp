@@ -232,6 +232,9 @@ struct AssignReq {
   // centers are distinct cluster centers — Lloyd / predict; k-means|| candidate sets hold
   // several near-identical points per cluster, whose ties are genuine, so init passes opt out)
   bool defer = true;
+  // single launch, pruning on: delta accumulation over req.tile_list (see KMeansAssignArgs)
+  bool delta = false;
+  float* xnorm = nullptr;
 };
 
 // Returns the number of cost partials written to req.cost_slab.
@@ -265,9 +268,19 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   a.pruned_tiles = req.pruned_tiles;
   OAP_CHECK(!req.bounds || (x.cols <= 128 && !req.precise && req.labels),
             "kmeans pruning needs the fast path (d <= 128) and persistent labels");
+  a.xnorm = req.xnorm;
   const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
-  if (x.cols > 128 || g.kpad <= kmax || kmax == 0)
+  if (x.cols > 128 || g.kpad <= kmax || kmax == 0) {
+    if (req.delta) {
+      OAP_CHECK(req.bounds && req.drift && req.tile_list && req.labels_valid,
+                "kmeans delta accumulation needs the pruning scan's tile list");
+      a.delta = true;
+      a.tile_list = req.tile_list;
+      a.tile_count = req.tile_count;
+    }
     return kern::kmeans_assign(a, ctx.info().cu_count, s);
+  }
+  OAP_CHECK(!req.delta, "kmeans delta accumulation is single-launch only");
   // ---- chunked path (more centroids than one LDS plan holds)
   Buffer lab, dist;
   int32_t* labels = req.labels;
@@ -904,6 +917,24 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     }
   }
 
+  // delta accumulation (single launch + pruning): persistent local statistics, |x|^2 per row,
+  // the scan's tile list, and the centers each iteration assigned against (final exact cost)
+  const bool delta = prune && !chunked && p.delta;
+  Buffer loc_b, xnorm_b, dlist_b, cbak_b;
+  if (delta) {
+    loc_b = ctx.alloc(sizeof(u64) * (kd + k));
+    xnorm_b = ctx.alloc(sizeof(float) * x.rows);
+    const int64_t nt = (x.rows + 31) / 32;
+    dlist_b = ctx.alloc(sizeof(int32_t) * nt + 64);
+    cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
+    req.xnorm = xnorm_b.as<float>();
+    req.sums = loc_b.as<u64>();
+    req.counts = loc_b.as<u64>() + kd;
+  }
+  unsigned* dcount =
+      delta ? reinterpret_cast<unsigned*>(dlist_b.as<char>() + sizeof(int32_t) * ((x.rows + 31) / 32))
+            : nullptr;
+
   kern::KMeansFinalizeArgs fa;
   fa.sums = sums;
   fa.counts = counts;
@@ -946,13 +977,34 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       maybe_inject_fault(comm.rank(), "kmeans_iter", it);
       roctx_push("kmeans/iteration");
       ev[b].e0.record(s);
-      OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
+      if (!delta || it == 0)
+        OAP_HIP_CHECK(hipMemsetAsync(delta ? loc_b.data() : stats.data(), 0,
+                                     sizeof(u64) * (kd + k), s));
       req.labels_valid = it > 0;
       if (prune) {
         req.drift = it > 0 ? drift_b.as<float>() : nullptr;
         req.drift_max = it > 0 ? drift_b.as<float>() + k : nullptr;
       }
+      req.delta = delta && it > 0;
+      if (req.delta) {
+        OAP_HIP_CHECK(hipMemsetAsync(dcount, 0, sizeof(unsigned), s));
+        kern::kmeans_prune_scan(x.rows, k, d, req.bounds, req.labels, req.xnorm, req.drift,
+                                req.drift_max, g.cstat.as<float>(), dlist_b.as<int32_t>(),
+                                dcount, req.pruned_tiles, s);
+        req.tile_list = dlist_b.as<int32_t>();
+        req.tile_count = dcount;
+      } else if (!chunked) {
+        req.tile_list = nullptr;
+        req.tile_count = nullptr;
+      }
       int nb = gpu_assign(ctx, x, g, req, s);
+      if (delta) {
+        OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
+                                     hipMemcpyDeviceToDevice, s));
+        OAP_HIP_CHECK(hipMemcpyAsync(cbak_b.data(), g.c32.data(),
+                                     sizeof(float) * size_t(g.kpad) * g.dp,
+                                     hipMemcpyDeviceToDevice, s));
+      }
       if (nb > 0)
         kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
       else
@@ -997,8 +1049,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
            << (ms_assign > 0 ? double(flops_per_iter) / (ms_assign * 1e-3) / 1e12 : 0.0);
         Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
       }
-      res.cost = fl.cost;
-      res.cost_history.push_back(fl.cost);
+      // delta iterations sum the cost of the tiles they read only: not a cost
+      const double c_it = (delta && it > 0) ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
+      res.cost = c_it;
+      res.cost_history.push_back(c_it);
       res.num_iter = it + 1;
       if (fl.converged && p.tol >= 0) {  // (B == 1 here: nothing was enqueued past it)
         res.converged = true;
@@ -1016,6 +1070,31 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
       tier2_seen = t2;
     }
+  }
+  if (delta && res.num_iter > 1) {
+    // exact cost of the last iteration: every row against the centers it was assigned to, with
+    // the assign kernel's per-row fp32 arithmetic (kmeans_seed_mindist), summed in fp64
+    TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
+    Buffer md = ctx.alloc(sizeof(float) * x.rows);
+    kern::KMeansAssignArgs ca;
+    ca.x = x.data.data();
+    ca.xbf16 = x.dtype == DType::BF16;
+    ca.n = x.rows;
+    ca.ld = static_cast<int>(x.ld);
+    ca.d = x.cols;
+    ca.centers = cbak_b.as<float>();
+    ca.k = k;
+    ca.kpad = g.kpad;
+    ca.labels = req.labels;
+    ca.mindist = md.as<float>();
+    kern::kmeans_seed_mindist(ca, s);
+    const int nb = kern::reduce_sum_f32(md.as<float>(), x.rows, slab.as<double>(), s);
+    kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
+    if (comm.size() > 1) comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+    double c = 0.0;
+    ctx.copy_to_host(&c, cost_d.data(), sizeof(double), s);
+    res.cost = c;
+    res.cost_history.back() = c;
   }
   res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);
   res.centers.resize(kd);

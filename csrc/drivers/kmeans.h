@@ -34,6 +34,11 @@ struct KMeansParams {
   // bound-based pruning of the distance work in Lloyd iterations after the first (GPU fast
   // path, d <= 128); exact: assignments, centers and costs are bitwise those without it
   bool prune = true;
+  // with pruning on the single-launch path: iterations after the first keep the local
+  // statistics and read only the rows of tiles whose labels may change (delta accumulation);
+  // per-iteration costs are then computed only on full passes, the final cost by an exact
+  // pass over the labels (cost_history holds NaN for the delta iterations before the last)
+  bool delta = true;
 };
 
 struct KMeansResult {

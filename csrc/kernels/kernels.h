@@ -97,7 +97,23 @@ struct KMeansAssignArgs {
   unsigned* defer_count = nullptr;
   bool seg_list = false;
   bool fresh_bound = true;  // merge + bounds: this pass starts the row's running bound afresh
+  // Delta accumulation (single launch, Lloyd iterations > 0, with tile_list from
+  // kmeans_prune_scan): sums / counts hold the previous iteration's local statistics and only
+  // rows whose label changes add +x to the new and -x to the old cluster (fixed point: exactly
+  // the full recount).  Pruned tiles are never read.
+  bool delta = false;
+  // optional [n]: |x|^2 as the assign kernel computes it (the scan's pruning margin)
+  float* xnorm = nullptr;
 };
+// Delta-mode pruning scan (single launch): per 32-row tile, tests every row's bounds (labels,
+// xnorm, the centers' drift) exactly as the assign kernel's own pruning test does.  Tiles that
+// provably keep all labels get their bounds advanced in place (u + drift, l - max drift, rounded
+// outward) and are counted in *pruned; the others are appended to tile_list (*tile_count must be
+// zero on entry).  Reads 16 bytes per row and no row data.
+void kmeans_prune_scan(int64_t n, int k, int d, float* bounds, const int32_t* labels,
+                       const float* xnorm, const float* drift, const float* drift_max,
+                       const float* cstat, int32_t* tile_list, unsigned* tile_count,
+                       unsigned long long* pruned, hipStream_t s);
 // Upper bound on rows one assign workgroup processes for n local rows (device independent); the
 // fixed-point scale keeps per-workgroup LDS partial sums below 2^53 with it.
 int64_t kmeans_rows_per_block_bound(int64_t n);

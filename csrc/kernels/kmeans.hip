@@ -632,6 +632,82 @@ void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
   OAP_HIP_CHECK(hipGetLastError());
 }
 
+// Delta-mode pruning scan: one thread per row, a wave = two 32-row tiles.  The test is the assign
+// kernel's own single-launch pruning test (kmeans_assign.hip, `prune_single`) on the stored |x|^2.
+__global__ __launch_bounds__(256) void oap_kmeans_prune_scan(
+    int64_t n, int k, int d, float2* __restrict__ bounds, const int32_t* __restrict__ labels,
+    const float* __restrict__ xnorm, const float* __restrict__ drift,
+    const float* __restrict__ drift_max, const float* __restrict__ cstat,
+    int32_t* __restrict__ tile_list, unsigned* __restrict__ tile_count,
+    unsigned long long* __restrict__ pruned) {
+  __shared__ unsigned wcnt[4], wbase[4];
+  __shared__ unsigned long long bpruned;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const float dmax = drift_max[0];
+  const float cmax = cstat[0];
+  const float mrel = 4e-7f * float(d + 8);
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t nchunks = (n + 255) / 256;  // a chunk = 256 rows = 8 tiles, one per block step
+  if (threadIdx.x == 0) bpruned = 0;
+  unsigned long long n_pruned = 0;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {  // block-uniform trip count
+    const int64_t w = c * 4 + wave;  // this wave's tile pair
+    const int64_t row = w * 64 + lane;
+    const bool valid = row < n;
+    bool ok = true;
+    float2 bnew = make_float2(0.f, 0.f);
+    if (valid) {
+      const float2 b = bounds[row];
+      const int lab = min(max(labels[row], 0), k - 1);
+      const float u = b.x + drift[lab];
+      const float lk = b.y - dmax;
+      ok = lk > 0.f && (lk - u) * (lk + u) > mrel * (xnorm[row] + cmax * cmax);
+      // outward rounding: the advanced bounds stay bounds whatever fp32 did to the sums
+      bnew = make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f));
+    }
+    const unsigned long long all_ok = __ballot(ok);
+    const bool pr0 = static_cast<unsigned>(all_ok) == 0xffffffffu;
+    const bool pr1 = static_cast<unsigned>(all_ok >> 32) == 0xffffffffu;
+    if (valid && (h ? pr1 : pr0)) bounds[row] = bnew;
+    const bool has0 = 2 * w < ntiles, has1 = 2 * w + 1 < ntiles;
+    const bool act0 = has0 && !pr0, act1 = has1 && !pr1;
+    if (lane == 0) {
+      wcnt[wave] = unsigned(act0) + unsigned(act1);
+      n_pruned += unsigned(has0 && pr0) + unsigned(has1 && pr1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      unsigned pos = tot ? atomicAdd(tile_count, tot) : 0u;
+      for (int i = 0; i < 4; ++i) {
+        wbase[i] = pos;
+        pos += wcnt[i];
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      unsigned pos = wbase[wave];
+      if (act0) tile_list[pos++] = static_cast<int32_t>(2 * w);
+      if (act1) tile_list[pos] = static_cast<int32_t>(2 * w + 1);
+    }
+  }
+  if (lane == 0 && n_pruned) atomicAdd(&bpruned, n_pruned);
+  __syncthreads();
+  if (threadIdx.x == 0 && bpruned && pruned) atomicAdd(pruned, bpruned);
+}
+
+void kmeans_prune_scan(int64_t n, int k, int d, float* bounds, const int32_t* labels,
+                       const float* xnorm, const float* drift, const float* drift_max,
+                       const float* cstat, int32_t* tile_list, unsigned* tile_count,
+                       unsigned long long* pruned, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = static_cast<int>(std::min<int64_t>((n + 255) / 256, 8192));
+  hipLaunchKernelGGL(oap_kmeans_prune_scan, dim3(grid), dim3(256), 0, s, n, k, d,
+                     reinterpret_cast<float2*>(bounds), labels, xnorm, drift, drift_max, cstat,
+                     tile_list, tile_count, pruned);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
 namespace {
 // counts without sums: label histogram (labels must be 16-byte aligned, as device buffers are)
 bool count_labels(const int32_t* labels, int64_t n, int k, unsigned long long* counts,

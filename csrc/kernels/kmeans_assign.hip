@@ -267,6 +267,51 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     float l = 0.f, lo = 0.f, lin = INFINITY, yin = -1.f;
     int i1 = -1;
     bool same = false;  // pruned row: its stored label is already right
+    int old = -1;       // delta mode: the row's label from the previous iteration
+  };
+
+  // fixed-point accumulation of one row into cluster b (neg: subtract it)
+  auto add_row = [&](const F& xv, int b, bool neg) {
+    const float sgn = neg ? -1.f : 1.f;
+    if constexpr (LDSACC) {
+      if (h == 0) atomicAdd(&cnt_l[b], neg ? 0xffffffffu : 1u);
+      if (!a.sums_too) return;
+      double* ap = acc_l + b * (d | 1) + 8 * h;
+      // k-steps below KS-1 are all real features (KS = ceil(d/16)): no per-element guards
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int f0 = 16 * s + 8 * h;
+        const float4 s0 = *reinterpret_cast<const float4*>(sc_l + f0);
+        const float4 s1 = *reinterpret_cast<const float4*>(sc_l + f0 + 4);
+        const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        if (s < KS - 1 || d == DP) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            atomicAdd(ap + 16 * s + j, sgn * static_cast<double>(rintf(xv.at(s, j) * scv[j])));
+        } else {
+          const int nv = d - f0;  // real features of this lane's half of the last k-step
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (j < nv)
+              atomicAdd(ap + 16 * s + j, sgn * static_cast<double>(rintf(xv.at(s, j) * scv[j])));
+        }
+      }
+    } else {
+      if (h == 0) atomicAdd(&a.counts[b], neg ? ~0ull : 1ull);
+      if (a.sums_too) {
+        u64* gp = a.sums + size_t(b) * d;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int f = 16 * s + 8 * h + j;
+            if (f < d) {
+              const long long qv = static_cast<long long>(sgn * rintf(xv.at(s, j) * sc_l[f]));
+              atomicAdd(gp + f, static_cast<u64>(qv));
+            }
+          }
+      }
+    }
   };
 
   // ---- per-row epilogue: exact cost, outputs, fixed-point accumulation
@@ -311,44 +356,14 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       my_cost += double(rowcost);
     }
     if (!accumulate) return;
-    if constexpr (LDSACC) {
-      if (h == 0) atomicAdd(&cnt_l[b], 1u);
-      if (!a.sums_too) return;
-      double* ap = acc_l + b * (d | 1) + 8 * h;
-      // k-steps below KS-1 are all real features (KS = ceil(d/16)): no per-element guards
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int f0 = 16 * s + 8 * h;
-        const float4 s0 = *reinterpret_cast<const float4*>(sc_l + f0);
-        const float4 s1 = *reinterpret_cast<const float4*>(sc_l + f0 + 4);
-        const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        if (s < KS - 1 || d == DP) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv.at(s, j) * scv[j])));
-        } else {
-          const int nv = d - f0;  // real features of this lane's half of the last k-step
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (j < nv)
-              atomicAdd(ap + 16 * s + j, static_cast<double>(rintf(xv.at(s, j) * scv[j])));
-        }
-      }
+    // delta mode: a row that keeps its label contributes nothing; a moved row adds +x to its new
+    // and -x to its old cluster (integer-valued fixed point, so exactly the full recount)
+    if (a.delta) {
+      if (bu.same || bu.old == b || bu.old < 0) return;
+      add_row(xv, b, false);
+      add_row(xv, bu.old, true);
     } else {
-      if (h == 0) atomicAdd(&a.counts[b], 1ull);
-      if (a.sums_too) {
-        u64* gp = a.sums + size_t(b) * d;
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int f = 16 * s + 8 * h + j;
-            if (f < d) {
-              const long long qv = static_cast<long long>(rintf(xv.at(s, j) * sc_l[f]));
-              atomicAdd(gp + f, static_cast<u64>(qv));
-            }
-          }
-      }
+      add_row(xv, b, false);
     }
   };
 
@@ -464,6 +479,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += __shfl_xor(nx2, 32, 64);
+      if (a.xnorm && h == 0 && valid) a.xnorm[row] = nx2;
       const float marg = mrel * (nx2 + cmax * cmax);
       // Pruning: a tile whose rows all keep their center provably (bounds) skips the distance
       // work; its rows still get the exact cost, outputs and accumulation from their label.
@@ -714,6 +730,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         load_meta(pf, mn);
       }
       BUpd bu;
+      if (a.delta) bu.old = min(max(m.lab, 0), k - 1);
       if (a.bounds) {
         // every candidate's true distance is >= its key - tt; the pick's rivals are the other
         // keys (the second key, or the first when the exact pass picked another center)
@@ -777,8 +794,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
       if (v != 0.0) atomicAdd(&a.sums[i], static_cast<u64>(static_cast<long long>(v)));
     }
     for (int i = tid; i < k; i += kThreads) {
-      const unsigned c = cnt_l[i];
-      if (c) atomicAdd(&a.counts[i], static_cast<u64>(c));
+      const int c = static_cast<int>(cnt_l[i]);  // signed: delta mode subtracts
+      if (c) atomicAdd(&a.counts[i], static_cast<u64>(static_cast<long long>(c)));
     }
   }
 }
