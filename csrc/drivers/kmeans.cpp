@@ -919,7 +919,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
 
   // delta accumulation (single launch + pruning): persistent local statistics, |x|^2 per row,
   // the scan's tile list, and the centers each iteration assigned against (final exact cost)
-  const bool delta = prune && !chunked && p.delta;
+  // (rank-uniform form: a rank with no rows still joins the final-cost collective)
+  const bool delta_all = p.prune && !p.precise && x.cols <= 128 && !chunked && p.delta;
+  const bool delta = delta_all && prune;
   Buffer loc_b, xnorm_b, dlist_b, cbak_b;
   if (delta) {
     loc_b = ctx.alloc(sizeof(u64) * (kd + k));
@@ -1050,7 +1052,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
       }
       // delta iterations sum the cost of the tiles they read only: not a cost
-      const double c_it = (delta && it > 0) ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
+      const double c_it =
+          (delta_all && it > 0) ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
       res.cost = c_it;
       res.cost_history.push_back(c_it);
       res.num_iter = it + 1;
@@ -1071,26 +1074,32 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       tier2_seen = t2;
     }
   }
-  if (delta && res.num_iter > 1) {
+  if (delta_all && res.num_iter > 1) {
     // exact cost of the last iteration: every row against the centers it was assigned to, with
     // the assign kernel's per-row fp32 arithmetic (kmeans_seed_mindist), summed in fp64
     TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
-    Buffer md = ctx.alloc(sizeof(float) * x.rows);
-    kern::KMeansAssignArgs ca;
-    ca.x = x.data.data();
-    ca.xbf16 = x.dtype == DType::BF16;
-    ca.n = x.rows;
-    ca.ld = static_cast<int>(x.ld);
-    ca.d = x.cols;
-    ca.centers = cbak_b.as<float>();
-    ca.k = k;
-    ca.kpad = g.kpad;
-    ca.labels = req.labels;
-    ca.mindist = md.as<float>();
-    kern::kmeans_seed_mindist(ca, s);
-    const int nb = kern::reduce_sum_f32(md.as<float>(), x.rows, slab.as<double>(), s);
-    kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
-    if (comm.size() > 1) comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+    Buffer md;  // outlives the copy_to_host below (which synchronizes the stream)
+    if (!delta) {
+      OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+    } else {
+      md = ctx.alloc(sizeof(float) * x.rows);
+      kern::KMeansAssignArgs ca;
+      ca.x = x.data.data();
+      ca.xbf16 = x.dtype == DType::BF16;
+      ca.n = x.rows;
+      ca.ld = static_cast<int>(x.ld);
+      ca.d = x.cols;
+      ca.centers = cbak_b.as<float>();
+      ca.k = k;
+      ca.kpad = g.kpad;
+      ca.labels = req.labels;
+      ca.mindist = md.as<float>();
+      kern::kmeans_seed_mindist(ca, s);
+      const int nb = kern::reduce_sum_f32(md.as<float>(), x.rows, slab.as<double>(), s);
+      kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
+    }
+    if (comm.size() > 1)
+      comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
     double c = 0.0;
     ctx.copy_to_host(&c, cost_d.data(), sizeof(double), s);
     res.cost = c;
