@@ -917,7 +917,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     }
   }
 
-  // delta accumulation (single launch + pruning): persistent local statistics, |x|^2 per row,
+  // delta accumulation (single launch + pruning): persistent local statistics, max |x|^2 per tile,
   // the scan's tile list, and the centers each iteration assigned against (final exact cost)
   // (rank-uniform form: a rank with no rows still joins the final-cost collective)
   const bool delta_all = p.prune && !p.precise && x.cols <= 128 && !chunked && p.delta;
@@ -925,8 +925,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer loc_b, xnorm_b, dlist_b, cbak_b;
   if (delta) {
     loc_b = ctx.alloc(sizeof(u64) * (kd + k));
-    xnorm_b = ctx.alloc(sizeof(float) * x.rows);
     const int64_t nt = (x.rows + 31) / 32;
+    xnorm_b = ctx.alloc(sizeof(float) * nt);
     dlist_b = ctx.alloc(sizeof(int32_t) * nt + 64);
     cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
     req.xnorm = xnorm_b.as<float>();
@@ -1076,13 +1076,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   }
   if (delta_all && res.num_iter > 1) {
     // exact cost of the last iteration: every row against the centers it was assigned to, with
-    // the assign kernel's per-row fp32 arithmetic (kmeans_seed_mindist), summed in fp64
+    // the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
     TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
     Buffer md;  // outlives the copy_to_host below (which synchronizes the stream)
     if (!delta) {
       OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
     } else {
-      md = ctx.alloc(sizeof(float) * x.rows);
       kern::KMeansAssignArgs ca;
       ca.x = x.data.data();
       ca.xbf16 = x.dtype == DType::BF16;
@@ -1093,9 +1092,13 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       ca.k = k;
       ca.kpad = g.kpad;
       ca.labels = req.labels;
-      ca.mindist = md.as<float>();
-      kern::kmeans_seed_mindist(ca, s);
-      const int nb = kern::reduce_sum_f32(md.as<float>(), x.rows, slab.as<double>(), s);
+      int nb = kern::kmeans_label_cost(ca, slab.as<double>(), std::min(nslab, 2048), s);
+      if (nb < 0) {  // centers beyond LDS: per-row costs through the seed kernel
+        md = ctx.alloc(sizeof(float) * x.rows);
+        ca.mindist = md.as<float>();
+        kern::kmeans_seed_mindist(ca, s);
+        nb = kern::reduce_sum_f32(md.as<float>(), x.rows, slab.as<double>(), s);
+      }
       kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
     }
     if (comm.size() > 1)

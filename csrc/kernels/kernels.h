@@ -102,14 +102,15 @@ struct KMeansAssignArgs {
   // rows whose label changes add +x to the new and -x to the old cluster (fixed point: exactly
   // the full recount).  Pruned tiles are never read.
   bool delta = false;
-  // optional [n]: |x|^2 as the assign kernel computes it (the scan's pruning margin)
+  // optional [ceil(n/32)]: per 32-row tile, the largest |x|^2 as the assign kernel computes it
+  // (the scan's pruning margin)
   float* xnorm = nullptr;
 };
 // Delta-mode pruning scan (single launch): per 32-row tile, tests every row's bounds (labels,
 // xnorm, the centers' drift) exactly as the assign kernel's own pruning test does.  Tiles that
 // provably keep all labels get their bounds advanced in place (u + drift, l - max drift, rounded
 // outward) and are counted in *pruned; the others are appended to tile_list (*tile_count must be
-// zero on entry).  Reads 16 bytes per row and no row data.
+// zero on entry).  Reads 12 bytes per row (+4 per tile) and no row data.
 void kmeans_prune_scan(int64_t n, int k, int d, float* bounds, const int32_t* labels,
                        const float* xnorm, const float* drift, const float* drift_max,
                        const float* cstat, int32_t* tile_list, unsigned* tile_count,
@@ -124,6 +125,10 @@ int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s);
 // Chunked path (d <= 128): mindist[i] = |x_i - centers[labels[i]]|^2, bitwise as the assign
 // kernel computes it, so later merge passes can skip chunks that cannot beat it.
 void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s);
+// Exact cost of an assignment: sum_i |x_i - centers[labels[i]]|^2 with the assign kernel's
+// per-row fp32 arithmetic, centers staged in LDS.  Writes at most max_blocks fp64 partials to
+// slab and returns their number, or -1 when the centers do not fit LDS.
+int kmeans_label_cost(const KMeansAssignArgs& a, double* slab, int max_blocks, hipStream_t s);
 // *pruned += (ntiles - *listed) * passes (device side: no host round trip)
 void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
                          unsigned long long* pruned, hipStream_t s);

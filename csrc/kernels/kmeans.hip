@@ -619,6 +619,10 @@ void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
   launch_kmeans_seed_mindist(a, s);
 }
 
+int kmeans_label_cost(const KMeansAssignArgs& a, double* slab, int max_blocks, hipStream_t s) {
+  return launch_kmeans_label_cost(a, slab, max_blocks, s);
+}
+
 __global__ void oap_kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
                                         unsigned long long* pruned) {
   if (threadIdx.x == 0)
@@ -633,7 +637,8 @@ void kmeans_count_pruned(const unsigned* listed, int64_t ntiles, int passes,
 }
 
 // Delta-mode pruning scan: one thread per row, a wave = two 32-row tiles.  The test is the assign
-// kernel's own single-launch pruning test (kmeans_assign.hip, `prune_single`) on the stored |x|^2.
+// kernel's own single-launch pruning test (kmeans_assign.hip, `prune_single`) with the tile's
+// largest |x|^2 (stored per tile by the assign kernel) in the margin — never looser per row.
 __global__ __launch_bounds__(256) void oap_kmeans_prune_scan(
     int64_t n, int k, int d, float2* __restrict__ bounds, const int32_t* __restrict__ labels,
     const float* __restrict__ xnorm, const float* __restrict__ drift,
@@ -661,7 +666,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_prune_scan(
       const int lab = min(max(labels[row], 0), k - 1);
       const float u = b.x + drift[lab];
       const float lk = b.y - dmax;
-      ok = lk > 0.f && (lk - u) * (lk + u) > mrel * (xnorm[row] + cmax * cmax);
+      ok = lk > 0.f && (lk - u) * (lk + u) > mrel * (xnorm[row >> 5] + cmax * cmax);
       // outward rounding: the advanced bounds stay bounds whatever fp32 did to the sums
       bnew = make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f));
     }

@@ -479,7 +479,12 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += __shfl_xor(nx2, 32, 64);
-      if (a.xnorm && h == 0 && valid) a.xnorm[row] = nx2;
+      if (a.xnorm) {  // per-tile max |x|^2 (the scan's margin: conservative for every row)
+        float tmax = nx2;
+#pragma unroll
+        for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));
+        if (lane == 0) a.xnorm[t] = tmax;
+      }
       const float marg = mrel * (nx2 + cmax * cmax);
       // Pruning: a tile whose rows all keep their center provably (bounds) skips the distance
       // work; its rows still get the exact cost, outputs and accumulation from their label.
@@ -986,6 +991,121 @@ void launch_xb(const KMeansAssignArgs& a, int grid, hipStream_t s, bool lds_acc)
   }
 }
 
+// sum over rows of |x_row - c_{labels[row]}|^2: per row exactly the assign kernel's fp32 lane
+// layout and summation order (bitwise its per-row cost), the centers staged in LDS (no L2 vector
+// loads next to the row stream), rows prefetched two tiles ahead.  One fp64 partial per block
+// (waves in index order) into slab.
+template <int KS, bool XB>
+__global__ __launch_bounds__(256) void oap_kmeans_label_cost(KMeansAssignArgs a, double* slab) {
+  constexpr int DP = 16 * KS;
+  using F = Frag<KS, XB>;
+  extern __shared__ float4 dyn_lds[];
+  float* cl = reinterpret_cast<float*>(dyn_lds);
+  __shared__ double wsum[4];
+  for (int i = threadIdx.x; i < a.k * DP / 4; i += blockDim.x)
+    reinterpret_cast<float4*>(cl)[i] = reinterpret_cast<const float4*>(a.centers)[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t ntiles = (a.n + 31) / 32;
+  struct T {
+    F x;
+    int lab = 0;
+  };
+  auto load = [&](int64_t tt, T& d) {
+    int64_t row = tt * 32 + r;
+    row = row < a.n ? (row < 0 ? 0 : row) : a.n - 1;
+    d.lab = a.labels[row];
+    if constexpr (XB) {
+      const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int f = 16 * s + 8 * h;
+        d.x.v[s] = (s < KS - 1 || f < a.ld) ? *reinterpret_cast<const bf16x8*>(p + 16 * s)
+                                            : bf16x8{};
+      }
+    } else {
+      const float* p = static_cast<const float*>(a.x) + row * a.ld + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int f = 16 * s + 8 * h + 4 * q;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (s < KS - 1 || f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+          d.x.v[s][4 * q + 0] = v.x;
+          d.x.v[s][4 * q + 1] = v.y;
+          d.x.v[s][4 * q + 2] = v.z;
+          d.x.v[s][4 * q + 3] = v.w;
+        }
+    }
+  };
+  double my = 0.0;
+  auto step = [&](int64_t t, const T& c, T& nx, int64_t tn) {
+    load(tn, nx);  // prefetch: in flight while this tile computes
+    const bool valid = t * 32 + r < a.n;
+    int b = c.lab;
+    if (b < 0 || b >= a.k) b = 0;
+    float cv[KS][8];
+    load_row8<KS>(cl + size_t(b) * DP + 8 * h, cv);
+    float part = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = c.x.at(s, j) - cv[s][j];
+        part = fmaf(e, e, part);
+      }
+    const float rowcost = part + __shfl_xor(part, 32, 64);
+    if (valid && h == 0) my += double(rowcost);
+  };
+  const int64_t stride = int64_t(gridDim.x) * 4;
+  int64_t t = int64_t(blockIdx.x) * 4 + wave;
+  T ta, tb;
+  load(t, ta);
+  for (; t < ntiles; t += 2 * stride) {  // wave-uniform trip count
+    step(t, ta, tb, t + stride);
+    if (t + stride >= ntiles) break;
+    step(t + stride, tb, ta, t + 2 * stride);
+  }
+  const double ws = wave_sum_f64(my);
+  if (lane == 0) wsum[wave] = ws;
+  __syncthreads();
+  if (threadIdx.x == 0) slab[blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+}
+
+template <int KS, bool XB>
+int launch_label_cost(const KMeansAssignArgs& a, double* slab, int max_blocks, hipStream_t s) {
+  const size_t lds = size_t(a.k) * 16 * KS * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_kmeans_label_cost<KS, XB>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(kLdsLimit - 1024)));
+    attr_set = true;
+  }
+  const int64_t tiles = (a.n + 31) / 32;
+  const int grid = static_cast<int>(std::min<int64_t>(tiles / 8 + 1, max_blocks));
+  hipLaunchKernelGGL((oap_kmeans_label_cost<KS, XB>), dim3(grid), dim3(256), lds, s, a, slab);
+  OAP_HIP_CHECK(hipGetLastError());
+  return grid;
+}
+
+template <bool XB>
+int label_cost_xb(const KMeansAssignArgs& a, double* slab, int max_blocks, hipStream_t s) {
+  switch ((a.d + 15) / 16) {
+    case 1: return launch_label_cost<1, XB>(a, slab, max_blocks, s);
+    case 2: return launch_label_cost<2, XB>(a, slab, max_blocks, s);
+    case 3: return launch_label_cost<3, XB>(a, slab, max_blocks, s);
+    case 4: return launch_label_cost<4, XB>(a, slab, max_blocks, s);
+    case 5: return launch_label_cost<5, XB>(a, slab, max_blocks, s);
+    case 6: return launch_label_cost<6, XB>(a, slab, max_blocks, s);
+    case 7: return launch_label_cost<7, XB>(a, slab, max_blocks, s);
+    case 8: return launch_label_cost<8, XB>(a, slab, max_blocks, s);
+    default: OAP_THROW(ConfigError, "kmeans_label_cost: unsupported d=" << a.d);
+  }
+}
+
 }  // namespace
 
 void launch_kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
@@ -995,6 +1115,14 @@ void launch_kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
     seed_xb<true>(a, s);
   else
     seed_xb<false>(a, s);
+}
+
+int launch_kmeans_label_cost(const KMeansAssignArgs& a, double* slab, int max_blocks,
+                             hipStream_t s) {
+  OAP_CHECK(a.d <= 128 && a.labels && a.centers && a.n > 0, "kmeans_label_cost: bad arguments");
+  if (size_t(a.k) * kmeans_dp(a.d) * sizeof(float) > kLdsLimit - 1024) return -1;
+  return a.xbf16 ? label_cost_xb<true>(a, slab, max_blocks, s)
+                 : label_cost_xb<false>(a, slab, max_blocks, s);
 }
 
 int kmeans_mfma_kmax(int d, bool precise) {

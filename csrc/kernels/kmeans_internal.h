@@ -13,6 +13,9 @@ constexpr size_t kLdsLimit = 160 * 1024;
 void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s);
 // mindist/labels of the chunked path seeded from labels (the previous assignment).
 void launch_kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s);
+// -1 when the k centers do not fit LDS, else the number of fp64 partials written to slab
+int launch_kmeans_label_cost(const KMeansAssignArgs& a, double* slab, int max_blocks,
+                             hipStream_t s);
 // Largest kpad (multiple of 32) whose centroid planes fit LDS for d features.
 int kmeans_mfma_kmax(int d, bool precise);
 // Grid the MFMA assign kernel uses for n rows (>= 256 blocks once there is work for them, so the
