@@ -673,7 +673,8 @@ __global__ __launch_bounds__(256) void oap_kmeans_prune_scan(
     const unsigned long long all_ok = __ballot(ok);
     const bool pr0 = static_cast<unsigned>(all_ok) == 0xffffffffu;
     const bool pr1 = static_cast<unsigned>(all_ok >> 32) == 0xffffffffu;
-    if (valid && (h ? pr1 : pr0)) bounds[row] = bnew;
+    // no center moved (dmax == 0, every drift is 0): the stored bounds already hold, no write
+    if (dmax > 0.f && valid && (h ? pr1 : pr0)) bounds[row] = bnew;
     const bool has0 = 2 * w < ntiles, has1 = 2 * w + 1 < ntiles;
     const bool act0 = has0 && !pr0, act1 = has1 && !pr1;
     if (lane == 0) {
