@@ -1,24 +1,37 @@
 #!/usr/bin/env python
 """Headline benchmark: K-Means Lloyd iterations, k=200, 100M x 50 dense fp32 (BASELINE.json).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]            # 1 GPU
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+With ``--gpus N`` (N > 1) and no launcher environment, bench.py starts N rank processes itself
+(oap_mllib_amd/parallel/launcher.py: one process per GPU, LOCAL_RANK pinning, gang kill) before
+anything touches a GPU; under ``torchrun`` / ``torch.distributed.run`` it uses the given world.
+Every rank forms the RCCL communicator; the JSON reports the world it actually formed
+(``extra.comm``, ``extra.rccl_ranks``).
 
 A "step" is one full Lloyd iteration of the distributed fit (every local row gets its exact
-assignment: exact Hamerly bounds prove most labels unchanged, a 16-byte-per-row scan lists the
+assignment: exact Hamerly bounds prove some labels unchanged, a 16-byte-per-row scan lists the
 tiles that may change, the fused MFMA assign kernel runs on those and adds the moved rows' deltas
 to the fixed-point statistics; then one RCCL allreduce of the full statistics + the finalize
 kernel + the convergence read-back; the fit's final exact-cost pass over all rows is inside the
 timed region) — nothing is skipped: tol=-1 disables the convergence exit, so exactly K
 iterations run, and the centers are bitwise those of the unpruned fit (asserted below).
+
+Data regime (the headline ``value``): synthetic Gaussian blobs whose per-cluster spread is
+comparable to the distance between cluster centers (--sigma, default 8 with centers uniform in
+[-10, 10]^50: cluster radius sqrt(50)*8 = 57, nearest center ~45-58 apart), so clusters overlap,
+the centers still move at the last timed step (``extra.max_center_shift_last``) and most tiles
+cannot be pruned (``extra.pruned_frac``).  The well-separated regime of round 1 (sigma 1: the fit
+converges in 2 iterations and later iterations are almost all pruned) is reported as
+``extra.separable_regime`` for reference only.
 Scaling is STRONG: the global dataset is 100M rows for every N, each rank generating its own
-contiguous shard directly in HBM (synthetic Gaussian blobs, identical values for any N).
+contiguous shard directly in HBM (identical values for any N).
 --config kmeans_bf16 is BASELINE config #5: k=1000, 1B x 100 bf16 (208 GB of rows on one GPU —
 the 288 GB HBM partition sizing case), same protocol.
 The timed region is bracketed by a barrier + device synchronize on both sides and the MAX over
 ranks is reported.  `value` is whole-job samples/s = global_rows * K / t.  The end-to-end fit()
-wall clock (k-means|| init + Lloyd to convergence, maxIter=20) is reported alongside.
-Other BASELINE configs: --config pca | als | kmeans_bf16 (see bench/).
+wall clock (k-means|| init + Lloyd to convergence, maxIter=20, tol=1e-4) is reported alongside.
+Other BASELINE configs: benchmarks/bench_pca.py, benchmarks/bench_als.py.
 """
 from __future__ import annotations
 
@@ -38,9 +51,27 @@ def _barrier_sync(w):
         w.barrier()
     if w.device >= 0:
         torch.cuda.set_device(w.device)  # sync (and create torch's context on) OUR GPU only
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
     if w.ctx is not None:
         w.ctx.sync()
+
+
+def _timed_fit(args, w, N, table, init, steps, prune=True):
+    _barrier_sync(w)
+    t0 = time.perf_counter()
+    r = N.kmeans_fit(w.ctx, w.comm, table, init, args.k, steps, -1.0, precise=args.precise,
+                     prune=prune)
+    _barrier_sync(w)
+    el = float(w.allreduce_np(np.array([time.perf_counter() - t0]), "max")[0])
+    assert r["num_iter"] == steps, r["num_iter"]
+    return r, el
+
+
+def _shard(args, w):
+    base, rem = divmod(args.rows, w.size)
+    local = base + (1 if w.rank < rem else 0)
+    row0 = w.rank * base + min(w.rank, rem)
+    return local, row0
 
 
 def bench_kmeans(args, w):
@@ -48,13 +79,11 @@ def bench_kmeans(args, w):
 
     N = _loader.load()
     rows_total, d, k = args.rows, args.dim, args.k
-    base, rem = divmod(rows_total, w.size)
-    local = base + (1 if w.rank < rem else 0)
-    row0 = w.rank * base + min(w.rank, rem)
+    local, row0 = _shard(args, w)
     st = args.dtype
     ld = N.kmeans_ld(d, st)
     t_ing = time.time()
-    table = N.synth_blobs(w.ctx, local, d, ld, row0, k, 10.0, 1.0, 20240917, st)
+    table = N.synth_blobs(w.ctx, local, d, ld, row0, k, args.box, args.sigma, 20240917, st)
     table.set_global(row0, rows_total)
     _barrier_sync(w)
     ingest_s = time.time() - t_ing
@@ -62,29 +91,21 @@ def bench_kmeans(args, w):
     t0 = time.time()
     init = N.kmeans_init(w.ctx, w.comm, table, k, "k-means||", 2, 7)
     init_s = time.time() - t0
-    # warmup iterations
+    # warmup iterations (same fit from the same init; results discarded)
     if args.warmup > 0:
-        N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, -1.0)
-    _barrier_sync(w)
-    t0 = time.perf_counter()
-    r = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, -1.0, precise=args.precise,
+        N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, -1.0, precise=args.precise,
                      prune=not args.no_prune)
-    _barrier_sync(w)
-    el = time.perf_counter() - t0
-    el_max = float(w.allreduce_np(np.array([el]), "max")[0])
-    assert r["num_iter"] == args.steps, r["num_iter"]
+    w.ctx.reset_metrics()
+    r, el_max = _timed_fit(args, w, N, table, init, args.steps, prune=not args.no_prune)
+    m = w.ctx.metrics()["phases"]
     # the same timed run with every distance evaluated (no bound-based pruning), for reference
     ms_unpruned = None
     if not args.no_prune and not args.precise and not args.skip_unpruned:
-        _barrier_sync(w)
-        t2 = time.perf_counter()
-        ru = N.kmeans_fit(w.ctx, w.comm, table, init, k, args.steps, -1.0, prune=False)
-        _barrier_sync(w)
-        el_u = float(w.allreduce_np(np.array([time.perf_counter() - t2]), "max")[0])
+        ru, el_u = _timed_fit(args, w, N, table, init, args.steps, prune=False)
         ms_unpruned = el_u / args.steps * 1e3
         assert np.array_equal(ru["centers"], r["centers"]), "pruning changed the result"
     # end-to-end fit(): init + Lloyd to convergence (maxIter 20, tol 1e-4)
-    fit_s = None
+    fit_s = fit_iters = None
     if not args.skip_fit:
         _barrier_sync(w)
         t1 = time.perf_counter()
@@ -92,73 +113,98 @@ def bench_kmeans(args, w):
         _barrier_sync(w)
         fit_s = float(w.allreduce_np(np.array([time.perf_counter() - t1]), "max")[0])
         fit_iters = rf["num_iter"]
-    m = w.ctx.metrics()["phases"]
     ak = m.get("kmeans/assign_kernel", {"total_us": 0, "count": 1})
     ar = m.get("kmeans/allreduce", {"total_us": 0, "count": 1})
     itr = m.get("kmeans/iteration", {"total_us": 0, "count": 1})
+    tiles = (rows_total + 31) // 32
+    pruned_g = float(w.allreduce_np(np.array([float(r.get("pruned_tiles", 0))]), "sum")[0])
     samples = rows_total * args.steps / el_max
     flops = 2.0 * rows_total * k * d
+    comm_name = getattr(w.comm, "name", "none") if w.comm is not None else "none"
+    extra = {"fit_wall_s_end_to_end": fit_s, "fit_iters": fit_iters,
+             "init_kmeans_parallel_s": init_s, "ingest_synth_s": ingest_s,
+             "data_sigma": args.sigma, "data_box": args.box,
+             # centers still move at the last timed step (Lloyd not converged)
+             "max_center_shift_last": r["shift_history"][-1],
+             "center_shift_history": [round(v, 4) for v in r["shift_history"]],
+             # share of (tile, iteration) pairs whose distance work the exact bounds skipped
+             "pruned_frac": pruned_g / (tiles * args.steps),
+             "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
+             "allreduce_us": ar["total_us"] / max(ar["count"], 1),
+             # device time of one whole iteration minus assign and allreduce: finalize,
+             # the flag/count read-back and launch gaps
+             "iteration_rest_us": (itr["total_us"] / max(itr["count"], 1)
+                                   - ak["total_us"] / max(ak["count"], 1)
+                                   - ar["total_us"] / max(ar["count"], 1)),
+             # dense-equivalent rate (2 n k d flops per iteration over the timed wall clock)
+             "dense_equiv_tflops": flops / (el_max / args.steps) / 1e12,
+             "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
+             "tier3_tiles_per_iter": r["tier3_tiles"] / max(args.steps, 1),
+             "tiles_per_pass": tiles,
+             "ms_per_step_unpruned": ms_unpruned,
+             "storage": st,
+             "comm": comm_name,
+             "rccl_ranks": w.size if comm_name == "rccl" else 0,
+             "world_size": w.size,
+             "distance_path": "fp32-exact MFMA" if args.precise else
+             ("tiered bf16 MFMA (1 product, then bf16x3 split where unsure) + exact-fp32 "
+              "refinement (assignments identical to fp32)"
+              if st == "f32" else "bf16 rows x bf16-split centroids on MFMA + exact-fp32 "
+              "refinement (assignments identical to exact fp32 on the bf16 data)"),
+             "cost": r["cost"]}
+    del table
+    if args.separable_extra and args.sigma != 1.0:
+        # round-1 regime (well-separated blobs): converges in ~2 iterations, later iterations
+        # are mostly pruned — reported for reference, NOT the headline
+        t2 = N.synth_blobs(w.ctx, local, d, ld, row0, k, args.box, 1.0, 20240917, st)
+        t2.set_global(row0, rows_total)
+        init2 = N.kmeans_init(w.ctx, w.comm, t2, k, "k-means||", 2, 7)
+        N.kmeans_fit(w.ctx, w.comm, t2, init2, k, 2, -1.0)
+        r2, el2 = _timed_fit(args, w, N, t2, init2, args.steps)
+        p2 = float(w.allreduce_np(np.array([float(r2.get("pruned_tiles", 0))]), "sum")[0])
+        extra["separable_regime"] = {
+            "data_sigma": 1.0, "samples_per_sec": rows_total * args.steps / el2,
+            "ms_per_step": el2 / args.steps * 1e3, "pruned_frac": p2 / (tiles * args.steps),
+            "max_center_shift_last": r2["shift_history"][-1]}
+        del t2
     out = {
         "metric": "kmeans_samples_per_sec", "value": samples, "unit": "samples/s",
         "n_gpus": w.size, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el_max / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "fp32" if st == "f32" else "bf16",
-        "data": "synthetic (gaussian blobs, on-device)",
+        "data": f"synthetic (overlapping gaussian blobs sigma={args.sigma}, box={args.box}, "
+                "generated on-device; random k-means|| init)",
         "config": {"model": f"kmeans k={k} d={d} (Lloyd, euclidean)", "global_batch": rows_total,
                    "seq_len": d, "parallelism": f"dp{w.size}", "k": k,
                    "rows": rows_total, "dim": d},
-        "extra": {"fit_wall_s_end_to_end": fit_s,
-                  "fit_iters": fit_iters if fit_s is not None else None,
-                  "init_kmeans_parallel_s": init_s, "ingest_synth_s": ingest_s,
-                  "init_phases_ms": {kk.split("/")[-1]: round(vv["total_us"] / 1e3, 1)
-                                     for kk, vv in m.items() if kk.startswith("kmeans/init/")},
-                  "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
-                  "allreduce_us": ar["total_us"] / max(ar["count"], 1),
-                  # device time of one whole iteration minus assign and allreduce: finalize,
-                  # the flag/count read-back and launch gaps
-                  "iteration_rest_us": (itr["total_us"] / max(itr["count"], 1)
-                                        - ak["total_us"] / max(ak["count"], 1)
-                                        - ar["total_us"] / max(ar["count"], 1)),
-                  # dense-equivalent rate (2 n k d flops per iteration over the timed wall
-                  # clock); pruning and delta accumulation skip most of that work, so this is
-                  # NOT the MFMA throughput (see ms_per_step_unpruned for the unpruned run)
-                  "dense_equiv_tflops": flops / (el_max / args.steps) / 1e12,
-                  "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
-                  "tier3_tiles_per_iter": r["tier3_tiles"] / max(args.steps, 1),
-                  # 32-row tile passes whose distance work the exact bounds skipped (pruning:
-                  # labels provably unchanged; with delta accumulation their rows are not even
-                  # read — only the 16-byte per-row bounds scan runs)
-                  "pruned_tiles_per_iter": r.get("pruned_tiles", 0) / max(args.steps, 1),
-                  "tiles_per_pass": (rows_total + 31) // 32,
-                  "ms_per_step_unpruned": ms_unpruned,
-                  "storage": st,
-                  "distance_path": "fp32-exact MFMA" if args.precise else
-                  ("tiered bf16 MFMA (1 product, then bf16x3 split where unsure) + exact-fp32 "
-                   "refinement (assignments identical to fp32)"
-                   if st == "f32" else "bf16 rows x bf16-split centroids on MFMA + exact-fp32 "
-                   "refinement (assignments identical to exact fp32 on the bf16 data)"),
-                  "cost": r["cost"]},
+        "extra": extra,
     }
     return out
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="kmeans", choices=["kmeans", "kmeans_bf16"],
                     help="kmeans: k=200, 100M x 50 f32 (headline); kmeans_bf16: k=1000, "
                     "1B x 100 bf16")
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--k", type=int, default=None)
+    ap.add_argument("--sigma", type=float, default=8.0,
+                    help="per-feature spread of the synthetic blobs (centers in [-box, box]^d)")
+    ap.add_argument("--box", type=float, default=10.0)
     ap.add_argument("--skip-fit", action="store_true")
     ap.add_argument("--no-prune", action="store_true",
                     help="evaluate every distance (disable the exact bound-based pruning)")
     ap.add_argument("--skip-unpruned", action="store_true",
                     help="do not repeat the timed run without pruning for reference")
+    ap.add_argument("--no-separable-extra", dest="separable_extra", action="store_false",
+                    help="skip the well-separated (sigma=1) reference run")
     ap.add_argument("--precise", action="store_true",
                     help="exact-fp32 MFMA distances only (no bf16-split fast path)")
     args = ap.parse_args(argv)
@@ -169,15 +215,24 @@ def main(argv=None):
     args.k = args.k or preset[2]
     args.dtype = preset[3]
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # self-launch one rank per GPU BEFORE anything initialises a GPU in this process
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location(
+            "_oap_launcher", os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                          "oap_mllib_amd", "parallel", "launcher.py"))
+        launcher = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(launcher)
+        return launcher.launch([sys.executable, os.path.abspath(__file__)] + argv, args.gpus)
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 and ws != args.gpus:
-        print(f"--gpus {args.gpus} requires a launcher with WORLD_SIZE={args.gpus} "
-              f"(python -m torch.distributed.run --nproc-per-node {args.gpus} bench.py ...)",
-              file=sys.stderr)
+    if ws != args.gpus:
+        print(f"--gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
         return 2
     import oap_mllib_amd as O
 
-    w = O.init_world(O.get_config().replace(device="gpu"))
+    dev = os.environ.get("OAP_BENCH_DEVICE", "gpu")  # "cpu": CPU-engine rehearsal (tests)
+    w = O.init_world(O.get_config().replace(device=dev))
     out = bench_kmeans(args, w)
     if w.rank == 0:
         print(json.dumps(out), flush=True)

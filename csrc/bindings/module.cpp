@@ -420,6 +420,7 @@ PYBIND11_MODULE(_native, m) {
         out["num_iter"] = r.num_iter;
         out["converged"] = r.converged;
         out["cost_history"] = r.cost_history;
+        out["shift_history"] = r.shift_history;
         out["last_counts"] = r.last_counts;
         out["init_seconds"] = r.init_seconds;
         out["iter_seconds"] = r.iter_seconds;
@@ -427,6 +428,7 @@ PYBIND11_MODULE(_native, m) {
         out["refine_tiles"] = r.refine_tiles;
         out["tier3_tiles"] = r.tier3_tiles;
         out["pruned_tiles"] = r.pruned_tiles;
+        out["deferred_rows"] = r.deferred_rows;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),
@@ -472,6 +474,8 @@ PYBIND11_MODULE(_native, m) {
         }
         return py::make_tuple(labels, dist);
       });
+  m.def("kmeans_set_lean_variant", &kmeans_set_lean_variant);
+  m.def("kmeans_last_timing_deferred", []() { return last_timing_deferred(); });
   m.def(
       "kmeans_assign_timing",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> centers,

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <limits>
@@ -235,7 +236,36 @@ struct AssignReq {
   // single launch, pruning on: delta accumulation over req.tile_list (see KMeansAssignArgs)
   bool delta = false;
   float* xnorm = nullptr;
+  // single launch, fast1: the lean tier-1 kernel + the general kernel over its deferred rows
+  // (kmeans_lloyd.hip); defer_rows / defer_count: persistent buffers (allocated per call if null)
+  bool lean = true;
+  int32_t* defer_rows = nullptr;
+  unsigned* defer_count = nullptr;
+  u64* deferred_rows = nullptr;
 };
+
+int& lean_variant_ref() {
+  static int v = [] {
+    const char* e = std::getenv("OAP_KMEANS_LEAN_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+int lean_variant() { return lean_variant_ref(); }
+
+// Whether gpu_assign takes the lean path for this request.
+bool lean_applies(const DenseTable& x, int k, int kpad, const AssignReq& req) {
+  return req.lean && req.fast1 && !req.precise && x.cols <= 128 && !req.mindist_seeded &&
+         kern::kmeans_lloyd_supported(x.cols, k, req.accumulate, req.sums_too) &&
+         kpad <= kern::kmeans_lds_kmax(x.cols, false) &&
+         !(req.bounds && req.drift && !req.delta);  // the in-kernel pruning test: general kernel
+}
+
+size_t lean_defer_bytes(int64_t rows, int num_cus, int* grid, int64_t* cap) {
+  *grid = kern::kmeans_lloyd_grid(rows, num_cus);
+  *cap = kern::kmeans_lloyd_seg_cap(rows, *grid, kern::kmeans_lloyd_waves(lean_variant()));
+  return sizeof(int32_t) * size_t(*grid) * size_t(*cap) + sizeof(unsigned) * 16 * size_t(*grid);
+}
 
 // Returns the number of cost partials written to req.cost_slab.
 int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const AssignReq& req,
@@ -270,6 +300,46 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
             "kmeans pruning needs the fast path (d <= 128) and persistent labels");
   a.xnorm = req.xnorm;
   const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
+  if (x.rows > 0 && lean_applies(x, g.k, g.kpad, req)) {
+    // ---- lean tier-1 pass, then the general kernel re-decides the deferred rows exactly
+    int grid = 0;
+    int64_t cap = 0;
+    const size_t dbytes = lean_defer_bytes(x.rows, ctx.info().cu_count, &grid, &cap);
+    Buffer dbuf;
+    int32_t* drows = req.defer_rows;
+    unsigned* dcnt = req.defer_count;
+    if (!drows) {
+      dbuf = ctx.alloc(dbytes);
+      drows = dbuf.as<int32_t>();
+      dcnt = reinterpret_cast<unsigned*>(drows + size_t(grid) * size_t(cap));
+    }
+    a.defer_rows = drows;
+    a.defer_row_count = dcnt;
+    a.row_seg_cap = cap;
+    a.deferred_rows = req.deferred_rows;
+    if (req.delta) {
+      OAP_CHECK(req.bounds && req.drift && req.tile_list && req.labels_valid,
+                "kmeans delta accumulation needs the pruning scan's tile list");
+      a.delta = true;
+      a.tile_list = req.tile_list;
+      a.tile_count = req.tile_count;
+    }
+    kern::kmeans_lloyd(a, grid, lean_variant(), s);
+    kern::KMeansAssignArgs b = a;
+    b.defer_rows = nullptr;
+    b.defer_row_count = nullptr;
+    b.deferred_rows = nullptr;
+    b.row_list = drows;
+    b.row_count = dcnt;
+    b.row_subs = kern::kmeans_lloyd_waves(lean_variant());
+    b.fast1 = false;  // deferred rows are near ties at tier 1: start at the bf16x3 split
+    b.tile_list = nullptr;
+    b.tile_count = nullptr;
+    b.xnorm = nullptr;
+    b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
+    kern::kmeans_assign_rows(b, grid, s);
+    return a.cost_slab ? 2 * grid : 0;
+  }
   if (x.cols > 128 || g.kpad <= kmax || kmax == 0) {
     if (req.delta) {
       OAP_CHECK(req.bounds && req.drift && req.tile_list && req.labels_valid,
@@ -827,6 +897,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         host_allreduce(ctx, comm, &cost, 1, DType::F64, ReduceOp::Sum);
       }
       bool conv = true;
+      double max_sh = 0.0;
       for (int c = 0; c < k; ++c) {
         int64_t cnt = stats[kd + c];
         if (cnt <= 0) continue;
@@ -838,9 +909,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           centers[size_t(c) * d + f] = nv;
         }
         if (sh > p.tol * p.tol) conv = false;
+        max_sh = std::max(max_sh, sh);
       }
       res.cost = cost;
       res.cost_history.push_back(cost);
+      res.shift_history.push_back(std::sqrt(max_sh));
       res.last_counts.assign(stats.begin() + kd, stats.end());
       res.num_iter = it + 1;
       if (conv && p.tol >= 0) {  // tol < 0: run exactly max_iter iterations
@@ -936,6 +1009,26 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   unsigned* dcount =
       delta ? reinterpret_cast<unsigned*>(dlist_b.as<char>() + sizeof(int32_t) * ((x.rows + 31) / 32))
             : nullptr;
+  // lean tier-1 path: persistent deferral list + a counter of deferred rows (adaptive tier)
+  Buffer ldefer_b, ldstat_b, ldstat_h;
+  if (x.rows > 0 && lean_applies(x, k, g.kpad, req)) {
+    int lg = 0;
+    int64_t lcap = 0;
+    ldefer_b = ctx.alloc(lean_defer_bytes(x.rows, ctx.info().cu_count, &lg, &lcap));
+    req.defer_rows = ldefer_b.as<int32_t>();
+    req.defer_count = reinterpret_cast<unsigned*>(req.defer_rows + size_t(lg) * size_t(lcap));
+    ldstat_b = ctx.alloc(sizeof(u64));
+    ldstat_h = ctx.alloc_pinned(sizeof(u64));
+    ctx.memset(ldstat_b.data(), 0, sizeof(u64), s);
+    req.deferred_rows = ldstat_b.as<u64>();
+  }
+  u64 deferred_seen = 0;
+  // adaptive delta: when the scan prunes few tiles (overlapping clusters), its pass and the
+  // delta bookkeeping cost more than they save — run full passes (which refresh labels and
+  // bounds) and probe the scan again every few iterations
+  bool delta_on = true;
+  int delta_probe = 0;
+  u64 pruned_seen = 0;
 
   kern::KMeansFinalizeArgs fa;
   fa.sums = sums;
@@ -979,15 +1072,18 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       maybe_inject_fault(comm.rank(), "kmeans_iter", it);
       roctx_push("kmeans/iteration");
       ev[b].e0.record(s);
-      if (!delta || it == 0)
+      const bool delta_it = delta && it > 0 && delta_on;
+      if (!delta_it)
         OAP_HIP_CHECK(hipMemsetAsync(delta ? loc_b.data() : stats.data(), 0,
                                      sizeof(u64) * (kd + k), s));
       req.labels_valid = it > 0;
       if (prune) {
-        req.drift = it > 0 ? drift_b.as<float>() : nullptr;
-        req.drift_max = it > 0 ? drift_b.as<float>() + k : nullptr;
+        // a full pass of the delta path refreshes labels and bounds without the pruning test
+        const bool drift_in = it > 0 && (!delta || delta_it);
+        req.drift = drift_in ? drift_b.as<float>() : nullptr;
+        req.drift_max = drift_in ? drift_b.as<float>() + k : nullptr;
       }
-      req.delta = delta && it > 0;
+      req.delta = delta_it;
       if (req.delta) {
         OAP_HIP_CHECK(hipMemsetAsync(dcount, 0, sizeof(unsigned), s));
         kern::kmeans_prune_scan(x.rows, k, d, req.bounds, req.labels, req.xnorm, req.drift,
@@ -1034,6 +1130,13 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         hipMemcpyAsync(counts_h.data(), counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
+    if (ldstat_b.data())
+      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), sizeof(u64),
+                                   hipMemcpyDeviceToHost, s));
+    u64 pruned_now = 0;
+    if (delta)
+      OAP_HIP_CHECK(hipMemcpyAsync(&pruned_now, pruned_d.data(), sizeof(u64),
+                                   hipMemcpyDeviceToHost, s));
     comm.wait(s);
     for (int b = 0; b < nb_it; ++b) {
       const int it = it0 + b;
@@ -1056,6 +1159,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           (delta_all && it > 0) ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
       res.cost = c_it;
       res.cost_history.push_back(c_it);
+      res.shift_history.push_back(std::sqrt(std::max(fl.max_shift2, 0.0)));
       res.num_iter = it + 1;
       if (fl.converged && p.tol >= 0) {  // (B == 1 here: nothing was enqueued past it)
         res.converged = true;
@@ -1072,6 +1176,35 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                "\"iter\":" + std::to_string(res.num_iter - 1));
       }
       tier2_seen = t2;
+      if (ldstat_b.data()) {  // lean path: deferral rate (a near-tie share this high means
+        // the bf16x3 tier pays from the start)
+        const u64 dr = ldstat_h.as<u64>()[0];
+        if (req.fast1 && double(dr - deferred_seen) > 0.25 * double(x.rows) * nb_it) {
+          req.fast1 = false;
+          Logger::instance().log(LogLevel::Info, "kmeans/lean_off",
+                                 "\"iter\":" + std::to_string(res.num_iter - 1));
+        }
+        deferred_seen = dr;
+      }
+    }
+    if (delta_all && !stop) {  // adaptive delta (decided per batch from the scan's pruned
+      // share); rank-uniform: ranks see the same drift but their own rows, so the smallest
+      // local share decides (a rank without rows reports 1)
+      double frac = 0.0;
+      const int delta_iters = delta_on ? nb_it - (it0 == 0 ? 1 : 0) : 0;
+      if (delta_iters > 0) {
+        frac = delta ? double(pruned_now - pruned_seen) /
+                           (double((x.rows + 31) / 32) * delta_iters + 1e-9)
+                     : 1.0;
+        frac = comm_allreduce_scalar(ctx, comm, frac, ReduceOp::Min);
+      }
+      pruned_seen = pruned_now;
+      if (delta_on && delta_iters > 0 && frac < 0.2) {
+        delta_on = false;
+        delta_probe = 0;
+      } else if (!delta_on && ++delta_probe >= (B == 1 ? 4 : 1)) {
+        delta_on = true;  // probe: the centers may have settled
+      }
     }
   }
   if (delta_all && res.num_iter > 1) {
@@ -1118,6 +1251,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     u64 pt = 0;
     ctx.copy_to_host(&pt, pruned_d.data(), sizeof(u64), s);
     res.pruned_tiles = static_cast<int64_t>(pt);
+  }
+  if (ldstat_b.data()) {
+    u64 dr = 0;
+    ctx.copy_to_host(&dr, ldstat_b.data(), sizeof(u64), s);
+    res.deferred_rows = static_cast<int64_t>(dr);
   }
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
@@ -1174,6 +1312,13 @@ void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>
 
 namespace oap {
 
+void kmeans_set_lean_variant(int v) { lean_variant_ref() = v; }
+
+double& last_timing_deferred() {
+  static double v = 0.0;
+  return v;
+}
+
 double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
                             int k, int reps, bool precise, int ablate) {
   OAP_CHECK(ctx.is_gpu(), "kmeans_assign_timing needs a GPU context");
@@ -1209,6 +1354,30 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
   a.ablate = ablate;
   hipStream_t s = ctx.compute();
   Event e0, e1;
+  if (ablate & 64) {  // the Lloyd fit's path: lean tier-1 pass + exact re-decision of its rows
+    AssignReq req;
+    req.accumulate = !(ablate & 1);
+    req.scale = scale.as<float>();
+    req.sums = a.sums;
+    req.counts = a.counts;
+    req.cost_slab = a.cost_slab;
+    req.fast1 = true;
+    Buffer dr = ctx.alloc(sizeof(u64));
+    ctx.memset(dr.data(), 0, sizeof(u64), s);
+    req.deferred_rows = dr.as<u64>();
+    OAP_CHECK(lean_applies(x, k, g.kpad, req), "lean path not applicable");
+    gpu_assign(ctx, x, g, req, s);  // warm
+    e0.record(s);
+    for (int i = 0; i < reps; ++i) gpu_assign(ctx, x, g, req, s);
+    e1.record(s);
+    e1.sync();
+    u64 n_def = 0;
+    ctx.copy_to_host(&n_def, dr.data(), sizeof(u64));
+    Logger::instance().log(LogLevel::Info, "kmeans/timing_deferred",
+                           "\"rows_per_pass\":" + std::to_string(double(n_def) / (reps + 1)));
+    last_timing_deferred() = double(n_def) / (reps + 1);
+    return Event::elapsed_ms(e0, e1) / std::max(reps, 1);
+  }
   kern::kmeans_assign(a, ctx.info().cu_count, s);  // warm
   e0.record(s);
   for (int i = 0; i < reps; ++i) kern::kmeans_assign(a, ctx.info().cu_count, s);

@@ -49,6 +49,8 @@ struct KMeansResult {
   int num_iter = 0;
   bool converged = false;
   std::vector<double> cost_history;
+  // per iteration: the largest center movement |c_new - c_old| (Euclidean) of that update
+  std::vector<double> shift_history;
   std::vector<int64_t> last_counts;  // cluster sizes of the last assignment step
   double init_seconds = 0.0;
   double iter_seconds = 0.0;
@@ -56,6 +58,7 @@ struct KMeansResult {
   int64_t refine_tiles = 0;  // 32-row tiles re-decided by the exact pass (GPU fast path)
   int64_t tier3_tiles = 0;   // 32-row tiles whose tier-1 (one bf16 product) answer was unsure
   int64_t pruned_tiles = 0;  // 32-row tile passes whose distance work the bounds skipped
+  int64_t deferred_rows = 0;  // rows the lean tier-1 pass left to the exact re-decision
 };
 
 // Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for
@@ -79,6 +82,10 @@ void kmeans_predict_device(Context& ctx, const DenseTable& x, const std::vector<
 // ablations (kern::KMeansAssignArgs::ablate) — the per-phase cost breakdown used for tuning.
 double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
                             int k, int reps, bool precise, int ablate);
+// Workgroup shape of the lean tier-1 kernel (tuning; default from OAP_KMEANS_LEAN_VARIANT).
+void kmeans_set_lean_variant(int v);
+// Deferred rows per pass of the last lean-path timing (ablate bit 64).
+double& last_timing_deferred();
 
 // k-means++ over weighted candidates, then up to max_iter weighted Lloyd iterations (host,
 // elementwise loops on `pool` when given; identical results for any pool size).

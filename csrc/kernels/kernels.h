@@ -105,7 +105,37 @@ struct KMeansAssignArgs {
   // optional [ceil(n/32)]: per 32-row tile, the largest |x|^2 as the assign kernel computes it
   // (the scan's pruning margin)
   float* xnorm = nullptr;
+  // Row-list (refine) mode of the general kernel: the rows to process are the entries of this
+  // workgroup's segment of row_list ([grid][row_seg_cap], count row_count[blockIdx.x]), taken 32
+  // at a time — the rows the lean tier-1 kernel deferred.  No pruning test; delta reads each
+  // row's previous label.
+  const int32_t* row_list = nullptr;
+  const unsigned* row_count = nullptr;  // [grid][16]: rows per sub-segment
+  int64_t row_seg_cap = 0;
+  int row_subs = 1;  // sub-segments per workgroup segment (each row_seg_cap / row_subs long)
+  // Lean tier-1 kernel output: rows whose tier-1 top-2 gap is inside the tier's error bound are
+  // appended to this workgroup's segment ([grid][row_seg_cap], count defer_row_count[block]).
+  int32_t* defer_rows = nullptr;
+  unsigned* defer_row_count = nullptr;
+  unsigned long long* deferred_rows = nullptr;  // optional counter of deferred rows
 };
+// Lean tier-1 Lloyd kernel (kmeans_lloyd.hip): applicable when the centroid hi plane + the
+// fixed-point accumulator fit LDS and d + 4 bias features fit the padded width.
+bool kmeans_lloyd_supported(int d, int k, bool accumulate, bool sums_too);
+int kmeans_lloyd_grid(int64_t n, int num_cus);
+// Waves per workgroup of a lean-kernel variant; per-workgroup capacity of its deferral list
+// (rows; `waves` sub-segments of seg_cap / waves each, counts [grid][16]).
+int kmeans_lloyd_waves(int variant);
+int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves);
+// One pass: rows whose tier-1 answer is sure are finished (labels / mindist / bounds / cost /
+// fixed-point statistics, delta mode over tile_list); the others go to a.defer_rows.  variant
+// selects the workgroup shape (0: 16 waves; tuning: 1-3).  Writes `grid`
+// cost partials.
+int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s);
+// The general fused kernel over the rows kmeans_lloyd deferred (a.row_list / row_count /
+// row_seg_cap from its defer outputs), on the same `grid`.
+void kmeans_assign_rows(const KMeansAssignArgs& a, int grid, hipStream_t s);
+
 // Delta-mode pruning scan (single launch): per 32-row tile, tests every row's bounds (labels,
 // xnorm, the centers' drift) exactly as the assign kernel's own pruning test does.  Tiles that
 // provably keep all labels get their bounds advanced in place (u + drift, l - max drift, rounded

@@ -615,6 +615,14 @@ int kmeans_assign(const KMeansAssignArgs& a, int num_cus, hipStream_t s) {
   return grid;
 }
 
+void kmeans_assign_rows(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  OAP_CHECK(a.row_list && a.row_count && a.row_seg_cap > 0 && !a.merge && !a.precise &&
+                a.d <= 128 && a.kpad <= kmeans_mfma_kmax(a.d, false) && !a.tile_list,
+            "kmeans_assign_rows: unsupported arguments");
+  if (a.n == 0) return;
+  launch_kmeans_assign_mfma(a, grid, s);
+}
+
 void kmeans_seed_mindist(const KMeansAssignArgs& a, hipStream_t s) {
   launch_kmeans_seed_mindist(a, s);
 }

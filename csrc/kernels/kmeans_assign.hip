@@ -44,6 +44,7 @@
 #include <type_traits>
 
 #include "kernels/device_utils.h"
+#include "kernels/kmeans_frag.h"
 #include "kernels/kmeans_internal.h"
 
 namespace oap {
@@ -51,15 +52,13 @@ namespace kern {
 
 namespace {
 
+using namespace kmdev;
+
 constexpr int kThreads = kAssignThreads;
 constexpr int kWaves = kThreads / 64;
 
-__host__ __device__ inline size_t round16(size_t v) { return (v + 15) / 16 * 16; }
-__host__ __device__ inline int stride_bf16(int dp) { return dp + 8; }  // (dp+8)/8 odd slots
-__host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)/4 odd slots
-
 struct Smem {
-  size_t planes, cn, dr, sc, acc, cnt, wcost, total;
+  size_t planes, cn, dr, sc, acc, cnt, wcost, pref, total;
 };
 // lds_acc: LDS counters (+ the fp64 fixed-point sum accumulator when lds_sums).
 __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool precise,
@@ -84,6 +83,9 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
   off = round16(off);
   m.wcost = off;
   off += kWaves * 8;
+  off = round16(off);
+  m.pref = off;  // row-list mode: sub-segment prefix sums
+  off += (kDeferSubs + 1) * 4;
   m.total = round16(off);
   return m;
 }
@@ -93,85 +95,6 @@ __host__ __device__ inline Smem smem_plan(int dp, int kpad, int k, int d, bool p
 __host__ __device__ inline int64_t defer_segment(int64_t ntiles, int64_t grid) {
   const int64_t stride = grid * kWaves;
   return (ntiles + stride - 1) / stride * kWaves;
-}
-
-__device__ inline int med3_i32(int a, int b, int c) {
-  int r;
-  asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-// The lane's slice of one 32-row tile: features f = 16s + 8h + j (s < KS, j < 8) of row r.
-// f32 tables keep the fp32 values; bf16 tables keep the raw bf16 vectors, which are already
-// the MFMA B operand (and exact: bf16 -> fp32 is a shift).
-template <int KS, bool XB>
-struct Frag;
-template <int KS>
-struct Frag<KS, false> {
-  float v[KS][8];
-  __device__ float at(int s, int j) const { return v[s][j]; }
-};
-template <int KS>
-struct Frag<KS, true> {
-  bf16x8 v[KS];
-  __device__ float at(int s, int j) const { return static_cast<float>(v[s][j]); }
-};
-
-// Exact fp32 argmin over kpad centroids for the lane's row (both halves get the result).
-template <int KS, class F>
-__device__ inline void exact_argmin(const float* __restrict__ cbase, int stride, const F& x,
-                                    const float* __restrict__ cn, int kpad, int d, int r, int h,
-                                    int& bidx) {
-  float best = INFINITY;
-  bidx = 0x7fffffff;
-  for (int c0 = 0; c0 < kpad; c0 += 32) {
-    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    const float* cp = cbase + size_t(c0 + r) * stride + 8 * h;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (16 * s + 4 * q < d) {  // wave-uniform: skip all-padding groups
-          float4 a4 = *reinterpret_cast<const float4*>(cp + 16 * s + 4 * q);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, x.at(s, 4 * q + 0), acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, x.at(s, 4 * q + 1), acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, x.at(s, 4 * q + 2), acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, x.at(s, 4 * q + 3), acc, 0, 0, 0);
-        }
-      }
-    }
-    // accumulator element 4g+q <-> centroid c0 + 8g + 4h + q, data row r
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
-      float cv[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float dist = fmaf(-2.f, acc[4 * g + q], cv[q]);
-        if (dist < best) {
-          best = dist;
-          bidx = c0 + 8 * g + 4 * h + q;
-        }
-      }
-    }
-  }
-  float ob = __shfl_xor(best, 32, 64);
-  int oi = __shfl_xor(bidx, 32, 64);
-  if (ob < best || (ob == best && oi < bidx)) bidx = oi;
-}
-
-template <int KS>
-__device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8]) {
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      float4 v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
-      dst[s][4 * q + 0] = v.x;
-      dst[s][4 * q + 1] = v.y;
-      dst[s][4 * q + 2] = v.z;
-      dst[s][4 * q + 3] = v.w;
-    }
 }
 
 // BIAS (fast path): padding features carry the norms through the MFMAs so accumulators start at
@@ -228,9 +151,18 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   for (int c = tid; c < kpad; c += kThreads) cn[c] = (c < k) ? a.cnorm[c] : 1e30f;
   // Pruning (see the header): single launches test each row's bounds against the drift of its
   // own center; chunked passes only read the seed pass's per-row verdict.
-  const bool prune_single = !PRECISE && a.bounds && a.drift && !a.merge;
+  // row-list (refine) mode: this workgroup's segment of deferred rows, 32 per position
+  const int32_t* rlist = a.row_list ? a.row_list + blockIdx.x * a.row_seg_cap : nullptr;
+  unsigned* s_pref = reinterpret_cast<unsigned*>(smem + L.pref);
+  if (rlist && tid == 0) {
+    s_pref[0] = 0u;
+    for (int w = 0; w < a.row_subs; ++w)
+      s_pref[w + 1] = s_pref[w] + a.row_count[blockIdx.x * kDeferSubs + w];
+  }
+  const bool prune_single = !PRECISE && a.bounds && a.drift && !a.merge && !rlist;
   const bool prune_merge = !PRECISE && a.bounds && a.drift && a.merge;
-  const bool need_meta = !PRECISE && a.bounds && (a.drift || a.merge);
+  const bool need_meta =
+      (!PRECISE && a.bounds && (a.drift || a.merge) && !rlist) || (rlist && a.delta);
   if (prune_single)
     for (int c = tid; c < kpad; c += kThreads) dr_l[c] = (c < k) ? a.drift[a.base + c] : 0.f;
   for (int f = tid; f < DP; f += kThreads)
@@ -244,6 +176,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  const int64_t rcnt = rlist ? int64_t(s_pref[a.row_subs]) : 0;
+  const int64_t rsub = rlist ? a.row_seg_cap / a.row_subs : 0;
   float thr1 = 0.f, thr0 = 0.f, cmax = 0.f;
   if constexpr (!PRECISE) {
     cmax = a.cstat ? a.cstat[0] : 0.f;
@@ -372,11 +306,27 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   // seg_list — this workgroup's own segment of a deferral list (see defer_list below).
   const int64_t seg_cap = defer_segment(ntiles_all, gridDim.x);
   const int32_t* list = a.tile_list ? a.tile_list + (a.seg_list ? blockIdx.x * seg_cap : 0) : nullptr;
-  const int64_t ntiles = !a.tile_list  ? ntiles_all
-                         : a.seg_list ? int64_t(a.tile_count[blockIdx.x])
-                                      : int64_t(*a.tile_count);
-  const int64_t stride = a.seg_list ? int64_t(kWaves) : int64_t(gridDim.x) * kWaves;
-  int64_t t = a.seg_list ? int64_t(wave) : int64_t(blockIdx.x) * kWaves + wave;
+  const int64_t ntiles = rlist         ? (rcnt + 31) / 32
+                         : !a.tile_list ? ntiles_all
+                         : a.seg_list  ? int64_t(a.tile_count[blockIdx.x])
+                                       : int64_t(*a.tile_count);
+  const bool local_seg = a.seg_list || rlist;
+  const int64_t stride = local_seg ? int64_t(kWaves) : int64_t(gridDim.x) * kWaves;
+  int64_t t = local_seg ? int64_t(wave) : int64_t(blockIdx.x) * kWaves + wave;
+  // the row a lane works on at position tt (clamped to a real row; valid_of tells if it counts)
+  auto row_of = [&](int64_t tt) -> int64_t {
+    if (rlist) {  // (an empty segment still prefetches: row 0 is a real row)
+      if (rcnt == 0) return int64_t(0);
+      int64_t i = tt * 32 + r;
+      i = i < rcnt ? i : rcnt - 1;
+      int w = 0;
+      while (w + 1 < a.row_subs && int64_t(s_pref[w + 1]) <= i) ++w;
+      return int64_t(rlist[w * rsub + (i - int64_t(s_pref[w]))]);
+    }
+    const int64_t row = tt * 32 + r;
+    return row < a.n ? row : a.n - 1;
+  };
+  auto valid_of = [&](int64_t tt) { return rlist ? tt * 32 + r < rcnt : tt * 32 + r < a.n; };
   auto tile_of = [&](int64_t q) -> int64_t {
     if (!list) return q;  // (past the end: load_tile clamps the rows)
     return q < ntiles ? int64_t(list[q]) : ntiles_all - 1;
@@ -392,8 +342,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   // Rows past n are clamped to row n-1 (their results are discarded, nothing needs zeroing);
   // only the last k-step can reach past the row stride, and it is zero-filled there.
   auto load_tile = [&](int64_t tt, F& dst) {
-    int64_t row = tt * 32 + r;
-    row = row < a.n ? row : a.n - 1;
+    const int64_t row = row_of(tt);
     if constexpr (XB) {
       const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
 #pragma unroll
@@ -431,12 +380,13 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   };
   auto load_meta = [&](int64_t tt, Meta& m) {
     if (!need_meta) return;
-    int64_t row = tt * 32 + r;
-    row = row < a.n ? row : a.n - 1;
-    const float2 b = reinterpret_cast<const float2*>(a.bounds)[row];
-    m.bx = b.x;
-    m.by = b.y;
-    if (prune_single) m.lab = a.labels[row];
+    const int64_t row = row_of(tt);
+    if (!rlist) {
+      const float2 b = reinterpret_cast<const float2*>(a.bounds)[row];
+      m.bx = b.x;
+      m.by = b.y;
+    }
+    if (prune_single || rlist) m.lab = a.labels[row];
   };
 
   // One tile: `x` holds its rows, `xn` receives the prefetch of tile `pf`.  DEEP: pf is two
@@ -445,8 +395,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   // two tile-times to land.  Otherwise pf is the next tile, issued before the MFMAs.  The loops
   // below rotate named buffers, so no register copies are needed.
   auto process = [&](const int64_t t, F& x, F& xn, const Meta& m, Meta& mn, const int64_t pf) {
-    const int64_t row = t * 32 + r;
-    const bool valid = row < a.n;
+    const int64_t row = row_of(t);
+    const bool valid = valid_of(t);
     int bidx;
     if constexpr (PRECISE) {
       load_tile(pf, xn);  // prefetch, hidden behind this tile's MFMAs
@@ -479,7 +429,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += __shfl_xor(nx2, 32, 64);
-      if (a.xnorm) {  // per-tile max |x|^2 (the scan's margin: conservative for every row)
+      if (a.xnorm && !rlist) {  // per-tile max |x|^2 (the scan's margin: conservative for every row)
         float tmax = nx2;
 #pragma unroll
         for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));

@@ -1,0 +1,100 @@
+// Device helpers shared by the K-Means assign kernels (kmeans_assign.hip: the general fused
+// kernel; kmeans_lloyd.hip: the lean tier-1 Lloyd kernel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels/device_utils.h"
+
+namespace oap {
+namespace kern {
+namespace kmdev {
+
+__host__ __device__ inline size_t round16(size_t v) { return (v + 15) / 16 * 16; }
+__host__ __device__ inline int stride_bf16(int dp) { return dp + 8; }  // (dp+8)/8 odd slots
+__host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)/4 odd slots
+
+__device__ inline int med3_i32(int a, int b, int c) {
+  int r;
+  asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// The lane's slice of one 32-row tile: features f = 16s + 8h + j (s < KS, j < 8) of row r.
+// f32 tables keep the fp32 values; bf16 tables keep the raw bf16 vectors, which are already
+// the MFMA B operand (and exact: bf16 -> fp32 is a shift).
+template <int KS, bool XB>
+struct Frag;
+template <int KS>
+struct Frag<KS, false> {
+  float v[KS][8];
+  __device__ float at(int s, int j) const { return v[s][j]; }
+};
+template <int KS>
+struct Frag<KS, true> {
+  bf16x8 v[KS];
+  __device__ float at(int s, int j) const { return static_cast<float>(v[s][j]); }
+};
+
+// Exact fp32 argmin over kpad centroids for the lane's row (both halves get the result).
+template <int KS, class F>
+__device__ inline void exact_argmin(const float* __restrict__ cbase, int stride, const F& x,
+                                    const float* __restrict__ cn, int kpad, int d, int r, int h,
+                                    int& bidx) {
+  float best = INFINITY;
+  bidx = 0x7fffffff;
+  for (int c0 = 0; c0 < kpad; c0 += 32) {
+    f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* cp = cbase + size_t(c0 + r) * stride + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (16 * s + 4 * q < d) {  // wave-uniform: skip all-padding groups
+          float4 a4 = *reinterpret_cast<const float4*>(cp + 16 * s + 4 * q);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, x.at(s, 4 * q + 0), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, x.at(s, 4 * q + 1), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, x.at(s, 4 * q + 2), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, x.at(s, 4 * q + 3), acc, 0, 0, 0);
+        }
+      }
+    }
+    // accumulator element 4g+q <-> centroid c0 + 8g + 4h + q, data row r
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * g + 4 * h);
+      float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float dist = fmaf(-2.f, acc[4 * g + q], cv[q]);
+        if (dist < best) {
+          best = dist;
+          bidx = c0 + 8 * g + 4 * h + q;
+        }
+      }
+    }
+  }
+  float ob = __shfl_xor(best, 32, 64);
+  int oi = __shfl_xor(bidx, 32, 64);
+  if (ob < best || (ob == best && oi < bidx)) bidx = oi;
+}
+
+template <int KS>
+__device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8]) {
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      float4 v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+      dst[s][4 * q + 0] = v.x;
+      dst[s][4 * q + 1] = v.y;
+      dst[s][4 * q + 2] = v.z;
+      dst[s][4 * q + 3] = v.w;
+    }
+}
+
+}  // namespace kmdev
+}  // namespace kern
+}  // namespace oap

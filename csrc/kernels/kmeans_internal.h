@@ -8,6 +8,8 @@ namespace kern {
 
 constexpr int kAssignThreads = 512;  // 8 waves: 2 per SIMD with one workgroup per CU
 constexpr size_t kLdsLimit = 160 * 1024;
+// Deferral sub-segments per workgroup (one per wave of the lean kernel; count stride)
+constexpr int kDeferSubs = 16;
 
 // Launches the MFMA assign kernel (d <= 128, centroids fit the LDS plan).  `grid` blocks.
 void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s);

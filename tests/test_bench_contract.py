@@ -1,6 +1,8 @@
-"""bench.py's driver contract on the CPU: presets, argument handling, refusal without a launcher."""
+"""bench.py's driver contract on the CPU: presets, argument handling, the self-launch of N ranks."""
 import importlib.util
+import json
 import os
+import subprocess
 import sys
 
 import pytest
@@ -15,10 +17,45 @@ def _bench():
     return mod
 
 
-def test_multi_gpu_without_launcher_is_refused(monkeypatch, capsys):
-    monkeypatch.delenv("WORLD_SIZE", raising=False)
+def test_world_size_mismatch_is_refused(monkeypatch, capsys):
+    monkeypatch.setenv("WORLD_SIZE", "3")
     assert _bench().main(["--gpus", "2"]) == 2
-    assert "torch.distributed.run" in capsys.readouterr().err
+    assert "WORLD_SIZE=3" in capsys.readouterr().err
+
+
+def _run_bench(args, extra_env=None):
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    env.update(OAP_BENCH_DEVICE="cpu", MASTER_ADDR="127.0.0.1")
+    env.update(extra_env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only prints
+    return json.loads(lines[0])
+
+
+SMALL = ["--rows", "6000", "--dim", "8", "--k", "5", "--steps", "3", "--warmup", "1",
+         "--skip-fit", "--box", "4", "--sigma", "3"]
+
+
+def test_self_launch_two_ranks_cpu():
+    """`bench.py --gpus 2` with no launcher environment starts its own 2-rank world (the driver's
+    8-GPU sweep path), every rank joins the collectives, rank 0 prints one JSON line."""
+    one = _run_bench(["--gpus", "1"] + SMALL)
+    two = _run_bench(["--gpus", "2"] + SMALL)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["extra"]["world_size"] == 2 and two["config"]["parallelism"] == "dp2"
+    assert two["steps"] == 3 and two["warmup"] == 1 and two["scaling"] == "strong"
+    # strong scaling over identical global data: same fit for any world size
+    assert one["extra"]["cost"] == two["extra"]["cost"]
+    assert one["extra"]["center_shift_history"] == two["extra"]["center_shift_history"]
+    assert two["extra"]["max_center_shift_last"] > 0  # overlapping blobs: centers still move
+    for key in ("metric", "value", "unit", "ms_per_step", "higher_is_better", "vs_baseline",
+                "dtype", "data", "config"):
+        assert key in two
 
 
 def test_presets_match_baseline_configs(monkeypatch):
