@@ -2,6 +2,8 @@
 // entry point catches, stores the message in a thread-local buffer and returns a negative code.
 #include "capi/oap_capi.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -233,5 +235,91 @@ const float* oap_als_result_factors(const oap_als_result* res, int which) {
 }
 
 void oap_als_result_free(oap_als_result* res) { delete res; }
+
+int oap_shuffle_ratings(oap_ctx* c, const void* records, int64_t n, int64_t n_total_keys,
+                        int n_blocks, void** out, int64_t* out_n, int64_t* out_distinct) {
+  return guarded([&] {
+    OAP_CHECK(c && c->ctx && c->comm && out && out_n && out_distinct, "null argument");
+    OAP_CHECK(n == 0 || records, "null record buffer");
+    const int P = c->comm->size();
+    OAP_CHECK(n_blocks == P, "n_blocks " << n_blocks << " != world size " << P);
+    constexpr size_t kRec = 20;
+    const int64_t per = std::max<int64_t>(n_total_keys / n_blocks, 1);
+    const auto* rec = static_cast<const unsigned char*>(records);
+    auto key_of = [&](const unsigned char* r) {
+      int64_t k;
+      std::memcpy(&k, r, 8);
+      return k;
+    };
+    std::vector<size_t> send_cnt(P, 0), recv_cnt(P, 0);
+    std::vector<int> dest(size_t(std::max<int64_t>(n, 0)));
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t k = key_of(rec + kRec * i);
+      OAP_CHECK(k >= 0, "negative rating key " << k);
+      dest[i] = int(std::min<int64_t>(k / per, P - 1));
+      ++send_cnt[dest[i]];
+    }
+    std::vector<size_t> off(P + 1, 0);
+    for (int q = 0; q < P; ++q) off[q + 1] = off[q] + send_cnt[q];
+    std::vector<unsigned char> sendbuf(size_t(n) * kRec);
+    {
+      std::vector<size_t> pos(off.begin(), off.end() - 1);
+      for (int64_t i = 0; i < n; ++i)
+        std::memcpy(&sendbuf[kRec * pos[dest[i]]++], rec + kRec * i, kRec);
+    }
+    // counts: one int64 per peer
+    std::vector<int64_t> sc(P), rc(P);
+    for (int q = 0; q < P; ++q) sc[q] = int64_t(send_cnt[q]);
+    oap::comm_alltoallv_host(*c->ctx, *c->comm, sc.data(), std::vector<size_t>(P, 1), rc.data(),
+                             std::vector<size_t>(P, 1), oap::DType::I64);
+    size_t rn = 0;
+    for (int q = 0; q < P; ++q) {
+      recv_cnt[q] = size_t(rc[q]);
+      rn += recv_cnt[q];
+    }
+    std::vector<size_t> sb(P), rb(P);
+    for (int q = 0; q < P; ++q) {
+      sb[q] = send_cnt[q] * kRec;
+      rb[q] = recv_cnt[q] * kRec;
+    }
+    auto* buf = static_cast<unsigned char*>(std::malloc(std::max<size_t>(rn * kRec, 1)));
+    OAP_CHECK(buf, "out of host memory");
+    oap::comm_alltoallv_host(*c->ctx, *c->comm, sendbuf.data(), sb, buf, rb, oap::DType::U8);
+    // sort by (key, other), then count distinct keys (ALSShuffle.cpp:111,121)
+    std::vector<std::pair<std::pair<int64_t, int64_t>, size_t>> order(rn);
+    for (size_t i = 0; i < rn; ++i) {
+      int64_t k, o;
+      std::memcpy(&k, buf + kRec * i, 8);
+      std::memcpy(&o, buf + kRec * i + 8, 8);
+      order[i] = {{k, o}, i};
+    }
+    std::sort(order.begin(), order.end());
+    auto* sorted = static_cast<unsigned char*>(std::malloc(std::max<size_t>(rn * kRec, 1)));
+    if (!sorted) {
+      std::free(buf);
+      OAP_THROW(oap::Error, "out of host memory");
+    }
+    int64_t distinct = 0;
+    for (size_t i = 0; i < rn; ++i) {
+      std::memcpy(sorted + kRec * i, buf + kRec * order[i].second, kRec);
+      if (i == 0 || order[i].first.first != order[i - 1].first.first) ++distinct;
+    }
+    std::free(buf);
+    *out = sorted;
+    *out_n = int64_t(rn);
+    *out_distinct = distinct;
+  });
+}
+
+int oap_allreduce_i64(oap_ctx* c, int64_t* vals, int count, int op) {
+  return guarded([&] {
+    OAP_CHECK(c && c->ctx && c->comm && (vals || count == 0), "null argument");
+    const oap::ReduceOp o =
+        op == 1 ? oap::ReduceOp::Max : op == 2 ? oap::ReduceOp::Min : oap::ReduceOp::Sum;
+    oap::comm_allreduce_host(*c->ctx, *c->comm, vals, size_t(count), oap::DType::I64, o);
+  });
+}
+
+void oap_free(void* p) { std::free(p); }
 
 }  // extern "C"

@@ -84,6 +84,19 @@ OAP_API const int32_t* oap_als_result_ids(const oap_als_result* res, int which);
 OAP_API const float* oap_als_result_factors(const oap_als_result* res, int which);
 OAP_API void oap_als_result_free(oap_als_result* res);
 
+/* The reference's ratings shuffle (ALSShuffle.cpp:62-127 behind cShuffleData): records are
+ * packed 20-byte little-endian {int64 key; int64 other; float rating}; each goes to rank
+ * min(key / max(n_total_keys / n_blocks, 1), n_blocks - 1) (n_blocks == world size).  *out gets
+ * this rank's received records sorted by (key, other) (free with oap_free), *out_n their number
+ * and *out_distinct the number of distinct keys (the CSR row count). */
+OAP_API int oap_shuffle_ratings(oap_ctx* ctx, const void* records, int64_t n,
+                                int64_t n_total_keys, int n_blocks, void** out, int64_t* out_n,
+                                int64_t* out_distinct);
+/* In-place allreduce of count int64 values across the context's world (op: 0 sum, 1 max,
+ * 2 min). */
+OAP_API int oap_allreduce_i64(oap_ctx* ctx, int64_t* vals, int count, int op);
+OAP_API void oap_free(void* p);
+
 #ifdef __cplusplus
 }
 #endif

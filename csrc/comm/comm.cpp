@@ -3,6 +3,7 @@
 #include <rccl/rccl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <sstream>
@@ -282,6 +283,30 @@ void comm_allreduce_host(Context& ctx, Comm& comm, void* host, size_t count, DTy
   OAP_HIP_CHECK(hipMemcpyAsync(d.data(), host, bytes, hipMemcpyHostToDevice, s));
   comm.allreduce(d.data(), count, dt, op, s);
   OAP_HIP_CHECK(hipMemcpyAsync(host, d.data(), bytes, hipMemcpyDeviceToHost, s));
+  comm.wait(s);
+}
+
+void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
+                         const std::vector<size_t>& send_counts, void* recv,
+                         const std::vector<size_t>& recv_counts, DType dt) {
+  const size_t es = dtype_size(dt);
+  size_t sn = 0, rn = 0;
+  for (auto c : send_counts) sn += c;
+  for (auto c : recv_counts) rn += c;
+  if (comm.size() == 1) {
+    OAP_CHECK(sn == rn, "alltoallv: world of one with mismatched counts");
+    if (sn) std::memmove(recv, send, sn * es);
+    return;
+  }
+  if (!comm.on_device()) {
+    comm.alltoallv(send, send_counts, recv, recv_counts, dt, nullptr);
+    return;
+  }
+  Buffer ds = ctx.alloc(std::max<size_t>(sn * es, 16)), dr = ctx.alloc(std::max<size_t>(rn * es, 16));
+  hipStream_t s = ctx.comm_stream();
+  if (sn) OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send, sn * es, hipMemcpyHostToDevice, s));
+  comm.alltoallv(ds.data(), send_counts, dr.data(), recv_counts, dt, s);
+  if (rn) OAP_HIP_CHECK(hipMemcpyAsync(recv, dr.data(), rn * es, hipMemcpyDeviceToHost, s));
   comm.wait(s);
 }
 

@@ -113,6 +113,10 @@ void comm_bcast(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, int
 // Host memory in, host memory out, whatever memory the comm works on.
 void comm_allreduce_host(Context& ctx, Comm& comm, void* host, size_t count, DType dt,
                          ReduceOp op);
+// Variable-size exchange of HOST buffers over any comm (device comms stage through HBM).
+void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
+                         const std::vector<size_t>& send_counts, void* recv,
+                         const std::vector<size_t>& recv_counts, DType dt);
 // Host-side scalar convenience (always host memory in, host memory out).
 double comm_allreduce_scalar(Context& ctx, Comm& comm, double v, ReduceOp op);
 std::vector<int64_t> comm_allgather_i64(Context& ctx, Comm& comm, int64_t v);

@@ -1234,8 +1234,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
       kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
     }
-    if (comm.size() > 1)
+    if (comm.size() > 1) {
       comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+      if (comm.on_device()) comm.wait(s);  // the watchdog covers this collective too
+    }
     double c = 0.0;
     ctx.copy_to_host(&c, cost_d.data(), sizeof(double), s);
     res.cost = c;

@@ -1,24 +1,38 @@
-// JNI shim: the reference's native method names (mllib-dal/src/main/native/javah/*.h, SURVEY.md
-// §2.8) implemented over the C ABI (capi/oap_capi.h).  Compiled into liboap_mllib.so only when
-// JAVA_HOME points at a JDK (oap_mllib_amd/build.py); no JDK exists in the build container, so
-// this file is exercised by the Scala shadow classes on a Spark cluster, not by the test suite.
+// JNI shim: the reference's native methods (mllib-dal/src/main/native/javah/*.h)
+// with the reference's exact JNI names AND signatures, implemented over the C ABI
+// (capi/oap_capi.h).  Compiled into liboap_mllib.so only when JAVA_HOME points at a JDK
+// (oap_mllib_amd/build.py); the test suite compiles it against tests/native/jni_stub and drives
+// every entry point through a recording JNIEnv (tests/native/jni_harness.cpp).
 //
 // Mapping (reference -> here):
-//  * OneCCL$.c_init(size, rank, "ip_port", CCLParam): the string carries the hex-encoded RCCL
-//    unique id that rank 0 made with c_uniqueId() and Spark's BarrierTaskContext.allGather
-//    distributed — no KVS server, no port scan (OneCCL.cpp:47-247).  One persistent context
-//    per executor process (device = the executor's GPU), reused across fits.
-//  * OneDAL$ tables: a native row buffer handle (f64, row-major) filled by cSetDoubleBatch
-//    (one JNI call per row batch, OneDAL.cpp:50-60); cAddNumericTable appends rows;
-//    cGetDoubleArray / cNumRows / cNumCols read results back (replaces the oneDAL Java
-//    NumericTable accessors, OneDAL.scala:37-52).
-//  * KMeansDALImpl / PCADALImpl / ALSDALImpl train entry points call oap_kmeans_fit /
-//    oap_pca_fit / oap_als_fit; errors raise java.lang.RuntimeException (never exit()).
+//  * OneCCL$: c_init(size, rank, "ip_port" | hex unique id, CCLParam{long commSize, rankId}).
+//    With size > 1 the string must carry the hex RCCL unique id that rank 0 made with
+//    c_uniqueId() and the launcher distributed (Spark BarrierTaskContext.allGather): no KVS
+//    server, no port scan (OneCCL.cpp:47-247).  One persistent context per executor process.
+//    setEnv / c_getAvailPort keep the reference's behaviour (OneCCL.cpp:127-247).
+//  * OneDAL$: native row tables (f64, row-major) — setNumericTableValue (one value,
+//    OneDAL.cpp:35-43), cSetDoubleBatch (row batch, :50-60), cAddNumericTable (append, :67-76),
+//    cFreeDataMemory, cCheckPlatformCompatibility (gfx950 present, :96-102) and
+//    cNewCSRNumericTable (1-based CSR from Java arrays, :109-145).  Results are read back with
+//    cNumRows / cNumCols / cGetDoubleArray (the reference reads oneDAL Java NumericTables).
+//  * KMeansDALImpl / PCADALImpl / ALSDALImpl: the train entry points with the reference
+//    signatures; ALS runs the shuffle (cShuffleData: range partition by key + alltoallv + sort,
+//    ALSShuffle.cpp:62-127) and cDALImplictALS(csr, nUsers, ...) returns this rank's contiguous
+//    user / item factor blocks with their offsets (ALSDALImpl.cpp:500-576 contract).
+// Errors raise java.lang.RuntimeException (never exit()).
+#include <arpa/inet.h>
+#include <ifaddrs.h>
 #include <jni.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -33,8 +47,19 @@ struct RowTable {
   std::vector<double> data;
 };
 
+// 0-based CSR (the reference's oneDAL CSRNumericTable is 1-based; converted on entry)
+struct CsrTable {
+  int64_t rows = 0, cols = 0;
+  std::vector<int64_t> rowptr, colidx;
+  std::vector<float> vals;
+};
+
 std::mutex g_mu;
 oap_ctx* g_ctx = nullptr;  // one per executor process
+// last cShuffleData output (the reference also keeps it in a native global, ALSShuffle.cpp:28):
+// the records handed to Java as a direct ByteBuffer, and the distinct keys (CSR row -> key)
+void* g_shuffled = nullptr;
+std::vector<int64_t> g_shuffle_keys;
 
 void throw_java(JNIEnv* env, const std::string& msg) {
   jclass ex = env->FindClass("java/lang/RuntimeException");
@@ -47,26 +72,57 @@ bool check(JNIEnv* env, int rc) {
   return false;
 }
 
-void set_int(JNIEnv* env, jobject o, const char* f, jint v) {
-  jclass c = env->GetObjectClass(o);
-  env->SetIntField(o, env->GetFieldID(c, f, "I"), v);
+// Field setters: a missing field leaves Java's NoSuchFieldError pending and writes nothing.
+bool set_int(JNIEnv* env, jobject o, const char* f, jint v) {
+  jfieldID id = env->GetFieldID(env->GetObjectClass(o), f, "I");
+  if (!id) return false;
+  env->SetIntField(o, id, v);
+  return true;
 }
-void set_long(JNIEnv* env, jobject o, const char* f, jlong v) {
-  jclass c = env->GetObjectClass(o);
-  env->SetLongField(o, env->GetFieldID(c, f, "J"), v);
+bool set_long(JNIEnv* env, jobject o, const char* f, jlong v) {
+  jfieldID id = env->GetFieldID(env->GetObjectClass(o), f, "J");
+  if (!id) return false;
+  env->SetLongField(o, id, v);
+  return true;
 }
-void set_double(JNIEnv* env, jobject o, const char* f, jdouble v) {
-  jclass c = env->GetObjectClass(o);
-  env->SetDoubleField(o, env->GetFieldID(c, f, "D"), v);
+bool set_double(JNIEnv* env, jobject o, const char* f, jdouble v) {
+  jfieldID id = env->GetFieldID(env->GetObjectClass(o), f, "D");
+  if (!id) return false;
+  env->SetDoubleField(o, id, v);
+  return true;
 }
 
 RowTable* table(jlong h) { return reinterpret_cast<RowTable*>(h); }
+CsrTable* csr(jlong h) { return reinterpret_cast<CsrTable*>(h); }
 
 int hexval(char ch) {
   if (ch >= '0' && ch <= '9') return ch - '0';
   if (ch >= 'a' && ch <= 'f') return ch - 'a' + 10;
   if (ch >= 'A' && ch <= 'F') return ch - 'A' + 10;
   return -1;
+}
+
+bool ensure_ctx(JNIEnv* env) {
+  if (g_ctx) return true;
+  const int dev = oap_device_count() > 0 ? 0 : -1;  // an executor sees its own GPU as device 0
+  g_ctx = oap_ctx_create(dev, 0.9, 0);
+  return check(env, g_ctx ? 0 : -1);
+}
+
+// Is `ip` one of this host's IPv4 addresses (OneCCL.cpp:141-200)?
+bool is_local_ip(const char* ip) {
+  struct ifaddrs* ifs = nullptr;
+  if (getifaddrs(&ifs) != 0) return false;
+  bool found = false;
+  for (struct ifaddrs* p = ifs; p && !found; p = p->ifa_next) {
+    if (!p->ifa_addr || p->ifa_addr->sa_family != AF_INET) continue;
+    char buf[INET_ADDRSTRLEN] = {0};
+    auto* sin = reinterpret_cast<struct sockaddr_in*>(p->ifa_addr);
+    if (inet_ntop(AF_INET, &sin->sin_addr, buf, sizeof(buf)) && std::strcmp(buf, ip) == 0)
+      found = true;
+  }
+  freeifaddrs(ifs);
+  return found;
 }
 
 }  // namespace
@@ -87,30 +143,33 @@ JNIEXPORT jstring JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_c_1uniqueId
   return env->NewStringUTF(hex.c_str());
 }
 
+// (IILjava/lang/String;Lorg/apache/spark/ml/util/CCLParam;)I
 JNIEXPORT jint JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_c_1init(JNIEnv* env, jobject,
                                                                          jint size, jint rank,
                                                                          jstring uid_hex,
                                                                          jobject param) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_ctx) {
-    const int dev = oap_device_count() > 0 ? 0 : -1;  // executor sees its own GPU as device 0
-    g_ctx = oap_ctx_create(dev, 0.9, 0);
-    if (!g_ctx) {
-      check(env, -1);
-      return -1;
-    }
-  }
+  if (!ensure_ctx(env)) return -1;
   if (size > 1) {
     const char* s = env->GetStringUTFChars(uid_hex, nullptr);
+    const size_t n = s ? std::strlen(s) : 0;
     unsigned char id[OAP_UNIQUE_ID_BYTES] = {0};
-    const size_t n = std::strlen(s);
-    for (size_t i = 0; i + 1 < n && i / 2 < OAP_UNIQUE_ID_BYTES; i += 2)
-      id[i / 2] = static_cast<unsigned char>(hexval(s[i]) * 16 + hexval(s[i + 1]));
-    env->ReleaseStringUTFChars(uid_hex, s);
+    bool ok = n == 2 * OAP_UNIQUE_ID_BYTES;
+    for (size_t i = 0; ok && i < n; i += 2) {
+      const int hi = hexval(s[i]), lo = hexval(s[i + 1]);
+      ok = hi >= 0 && lo >= 0;
+      id[i / 2] = static_cast<unsigned char>(hi * 16 + lo);
+    }
+    if (s) env->ReleaseStringUTFChars(uid_hex, s);
+    if (!ok) {
+      throw_java(env, "c_init: expected the hex RCCL unique id from c_uniqueId() (no KVS)");
+      return -1;
+    }
     if (!check(env, oap_ctx_join(g_ctx, id, size, rank, 600.0))) return -1;
   }
-  set_int(env, param, "commSize", oap_ctx_world_size(g_ctx));
-  set_int(env, param, "rankId", oap_ctx_rank(g_ctx));
+  // CCLParam.commSize / rankId are Java longs (CCLParam.java:20-21)
+  if (!set_long(env, param, "commSize", oap_ctx_world_size(g_ctx))) return -1;
+  if (!set_long(env, param, "rankId", oap_ctx_rank(g_ctx))) return -1;
   return 0;
 }
 
@@ -118,6 +177,9 @@ JNIEXPORT void JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_c_1cleanup(JNI
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_ctx) oap_ctx_destroy(g_ctx);
   g_ctx = nullptr;
+  oap_free(g_shuffled);
+  g_shuffled = nullptr;
+  g_shuffle_keys.clear();
 }
 
 JNIEXPORT jboolean JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_isRoot(JNIEnv*, jobject) {
@@ -126,6 +188,43 @@ JNIEXPORT jboolean JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_isRoot(JNI
 
 JNIEXPORT jint JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_rankID(JNIEnv*, jobject) {
   return g_ctx ? oap_ctx_rank(g_ctx) : -1;
+}
+
+// (Ljava/lang/String;Ljava/lang/String;Z)I
+JNIEXPORT jint JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_setEnv(JNIEnv* env, jobject,
+                                                                        jstring key,
+                                                                        jstring value,
+                                                                        jboolean overwrite) {
+  const char* k = env->GetStringUTFChars(key, nullptr);
+  const char* v = env->GetStringUTFChars(value, nullptr);
+  const int rc = (k && v) ? setenv(k, v, overwrite ? 1 : 0) : -1;
+  if (k) env->ReleaseStringUTFChars(key, k);
+  if (v) env->ReleaseStringUTFChars(value, v);
+  return rc;
+}
+
+// (Ljava/lang/String;)I: first bindable TCP port >= 3000 on `ip` (which must be local), else -1
+JNIEXPORT jint JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_c_1getAvailPort(JNIEnv* env,
+                                                                                 jobject,
+                                                                                 jstring ip) {
+  const char* s = env->GetStringUTFChars(ip, nullptr);
+  if (!s) return -1;
+  std::string addr(s);
+  env->ReleaseStringUTFChars(ip, s);
+  if (!is_local_ip(addr.c_str())) return -1;
+  for (int port = 3000; port < 65535; ++port) {
+    const int fd = socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) return -1;
+    struct sockaddr_in sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons(static_cast<uint16_t>(port));
+    inet_pton(AF_INET, addr.c_str(), &sa.sin_addr);
+    const int rc = bind(fd, reinterpret_cast<struct sockaddr*>(&sa), sizeof(sa));
+    close(fd);
+    if (rc == 0) return port;
+  }
+  return -1;
 }
 
 // ---------------------------------------------------------------- OneDAL$ (row tables)
@@ -144,10 +243,22 @@ JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cNewRowTable(
   return reinterpret_cast<jlong>(t);
 }
 
+// (JIID)V
+JNIEXPORT void JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_setNumericTableValue(
+    JNIEnv* env, jobject, jlong h, jint row, jint col, jdouble v) {
+  RowTable* t = table(h);
+  if (!t || row < 0 || row >= t->rows || col < 0 || col >= t->cols) {
+    throw_java(env, "setNumericTableValue: index out of the table's bounds");
+    return;
+  }
+  t->data[size_t(row) * t->cols + col] = v;
+}
+
+// (JI[DII)V
 JNIEXPORT void JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cSetDoubleBatch(
     JNIEnv* env, jobject, jlong h, jint row0, jdoubleArray batch, jint nrows, jint cols) {
   RowTable* t = table(h);
-  if (!t || cols != t->cols || row0 < 0 || int64_t(row0) + nrows > t->rows) {
+  if (!t || cols != t->cols || row0 < 0 || nrows < 0 || int64_t(row0) + nrows > t->rows) {
     throw_java(env, "cSetDoubleBatch: batch out of the table's bounds");
     return;
   }
@@ -168,9 +279,53 @@ JNIEXPORT void JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cAddNumericTab
   a->rows += b->rows;
 }
 
+// frees a row table or a CSR table handle (the reference frees its oneDAL tables here)
 JNIEXPORT void JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cFreeDataMemory(JNIEnv*, jobject,
                                                                                  jlong h) {
   delete table(h);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cFreeCSRTable(JNIEnv*, jobject,
+                                                                               jlong h) {
+  delete csr(h);
+}
+
+// ([F[J[JJJ)J: 1-based CSR arrays (values, column indices, row offsets), nFeatures columns,
+// nVectors rows (OneDAL.cpp:109-145)
+JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cNewCSRNumericTable(
+    JNIEnv* env, jobject, jfloatArray data, jlongArray col_indices, jlongArray row_offsets,
+    jlong n_features, jlong n_vectors) {
+  const jsize nnz = env->GetArrayLength(data);
+  if (env->GetArrayLength(col_indices) != nnz || n_vectors < 0 ||
+      env->GetArrayLength(row_offsets) != n_vectors + 1) {
+    throw_java(env, "cNewCSRNumericTable: inconsistent CSR array lengths");
+    return 0;
+  }
+  auto* t = new CsrTable;
+  t->rows = n_vectors;
+  t->cols = n_features;
+  t->vals.resize(size_t(nnz));
+  t->colidx.resize(size_t(nnz));
+  t->rowptr.resize(size_t(n_vectors) + 1);
+  if (nnz) {
+    env->GetFloatArrayRegion(data, 0, nnz, t->vals.data());
+    env->GetLongArrayRegion(col_indices, 0, nnz, reinterpret_cast<jlong*>(t->colidx.data()));
+  }
+  env->GetLongArrayRegion(row_offsets, 0, jsize(n_vectors + 1),
+                          reinterpret_cast<jlong*>(t->rowptr.data()));
+  bool ok = t->rowptr[0] == 1 && t->rowptr[size_t(n_vectors)] == int64_t(nnz) + 1;
+  for (int64_t i = 0; ok && i < n_vectors; ++i) ok = t->rowptr[i] <= t->rowptr[i + 1];
+  for (auto& v : t->rowptr) --v;
+  for (auto& c : t->colidx) {
+    ok = ok && c >= 1 && c <= n_features;
+    --c;
+  }
+  if (!ok) {
+    delete t;
+    throw_java(env, "cNewCSRNumericTable: not a valid 1-based CSR");
+    return 0;
+  }
+  return reinterpret_cast<jlong>(t);
 }
 
 JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cNumRows(JNIEnv*, jobject,
@@ -193,8 +348,8 @@ JNIEXPORT jdoubleArray JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cGetDo
 }
 
 // ---------------------------------------------------------------- K-Means
-// (data, initial centers) tables -> new centers table (every rank; the reference returns it on
-// rank 0 only, KMeansDALImpl.cpp:175-249).
+// (JJIDIIILorg/apache/spark/ml/clustering/KMeansResult;)J: (data, initial centers) tables ->
+// new centers table (every rank; the reference returns it on rank 0 only).
 JNIEXPORT jlong JNICALL
 Java_org_apache_spark_ml_clustering_KMeansDALImpl_cKMeansDALComputeWithInitCenters(
     JNIEnv* env, jobject, jlong data, jlong centers, jint k, jdouble tol, jint max_iter,
@@ -215,12 +370,16 @@ Java_org_apache_spark_ml_clustering_KMeansDALImpl_cKMeansDALComputeWithInitCente
     delete out;
     return 0;
   }
-  set_int(env, result, "iterationNum", iters);
-  set_double(env, result, "totalCost", cost);
+  if (!set_int(env, result, "iterationNum", iters) ||
+      !set_double(env, result, "totalCost", cost)) {
+    delete out;
+    return 0;
+  }
   return reinterpret_cast<jlong>(out);
 }
 
 // ---------------------------------------------------------------- PCA
+// (JIIILorg/apache/spark/ml/feature/PCAResult;)J
 JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_feature_PCADALImpl_cPCATrainDAL(
     JNIEnv* env, jobject, jlong data, jint k, jint /*executor_num*/, jint /*executor_cores*/,
     jobject result) {
@@ -243,65 +402,132 @@ JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_feature_PCADALImpl_cPCATrainDAL
     delete ev;
     return 0;
   }
-  set_long(env, result, "pcNumericTable", reinterpret_cast<jlong>(pc));
-  set_long(env, result, "explainedVarianceNumericTable", reinterpret_cast<jlong>(ev));
+  if (!set_long(env, result, "pcNumericTable", reinterpret_cast<jlong>(pc)) ||
+      !set_long(env, result, "explainedVarianceNumericTable", reinterpret_cast<jlong>(ev))) {
+    delete pc;
+    delete ev;
+  }
   return 0;
 }
 
 // ---------------------------------------------------------------- ALS
-// Ratings arrive as the reference's packed 20-byte little-endian records {int64 user; int64 item;
-// float rating} in a direct ByteBuffer (ALSShuffle.h:22-28); the id shuffle, CSR build and the
-// factor exchange happen inside oap_als_fit.  Factor tables: rows = owned ids, cols = 1 + rank
-// (column 0 = the id as a double, exact below 2^53).
-JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_recommendation_ALSDALImpl_cDALImplictALS(
-    JNIEnv* env, jobject, jobject ratings_buf, jlong n, jint rank, jint max_iter,
-    jdouble reg, jdouble alpha, jint /*executor_num*/, jint /*executor_cores*/, jlong seed,
-    jobject result) {
+// (Ljava/nio/ByteBuffer;IILorg/apache/spark/ml/recommendation/ALSPartitionInfo;)
+// Ljava/nio/ByteBuffer;  — packed 20-byte little-endian {int64 key; int64 other; float rating}
+// records (ALSShuffle.h:22-28), range-partitioned by key over the world, sorted by (key, other);
+// the returned direct buffer stays valid until the next call or c_cleanup.
+JNIEXPORT jobject JNICALL Java_org_apache_spark_ml_recommendation_ALSDALImpl_cShuffleData(
+    JNIEnv* env, jobject, jobject data_buffer, jint n_total_keys, jint n_blocks, jobject info) {
+  std::lock_guard<std::mutex> lk(g_mu);
   if (!g_ctx) {
-    throw_java(env, "cDALImplictALS: not initialised");
-    return 0;
+    throw_java(env, "cShuffleData: OneCCL.init first");
+    return nullptr;
   }
-  const auto* rec = static_cast<const unsigned char*>(env->GetDirectBufferAddress(ratings_buf));
-  if (!rec && n > 0) {
-    throw_java(env, "cDALImplictALS: ratings must be a direct ByteBuffer");
-    return 0;
+  const auto* rec = static_cast<const unsigned char*>(env->GetDirectBufferAddress(data_buffer));
+  const jlong cap = env->GetDirectBufferCapacity(data_buffer);
+  if ((!rec && cap > 0) || cap < 0 || cap % 20 != 0) {
+    throw_java(env, "cShuffleData: ratings must be a direct ByteBuffer of 20-byte records");
+    return nullptr;
   }
-  std::vector<int32_t> u(n), it(n);
-  std::vector<float> r(n);
+  oap_free(g_shuffled);
+  g_shuffled = nullptr;
+  g_shuffle_keys.clear();
+  int64_t n = 0, distinct = 0;
+  if (!check(env, oap_shuffle_ratings(g_ctx, rec, cap / 20, n_total_keys, n_blocks, &g_shuffled,
+                                      &n, &distinct)))
+    return nullptr;
+  if (n > std::numeric_limits<jint>::max()) {  // ALSPartitionInfo fields are Java ints
+    throw_java(env, "cShuffleData: more ratings on one rank than a Java int holds");
+    return nullptr;
+  }
+  const auto* out = static_cast<const unsigned char*>(g_shuffled);
+  g_shuffle_keys.reserve(size_t(distinct));
   for (int64_t i = 0; i < n; ++i) {
-    int64_t uu, ii;
-    float rv;
-    std::memcpy(&uu, rec + 20 * i, 8);
-    std::memcpy(&ii, rec + 20 * i + 8, 8);
-    std::memcpy(&rv, rec + 20 * i + 16, 4);
-    u[i] = static_cast<int32_t>(uu);
-    it[i] = static_cast<int32_t>(ii);
-    r[i] = rv;
+    int64_t key;
+    std::memcpy(&key, out + 20 * i, 8);
+    if (g_shuffle_keys.empty() || g_shuffle_keys.back() != key) g_shuffle_keys.push_back(key);
   }
-  oap_als_result* res = nullptr;
-  if (!check(env, oap_als_fit(g_ctx, u.data(), it.data(), r.data(), n, rank, max_iter, reg, alpha,
-                              1, static_cast<uint64_t>(seed), &res)))
+  if (!set_int(env, info, "ratingsNum", jint(n)) || !set_int(env, info, "csrRowNum", jint(distinct)))
+    return nullptr;
+  return env->NewDirectByteBuffer(g_shuffled, n * 20);
+}
+
+// (JJIIDDIIILorg/apache/spark/ml/recommendation/ALSResult;)J: the CSR of this rank's shuffled
+// ratings (rows = its distinct keys in order — the reference's transposed items — columns =
+// user index + 1), nUsers, rank, iterations, regParam, alpha.  Spark computeFactors semantics
+// (regParam and alpha honoured, unlike the reference).  ALSResult gets this rank's contiguous
+// blocks of the user and item factors ([offset, offset + rows) with ceil(n / P) ids per rank;
+// ids without ratings get zero rows) as row tables of nFactors columns.
+JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_recommendation_ALSDALImpl_cDALImplictALS(
+    JNIEnv* env, jobject, jlong csr_handle, jlong n_users, jint n_factors, jint max_iter,
+    jdouble reg, jdouble alpha, jint /*executor_num*/, jint /*executor_cores*/,
+    jint partition_id, jobject result) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  CsrTable* t = csr(csr_handle);
+  if (!g_ctx || !t) {
+    throw_java(env, "cDALImplictALS: not initialised or bad CSR table");
     return 0;
-  auto factors = [&](int which) {
-    const int64_t cnt = oap_als_result_count(res, which);
-    const int32_t* ids = oap_als_result_ids(res, which);
-    const float* f = oap_als_result_factors(res, which);
-    auto* t = new RowTable;
-    t->rows = cnt;
-    t->cols = 1 + rank;
-    t->data.resize(size_t(cnt) * (1 + rank));
-    for (int64_t i = 0; i < cnt; ++i) {
-      t->data[size_t(i) * (1 + rank)] = ids[i];
-      for (int j = 0; j < rank; ++j) t->data[size_t(i) * (1 + rank) + 1 + j] = f[i * rank + j];
+  }
+  if (int64_t(g_shuffle_keys.size()) != t->rows) {
+    throw_java(env, "cDALImplictALS: the CSR rows do not match the last cShuffleData output");
+    return 0;
+  }
+  const int64_t nnz = int64_t(t->vals.size());
+  constexpr int64_t kMaxId = std::numeric_limits<int32_t>::max();
+  std::vector<int32_t> u(static_cast<size_t>(nnz)), it(static_cast<size_t>(nnz));
+  int64_t max_item = -1;
+  for (int64_t row = 0; row < t->rows; ++row) {
+    const int64_t key = g_shuffle_keys[size_t(row)];
+    if (key < 0 || key > kMaxId) {
+      throw_java(env, "cDALImplictALS: item id beyond the int32 range");
+      return 0;
     }
-    return reinterpret_cast<jlong>(t);
+    max_item = std::max(max_item, key);
+    for (int64_t j = t->rowptr[row]; j < t->rowptr[row + 1]; ++j) {
+      if (t->colidx[j] > kMaxId) {
+        throw_java(env, "cDALImplictALS: user id beyond the int32 range");
+        return 0;
+      }
+      u[size_t(j)] = int32_t(t->colidx[j]);
+      it[size_t(j)] = int32_t(key);
+    }
+  }
+  int64_t n_items = max_item + 1;
+  if (!check(env, oap_allreduce_i64(g_ctx, &n_items, 1, 1))) return 0;
+  oap_als_result* res = nullptr;
+  if (!check(env, oap_als_fit(g_ctx, u.data(), it.data(), t->vals.data(), nnz, n_factors,
+                              max_iter, reg, alpha, 1, 0, &res)))
+    return 0;
+  const int P = oap_ctx_world_size(g_ctx), me = oap_ctx_rank(g_ctx);
+  auto block = [&](int which, int64_t n_ids, int64_t* offset) {
+    const int64_t per = (n_ids + P - 1) / P;
+    const int64_t lo = std::min<int64_t>(n_ids, per * me), hi = std::min<int64_t>(n_ids, lo + per);
+    auto* tab = new RowTable;
+    tab->rows = hi - lo;
+    tab->cols = n_factors;
+    tab->data.assign(size_t(hi - lo) * n_factors, 0.0);
+    const int64_t cnt = oap_als_result_count(res, which);
+    const int32_t* ids = oap_als_result_ids(res, which);  // ascending
+    const float* f = oap_als_result_factors(res, which);
+    const int32_t* b = std::lower_bound(ids, ids + cnt, int32_t(std::min<int64_t>(lo, kMaxId)));
+    for (; b != ids + cnt && *b < hi; ++b) {
+      const int64_t i = b - ids;
+      for (int j = 0; j < n_factors; ++j)
+        tab->data[size_t(*b - lo) * n_factors + j] = f[size_t(i) * n_factors + j];
+    }
+    *offset = lo;
+    return reinterpret_cast<jlong>(tab);
   };
-  set_int(env, result, "rankId", oap_ctx_rank(g_ctx));
-  set_long(env, result, "cUsersFactorsNumTab", factors(0));
-  set_long(env, result, "cItemsFactorsNumTab", factors(1));
-  set_long(env, result, "cUserOffset", 0);  // ids travel inside the tables (no range offsets)
-  set_long(env, result, "cItemOffset", 0);
+  int64_t uoff = 0, ioff = 0;
+  const jlong ut = block(0, n_users, &uoff), itab = block(1, n_items, &ioff);
   oap_als_result_free(res);
+  if (partition_id != me)
+    std::fprintf(stderr, "cDALImplictALS: partition %d runs as rank %d\n", partition_id, me);
+  if (!set_long(env, result, "rankId", me) || !set_long(env, result, "cUsersFactorsNumTab", ut) ||
+      !set_long(env, result, "cItemsFactorsNumTab", itab) ||
+      !set_long(env, result, "cUserOffset", uoff) || !set_long(env, result, "cItemOffset", ioff)) {
+    delete table(ut);
+    delete table(itab);
+  }
   return 0;
 }
 

@@ -53,7 +53,9 @@ def _view(x, w, layout: str):
     else:
         x, dt = x.float(), "f32"
     ld = N.kmeans_ld(d, dt) if layout == "kmeans" else (d + 3) // 4 * 4
-    ok = (x.stride(1) == 1 and x.stride(0) == ld and x.data_ptr() % 16 == 0)
+    # zero-copy only when the row IS the kernel layout: with ld > d the kernels read columns
+    # [d, ld) as zero padding, and a column-sliced view would have real data there
+    ok = (ld == d and x.stride(1) == 1 and x.stride(0) == ld and x.data_ptr() % 16 == 0)
     if not ok:
         xp = torch.zeros((n, ld), dtype=x.dtype, device=x.device)
         xp[:, :d] = x

@@ -53,3 +53,18 @@ def test_gpu_tensor_ops(gpu_world, native, d, dtype):
         pc, ev = ops.pca(x, 3)
         w = np.linalg.eigvalsh(np.cov(Xr.T))[::-1]
         np.testing.assert_allclose(ev.numpy(), w[:3] / w.sum(), rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_gpu_sliced_view_padding_not_read(gpu_world, native):
+    """A column-sliced view whose row stride equals the kernel's padded layout (52 floats for
+    d = 50) must not be used in place: columns 50-51 hold real data, not zero padding."""
+    X, c = _blobs(8000, 50, 5, 3)
+    wide = torch.full((8000, 52), 1e3, dtype=torch.float32, device="cuda")
+    wide[:, :50] = torch.from_numpy(X).cuda()
+    x = wide[:, :50]
+    assert x.stride(0) == native.kmeans_ld(50)
+    lab, d2 = ops.kmeans_assign(x, torch.from_numpy(c))
+    ref_lab, ref_d = vanilla.find_closest(X.astype(np.float64), c)
+    assert np.array_equal(lab.cpu().numpy(), ref_lab)
+    np.testing.assert_allclose(d2.cpu().numpy(), ref_d, rtol=1e-4, atol=1e-4)
