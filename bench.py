@@ -138,8 +138,9 @@ def bench_kmeans(args, w):
                                    - ar["total_us"] / max(ar["count"], 1)),
              # dense-equivalent rate (2 n k d flops per iteration over the timed wall clock)
              "dense_equiv_tflops": flops / (el_max / args.steps) / 1e12,
+             # rows the tier-1 pass left to the exact fp32 MFMA re-decision (near ties)
+             "deferred_rows_per_iter": r.get("deferred_rows", 0) / max(args.steps, 1),
              "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
-             "tier3_tiles_per_iter": r["tier3_tiles"] / max(args.steps, 1),
              "tiles_per_pass": tiles,
              "ms_per_step_unpruned": ms_unpruned,
              "storage": st,
@@ -147,10 +148,9 @@ def bench_kmeans(args, w):
              "rccl_ranks": w.size if comm_name == "rccl" else 0,
              "world_size": w.size,
              "distance_path": "fp32-exact MFMA" if args.precise else
-             ("tiered bf16 MFMA (1 product, then bf16x3 split where unsure) + exact-fp32 "
-              "refinement (assignments identical to fp32)"
-              if st == "f32" else "bf16 rows x bf16-split centroids on MFMA + exact-fp32 "
-              "refinement (assignments identical to exact fp32 on the bf16 data)"),
+             ("lean pass: one fp16 MFMA product per k-step (v_mfma_f32_32x32x16_f16) with a "
+              "rigorous error bound; rows inside it re-decided by the exact fp32 MFMA argmin "
+              "(assignments identical to exact fp32); delta accumulation of moved rows"),
              "cost": r["cost"]}
     del table
     if args.separable_extra and args.sigma != 1.0:

@@ -242,6 +242,7 @@ struct AssignReq {
   int32_t* defer_rows = nullptr;
   unsigned* defer_count = nullptr;
   u64* deferred_rows = nullptr;
+  int ablate = 0;  // timing ablations (kern::KMeansAssignArgs::ablate)
 };
 
 int& lean_variant_ref() {
@@ -257,7 +258,6 @@ int lean_variant() { return lean_variant_ref(); }
 bool lean_applies(const DenseTable& x, int k, int kpad, const AssignReq& req) {
   return req.lean && req.fast1 && !req.precise && x.cols <= 128 && !req.mindist_seeded &&
          kern::kmeans_lloyd_supported(x.cols, k, req.accumulate, req.sums_too) &&
-         kpad <= kern::kmeans_lds_kmax(x.cols, false) &&
          !(req.bounds && req.drift && !req.delta);  // the in-kernel pruning test: general kernel
 }
 
@@ -299,6 +299,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   OAP_CHECK(!req.bounds || (x.cols <= 128 && !req.precise && req.labels),
             "kmeans pruning needs the fast path (d <= 128) and persistent labels");
   a.xnorm = req.xnorm;
+  a.ablate = req.ablate;
   const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
   if (x.rows > 0 && lean_applies(x, g.k, g.kpad, req)) {
     // ---- lean tier-1 pass, then the general kernel re-decides the deferred rows exactly
@@ -317,12 +318,17 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.defer_row_count = dcnt;
     a.row_seg_cap = cap;
     a.deferred_rows = req.deferred_rows;
-    if (req.delta) {
-      OAP_CHECK(req.bounds && req.drift && req.tile_list && req.labels_valid,
-                "kmeans delta accumulation needs the pruning scan's tile list");
+    a.tile_list = nullptr;
+    a.tile_count = nullptr;
+    if (req.delta) {  // delta accumulation; over the scan's tile list when there is one
+      OAP_CHECK(req.labels && req.labels_valid,
+                "kmeans delta accumulation needs the previous iteration's labels");
       a.delta = true;
-      a.tile_list = req.tile_list;
-      a.tile_count = req.tile_count;
+      if (req.tile_list) {
+        OAP_CHECK(req.bounds && req.drift && req.tile_count, "scan pass without bounds");
+        a.tile_list = req.tile_list;
+        a.tile_count = req.tile_count;
+      }
     }
     kern::kmeans_lloyd(a, grid, lean_variant(), s);
     kern::KMeansAssignArgs b = a;
@@ -332,12 +338,11 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.row_list = drows;
     b.row_count = dcnt;
     b.row_subs = kern::kmeans_lloyd_waves(lean_variant());
-    b.fast1 = false;  // deferred rows are near ties at tier 1: start at the bf16x3 split
     b.tile_list = nullptr;
     b.tile_count = nullptr;
     b.xnorm = nullptr;
     b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
-    kern::kmeans_assign_rows(b, grid, s);
+    kern::kmeans_exact_rows(b, grid, s);
     return a.cost_slab ? 2 * grid : 0;
   }
   if (x.cols > 128 || g.kpad <= kmax || kmax == 0) {
@@ -993,22 +998,42 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // delta accumulation (single launch + pruning): persistent local statistics, max |x|^2 per tile,
   // the scan's tile list, and the centers each iteration assigned against (final exact cost)
   // (rank-uniform form: a rank with no rows still joins the final-cost collective)
-  const bool delta_all = p.prune && !p.precise && x.cols <= 128 && !chunked && p.delta;
-  const bool delta = delta_all && prune;
+  // Delta accumulation (lean kernel): iterations after the first keep each rank's local
+  // statistics and add only the rows whose label changed (+x to the new, -x to the old cluster;
+  // integers, so bitwise the full recount).  Two forms per iteration: a full pass (every row
+  // assigned and costed, unmoved rows not re-accumulated) or, with pruning, a scan pass (the
+  // bounds scan lists the tiles that may change; only those are read, the cost is not
+  // computed).  delta_all / scan_all are rank-uniform (a rank with no rows still joins the
+  // final-cost collective).
+  const bool delta_all = !p.precise && x.cols <= 128 && !chunked && p.delta &&
+                         kern::kmeans_lloyd_supported(d, k, true, true);
+  const bool scan_all = delta_all && p.prune;
+  const bool delta = delta_all && x.rows > 0;
+  const bool scan = scan_all && prune;
+  if (delta && !req.labels) {
+    lab_keep = ctx.alloc(sizeof(int32_t) * x.rows);
+    req.labels = lab_keep.as<int32_t>();
+  }
   Buffer loc_b, xnorm_b, dlist_b, cbak_b;
+  const int lgrid = kern::kmeans_lloyd_grid(x.rows, ctx.info().cu_count);
+  const int64_t ltiles = kern::kmeans_lloyd_tiles_per_block(x.rows, lgrid);
   if (delta) {
     loc_b = ctx.alloc(sizeof(u64) * (kd + k));
-    const int64_t nt = (x.rows + 31) / 32;
-    xnorm_b = ctx.alloc(sizeof(float) * nt);
-    dlist_b = ctx.alloc(sizeof(int32_t) * nt + 64);
-    cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
-    req.xnorm = xnorm_b.as<float>();
     req.sums = loc_b.as<u64>();
     req.counts = loc_b.as<u64>() + kd;
   }
+  if (scan) {
+    const int64_t nt = (x.rows + 31) / 32;
+    xnorm_b = ctx.alloc(sizeof(float) * nt);
+    dlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) +
+                        sizeof(unsigned) * size_t(lgrid) + 64);
+    req.xnorm = xnorm_b.as<float>();
+  }
+  if (delta) cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
   unsigned* dcount =
-      delta ? reinterpret_cast<unsigned*>(dlist_b.as<char>() + sizeof(int32_t) * ((x.rows + 31) / 32))
-            : nullptr;
+      scan ? reinterpret_cast<unsigned*>(dlist_b.as<int32_t>() + size_t(lgrid) * size_t(ltiles))
+           : nullptr;
+  bool last_scanned = false;  // the last iteration was a scan pass (its cost is not computed)
   // lean tier-1 path: persistent deferral list + a counter of deferred rows (adaptive tier)
   Buffer ldefer_b, ldstat_b, ldstat_h;
   if (x.rows > 0 && lean_applies(x, k, g.kpad, req)) {
@@ -1065,30 +1090,40 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer flags_hb = ctx.alloc_pinned(sizeof(kern::KMeansFlags) * B);
   auto* flh = flags_hb.as<kern::KMeansFlags>();
   bool stop = false;
-  for (int it0 = 0; it0 < p.max_iter && !stop; it0 += B) {
-    const int nb_it = std::min(B, p.max_iter - it0);
+  int scan_iters = 0;  // scan passes in the current batch
+  std::vector<char> it_scanned(B, 0);
+  for (int it0 = 0, nb_it = 0; it0 < p.max_iter && !stop; it0 += nb_it) {
+    // the first batch is short so the adaptive choices (tier, scan) are made early
+    nb_it = std::min(it0 == 0 && B > 3 ? 3 : B, p.max_iter - it0);
+    scan_iters = 0;
     for (int b = 0; b < nb_it; ++b) {
       const int it = it0 + b;
       maybe_inject_fault(comm.rank(), "kmeans_iter", it);
       roctx_push("kmeans/iteration");
       ev[b].e0.record(s);
-      const bool delta_it = delta && it > 0 && delta_on;
+      // (req.fast1: the lean kernel runs; only it does delta accumulation)
+      const bool delta_it = delta && it > 0 && req.fast1;
+      const bool scan_it_all = scan_all && it > 0 && req.fast1 && delta_on;  // rank-uniform
+      const bool scan_it = scan_it_all && scan;
+      last_scanned = scan_it_all;
+      it_scanned[b] = scan_it_all;
+      scan_iters += scan_it_all ? 1 : 0;
       if (!delta_it)
         OAP_HIP_CHECK(hipMemsetAsync(delta ? loc_b.data() : stats.data(), 0,
                                      sizeof(u64) * (kd + k), s));
       req.labels_valid = it > 0;
       if (prune) {
-        // a full pass of the delta path refreshes labels and bounds without the pruning test
-        const bool drift_in = it > 0 && (!delta || delta_it);
+        // the general kernel's in-kernel pruning test (lean off) or the scan read the drift;
+        // a lean full pass refreshes labels and bounds without it
+        const bool drift_in = it > 0 && (scan_it || !req.fast1 || !delta_all);
         req.drift = drift_in ? drift_b.as<float>() : nullptr;
         req.drift_max = drift_in ? drift_b.as<float>() + k : nullptr;
       }
       req.delta = delta_it;
-      if (req.delta) {
-        OAP_HIP_CHECK(hipMemsetAsync(dcount, 0, sizeof(unsigned), s));
-        kern::kmeans_prune_scan(x.rows, k, d, req.bounds, req.labels, req.xnorm, req.drift,
-                                req.drift_max, g.cstat.as<float>(), dlist_b.as<int32_t>(),
-                                dcount, req.pruned_tiles, s);
+      if (scan_it) {
+        kern::kmeans_lean_scan(x.rows, k, d, lgrid, req.bounds, req.labels, req.xnorm,
+                               req.drift, req.drift_max, g.cstat.as<float>(),
+                               dlist_b.as<int32_t>(), dcount, req.pruned_tiles, s);
         req.tile_list = dlist_b.as<int32_t>();
         req.tile_count = dcount;
       } else if (!chunked) {
@@ -1134,7 +1169,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     u64 pruned_now = 0;
-    if (delta)
+    if (scan)
       OAP_HIP_CHECK(hipMemcpyAsync(&pruned_now, pruned_d.data(), sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     comm.wait(s);
@@ -1154,9 +1189,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
            << (ms_assign > 0 ? double(flops_per_iter) / (ms_assign * 1e-3) / 1e12 : 0.0);
         Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
       }
-      // delta iterations sum the cost of the tiles they read only: not a cost
-      const double c_it =
-          (delta_all && it > 0) ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
+      // scan iterations sum the cost of the tiles they read only: not a cost
+      const double c_it = it_scanned[b] ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
       res.cost = c_it;
       res.cost_history.push_back(c_it);
       res.shift_history.push_back(std::sqrt(std::max(fl.max_shift2, 0.0)));
@@ -1167,39 +1201,38 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         break;
       }
     }
-    {  // adaptive tier: tier-1 first pays off only while tier-3 re-runs stay rare
+    if (req.fast1 && !stop) {
+      // adaptive tier (rank-uniform: the largest local share decides): tier-1 first pays off
+      // only while the re-decisions it leaves stay rare — tier-3 tile re-runs (general kernel)
+      // or deferred rows (lean kernel)
       const u64 t2 = refine_h.as<u64>()[1];
       const double tiles = double((x.rows + 31) / 32) * nb_it;
-      if (req.fast1 && tiles > 0 && double(t2 - tier2_seen) > 0.02 * tiles) {
+      double share = tiles > 0 ? double(t2 - tier2_seen) / (0.02 * tiles) : 0.0;
+      if (ldstat_b.data() && x.rows > 0)
+        share = std::max(share, double(ldstat_h.as<u64>()[0] - deferred_seen) /
+                                    (0.25 * double(x.rows) * nb_it));
+      tier2_seen = t2;
+      if (ldstat_b.data()) deferred_seen = ldstat_h.as<u64>()[0];
+      if (comm.size() > 1) share = comm_allreduce_scalar(ctx, comm, share, ReduceOp::Max);
+      if (share > 1.0) {
         req.fast1 = false;
         Logger::instance().log(LogLevel::Info, "kmeans/tier1_off",
                                "\"iter\":" + std::to_string(res.num_iter - 1));
       }
-      tier2_seen = t2;
-      if (ldstat_b.data()) {  // lean path: deferral rate (a near-tie share this high means
-        // the bf16x3 tier pays from the start)
-        const u64 dr = ldstat_h.as<u64>()[0];
-        if (req.fast1 && double(dr - deferred_seen) > 0.25 * double(x.rows) * nb_it) {
-          req.fast1 = false;
-          Logger::instance().log(LogLevel::Info, "kmeans/lean_off",
-                                 "\"iter\":" + std::to_string(res.num_iter - 1));
-        }
-        deferred_seen = dr;
-      }
     }
-    if (delta_all && !stop) {  // adaptive delta (decided per batch from the scan's pruned
-      // share); rank-uniform: ranks see the same drift but their own rows, so the smallest
-      // local share decides (a rank without rows reports 1)
+    if (scan_all && !stop) {  // adaptive scan (decided per batch from its pruned share);
+      // rank-uniform: ranks see the same drift but their own rows, so the smallest local share
+      // decides (a rank without rows reports 1)
       double frac = 0.0;
-      const int delta_iters = delta_on ? nb_it - (it0 == 0 ? 1 : 0) : 0;
-      if (delta_iters > 0) {
-        frac = delta ? double(pruned_now - pruned_seen) /
-                           (double((x.rows + 31) / 32) * delta_iters + 1e-9)
-                     : 1.0;
+      if (scan_iters > 0) {
+        frac = scan ? double(pruned_now - pruned_seen) /
+                          (double((x.rows + 31) / 32) * scan_iters + 1e-9)
+                    : 1.0;
         frac = comm_allreduce_scalar(ctx, comm, frac, ReduceOp::Min);
       }
       pruned_seen = pruned_now;
-      if (delta_on && delta_iters > 0 && frac < 0.2) {
+      // (one scan right after a large move says little: turn off on two, or on a hopeless one)
+      if (delta_on && scan_iters > 0 && (frac < 0.02 || (scan_iters > 1 && frac < 0.2))) {
         delta_on = false;
         delta_probe = 0;
       } else if (!delta_on && ++delta_probe >= (B == 1 ? 4 : 1)) {
@@ -1207,9 +1240,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
     }
   }
-  if (delta_all && res.num_iter > 1) {
-    // exact cost of the last iteration: every row against the centers it was assigned to, with
-    // the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
+  if (scan_all && last_scanned && res.num_iter > 1) {
+    // exact cost of a last scan iteration: every row against the centers it was assigned to,
+    // with the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
     TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
     Buffer md;  // outlives the copy_to_host below (which synchronizes the stream)
     if (!delta) {
@@ -1358,7 +1391,8 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
   Event e0, e1;
   if (ablate & 64) {  // the Lloyd fit's path: lean tier-1 pass + exact re-decision of its rows
     AssignReq req;
-    req.accumulate = !(ablate & 1);
+    req.accumulate = true;
+    req.ablate = ablate & 11;
     req.scale = scale.as<float>();
     req.sums = a.sums;
     req.counts = a.counts;

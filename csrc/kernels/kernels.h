@@ -118,6 +118,12 @@ struct KMeansAssignArgs {
   int32_t* defer_rows = nullptr;
   unsigned* defer_row_count = nullptr;
   unsigned long long* deferred_rows = nullptr;  // optional counter of deferred rows
+  // Row-list (refine) mode: rows still unsure after the bf16x3 tier are appended to
+  // exact_rows ([grid][8][exact_sub_cap], one sub-segment per wave, counts exact_count
+  // [grid][8]) instead of re-deciding their whole 32-row group; kmeans_exact_rows finishes them.
+  int32_t* exact_rows = nullptr;
+  unsigned* exact_count = nullptr;
+  int64_t exact_sub_cap = 0;
 };
 // Lean tier-1 Lloyd kernel (kmeans_lloyd.hip): applicable when the centroid hi plane + the
 // fixed-point accumulator fit LDS and d + 4 bias features fit the padded width.
@@ -135,6 +141,20 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
 // The general fused kernel over the rows kmeans_lloyd deferred (a.row_list / row_count /
 // row_seg_cap from its defer outputs), on the same `grid`.
 void kmeans_assign_rows(const KMeansAssignArgs& a, int grid, hipStream_t s);
+// Exact fp32 re-decision of the rows kmeans_lloyd deferred (a.row_list / row_count /
+// row_seg_cap / row_subs = its defer outputs, same `grid`): one wave per row, the centers in
+// LDS, every candidate's distance on the VALU in the exact MFMA kernel's arithmetic (bitwise its
+// answer), then the row's cost, outputs and fixed-point statistics (global atomics).  Writes
+// `grid` cost partials.
+void kmeans_exact_rows(const KMeansAssignArgs& a, int grid, hipStream_t s);
+// Tiles per lean workgroup (each owns a contiguous range).
+int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid);
+// Delta-mode pruning scan in the lean layout: tile_list [lean_grid][tiles_per_block] segments,
+// tile_count [lean_grid] (zeroed here); otherwise as kmeans_prune_scan.
+void kmeans_lean_scan(int64_t n, int k, int d, int lean_grid, float* bounds,
+                      const int32_t* labels, const float* xnorm, const float* drift,
+                      const float* drift_max, const float* cstat, int32_t* tile_list,
+                      unsigned* tile_count, unsigned long long* pruned, hipStream_t s);
 
 // Delta-mode pruning scan (single launch): per 32-row tile, tests every row's bounds (labels,
 // xnorm, the centers' drift) exactly as the assign kernel's own pruning test does.  Tiles that

@@ -191,6 +191,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   const float mrel = 4e-7f * float(d + 8);
   const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);  // direct-form |x - c|^2 rounding
   unsigned long long n_pruned = 0;
+  unsigned n_exact = 0;  // row-list mode: rows this wave sent to the exact pass
   double my_cost = 0.0;
 
   // Bounds update carried into finish(): single launch: l = the row's new lower bound (distance);
@@ -665,7 +666,20 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
         }
       }
       bidx = k1 & 0x3ff;
-      if (__any(unsure)) {
+      bool to_exact = false;
+      if (a.exact_rows && rlist) {
+        // row-list mode: only the still-unsure rows go to the exact VALU pass (per-wave
+        // sub-segment, filled in position order: deterministic)
+        const unsigned long long um = __ballot(unsure && h == 0);
+        if (um) {
+          int32_t* seg = a.exact_rows + (int64_t(blockIdx.x) * kWaves + wave) * a.exact_sub_cap;
+          if (unsure && h == 0)
+            seg[n_exact + __popcll(um & ((1ull << lane) - 1ull))] = static_cast<int32_t>(row);
+          n_exact += static_cast<unsigned>(__popcll(um));
+          if (lane == 0 && a.refine_tiles) atomicAdd(a.refine_tiles, u64(__popcll(um)));
+        }
+        to_exact = unsure;
+      } else if (__any(unsure)) {
         // rare: re-decide the whole tile exactly (bitwise the PRECISE kernel's answer)
         exact_argmin<KS>(a.centers, DP, x, cn, kpad, d, r, h, bidx);
         if (lane == 0 && a.refine_tiles) atomicAdd(a.refine_tiles, 1ull);
@@ -702,7 +716,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
           bu.l = sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f);  // NaN (no second key) -> 0
         }
       }
-      finish(x, cb, bidx, row, valid, bu);
+      finish(x, cb, bidx, row, valid && !to_exact, bu);
     }
   };
 
@@ -732,6 +746,7 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
     }
   }
   if (lane == 0 && n_pruned && a.pruned_tiles) atomicAdd(a.pruned_tiles, n_pruned);
+  if (lane == 0 && a.exact_count && rlist) a.exact_count[blockIdx.x * kWaves + wave] = n_exact;
 
   // ---- deterministic per-block cost: fixed shuffle tree, waves in index order
   const double wsum = wave_sum_f64(my_cost);

@@ -10,6 +10,8 @@ constexpr int kAssignThreads = 512;  // 8 waves: 2 per SIMD with one workgroup p
 constexpr size_t kLdsLimit = 160 * 1024;
 // Deferral sub-segments per workgroup (one per wave of the lean kernel; count stride)
 constexpr int kDeferSubs = 16;
+// Exact-list sub-segments per workgroup (one per wave of the general kernel)
+constexpr int kExactSubs = kAssignThreads / 64;
 
 // Launches the MFMA assign kernel (d <= 128, centroids fit the LDS plan).  `grid` blocks.
 void launch_kmeans_assign_mfma(const KMeansAssignArgs& a, int grid, hipStream_t s);

@@ -2,28 +2,35 @@
 //
 // One pass over the local rows per Lloyd iteration (the reference's hot loop
 // is oneDAL's step1Local, mllib-dal/src/main/native/KMeansDALImpl.cpp:70-77): distances on the
-// bf16 matrix cores, top-2 argmin in registers, exact fp32 per-row cost, fixed-point per-cluster
-// sums in LDS.  Unlike the general fused kernel (kmeans_assign.hip) it evaluates ONE product per
-// k-step only (tier 1) and never escalates a whole 32-row tile: a row whose top-2 gap is inside
-// tier 1's rigorous error bound is appended to its workgroup's segment of a deferral list and
-// left untouched; the general kernel then re-decides exactly those rows (row-list mode: the
-// bf16x3 split, then exact fp32 where still unsure) and accumulates them.  So the answer is the
-// general kernel's — assignments identical to an exact fp32 evaluation — while the hot pass keeps
-// a fixed, branch-free instruction stream whatever the data's share of near ties.
+// fp16 matrix cores, top-2 argmin in registers, exact fp32 per-row cost, fixed-point per-cluster
+// sums in LDS.  It evaluates ONE product per k-step (tier 1) and never escalates a 32-row tile:
+// a row whose top-2 gap is inside the tier's rigorous error bound is appended to its wave's
+// segment of a deferral list and left untouched; oap_kmeans_exact_rows then re-decides exactly
+// those rows with the exact fp32 MFMA argmin (v_mfma_f32_32x32x2_f32) and accumulates them.  So
+// assignments are identical to an exact fp32 evaluation while the hot pass keeps a fixed,
+// branch-free instruction stream whatever the data's share of near ties.
 //
 // Design points (CDNA4):
 // * A wave owns a 32-row tile: lane (r = l & 31, h = l >> 5) holds features 16s + 8h + j of row
-//   r.  The centroid plane (bf16 hi part of -2c, plus bias features) is the MFMA A operand,
+//   r.  The centroid plane (fp16 of -2 alpha c, plus bias features) is the MFMA A operand,
 //   staged once per workgroup in LDS with an odd 16-byte-slot stride (conflict-free
-//   ds_read_b128); rows are the B operand straight from registers.
-// * Bias features carry both norms through the MFMA as hi/lo pairs: x' = [x, 1, 1, hi|x|^2,
-//   lo|x|^2], c' = [-2c, hi|c|^2, lo|c|^2, 1, 1], so the 32x32 accumulator ends at |x - c|^2
-//   with no seeding VALU and only the cross term carrying bf16 error.
-// * Only the hi plane lives in LDS (the general kernel also keeps the lo plane): the fixed-point
-//   fp64 accumulator fits beside it and the workgroup has 12-16 waves (3-4 per SIMD), so one
-//   wave's VALU epilogue, another's MFMAs and a third's HBM loads overlap.
-// * Tiles are dealt block-strided (block b: positions b, b + grid, ...), so a workgroup never
-//   processes more rows than kmeans_rows_per_block_bound assumes (fixed-point exactness).
+//   ds_read_b128); rows (fp16 of alpha x) are the B operand straight from registers.
+// * fp16, not bf16: 11 significant bits make tier 1's bound 8x tighter than bf16 at the same
+//   MFMA rate (v_mfma_f32_32x32x16_f16), so several times fewer rows are deferred on
+//   overlapping clusters.  alpha is a power of two with alpha * max|c| <= 2^8 (exact scaling),
+//   so centers and typical rows sit in fp16's normal range; a row too large for it
+//   (alpha^2 |x|^2 >= 2^20) is simply deferred.
+// * Bias features carry both norms through the MFMA as hi/lo pairs scaled by 2^-4:
+//   x' = [alpha x, 16, 16, hi, lo (alpha^2 |x|^2 / 16)], c' = [-2 alpha c, hi, lo
+//   (alpha^2 |c|^2 / 16), 16, 16], so the accumulator ends at alpha^2 |x - c|^2 with no seeding
+//   VALU and only the cross term carrying fp16 error.
+// * Only the fp16 plane lives in LDS: the fixed-point fp64 accumulator fits beside it and the
+//   workgroup has 16 waves (4 per SIMD), so one wave's VALU epilogue, another's MFMAs and a
+//   third's HBM loads overlap.
+// * Each workgroup owns a contiguous range of ceil(tiles / grid) tiles (never more rows than
+//   kmeans_rows_per_block_bound assumes: fixed-point exactness).  Delta passes read the
+//   workgroup's own segment of the scan's tile list (oap_kmeans_lean_scan), so no counter is
+//   shared by the whole grid.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -39,6 +46,10 @@ namespace {
 
 using namespace kmdev;
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+constexpr float kBiasUnit = 16.f;  // bias features' unit (2^4)
+
 // The kernel's own compact argument block (fewer SGPRs than KMeansAssignArgs).
 struct LeanArgs {
   const void* x;
@@ -53,18 +64,19 @@ struct LeanArgs {
   float* mindist;
   float2* bounds;
   float* xnorm;
-  const int32_t* tile_list;
-  const unsigned* tile_count;
+  const int32_t* tile_list;   // delta: [grid][tiles_per_block] segments
+  const unsigned* tile_count;  // delta: [grid]
   int32_t* defer_rows;
   unsigned* defer_row_count;
   u64* deferred_rows;
-  int64_t n, seg_cap;
+  int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
   int accumulate, sums_too, delta;
+  int ablate;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work
 };
 
 struct LeanSmem {
-  size_t plane, sc, acc, cnt, wcost, dcnt, total;
+  size_t plane, sc, acc, cnt, wcost, total;
 };
 
 __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bool acc, bool sums,
@@ -72,7 +84,7 @@ __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bo
   LeanSmem m;
   size_t off = 0;
   m.plane = 0;
-  off = round16(size_t(kpad) * stride_bf16(dp) * 2);
+  off = round16(size_t(kpad) * stride_bf16(dp) * 2);  // fp16 plane, same 2-byte layout
   m.sc = off;
   off = round16(off + size_t(dp) * 4);
   m.acc = off;
@@ -83,10 +95,19 @@ __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bo
   off = round16(off);
   m.wcost = off;
   off += size_t(waves) * 8;
-  m.dcnt = off;
-  off += 16;
   m.total = round16(off);
   return m;
+}
+
+// alpha: power of two with alpha * cmax <= 2^8 (cmax = max |c|)
+__device__ inline float lean_alpha(float cmax) {
+  const float c = fmaxf(cmax, 1e-30f);
+  return exp2f(floorf(log2f(256.f / c)));
+}
+
+__device__ inline void split_f16(float v, _Float16& hi, _Float16& lo) {
+  hi = static_cast<_Float16>(v);
+  lo = static_cast<_Float16>(v - static_cast<float>(hi));
 }
 
 template <int KS, bool XB, int WAVES, bool PF>
@@ -97,27 +118,34 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
   const bool accumulate = a.accumulate != 0;
+  const bool do_acc = accumulate && !(a.ablate & 1);
+  const bool do_cost = !(a.ablate & 2);
+  const bool do_dist = !(a.ablate & 8);
   const LeanSmem L = lean_plan(DP, kpad, k, d, accumulate, a.sums_too != 0, WAVES);
   const int sb = stride_bf16(DP);
-  __bf16* ph = reinterpret_cast<__bf16*>(smem + L.plane);
+  _Float16* ph = reinterpret_cast<_Float16*>(smem + L.plane);
   float* sc_l = reinterpret_cast<float*>(smem + L.sc);
   double* acc_l = reinterpret_cast<double*>(smem + L.acc);
   unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
   double* wcost = reinterpret_cast<double*>(smem + L.wcost);
   const int tid = threadIdx.x;
+  const float cmax = a.cstat[0];
+  const float alpha = lean_alpha(cmax);
+  const float a2 = alpha * alpha;
 
-  // ---- stage the centroid plane c' = [-2c, hi|c|^2, lo|c|^2, 1, 1] (bf16) once per workgroup
+  // ---- stage c' = [-2 alpha c, hi, lo (alpha^2 |c|^2 / 16), 16, 16] (fp16) once per workgroup
   for (int idx = tid; idx < kpad * DP; idx += NT) {
     const int c = idx / DP, f = idx - c * DP;
-    __bf16 v;
+    _Float16 v;
     if (f < d) {
-      v = static_cast<__bf16>(-2.f * a.centers[idx]);  // exact scaling: hi(-2c) == -2 hi(c)
+      v = static_cast<_Float16>(-2.f * alpha * a.centers[idx]);
     } else if (f == d || f == d + 1) {
-      __bf16 hi, lo;
-      bf16_split((c < k) ? a.cnorm[c] : 1e30f, hi, lo);  // padded centers: huge, finite
+      _Float16 hi, lo;
+      // padded centers: the largest finite bias (their distance never wins)
+      split_f16((c < k) ? a2 * a.cnorm[c] * (1.f / kBiasUnit) : 60000.f, hi, lo);
       v = (f == d) ? hi : lo;
     } else {
-      v = static_cast<__bf16>((f == d + 2 || f == d + 3) ? 1.f : 0.f);
+      v = static_cast<_Float16>((f == d + 2 || f == d + 3) ? kBiasUnit : 0.f);
     }
     ph[c * sb + f] = v;
   }
@@ -131,21 +159,25 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 
   const int lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const float cmax = a.cstat[0];
-  // tier-1 bound on two candidates' distance error: the cross term 2 x 2(2^-8 + 2^-18)|c||x|
-  // (times |x| below), the bias pairs 2^-17 (|c|^2 + |x|^2) each, fp32 accumulation
-  // 4e-5 (cmax^2 + |x|^2)
-  const float thr_c = 0.0157f * cmax;
-  const float thr_k = 6e-5f * cmax * cmax + 1e-30f;
+  // tier-1 bound on two candidates' distance error (alpha^2 units): the cross term
+  // 2 x 2 x 2^-10 |alpha c||alpha x| (fp16 products), fp16 subnormals d 2^-14, the bias pairs
+  // 2^-21 (|c|^2 + |x|^2), fp32 accumulation 4e-5 (cmax^2 + |x|^2), plus the key truncation
+  const float cm_s = alpha * cmax;
+  const float thr_c = 0.0040f * cm_s;
+  const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
   const float mrel = 4e-7f * float(d + 8);                // fp32 evaluation margin (bounds)
   const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);  // direct-form |x - c|^2 rounding
   const int64_t ntiles_all = (a.n + 31) / 32;
   const bool listed = a.tile_list != nullptr;
-  const int64_t npos = listed ? int64_t(*a.tile_count) : ntiles_all;
-  const int64_t stride = int64_t(gridDim.x) * WAVES;
-  int64_t t = int64_t(blockIdx.x) + int64_t(gridDim.x) * wave;
+  const int64_t T = a.tiles_per_block;
+  const int64_t t0 = int64_t(blockIdx.x) * T;  // this workgroup's first tile
+  const int64_t npos = listed ? int64_t(a.tile_count[blockIdx.x])
+                              : (t0 < ntiles_all ? (ntiles_all - t0 < T ? ntiles_all - t0 : T) : 0);
+  const int32_t* seg = listed ? a.tile_list + blockIdx.x * T : nullptr;
+  const int64_t stride = WAVES;
+  int64_t t = wave;
   // deferral: each wave owns a sub-segment of its workgroup's segment, filled in tile order, so
-  // the list (and everything the re-decision pass sums over it) is deterministic
+  // the list (and everything the exact pass sums over it) is deterministic
   const int64_t sub_cap = a.seg_cap / WAVES;
   int32_t* dseg = a.defer_rows + blockIdx.x * a.seg_cap + wave * sub_cap;
   unsigned n_def = 0;  // wave-uniform
@@ -153,9 +185,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const int jb = d - 16 * (KS - 1) - 8 * h;  // lane-local slot of bias feature d (may be < 0)
 
   auto tile_of = [&](int64_t q) -> int64_t {
-    if (!listed) return q < ntiles_all ? q : ntiles_all - 1;
-    if (npos == 0) return 0;  // (prefetch of an empty list: any real tile)
-    const int64_t tl = int64_t(a.tile_list[q < npos ? q : npos - 1]);
+    if (npos == 0) return 0;  // (prefetch of an empty range: any real tile)
+    q = q < npos ? q : npos - 1;
+    if (!listed) return t0 + q;
+    const int64_t tl = int64_t(seg[q]);
     return tl < 0 ? 0 : (tl < ntiles_all ? tl : ntiles_all - 1);
   };
   auto load_tile = [&](int64_t tile, F& dst) {
@@ -212,8 +245,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
   };
 
-  auto process = [&](const int64_t pos, const F& x, F& xn, const int64_t pf) {
-    const int64_t tile = tile_of(pos);
+  auto process = [&](const int64_t pos, const int64_t tile, const F& x, F& xn,
+                     const int64_t pf) {
     const int64_t row = tile * 32 + r;
     const bool valid = pos < npos && row < a.n;
     if constexpr (PF) load_tile(tile_of(pf), xn);  // next tile: in flight under this one's work
@@ -231,25 +264,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));
       if (lane == 0) a.xnorm[tile] = tmax;
     }
-    // MFMA B operand: the row's bf16 values with the bias slots [1, 1, hi|x|^2, lo|x|^2]
-    bf16x8 xh[KS];
+    const float nx2_s = a2 * nx2;
+    // MFMA B operand: fp16 of alpha x with the bias slots [16, 16, hi, lo (alpha^2 |x|^2 / 16)]
+    f16x8 xh[KS];
     {
-      __bf16 nh, nl;
-      bf16_split(nx2, nh, nl);
-      const __bf16 one = static_cast<__bf16>(1.f);
+      _Float16 nh, nl;
+      split_f16(nx2_s * (1.f / kBiasUnit), nh, nl);
+      const _Float16 unit = static_cast<_Float16>(kBiasUnit);
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
-        bf16x8 v;
-        if constexpr (XB) {
-          v = x.v[s];
-        } else {
+        f16x8 v;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = static_cast<__bf16>(x.v[s][j]);
-        }
+        for (int j = 0; j < 8; ++j) v[j] = static_cast<_Float16>(alpha * x.at(s, j));
         if (s == KS - 1) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            v[j] = (j == jb || j == jb + 1) ? one : v[j];
+            v[j] = (j == jb || j == jb + 1) ? unit : v[j];
             v[j] = (j == jb + 2) ? nh : v[j];
             v[j] = (j == jb + 3) ? nl : v[j];
           }
@@ -257,23 +287,27 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         xh[s] = v;
       }
     }
-    // ---- tier 1: one bf16 product per k-step; top-2 on integer keys (the distance's bits with
+    // ---- tier 1: one fp16 product per k-step; top-2 on integer keys (the distance's bits with
     // the low 10 mantissa bits replaced by the in-chunk offset; value order, lowest index first)
     int k1 = 0x7fffffff, k2 = 0x7fffffff;
     auto mfma_chunk = [&](int c0, f32x16& acc) {
-      const __bf16* ap = ph + size_t(c0 + r) * sb + 8 * h;
-      bf16x8 av[KS];
+      const _Float16* ap = ph + size_t(c0 + r) * sb + 8 * h;
+      f16x8 av[KS];
 #pragma unroll
-      for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const bf16x8*>(ap + 16 * s);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[0], xh[0], f32x16{}, 0, 0, 0);
+      for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], xh[0], f32x16{}, 0, 0, 0);
 #pragma unroll
       for (int s = 1; s < KS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[s], xh[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], xh[s], acc, 0, 0, 0);
     };
     auto epilogue = [&](int c0, const f32x16& acc) {
       int t1[4], t2[4];
+      // candidate groups of 8 centers at or past k are padding: skip them (wave-uniform; only
+      // the last chunk has any)
+      const int ng = k - c0 >= 32 ? 4 : (k - c0 + 7) / 8;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
+        if (e >= 4 && (e >> 2) >= ng) break;
         const int off = 8 * (e >> 2) + (e & 3);
         const int key = (__float_as_int(acc[e]) & ~0x3ff) | off;
         const int q = e & 3;
@@ -297,20 +331,28 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       k2 = min(max(k1, i1), min(k2, i2));
       k1 = min(k1, i1);
     };
-    for (int c0 = 0; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
-      f32x16 acc;
-      mfma_chunk(c0, acc);
-      epilogue(c0, acc);
-    }
-    {
+    bool unsure;
+    float b2 = 0.f, tt = 0.f;
+    if (do_dist) {
+      for (int c0 = 0; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
+        f32x16 acc;
+        mfma_chunk(c0, acc);
+        epilogue(c0, acc);
+      }
       const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
       k2 = min(max(k1, o1), min(k2, o2));
       k1 = min(k1, o1);
+      const float b1 = __int_as_float(k1 & ~0x3ff);
+      b2 = __int_as_float(k2 & ~0x3ff);
+      tt = fmaf(thr_c, sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
+      // rows beyond fp16's comfortable range (alpha |x| >= 2^10) are always re-decided
+      unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
+    } else {
+      k1 = r % k;
+      b2 = 3e38f;
+      unsure = false;
     }
-    const float b1 = __int_as_float(k1 & ~0x3ff), b2 = __int_as_float(k2 & ~0x3ff);
-    const float tt = fmaf(thr_c, sqrtf(nx2), thr_k) + 2.5e-4f * fabsf(b2);  // + key truncation
-    const bool unsure = valid && !(b2 - b1 > tt);
-    // ---- defer unsure rows to the exact re-decision (one LDS atomic per wave with any)
+    // ---- defer unsure rows to the exact re-decision (wave-private sub-segment, in order)
     const unsigned long long um = __ballot(unsure && h == 0);
     if (um) {
       if (unsure && h == 0)
@@ -321,8 +363,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     int b = k1 & 0x3ff;
     b = (b < k) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
     float cb[KS][8];
-    load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cb);  // L2-resident; lands under the adds
-    if (done && accumulate) {
+    if (do_cost) {
+      load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cb);  // L2-resident; lands under the adds
+    } else {
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
+    }
+    if (done && do_acc) {
       if (!a.delta) {
         add_row(x, b, false);
       } else if (old >= 0 && old != b) {  // delta: only moved rows change the statistics
@@ -343,8 +392,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       if (a.labels) a.labels[row] = b;
       if (a.mindist) a.mindist[row] = rowcost;
       if (a.bounds) {
-        const float lo = b2 - (tt + mrel * (nx2 + cmax * cmax));
-        a.bounds[row] = make_float2(sqrtf(rowcost) * ueps + 1e-30f, sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
+        // every other candidate's alpha^2 distance is >= b2 - tt; back to data units
+        const float lo = (b2 - (tt + mrel * (nx2_s + cm_s * cm_s))) / a2;
+        a.bounds[row] =
+            make_float2(sqrtf(rowcost) * ueps + 1e-30f, sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
       }
       my_cost += double(rowcost);
     }
@@ -354,15 +405,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     F xa, xb;
     load_tile(tile_of(t), xa);
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      process(t, xa, xb, t + stride);
+      process(t, tile_of(t), xa, xb, t + stride);
       if (t + stride >= npos) break;
-      process(t + stride, xb, xa, t + 2 * stride);
+      process(t + stride, tile_of(t + stride), xb, xa, t + 2 * stride);
     }
   } else {
     F xa;
+    int64_t tl = tile_of(t);
     for (; t < npos; t += stride) {
-      load_tile(tile_of(t), xa);
-      process(t, xa, xa, 0);
+      const int64_t tcur = tl;
+      load_tile(tcur, xa);
+      tl = tile_of(t + stride);  // listed passes: the next tile index lands under this tile
+      process(t, tcur, xa, xa, 0);
     }
   }
 
@@ -432,6 +486,361 @@ void launch_lean_xb(const LeanArgs& a, int grid, int variant, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------- exact re-decision
+// The rows the lean pass deferred, 32 per wave step (gathered by index), re-decided with the
+// exact fp32 MFMA argmin (v_mfma_f32_32x32x2_f32, the PRECISE kernel's arithmetic: bitwise its
+// answer) against fp32 centers staged in LDS, then finished as the assign kernels finish a row:
+// exact cost, labels / mindist / bounds, fixed-point statistics (LDS fp64 accumulator when it
+// fits, else global int64 atomics).  Rows: the lean workgroup's deferral sub-segments in order
+// (deterministic).
+constexpr int kExactWaves = 8;
+
+struct ExactSmem {
+  size_t ct, cn, sc, acc, cnt, wc, pref, total;
+  bool lds_acc;
+};
+
+__host__ __device__ inline ExactSmem exact_plan(int kpad, int k, int d, bool acc, bool sums) {
+  const int dp = (d + 15) / 16 * 16;
+  ExactSmem m;
+  size_t off = 0;
+  m.ct = 0;
+  off = round16(size_t(kpad) * (dp + 4) * 4);  // row stride dp + 4: 16-byte reads spread banks
+  m.cn = off;
+  off = round16(off + size_t(kpad) * 4);
+  m.sc = off;
+  off = round16(off + size_t(dp) * 4);
+  m.acc = off;
+  const size_t base = off;
+  size_t accb = (acc && sums) ? size_t(k) * (d | 1) * 8 : 0;
+  size_t cntb = acc ? size_t(k) * 4 : 0;
+  m.lds_acc = acc && round16(base + accb) + round16(cntb) + 256 <= kLdsLimit - 1024;
+  if (!m.lds_acc) accb = cntb = 0;
+  off = round16(off + accb);
+  m.cnt = off;
+  off = round16(off + cntb);
+  m.wc = off;
+  off += kExactWaves * 8;
+  m.pref = off;
+  off += (kDeferSubs + 1) * 4;
+  m.total = round16(off);
+  return m;
+}
+
+template <int KS, bool XB>
+__global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeansAssignArgs a) {
+  constexpr int DP = 16 * KS;
+  constexpr int CS = DP + 4;
+  using F = Frag<KS, XB>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int k = a.k, d = a.d, kpad = a.kpad;
+  const bool accumulate = a.accumulate;
+  const ExactSmem L = exact_plan(kpad, k, d, accumulate, a.sums_too);
+  float* ct = reinterpret_cast<float*>(smem + L.ct);
+  float* cn = reinterpret_cast<float*>(smem + L.cn);
+  float* sc_l = reinterpret_cast<float*>(smem + L.sc);
+  double* acc_l = reinterpret_cast<double*>(smem + L.acc);
+  unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
+  double* wc = reinterpret_cast<double*>(smem + L.wc);
+  unsigned* pref = reinterpret_cast<unsigned*>(smem + L.pref);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  constexpr int NT = kExactWaves * 64;
+  if (tid == 0) {
+    pref[0] = 0u;
+    for (int w = 0; w < a.row_subs; ++w)
+      pref[w + 1] = pref[w] + a.row_count[blockIdx.x * kDeferSubs + w];
+  }
+  __syncthreads();
+  const unsigned total = pref[a.row_subs];
+  if (total == 0) {  // nothing deferred here: still write this block's (zero) cost partial
+    if (tid == 0 && a.cost_slab) a.cost_slab[blockIdx.x] = 0.0;
+    return;
+  }
+  for (int i = tid; i < kpad * DP; i += NT) {
+    const int c = i / DP, f = i - c * DP;
+    ct[c * CS + f] = a.centers[i];
+  }
+  for (int c = tid; c < kpad; c += NT) cn[c] = (c < k) ? a.cnorm[c] : 1e30f;
+  for (int f = tid; f < DP; f += NT) sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
+  if (L.lds_acc) {
+    if (a.sums_too)
+      for (int i = tid; i < k * (d | 1); i += NT) acc_l[i] = 0.0;
+    for (int i = tid; i < k; i += NT) cnt_l[i] = 0u;
+  }
+  __syncthreads();
+  const int64_t sub = a.row_seg_cap / a.row_subs;
+  const float cmax = a.cstat[0];
+  const float mrel = 4e-7f * float(d + 8);
+  const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);
+  const int64_t ngroups = (int64_t(total) + 31) / 32;
+  auto row_at = [&](int64_t i) -> int64_t {  // i-th deferred row of this workgroup (clamped)
+    i = i < int64_t(total) ? i : int64_t(total) - 1;
+    int w = 0;
+    while (w + 1 < a.row_subs && int64_t(pref[w + 1]) <= i) ++w;
+    return int64_t(a.row_list[int64_t(blockIdx.x) * a.row_seg_cap + w * sub + (i - pref[w])]);
+  };
+  auto load_rows = [&](int64_t g, F& dst) {
+    const int64_t row = row_at(g * 32 + r);
+    if constexpr (XB) {
+      const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const int f = 16 * s + 8 * h;
+        dst.v[s] = (s < KS - 1 || f < a.ld) ? *reinterpret_cast<const bf16x8*>(p + 16 * s)
+                                            : bf16x8{};
+      }
+    } else {
+      const float* p = static_cast<const float*>(a.x) + row * a.ld + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int f = 16 * s + 8 * h + 4 * q;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (s < KS - 1 || f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+          dst.v[s][4 * q + 0] = v.x;
+          dst.v[s][4 * q + 1] = v.y;
+          dst.v[s][4 * q + 2] = v.z;
+          dst.v[s][4 * q + 3] = v.w;
+        }
+    }
+  };
+  auto add_row = [&](const F& xv, int b, bool neg) {
+    if (L.lds_acc) {
+      if (h == 0) atomicAdd(&cnt_l[b], neg ? 0xffffffffu : 1u);
+    } else if (h == 0) {
+      atomicAdd(&a.counts[b], neg ? ~0ull : 1ull);
+    }
+    if (!a.sums_too) return;
+    const float sgn = neg ? -1.f : 1.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = 16 * s + 8 * h + j;
+        if (f < d) {
+          const float q = sgn * rintf(xv.at(s, j) * sc_l[f]);
+          if (L.lds_acc)
+            atomicAdd(acc_l + b * (d | 1) + f, static_cast<double>(q));
+          else
+            atomicAdd(&a.sums[size_t(b) * d + f], static_cast<u64>(static_cast<long long>(q)));
+        }
+      }
+  };
+  double my_cost = 0.0;
+  F xa, xb;
+  int64_t g = wave;
+  load_rows(g, xa);
+  for (; g < ngroups; g += kExactWaves) {  // wave-uniform
+    const int64_t i = g * 32 + r;
+    const bool valid = i < int64_t(total);
+    const int64_t row = row_at(i);
+    F& x = xa;
+    load_rows(g + kExactWaves, xb);  // next group: in flight under this one's MFMAs
+    // exact argmin with the best and second-best exact distances (the second for the bounds)
+    float best = INFINITY, second = INFINITY;
+    int bidx = 0x7fffffff;
+    for (int c0 = 0; c0 < kpad; c0 += 32) {
+      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const float* cp = ct + size_t(c0 + r) * CS + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (16 * s + 4 * q < d) {  // wave-uniform: skip all-padding groups (as exact_argmin)
+            const float4 a4 = *reinterpret_cast<const float4*>(cp + 16 * s + 4 * q);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, x.at(s, 4 * q + 0), acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, x.at(s, 4 * q + 1), acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, x.at(s, 4 * q + 2), acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, x.at(s, 4 * q + 3), acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const float4 c4 = *reinterpret_cast<const float4*>(cn + c0 + 8 * gq + 4 * h);
+        const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float dist = fmaf(-2.f, acc[4 * gq + q], cv[q]);
+          if (dist < best) {
+            second = best;
+            best = dist;
+            bidx = c0 + 8 * gq + 4 * h + q;
+          } else if (dist < second) {
+            second = dist;
+          }
+        }
+      }
+    }
+    {
+      const float ob = __shfl_xor(best, 32, 64), os = __shfl_xor(second, 32, 64);
+      const int oi = __shfl_xor(bidx, 32, 64);
+      const bool take = ob < best || (ob == best && oi < bidx);
+      second = take ? fminf(best, os) : fminf(second, ob);
+      if (take) {
+        best = ob;
+        bidx = oi;
+      }
+    }
+    const int b = (bidx >= 0 && bidx < k) ? bidx : 0;
+    int old = -1;
+    if (a.delta && valid) old = a.labels[row];
+    // exact cost and |x|^2 in the assign kernels' lane order
+    float part = 0.f, px = 0.f;
+    const float* cb = ct + size_t(b) * CS + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = x.at(s, j) - cb[16 * s + j];
+        part = fmaf(e, e, part);
+        px = fmaf(x.at(s, j), x.at(s, j), px);
+      }
+    const float rowcost = part + __shfl_xor(part, 32, 64);
+    const float nx2 = px + __shfl_xor(px, 32, 64);
+    if (valid && accumulate && !(a.delta && (old == b || old < 0))) {
+      add_row(x, b, false);
+      if (a.delta) add_row(x, min(old, k - 1), true);
+    }
+    if (valid && h == 0) {
+      if (a.labels) a.labels[row] = b;
+      if (a.mindist) a.mindist[row] = rowcost;
+      if (a.bounds) {
+        const float marg = mrel * (nx2 + cmax * cmax);
+        reinterpret_cast<float2*>(a.bounds)[row] =
+            make_float2(sqrtf(rowcost) * ueps + 1e-30f,
+                        sqrtf(fmaxf(second + nx2 - 2.f * marg, 0.f)) * (1.f - 1e-6f));
+      }
+      my_cost += double(rowcost);
+    }
+    xa = xb;
+  }
+  const double ws = wave_sum_f64(my_cost);
+  if (lane == 0) wc[wave] = ws;
+  __syncthreads();
+  if (tid == 0 && a.cost_slab) {
+    double tot = 0.0;
+    for (int w = 0; w < kExactWaves; ++w) tot += wc[w];
+    a.cost_slab[blockIdx.x] = tot;
+  }
+  if (L.lds_acc) {
+    for (int i = tid; a.sums_too && i < k * d; i += NT) {
+      const int c = i / d, f = i - c * d;
+      const double v = acc_l[c * (d | 1) + f];  // an exact integer
+      if (v != 0.0) atomicAdd(&a.sums[i], static_cast<u64>(static_cast<long long>(v)));
+    }
+    for (int i = tid; i < k; i += NT) {
+      const int c = static_cast<int>(cnt_l[i]);
+      if (c) atomicAdd(&a.counts[i], static_cast<u64>(static_cast<long long>(c)));
+    }
+  }
+}
+
+template <int KS, bool XB>
+void launch_exact(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  const ExactSmem L = exact_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too);
+  static bool attr_set = false;
+  if (!attr_set) {
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_kmeans_exact_rows<KS, XB>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(kLdsLimit)));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((oap_kmeans_exact_rows<KS, XB>), dim3(grid), dim3(kExactWaves * 64), L.total,
+                     s, a);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+template <bool XB>
+void launch_exact_xb(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  switch ((a.d + 15) / 16) {
+    case 1: launch_exact<1, XB>(a, grid, s); break;
+    case 2: launch_exact<2, XB>(a, grid, s); break;
+    case 3: launch_exact<3, XB>(a, grid, s); break;
+    case 4: launch_exact<4, XB>(a, grid, s); break;
+    case 5: launch_exact<5, XB>(a, grid, s); break;
+    case 6: launch_exact<6, XB>(a, grid, s); break;
+    case 7: launch_exact<7, XB>(a, grid, s); break;
+    case 8: launch_exact<8, XB>(a, grid, s); break;
+    default: OAP_THROW(ConfigError, "kmeans_exact_rows: unsupported d=" << a.d);
+  }
+}
+
+// ---------------------------------------------------------------- delta scan (lean layout)
+// The pruning test of every row of a lean workgroup's tile range (the assign kernels' own test,
+// with the tile's largest |x|^2 in the margin — never looser per row); pruned tiles get their
+// bounds advanced in place (rounded outward; no write once no center moves), the others are
+// appended to that workgroup's segment of tile_list.  Scan block (b, j) covers chunks j, j + S,
+// ... of lean workgroup b's range, so every counter is shared by S blocks only.
+constexpr int kScanSplit = 8;
+
+__global__ __launch_bounds__(256) void oap_kmeans_lean_scan(
+    int64_t n, int k, int d, int lean_grid, int64_t tiles_per_block, float2* __restrict__ bounds,
+    const int32_t* __restrict__ labels, const float* __restrict__ xnorm,
+    const float* __restrict__ drift, const float* __restrict__ drift_max,
+    const float* __restrict__ cstat, int32_t* __restrict__ tile_list,
+    unsigned* __restrict__ tile_count, unsigned long long* __restrict__ pruned) {
+  __shared__ unsigned wcnt[4], wbase[4];
+  __shared__ unsigned long long bpruned;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+  const int lb = blockIdx.x % lean_grid, j = blockIdx.x / lean_grid;
+  const float dmax = drift_max[0];
+  const float cmax = cstat[0];
+  const float mrel = 4e-7f * float(d + 8);
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t T = tiles_per_block;
+  const int64_t t0 = int64_t(lb) * T;
+  const int64_t t1 = t0 + T < ntiles ? t0 + T : ntiles;
+  const int64_t nchunks = t1 > t0 ? (t1 - t0 + 7) / 8 : 0;  // a chunk = 8 tiles, 2 per wave
+  int32_t* seg = tile_list + int64_t(lb) * T;
+  if (threadIdx.x == 0) bpruned = 0;
+  unsigned long long n_pruned = 0;
+  for (int64_t c = j; c < nchunks; c += kScanSplit) {  // block-uniform trip count
+    const int64_t w0 = t0 + c * 8 + 2 * wave;  // this wave's first tile
+    const int64_t row = w0 * 32 + lane;
+    const bool valid = w0 + h < t1 && row < n;
+    bool ok = true;
+    float2 bnew = make_float2(0.f, 0.f);
+    if (valid) {
+      const float2 b = bounds[row];
+      const int lab = min(max(labels[row], 0), k - 1);
+      const float u = b.x + drift[lab];
+      const float lk = b.y - dmax;
+      ok = lk > 0.f && (lk - u) * (lk + u) > mrel * (xnorm[row >> 5] + cmax * cmax);
+      bnew = make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f));
+    }
+    const unsigned long long all_ok = __ballot(ok);
+    const bool pr0 = static_cast<unsigned>(all_ok) == 0xffffffffu;
+    const bool pr1 = static_cast<unsigned>(all_ok >> 32) == 0xffffffffu;
+    if (dmax > 0.f && valid && (h ? pr1 : pr0)) bounds[row] = bnew;
+    const bool has0 = w0 < t1, has1 = w0 + 1 < t1;
+    const bool act0 = has0 && !pr0, act1 = has1 && !pr1;
+    if (lane == 0) {
+      wcnt[wave] = unsigned(act0) + unsigned(act1);
+      n_pruned += unsigned(has0 && pr0) + unsigned(has1 && pr1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      unsigned pos = tot ? atomicAdd(tile_count + lb, tot) : 0u;
+      for (int i = 0; i < 4; ++i) {
+        wbase[i] = pos;
+        pos += wcnt[i];
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      unsigned pos = wbase[wave];
+      if (act0) seg[pos++] = static_cast<int32_t>(w0);
+      if (act1) seg[pos] = static_cast<int32_t>(w0 + 1);
+    }
+  }
+  if (lane == 0 && n_pruned) atomicAdd(&bpruned, n_pruned);
+  __syncthreads();
+  if (threadIdx.x == 0 && bpruned && pruned) atomicAdd(pruned, bpruned);
+}
+
 }  // namespace
 
 bool kmeans_lloyd_supported(int d, int k, bool accumulate, bool sums_too) {
@@ -440,13 +849,19 @@ bool kmeans_lloyd_supported(int d, int k, bool accumulate, bool sums_too) {
   if (dp != kmeans_dp(d)) return false;  // the centroid buffer's row stride must match
   const int kpad = (k + 31) / 32 * 32;
   if (kpad > 1024) return false;  // keys carry a 10-bit index
-  return lean_plan(dp, kpad, k, d, accumulate, sums_too, 16).total <= kLdsLimit;
+  return lean_plan(dp, kpad, k, d, accumulate, sums_too, 16).total <= kLdsLimit &&
+         exact_plan(kpad, k, d, accumulate, sums_too).total <= kLdsLimit;
 }
 
 int kmeans_lloyd_grid(int64_t n, int num_cus) {
   const int64_t tiles = (n + 31) / 32;
   const int64_t cap = num_cus > 256 ? num_cus : 256;
   return static_cast<int>(tiles < cap ? (tiles < 1 ? 1 : tiles) : cap);
+}
+
+int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid) {
+  const int64_t tiles = (n + 31) / 32;
+  return (tiles + grid - 1) / grid;
 }
 
 int kmeans_lloyd_waves(int variant) {
@@ -458,8 +873,7 @@ int kmeans_lloyd_waves(int variant) {
 }
 
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
-  const int64_t tiles = (n + 31) / 32;
-  const int64_t per_block = (tiles + grid - 1) / grid;  // positions of one workgroup
+  const int64_t per_block = kmeans_lloyd_tiles_per_block(n, grid);
   return int64_t(waves) * ((per_block + waves - 1) / waves) * 32;
 }
 
@@ -469,8 +883,8 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, kmeans_lloyd_waves(variant)) &&
                 a.ld == kmeans_ld(a.d, a.xbf16),
             "kmeans_lloyd: unsupported arguments");
-  OAP_CHECK(!a.delta || (a.labels && a.tile_list && a.tile_count),
-            "kmeans_lloyd: delta mode needs labels and the scan's tile list");
+  OAP_CHECK(!a.delta || a.labels, "kmeans_lloyd: delta mode needs the previous labels");
+  OAP_CHECK(!a.tile_list || (a.delta && a.tile_count), "kmeans_lloyd: tile list without delta");
   if (a.n == 0) return 0;
   LeanArgs l;
   l.x = a.x;
@@ -492,6 +906,7 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.deferred_rows = a.deferred_rows;
   l.n = a.n;
   l.seg_cap = a.row_seg_cap;
+  l.tiles_per_block = kmeans_lloyd_tiles_per_block(a.n, grid);
   l.ld = a.ld;
   l.d = a.d;
   l.k = a.k;
@@ -499,11 +914,39 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.accumulate = a.accumulate;
   l.sums_too = a.sums_too;
   l.delta = a.delta;
+  l.ablate = a.ablate;
   if (a.xbf16)
     launch_lean_xb<true>(l, grid, variant, s);
   else
     launch_lean_xb<false>(l, grid, variant, s);
   return grid;
+}
+
+void kmeans_exact_rows(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  OAP_CHECK(a.row_list && a.row_count && a.row_seg_cap > 0 && a.row_subs >= 1 &&
+                a.row_subs <= kDeferSubs && a.d <= 128 && a.cstat &&
+                a.ld == kmeans_ld(a.d, a.xbf16),
+            "kmeans_exact_rows: bad arguments");
+  if (a.n == 0) return;
+  OAP_CHECK(exact_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too).total <= kLdsLimit,
+            "kmeans_exact_rows: centers exceed LDS");
+  if (a.xbf16)
+    launch_exact_xb<true>(a, grid, s);
+  else
+    launch_exact_xb<false>(a, grid, s);
+}
+
+void kmeans_lean_scan(int64_t n, int k, int d, int lean_grid, float* bounds,
+                      const int32_t* labels, const float* xnorm, const float* drift,
+                      const float* drift_max, const float* cstat, int32_t* tile_list,
+                      unsigned* tile_count, unsigned long long* pruned, hipStream_t s) {
+  if (n <= 0) return;
+  OAP_HIP_CHECK(hipMemsetAsync(tile_count, 0, sizeof(unsigned) * lean_grid, s));
+  hipLaunchKernelGGL(oap_kmeans_lean_scan, dim3(lean_grid * kScanSplit), dim3(256), 0, s, n, k, d,
+                     lean_grid, kmeans_lloyd_tiles_per_block(n, lean_grid),
+                     reinterpret_cast<float2*>(bounds), labels, xnorm, drift, drift_max, cstat,
+                     tile_list, tile_count, pruned);
+  OAP_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace kern

@@ -246,7 +246,12 @@ def test_batched_iterations_match_stepwise(native):
     b = native.kmeans_fit(g, native.LocalComm(True), t, init, 16, 11, 0.0)
     assert a["num_iter"] == 11 and b["num_iter"] == 11
     assert np.array_equal(a["centers"], b["centers"])
-    np.testing.assert_array_equal(a["cost_history"], b["cost_history"])  # NaN-aware
+    # scan (pruned) iterations report no cost (NaN); where the batched and the stepwise loop
+    # chose them differs (adaptive per batch vs per iteration), every reported cost agrees
+    ha, hb = np.array(a["cost_history"]), np.array(b["cost_history"])
+    both = np.isfinite(ha) & np.isfinite(hb)
+    assert both[0] and np.isfinite(ha[-1]) and np.isfinite(hb[-1])
+    np.testing.assert_allclose(ha[both], hb[both], rtol=1e-12)
     assert a["last_counts"] == b["last_counts"]
 
 
