@@ -1091,7 +1091,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   auto* flh = flags_hb.as<kern::KMeansFlags>();
   bool stop = false;
   int scan_iters = 0;  // scan passes in the current batch
-  std::vector<char> it_scanned(B, 0);
+  std::vector<char> it_scanned(B, 0), it_costless(B, 0);
+  bool last_costless = false;  // the last iteration computed no cost (rank-uniform)
   for (int it0 = 0, nb_it = 0; it0 < p.max_iter && !stop; it0 += nb_it) {
     // the first batch is short so the adaptive choices (tier, scan) are made early
     nb_it = std::min(it0 == 0 && B > 3 ? 3 : B, p.max_iter - it0);
@@ -1120,6 +1121,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         req.drift_max = drift_in ? drift_b.as<float>() + k : nullptr;
       }
       req.delta = delta_it;
+      // lean iterations compute the exact cost only where it is reported: the first and a
+      // known last iteration (fixed count); otherwise the final cost comes from one exact pass
+      // over the labels after the loop
+      const bool cost_it = !req.fast1 || !delta_all || it == 0 ||
+                           (p.tol < 0 && it == p.max_iter - 1);
+      req.cost_slab = cost_it ? slab.as<double>() : nullptr;
+      it_costless[b] = !cost_it || scan_it_all;
+      last_costless = it_costless[b];
       if (scan_it) {
         kern::kmeans_lean_scan(x.rows, k, d, lgrid, req.bounds, req.labels, req.xnorm,
                                req.drift, req.drift_max, g.cstat.as<float>(),
@@ -1190,7 +1199,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         Logger::instance().log(LogLevel::Info, "kmeans/iteration", os.str());
       }
       // scan iterations sum the cost of the tiles they read only: not a cost
-      const double c_it = it_scanned[b] ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
+      const double c_it = it_costless[b] ? std::numeric_limits<double>::quiet_NaN() : fl.cost;
       res.cost = c_it;
       res.cost_history.push_back(c_it);
       res.shift_history.push_back(std::sqrt(std::max(fl.max_shift2, 0.0)));
@@ -1240,7 +1249,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
     }
   }
-  if (scan_all && last_scanned && res.num_iter > 1) {
+  if (delta_all && last_costless && res.num_iter > 1) {
     // exact cost of a last scan iteration: every row against the centers it was assigned to,
     // with the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
     TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
@@ -1396,7 +1405,7 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
     req.scale = scale.as<float>();
     req.sums = a.sums;
     req.counts = a.counts;
-    req.cost_slab = a.cost_slab;
+    req.cost_slab = (ablate & 4) ? nullptr : a.cost_slab;  // 4: the Lloyd pass without a cost
     req.fast1 = true;
     Buffer dr = ctx.alloc(sizeof(u64));
     ctx.memset(dr.data(), 0, sizeof(u64), s);

@@ -110,7 +110,15 @@ __device__ inline void split_f16(float v, _Float16& hi, _Float16& lo) {
   lo = static_cast<_Float16>(v - static_cast<float>(hi));
 }
 
-template <int KS, bool XB, int WAVES, bool PF>
+// PF: 0 = no prefetch; 1 = double-buffered rows (prefetch the next tile into a second register
+// set); 2 = the next tile is loaded into the current tile's registers as soon as its fp16
+// operands are built, and the current tile is re-read (L2 / Infinity Cache) for the cost and
+// the accumulation — a prefetch that costs no extra registers across the MFMA phase.
+// COST: compute each row's exact cost (|x - c|^2 in fp32, direct form) and mindist; without it
+// the row's f32 values are not needed after its fp16 operands are built (rows that accumulate
+// re-read theirs), so PF 2 can reuse their registers, and the bounds' upper half comes from the
+// tier-1 distance plus its error bound.
+template <int KS, bool XB, int WAVES, int PF, bool COST>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a) {
   constexpr int DP = 16 * KS;
   constexpr int NT = WAVES * 64;
@@ -245,11 +253,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
   };
 
-  auto process = [&](const int64_t pos, const int64_t tile, const F& x, F& xn,
-                     const int64_t pf) {
+  auto process = [&](const int64_t pos, const int64_t tile, F& x, F& xn, const int64_t pf) {
     const int64_t row = tile * 32 + r;
     const bool valid = pos < npos && row < a.n;
-    if constexpr (PF) load_tile(tile_of(pf), xn);  // next tile: in flight under this one's work
+    if constexpr (PF == 1) load_tile(tile_of(pf), xn);  // next tile: in flight under this one
     int old = -1;
     if (a.delta && valid) old = a.labels[row];
     float nx2 = 0.f;
@@ -287,6 +294,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         xh[s] = v;
       }
     }
+    if constexpr (PF == 2) load_tile(tile_of(pf), x);  // x's registers now carry the next tile
     // ---- tier 1: one fp16 product per k-step; top-2 on integer keys (the distance's bits with
     // the low 10 mantissa bits replaced by the in-chunk offset; value order, lowest index first)
     int k1 = 0x7fffffff, k2 = 0x7fffffff;
@@ -332,7 +340,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       k1 = min(k1, i1);
     };
     bool unsure;
-    float b2 = 0.f, tt = 0.f;
+    float b1 = 0.f, b2 = 0.f, tt = 0.f;
     if (do_dist) {
       for (int c0 = 0; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
         f32x16 acc;
@@ -342,7 +350,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
       k2 = min(max(k1, o1), min(k2, o2));
       k1 = min(k1, o1);
-      const float b1 = __int_as_float(k1 & ~0x3ff);
+      b1 = __int_as_float(k1 & ~0x3ff);
       b2 = __int_as_float(k2 & ~0x3ff);
       tt = fmaf(thr_c, sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
       // rows beyond fp16's comfortable range (alpha |x| >= 2^10) are always re-decided
@@ -362,46 +370,68 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     const bool done = valid && !unsure;
     int b = k1 & 0x3ff;
     b = (b < k) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
-    float cb[KS][8];
-    if (do_cost) {
-      load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cb);  // L2-resident; lands under the adds
-    } else {
+    const bool acc_row = done && do_acc && (!a.delta || (old >= 0 && old != b));
+    if constexpr (COST) {
+      F xr_buf;
+      if constexpr (PF == 2) load_tile(tile, xr_buf);  // re-read this tile (cache-resident)
+      const F& xr = (PF == 2) ? xr_buf : x;
+      float cb[KS][8];
+      if (do_cost) {
+        load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cb);  // L2-resident; lands under adds
+      } else {
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
+      }
+      if (acc_row) {
+        add_row(xr, b, false);
+        if (a.delta) add_row(xr, min(old, k - 1), true);  // delta: a moved row
+      }
+      float part = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
-    }
-    if (done && do_acc) {
-      if (!a.delta) {
-        add_row(x, b, false);
-      } else if (old >= 0 && old != b) {  // delta: only moved rows change the statistics
-        add_row(x, b, false);
-        add_row(x, min(old, k - 1), true);
+        for (int j = 0; j < 8; ++j) {
+          const float e = xr.at(s, j) - cb[s][j];
+          part = fmaf(e, e, part);
+        }
+      const float rowcost = part + __shfl_xor(part, 32, 64);
+      if (done && h == 0) {
+        if (a.labels) a.labels[row] = b;
+        if (a.mindist) a.mindist[row] = rowcost;
+        if (a.bounds) {
+          // every other candidate's alpha^2 distance is >= b2 - tt; back to data units
+          const float lo = (b2 - (tt + mrel * (nx2_s + cm_s * cm_s))) / a2;
+          a.bounds[row] = make_float2(sqrtf(rowcost) * ueps + 1e-30f,
+                                      sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
+        }
+        my_cost += double(rowcost);
       }
-    }
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float e = x.at(s, j) - cb[s][j];
-        part = fmaf(e, e, part);
+    } else {
+      if (acc_row) {  // only the rows that add re-read their values (x may hold the next tile)
+        F xr;
+        if constexpr (PF == 2)
+          load_tile(tile, xr);
+        else
+          xr = x;
+        add_row(xr, b, false);
+        if (a.delta) add_row(xr, min(old, k - 1), true);
       }
-    const float rowcost = part + __shfl_xor(part, 32, 64);
-    if (done && h == 0) {
-      if (a.labels) a.labels[row] = b;
-      if (a.mindist) a.mindist[row] = rowcost;
-      if (a.bounds) {
-        // every other candidate's alpha^2 distance is >= b2 - tt; back to data units
-        const float lo = (b2 - (tt + mrel * (nx2_s + cm_s * cm_s))) / a2;
-        a.bounds[row] =
-            make_float2(sqrtf(rowcost) * ueps + 1e-30f, sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
+      if (done && h == 0) {
+        if (a.labels) a.labels[row] = b;
+        if (a.bounds) {
+          // the pick's alpha^2 distance is <= b1 + tt, every other one >= b2 - tt
+          const float mg = mrel * (nx2_s + cm_s * cm_s);
+          const float up = (b1 + tt + mg) / a2, lo = (b2 - (tt + mg)) / a2;
+          a.bounds[row] = make_float2(sqrtf(fmaxf(up, 0.f)) * (1.f + 1e-6f) + 1e-30f,
+                                      sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
+        }
       }
-      my_cost += double(rowcost);
     }
   };
 
-  if constexpr (PF) {
+  if constexpr (PF == 1) {
     F xa, xb;
     load_tile(tile_of(t), xa);
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
@@ -409,6 +439,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       if (t + stride >= npos) break;
       process(t + stride, tile_of(t + stride), xb, xa, t + 2 * stride);
     }
+  } else if constexpr (PF == 2) {
+    F xa;
+    load_tile(tile_of(t), xa);
+    for (; t < npos; t += stride) process(t, tile_of(t), xa, xa, t + stride);
   } else {
     F xa;
     int64_t tl = tile_of(t);
@@ -446,42 +480,52 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   }
 }
 
-template <int KS, bool XB, int WAVES, bool PF>
+template <int KS, bool XB, int WAVES, int PF, bool COST>
 void launch_lean(const LeanArgs& a, int grid, hipStream_t s) {
   const LeanSmem L = lean_plan(16 * KS, a.kpad, a.k, a.d, a.accumulate, a.sums_too, WAVES);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF>),
+        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF>), dim3(grid), dim3(WAVES * 64),
-                     L.total, s, a);
+  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST>), dim3(grid),
+                     dim3(WAVES * 64), L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
 template <int KS, bool XB>
-void launch_lean_v(const LeanArgs& a, int grid, int variant, hipStream_t s) {
-  switch (variant) {  // workgroup shape (one workgroup per CU: the LDS plan)
-    case 1: launch_lean<KS, XB, 8, true>(a, grid, s); break;    // 2 waves/SIMD + prefetch
-    case 2: launch_lean<KS, XB, 12, true>(a, grid, s); break;   // 3 waves/SIMD + prefetch
-    case 3: launch_lean<KS, XB, 12, false>(a, grid, s); break;  // 3 waves/SIMD
-    default: launch_lean<KS, XB, 16, false>(a, grid, s); break; // 4 waves/SIMD
+void launch_lean_v(const LeanArgs& a, int grid, int variant, bool cost, hipStream_t s) {
+  // workgroup shape (one workgroup per CU: the LDS plan); with the cost: rows stay in
+  // registers; without: the next tile is prefetched into them (PF 2)
+  switch (variant) {
+    case 3:  // 3 waves/SIMD, no prefetch
+      if (cost) launch_lean<KS, XB, 12, 0, true>(a, grid, s);
+      else launch_lean<KS, XB, 12, 0, false>(a, grid, s);
+      break;
+    case 5:  // 3 waves/SIMD, prefetch
+      if (cost) launch_lean<KS, XB, 12, 2, true>(a, grid, s);
+      else launch_lean<KS, XB, 12, 2, false>(a, grid, s);
+      break;
+    default:  // 4 waves/SIMD
+      if (cost) launch_lean<KS, XB, 16, 0, true>(a, grid, s);
+      else launch_lean<KS, XB, 16, 2, false>(a, grid, s);
+      break;
   }
 }
 
 template <bool XB>
-void launch_lean_xb(const LeanArgs& a, int grid, int variant, hipStream_t s) {
+void launch_lean_xb(const LeanArgs& a, int grid, int variant, bool cost, hipStream_t s) {
   switch ((a.d + 4 + 15) / 16) {
-    case 1: launch_lean_v<1, XB>(a, grid, variant, s); break;
-    case 2: launch_lean_v<2, XB>(a, grid, variant, s); break;
-    case 3: launch_lean_v<3, XB>(a, grid, variant, s); break;
-    case 4: launch_lean_v<4, XB>(a, grid, variant, s); break;
-    case 5: launch_lean_v<5, XB>(a, grid, variant, s); break;
-    case 6: launch_lean_v<6, XB>(a, grid, variant, s); break;
-    case 7: launch_lean_v<7, XB>(a, grid, variant, s); break;
-    case 8: launch_lean_v<8, XB>(a, grid, variant, s); break;
+    case 1: launch_lean_v<1, XB>(a, grid, variant, cost, s); break;
+    case 2: launch_lean_v<2, XB>(a, grid, variant, cost, s); break;
+    case 3: launch_lean_v<3, XB>(a, grid, variant, cost, s); break;
+    case 4: launch_lean_v<4, XB>(a, grid, variant, cost, s); break;
+    case 5: launch_lean_v<5, XB>(a, grid, variant, cost, s); break;
+    case 6: launch_lean_v<6, XB>(a, grid, variant, cost, s); break;
+    case 7: launch_lean_v<7, XB>(a, grid, variant, cost, s); break;
+    case 8: launch_lean_v<8, XB>(a, grid, variant, cost, s); break;
     default: OAP_THROW(ConfigError, "kmeans_lloyd: unsupported d=" << a.d);
   }
 }
@@ -864,13 +908,7 @@ int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid) {
   return (tiles + grid - 1) / grid;
 }
 
-int kmeans_lloyd_waves(int variant) {
-  switch (variant) {
-    case 1: return 8;
-    case 2: case 3: return 12;
-    default: return 16;
-  }
-}
+int kmeans_lloyd_waves(int variant) { return (variant == 3 || variant == 5) ? 12 : 16; }
 
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
   const int64_t per_block = kmeans_lloyd_tiles_per_block(n, grid);
@@ -915,10 +953,12 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.sums_too = a.sums_too;
   l.delta = a.delta;
   l.ablate = a.ablate;
+  // the exact per-row cost is computed when a cost or mindist is asked for
+  const bool cost = a.cost_slab != nullptr || a.mindist != nullptr;
   if (a.xbf16)
-    launch_lean_xb<true>(l, grid, variant, s);
+    launch_lean_xb<true>(l, grid, variant, cost, s);
   else
-    launch_lean_xb<false>(l, grid, variant, s);
+    launch_lean_xb<false>(l, grid, variant, cost, s);
   return grid;
 }
 

@@ -280,12 +280,15 @@ def test_pruning_is_exact(native, d, k, dtype, n):
     for r in (rp, rn):
         assert r["last_counts"] == ru["last_counts"]
         assert np.array_equal(r["centers"], ru["centers"])
-    np.testing.assert_allclose(rn["cost_history"], ru["cost_history"], rtol=1e-12)
+    hn, hu0 = np.array(rn["cost_history"]), np.array(ru["cost_history"])
+    both = np.isfinite(hn) & np.isfinite(hu0)  # lean iterations report costs where needed
+    assert both[0] and both[-1]
+    np.testing.assert_allclose(hn[both], hu0[both], rtol=1e-12)
     # delta accumulation (single launch): per-iteration costs only on full passes, the final
     # cost from an exact pass over the labels (same per-row fp32 values, fp64 sum)
     hp, hu = np.array(rp["cost_history"]), np.array(ru["cost_history"])
-    fin = np.isfinite(hp)
-    assert fin[0] and fin[-1]
+    fin = np.isfinite(hp) & np.isfinite(hu)
+    assert fin[0] and np.isfinite(hp[-1]) and np.isfinite(hu[-1])
     np.testing.assert_allclose(hp[fin][:-1], hu[fin][:-1], rtol=1e-12)
     assert abs(hp[-1] - hu[-1]) <= 1e-12 * hu[-1]
     assert abs(rp["cost"] - ru["cost"]) <= 1e-12 * ru["cost"]
