@@ -140,6 +140,7 @@ def bench_kmeans(args, w):
              "dense_equiv_tflops": flops / (el_max / args.steps) / 1e12,
              # rows the tier-1 pass left to the exact fp32 MFMA re-decision (near ties)
              "deferred_rows_per_iter": r.get("deferred_rows", 0) / max(args.steps, 1),
+             "moved_rows_per_iter": r.get("moved_rows", 0) / max(args.steps, 1),
              "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
              "tiles_per_pass": tiles,
              "ms_per_step_unpruned": ms_unpruned,

@@ -429,6 +429,7 @@ PYBIND11_MODULE(_native, m) {
         out["tier3_tiles"] = r.tier3_tiles;
         out["pruned_tiles"] = r.pruned_tiles;
         out["deferred_rows"] = r.deferred_rows;
+        out["moved_rows"] = r.moved_rows;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

@@ -1042,16 +1042,22 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     ldefer_b = ctx.alloc(lean_defer_bytes(x.rows, ctx.info().cu_count, &lg, &lcap));
     req.defer_rows = ldefer_b.as<int32_t>();
     req.defer_count = reinterpret_cast<unsigned*>(req.defer_rows + size_t(lg) * size_t(lcap));
-    ldstat_b = ctx.alloc(sizeof(u64));
-    ldstat_h = ctx.alloc_pinned(sizeof(u64));
-    ctx.memset(ldstat_b.data(), 0, sizeof(u64), s);
+    ldstat_b = ctx.alloc(2 * sizeof(u64));  // [deferred rows, moved rows staged]
+    ldstat_h = ctx.alloc_pinned(2 * sizeof(u64));
+    ctx.memset(ldstat_b.data(), 0, 2 * sizeof(u64), s);
     req.deferred_rows = ldstat_b.as<u64>();
   }
   u64 deferred_seen = 0;
+  // with the adaptive scan off, full passes write the per-row bounds (8 B/row) only where a
+  // following iteration may scan, and the per-tile max |x|^2 (constant) once
+  float* const bounds_full = req.bounds;
+  float* const xnorm_full = req.xnorm;
+  bool xnorm_ready = false;
   // adaptive delta: when the scan prunes few tiles (overlapping clusters), its pass and the
   // delta bookkeeping cost more than they save — run full passes (which refresh labels and
   // bounds) and probe the scan again every few iterations
   bool delta_on = true;
+  bool probing = false;  // delta_on was set by a probe: scan one iteration, then decide
   int delta_probe = 0;
   u64 pruned_seen = 0;
 
@@ -1104,7 +1110,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       ev[b].e0.record(s);
       // (req.fast1: the lean kernel runs; only it does delta accumulation)
       const bool delta_it = delta && it > 0 && req.fast1;
-      const bool scan_it_all = scan_all && it > 0 && req.fast1 && delta_on;  // rank-uniform
+      // (a probe batch scans its first iteration only: the next batch decides from it)
+      const bool scan_it_all =
+          scan_all && it > 0 && req.fast1 && delta_on && (!probing || b == 0);  // rank-uniform
       const bool scan_it = scan_it_all && scan;
       last_scanned = scan_it_all;
       it_scanned[b] = scan_it_all;
@@ -1113,6 +1121,13 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         OAP_HIP_CHECK(hipMemsetAsync(delta ? loc_b.data() : stats.data(), 0,
                                      sizeof(u64) * (kd + k), s));
       req.labels_valid = it > 0;
+      if (scan_all && prune) {
+        const bool next_may_scan = b < nb_it - 1
+                                       ? delta_on && !probing
+                                       : delta_on || delta_probe + 1 >= (B == 1 ? 4 : 1);
+        req.bounds = (scan_it || next_may_scan) ? bounds_full : nullptr;
+        req.xnorm = xnorm_ready ? nullptr : xnorm_full;
+      }
       if (prune) {
         // the general kernel's in-kernel pruning test (lean off) or the scan read the drift;
         // a lean full pass refreshes labels and bounds without it
@@ -1130,7 +1145,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       it_costless[b] = !cost_it || scan_it_all;
       last_costless = it_costless[b];
       if (scan_it) {
-        kern::kmeans_lean_scan(x.rows, k, d, lgrid, req.bounds, req.labels, req.xnorm,
+        OAP_CHECK(xnorm_ready, "kmeans scan before any full pass");
+        kern::kmeans_lean_scan(x.rows, k, d, lgrid, req.bounds, req.labels, xnorm_full,
                                req.drift, req.drift_max, g.cstat.as<float>(),
                                dlist_b.as<int32_t>(), dcount, req.pruned_tiles, s);
         req.tile_list = dlist_b.as<int32_t>();
@@ -1140,6 +1156,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         req.tile_count = nullptr;
       }
       int nb = gpu_assign(ctx, x, g, req, s);
+      if (req.xnorm && !req.tile_list) xnorm_ready = true;
       if (delta) {
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
                                      hipMemcpyDeviceToDevice, s));
@@ -1241,11 +1258,15 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
       pruned_seen = pruned_now;
       // (one scan right after a large move says little: turn off on two, or on a hopeless one)
-      if (delta_on && scan_iters > 0 && (frac < 0.02 || (scan_iters > 1 && frac < 0.2))) {
+      const bool was_probe = probing;
+      probing = false;
+      if (delta_on && scan_iters > 0 &&
+          (frac < 0.02 || ((scan_iters > 1 || was_probe) && frac < 0.2))) {
         delta_on = false;
         delta_probe = 0;
       } else if (!delta_on && ++delta_probe >= (B == 1 ? 4 : 1)) {
         delta_on = true;  // probe: the centers may have settled
+        probing = B > 1;
       }
     }
   }
@@ -1297,9 +1318,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     res.pruned_tiles = static_cast<int64_t>(pt);
   }
   if (ldstat_b.data()) {
-    u64 dr = 0;
-    ctx.copy_to_host(&dr, ldstat_b.data(), sizeof(u64), s);
-    res.deferred_rows = static_cast<int64_t>(dr);
+    u64 dr[2] = {0, 0};
+    ctx.copy_to_host(dr, ldstat_b.data(), 2 * sizeof(u64), s);
+    res.deferred_rows = static_cast<int64_t>(dr[0]);
+    res.moved_rows = static_cast<int64_t>(dr[1]);
   }
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
@@ -1407,8 +1429,8 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
     req.counts = a.counts;
     req.cost_slab = (ablate & 4) ? nullptr : a.cost_slab;  // 4: the Lloyd pass without a cost
     req.fast1 = true;
-    Buffer dr = ctx.alloc(sizeof(u64));
-    ctx.memset(dr.data(), 0, sizeof(u64), s);
+    Buffer dr = ctx.alloc(2 * sizeof(u64));
+    ctx.memset(dr.data(), 0, 2 * sizeof(u64), s);
     req.deferred_rows = dr.as<u64>();
     OAP_CHECK(lean_applies(x, k, g.kpad, req), "lean path not applicable");
     gpu_assign(ctx, x, g, req, s);  // warm

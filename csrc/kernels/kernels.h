@@ -117,7 +117,8 @@ struct KMeansAssignArgs {
   // appended to this workgroup's segment ([grid][row_seg_cap], count defer_row_count[block]).
   int32_t* defer_rows = nullptr;
   unsigned* defer_row_count = nullptr;
-  unsigned long long* deferred_rows = nullptr;  // optional counter of deferred rows
+  // optional counters [deferred rows, moved rows staged by delta passes]
+  unsigned long long* deferred_rows = nullptr;
   // Row-list (refine) mode: rows still unsure after the bf16x3 tier are appended to
   // exact_rows ([grid][8][exact_sub_cap], one sub-segment per wave, counts exact_count
   // [grid][8]) instead of re-deciding their whole 32-row group; kmeans_exact_rows finishes them.

@@ -76,11 +76,13 @@ struct LeanArgs {
 };
 
 struct LeanSmem {
-  size_t plane, sc, acc, cnt, wcost, total;
+  size_t plane, sc, acc, cnt, mv, wcost, total;
 };
 
+constexpr int kMoveCap = 64;  // per-wave staging slots for moved rows (delta passes)
+
 __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bool acc, bool sums,
-                                              int waves) {
+                                              int waves, bool delta) {
   LeanSmem m;
   size_t off = 0;
   m.plane = 0;
@@ -93,6 +95,8 @@ __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bo
   m.cnt = off;
   if (acc) off += size_t(k) * 4;
   off = round16(off);
+  m.mv = off;  // delta: per wave kMoveCap (row, new | old << 16) pairs
+  if (acc && delta) off += size_t(waves) * kMoveCap * 8;
   m.wcost = off;
   off += size_t(waves) * 8;
   m.total = round16(off);
@@ -118,7 +122,8 @@ __device__ inline void split_f16(float v, _Float16& hi, _Float16& lo) {
 // the row's f32 values are not needed after its fp16 operands are built (rows that accumulate
 // re-read theirs), so PF 2 can reuse their registers, and the bounds' upper half comes from the
 // tier-1 distance plus its error bound.
-template <int KS, bool XB, int WAVES, int PF, bool COST>
+// U: k chunks per step of the distance loop (1 or 2).
+template <int KS, bool XB, int WAVES, int PF, bool COST, int U, bool SG = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a) {
   constexpr int DP = 16 * KS;
   constexpr int NT = WAVES * 64;
@@ -129,12 +134,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const bool do_acc = accumulate && !(a.ablate & 1);
   const bool do_cost = !(a.ablate & 2);
   const bool do_dist = !(a.ablate & 8);
-  const LeanSmem L = lean_plan(DP, kpad, k, d, accumulate, a.sums_too != 0, WAVES);
+  const LeanSmem L = lean_plan(DP, kpad, k, d, accumulate, a.sums_too != 0, WAVES, a.delta != 0);
   const int sb = stride_bf16(DP);
   _Float16* ph = reinterpret_cast<_Float16*>(smem + L.plane);
   float* sc_l = reinterpret_cast<float*>(smem + L.sc);
   double* acc_l = reinterpret_cast<double*>(smem + L.acc);
   unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
+  int2* mv_l = reinterpret_cast<int2*>(smem + L.mv) + (threadIdx.x >> 6) * kMoveCap;
   double* wcost = reinterpret_cast<double*>(smem + L.wcost);
   const int tid = threadIdx.x;
   const float cmax = a.cstat[0];
@@ -199,9 +205,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     const int64_t tl = int64_t(seg[q]);
     return tl < 0 ? 0 : (tl < ntiles_all ? tl : ntiles_all - 1);
   };
-  auto load_tile = [&](int64_t tile, F& dst) {
-    int64_t row = tile * 32 + r;
-    row = row < a.n ? row : a.n - 1;
+  auto load_row = [&](int64_t row, F& dst) {
     if constexpr (XB) {
       const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
 #pragma unroll
@@ -225,6 +229,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           dst.v[s][4 * q + 3] = v.w;
         }
     }
+  };
+  auto load_tile = [&](int64_t tile, F& dst) {
+    const int64_t row = tile * 32 + r;
+    load_row(row < a.n ? row : a.n - 1, dst);
   };
 
   // fixed-point accumulation of one row into cluster b (neg: subtract it)
@@ -251,6 +259,31 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
             atomicAdd(ap + 16 * s + j, sgn * static_cast<double>(rintf(xv.at(s, j) * scv[j])));
       }
     }
+  };
+
+  // delta passes: a tile's few moved rows would each cost the whole wave 2 KS x 8 predicated
+  // LDS atomics; instead they are staged in the wave's LDS slots and accumulated 32 at a time
+  // with every lane busy (rows re-read from L2: their tile was just streamed)
+  unsigned n_mv = 0;  // wave-uniform
+  u64 moved_total = 0;
+  auto flush_moved = [&](unsigned cnt) {  // accumulate staged entries [0, min(cnt, 32))
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const bool on = unsigned(r) < cnt;
+    const int2 e = mv_l[on ? r : 0];
+    if (on) {
+      F xr;
+      load_row(int64_t(e.x), xr);
+      add_row(xr, e.y & 0xffff, false);
+      add_row(xr, e.y >> 16, true);
+    }
+    if (cnt > 32) {  // slide the rest down (read all before any write: in-order LDS)
+      const int2 rest = mv_l[32 + r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (h == 0 && unsigned(r) < cnt - 32) mv_l[r] = rest;
+    }
+    moved_total += cnt < 32 ? cnt : 32;
   };
 
   auto process = [&](const int64_t pos, const int64_t tile, F& x, F& xn, const int64_t pf) {
@@ -307,15 +340,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 #pragma unroll
       for (int s = 1; s < KS; ++s)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], xh[s], acc, 0, 0, 0);
+      if constexpr (SG) {
+        // all KS fragment reads in flight before the first MFMA (the default schedule reuses
+        // one register quad and waits on each read in turn)
+        __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+      }
     };
     auto epilogue = [&](int c0, const f32x16& acc) {
       int t1[4], t2[4];
-      // candidate groups of 8 centers at or past k are padding: skip them (wave-uniform; only
-      // the last chunk has any)
-      const int ng = k - c0 >= 32 ? 4 : (k - c0 + 7) / 8;
+      // padded centers carry the largest finite bias: they never win, so no chunk needs a
+      // branch for them
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        if (e >= 4 && (e >> 2) >= ng) break;
         const int off = 8 * (e >> 2) + (e & 3);
         const int key = (__float_as_int(acc[e]) & ~0x3ff) | off;
         const int q = e & 3;
@@ -342,7 +379,52 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     bool unsure;
     float b1 = 0.f, b2 = 0.f, tt = 0.f;
     if (do_dist) {
-      for (int c0 = 0; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
+      int c0 = 0;
+      if constexpr (U == 2) {
+        // two chunks per step: all 2 KS fragment reads issue together, two independent MFMA
+        // chains, then both epilogues (ILP the single-chunk loop lacks)
+        for (; c0 + 32 < kpad; c0 += 64) {
+          const _Float16* apA = ph + size_t(c0 + r) * sb + 8 * h;
+          const _Float16* apB = apA + size_t(32) * sb;
+          f16x8 avA[KS], avB[KS];
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            avA[s] = *reinterpret_cast<const f16x8*>(apA + 16 * s);
+            avB[s] = *reinterpret_cast<const f16x8*>(apB + 16 * s);
+          }
+          f32x16 accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(avA[0], xh[0], f32x16{}, 0, 0, 0);
+          f32x16 accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(avB[0], xh[0], f32x16{}, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < KS; ++s) {
+            accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(avA[s], xh[s], accA, 0, 0, 0);
+            accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(avB[s], xh[s], accB, 0, 0, 0);
+          }
+          epilogue(c0, accA);
+          epilogue(c0 + 32, accB);
+        }
+      }
+      if constexpr (U == 3) {
+        // software-pipelined: the next chunk's fragments are read under this chunk's epilogue
+        f16x8 av[KS];
+        const _Float16* ap = ph + size_t(r) * sb + 8 * h;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
+        for (; c0 < kpad; c0 += 32) {
+          f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], xh[0], f32x16{}, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], xh[s], acc, 0, 0, 0);
+          ap += size_t(32) * sb;
+          const bool more = c0 + 32 < kpad;  // wave-uniform
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+            av[s] = more ? *reinterpret_cast<const f16x8*>(ap + 16 * s) : av[s];
+          __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
+          epilogue(c0, acc);
+        }
+      }
+      for (; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
         f32x16 acc;
         mfma_chunk(c0, acc);
         epilogue(c0, acc);
@@ -371,6 +453,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     int b = k1 & 0x3ff;
     b = (b < k) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
     const bool acc_row = done && do_acc && (!a.delta || (old >= 0 && old != b));
+    if (a.delta) {  // stage moved rows (wave-private slots, in row order)
+      const unsigned long long mm = __ballot(acc_row && h == 0);
+      if (mm) {
+        if (acc_row && h == 0)
+          mv_l[n_mv + __popcll(mm & ((1ull << lane) - 1ull))] =
+              make_int2(static_cast<int>(row), b | (min(old, k - 1) << 16));
+        n_mv += static_cast<unsigned>(__popcll(mm));
+        if (n_mv >= 32) {
+          flush_moved(n_mv);
+          n_mv -= 32;
+        }
+      }
+    }
     if constexpr (COST) {
       F xr_buf;
       if constexpr (PF == 2) load_tile(tile, xr_buf);  // re-read this tile (cache-resident)
@@ -384,10 +479,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 #pragma unroll
           for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
       }
-      if (acc_row) {
-        add_row(xr, b, false);
-        if (a.delta) add_row(xr, min(old, k - 1), true);  // delta: a moved row
-      }
+      if (acc_row && !a.delta) add_row(xr, b, false);
       float part = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -409,14 +501,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         my_cost += double(rowcost);
       }
     } else {
-      if (acc_row) {  // only the rows that add re-read their values (x may hold the next tile)
+      if (acc_row && !a.delta) {  // only rows that add re-read (x may hold the next tile)
         F xr;
         if constexpr (PF == 2)
           load_tile(tile, xr);
         else
           xr = x;
         add_row(xr, b, false);
-        if (a.delta) add_row(xr, min(old, k - 1), true);
       }
       if (done && h == 0) {
         if (a.labels) a.labels[row] = b;
@@ -454,12 +545,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
   }
 
+  if (n_mv) flush_moved(n_mv);
   // ---- deterministic per-block cost (fixed shuffle tree, waves in index order), flushes
   const double wsum = wave_sum_f64(my_cost);
   if (lane == 0) {
     wcost[wave] = wsum;
     a.defer_row_count[blockIdx.x * kDeferSubs + wave] = n_def;
     if (a.deferred_rows && n_def) atomicAdd(a.deferred_rows, u64(n_def));
+    if (a.deferred_rows && moved_total) atomicAdd(a.deferred_rows + 1, moved_total);
   }
   __syncthreads();
   if (tid == 0 && a.cost_slab) {
@@ -480,17 +573,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   }
 }
 
-template <int KS, bool XB, int WAVES, int PF, bool COST>
+template <int KS, bool XB, int WAVES, int PF, bool COST, int U = 1, bool SG = false>
 void launch_lean(const LeanArgs& a, int grid, hipStream_t s) {
-  const LeanSmem L = lean_plan(16 * KS, a.kpad, a.k, a.d, a.accumulate, a.sums_too, WAVES);
+  const LeanSmem L =
+      lean_plan(16 * KS, a.kpad, a.k, a.d, a.accumulate, a.sums_too, WAVES, a.delta != 0);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST>),
+        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST>), dim3(grid),
+  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG>), dim3(grid),
                      dim3(WAVES * 64), L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
@@ -507,6 +601,26 @@ void launch_lean_v(const LeanArgs& a, int grid, int variant, bool cost, hipStrea
     case 5:  // 3 waves/SIMD, prefetch
       if (cost) launch_lean<KS, XB, 12, 2, true>(a, grid, s);
       else launch_lean<KS, XB, 12, 2, false>(a, grid, s);
+      break;
+    case 6:  // 4 waves/SIMD, fragment reads grouped ahead of the MFMAs
+      if (cost) launch_lean<KS, XB, 16, 0, true, 1, true>(a, grid, s);
+      else launch_lean<KS, XB, 16, 2, false, 1, true>(a, grid, s);
+      break;
+    case 8:  // 3 waves/SIMD, grouped fragment reads
+      if (cost) launch_lean<KS, XB, 12, 0, true, 1, true>(a, grid, s);
+      else launch_lean<KS, XB, 12, 2, false, 1, true>(a, grid, s);
+      break;
+    case 9:  // 3 waves/SIMD, software-pipelined fragment reads
+      if (cost) launch_lean<KS, XB, 12, 0, true, 3>(a, grid, s);
+      else launch_lean<KS, XB, 12, 2, false, 3>(a, grid, s);
+      break;
+    case 10:  // 4 waves/SIMD, software-pipelined fragment reads, no prefetch
+      if (cost) launch_lean<KS, XB, 16, 0, true, 3>(a, grid, s);
+      else launch_lean<KS, XB, 16, 0, false, 3>(a, grid, s);
+      break;
+    case 7:  // 3 waves/SIMD, two chunks per step, prefetch without the cost
+      if (cost) launch_lean<KS, XB, 12, 0, true, 2>(a, grid, s);
+      else launch_lean<KS, XB, 12, 2, false, 2>(a, grid, s);
       break;
     default:  // 4 waves/SIMD
       if (cost) launch_lean<KS, XB, 16, 0, true>(a, grid, s);
@@ -893,7 +1007,7 @@ bool kmeans_lloyd_supported(int d, int k, bool accumulate, bool sums_too) {
   if (dp != kmeans_dp(d)) return false;  // the centroid buffer's row stride must match
   const int kpad = (k + 31) / 32 * 32;
   if (kpad > 1024) return false;  // keys carry a 10-bit index
-  return lean_plan(dp, kpad, k, d, accumulate, sums_too, 16).total <= kLdsLimit &&
+  return lean_plan(dp, kpad, k, d, accumulate, sums_too, 16, true).total <= kLdsLimit &&
          exact_plan(kpad, k, d, accumulate, sums_too).total <= kLdsLimit;
 }
 
@@ -908,7 +1022,9 @@ int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid) {
   return (tiles + grid - 1) / grid;
 }
 
-int kmeans_lloyd_waves(int variant) { return (variant == 3 || variant == 5) ? 12 : 16; }
+int kmeans_lloyd_waves(int variant) {
+  return (variant == 3 || variant == 5 || variant == 7 || variant == 8 || variant == 9) ? 12 : 16;
+}
 
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
   const int64_t per_block = kmeans_lloyd_tiles_per_block(n, grid);

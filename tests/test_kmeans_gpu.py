@@ -310,6 +310,7 @@ def test_lean_pass_bitwise_equals_precise_on_overlapping_data(native, d, k, sigm
     rf = native.kmeans_fit(t_g, comm, t, init, k, 6, -1.0, prune=False)  # lean full passes
     rp = native.kmeans_fit(t_g, comm, t, init, k, 6, -1.0, precise=True)
     assert rl["deferred_rows"] > 0 and rf["deferred_rows"] > 0
+    assert rl["moved_rows"] > 0 and rf["moved_rows"] > 0  # the staged delta accumulation ran
     assert rl["shift_history"][-1] > 0  # centers still move: the delta path carries state
     for r in (rl, rf):
         assert r["last_counts"] == rp["last_counts"]
@@ -321,7 +322,7 @@ def test_lean_pass_bitwise_equals_precise_on_overlapping_data(native, d, k, sigm
     assert rf2["cost"] == rf["cost"] and rf2["deferred_rows"] == rf["deferred_rows"]
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 3, 5, 7])
 def test_lean_variants_agree(native, variant):
     """Every workgroup shape of the lean kernel gives the same fit."""
     g = native.Context(0, 0.5, 0)

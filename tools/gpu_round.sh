@@ -1,16 +1,16 @@
 #!/bin/bash
-# usage: tools/gpu_round.sh <tag> [steps...]  -- on the GPU box: build, then the named steps
-# (default: test bench precise prof).  Any step ending in a fault/abort/timeout stops the script.
+# usage: tools/gpu_round.sh <tag> [steps...]  -- on the GPU box: the named steps (default: test
+# bench precise prof) against the extensions built in-tree beforehand on the CPU.  Any step ending in a fault/abort/timeout stops the script.
 set -u
 R=$GRAFT_REPO_ROOT; T=${1:-run}; shift || true
 STEPS=${*:-test bench precise prof}
 cd $R
-python -m oap_mllib_amd.build > gpurun_out/build_$T.log 2>&1 || { echo build_failed; exit 1; }
+mkdir -p gpurun_out
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2: stopping"; exit $1;; esac; }
 for st in $STEPS; do
   case $st in
     test)
-      timeout -k 10 600 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$T.log 2>&1
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu_$T.log 2>&1
       rc=$?; echo pytest_rc=$rc; tail -4 gpurun_out/pytest_gpu_$T.log; fatal $rc pytest;;
     bench)
       timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err
@@ -36,6 +36,9 @@ for st in $STEPS; do
     pcaprof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/pcaprof_$T -o run -- python3 $R/benchmarks/bench_pca.py --reps 2 > $R/gpurun_out/pcaprof_$T.log 2>&1)
       rc=$?; echo pcaprof_rc=$rc; fatal $rc pcaprof;;
+    trace)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/trace_$T -o run -- python3 $R/bench.py --steps 20 --warmup 0 --skip-fit --skip-unpruned --no-separable-extra > $R/gpurun_out/trace_$T.log 2>&1)
+      rc=$?; echo trace_rc=$rc; fatal $rc trace;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$T -o run -- python3 $R/bench.py --rows 20000000 --steps 5 --warmup 1 --skip-fit > $R/gpurun_out/prof_$T.log 2>&1)
       rc=$?; echo prof_rc=$rc; fatal $rc prof;;

@@ -1,13 +1,13 @@
 #!/bin/bash
-# usage (on the GPU box, after the build): tools/pmc_lean.sh <tag> [sigma]
+# usage (on the GPU box, after the build): tools/pmc_lean.sh <tag> [sigma] [variant] [ablation]
 # PMC passes over the lean K-Means pass (kernel trace + counters only — no sys/runtime traces).
 set -u
-R=$GRAFT_REPO_ROOT; T=${1:-pmc}; S=${2:-8}
+R=$GRAFT_REPO_ROOT; T=${1:-pmc}; S=${2:-8}; V=${3:-0}; A=${4:-0}
 cd /tmp && export TMPDIR=/tmp
 run() {  # $1 = pass name, rest = counters
   local P=$1; shift
   timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/${T}_$P -o run \
-    --pmc "$@" -- python3 $R/tools/kmeans_lean_probe.py 20000000 $S 3 0 0 \
+    --pmc "$@" -- python3 $R/tools/kmeans_lean_probe.py 20000000 $S 3 $V $A \
     > $R/gpurun_out/${T}_$P.log 2>&1
   local rc=$?; echo "pmc_${P}_rc=$rc"; return $rc
 }
