@@ -54,7 +54,8 @@ py::array host_view(void* p, size_t count, DType t) {
 // allreduce/allgather/alltoallv/bcast/barrier over numpy arrays).
 class HostComm final : public Comm {
  public:
-  HostComm(py::object impl, int rank, int world) : impl_(std::move(impl)), rank_(rank), world_(world) {}
+  HostComm(py::object impl, int rank, int world)
+      : impl_(std::move(impl)), rank_(rank), world_(world) {}
   ~HostComm() override {
     py::gil_scoped_acquire g;
     impl_ = py::object();
@@ -275,7 +276,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("ld", &DenseTable::ld)
       .def_readonly("global_offset", &DenseTable::global_offset)
       .def_readonly("global_rows", &DenseTable::global_rows)
-      .def_property_readonly("dtype", [](DenseTable& t) { return std::string(dtype_name(t.dtype)); })
+      .def_property_readonly("dtype",
+                             [](DenseTable& t) { return std::string(dtype_name(t.dtype)); })
       .def_property_readonly("nbytes", &DenseTable::bytes)
       .def_property_readonly("on_gpu", [](DenseTable& t) { return t.backend == Backend::GPU; })
       .def("to_numpy",
@@ -372,14 +374,16 @@ PYBIND11_MODULE(_native, m) {
       py::arg("ncenters") = 8, py::arg("box") = 10.0, py::arg("sigma") = 1.0,
       py::arg("seed") = 42, py::arg("storage") = "f32");
   m.def("assign_global_offsets",
-        [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t) {
+        [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,
+           std::shared_ptr<DenseTable> t) {
           py::gil_scoped_release r;
           assign_global_offsets(*ctx, *comm, *t);
         });
 
   // ---------------------------------------------------------------- K-Means
   m.def(
-      "kmeans_ld", [](int d, const std::string& dtype) { return kern::kmeans_ld(d, dtype == "bf16"); },
+      "kmeans_ld",
+      [](int d, const std::string& dtype) { return kern::kmeans_ld(d, dtype == "bf16"); },
       py::arg("d"), py::arg("dtype") = "f32");
   m.def(
       "kmeans_fit",
@@ -414,7 +418,8 @@ PYBIND11_MODULE(_native, m) {
         }
         py::dict out;
         py::array_t<double> c({int64_t(r.k), int64_t(r.d)});
-        if (!r.centers.empty()) std::memcpy(c.mutable_data(), r.centers.data(), r.centers.size() * 8);
+        if (!r.centers.empty())
+          std::memcpy(c.mutable_data(), r.centers.data(), r.centers.size() * 8);
         out["centers"] = c;
         out["cost"] = r.cost;
         out["num_iter"] = r.num_iter;

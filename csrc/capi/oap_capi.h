@@ -44,8 +44,8 @@ OAP_API void oap_ctx_destroy(oap_ctx* ctx);
 /* RCCL rendezvous: rank 0 creates the id, the launcher distributes it (e.g. Spark
  * BarrierTaskContext.allGather), every rank joins.  Replaces the oneCCL KVS + port scan. */
 OAP_API int oap_rccl_unique_id(unsigned char out[OAP_UNIQUE_ID_BYTES]);
-OAP_API int oap_ctx_join(oap_ctx* ctx, const unsigned char id[OAP_UNIQUE_ID_BYTES], int world, int rank,
-                 double timeout_s);
+OAP_API int oap_ctx_join(oap_ctx* ctx, const unsigned char id[OAP_UNIQUE_ID_BYTES], int world,
+                         int rank, double timeout_s);
 OAP_API int oap_ctx_world_size(const oap_ctx* ctx);
 OAP_API int oap_ctx_rank(const oap_ctx* ctx);
 
@@ -68,15 +68,15 @@ OAP_API int oap_kmeans_predict(oap_ctx* ctx, const double* x, int64_t rows, int 
 /* PCA: top-k principal components of the (globally) mean-centered rows.  out_pc[cols][k]
  * row-major (column j = component j), out_explained[k] = |lambda_j| / sum |lambda| (Spark
  * RowMatrix semantics).  Mirrors cPCATrainDAL (PCADALImpl.cpp:38-190). */
-OAP_API int oap_pca_fit(oap_ctx* ctx, const double* x, int64_t rows, int cols, int k, double* out_pc,
-                double* out_explained);
+OAP_API int oap_pca_fit(oap_ctx* ctx, const double* x, int64_t rows, int cols, int k,
+                        double* out_pc, double* out_explained);
 
 /* ALS: this rank's (user, item, rating) triples, any ids.  Spark computeFactors semantics
  * (implicit: c = alpha |r|, lambda * n_u).  Mirrors cShuffleData + cDALImplictALS
  * (ALSDALImpl.cpp:456-576); results are owned by the returned handle. */
-OAP_API int oap_als_fit(oap_ctx* ctx, const int32_t* users, const int32_t* items, const float* ratings,
-                int64_t n, int rank, int max_iter, double reg, double alpha, int implicit,
-                uint64_t seed, oap_als_result** out);
+OAP_API int oap_als_fit(oap_ctx* ctx, const int32_t* users, const int32_t* items,
+                        const float* ratings, int64_t n, int rank, int max_iter, double reg,
+                        double alpha, int implicit, uint64_t seed, oap_als_result** out);
 /* which = 0: users, 1: items.  *ids / *factors ([count][rank]) stay valid until the free. */
 OAP_API int64_t oap_als_result_count(const oap_als_result* res, int which);
 OAP_API int oap_als_result_rank(const oap_als_result* res);

@@ -302,7 +302,8 @@ void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
     comm.alltoallv(send, send_counts, recv, recv_counts, dt, nullptr);
     return;
   }
-  Buffer ds = ctx.alloc(std::max<size_t>(sn * es, 16)), dr = ctx.alloc(std::max<size_t>(rn * es, 16));
+  Buffer ds = ctx.alloc(std::max<size_t>(sn * es, 16));
+  Buffer dr = ctx.alloc(std::max<size_t>(rn * es, 16));
   hipStream_t s = ctx.comm_stream();
   if (sn) OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send, sn * es, hipMemcpyHostToDevice, s));
   comm.alltoallv(ds.data(), send_counts, dr.data(), recv_counts, dt, s);

@@ -38,7 +38,8 @@ std::vector<int64_t> allgather_i64(Context& ctx, Comm& comm, const std::vector<i
   if (comm.on_device()) {
     Buffer s = ctx.alloc(mine.size() * 8), r = ctx.alloc(all.size() * 8);
     hipStream_t st = ctx.comm_stream();
-    OAP_HIP_CHECK(hipMemcpyAsync(s.data(), mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st));
+    OAP_HIP_CHECK(
+        hipMemcpyAsync(s.data(), mine.data(), mine.size() * 8, hipMemcpyHostToDevice, st));
     comm.allgather(s.data(), r.data(), mine.size(), DType::I64, st);
     OAP_HIP_CHECK(hipMemcpyAsync(all.data(), r.data(), all.size() * 8, hipMemcpyDeviceToHost, st));
     comm.wait(st);
@@ -75,7 +76,8 @@ std::vector<Rec> exchange(Context& ctx, Comm& comm, std::vector<std::vector<Rec>
   if (comm.on_device()) {
     Buffer ds = ctx.alloc(std::max<size_t>(stot, 16)), dr = ctx.alloc(std::max<size_t>(rtot, 16));
     hipStream_t st = ctx.comm_stream();
-    if (stot) OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send.data(), stot, hipMemcpyHostToDevice, st));
+    if (stot)
+      OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send.data(), stot, hipMemcpyHostToDevice, st));
     comm.alltoallv(ds.data(), sc, dr.data(), rc, DType::U8, st);
     if (rtot)
       OAP_HIP_CHECK(hipMemcpyAsync(recv.data(), dr.data(), rtot, hipMemcpyDeviceToHost, st));
@@ -139,7 +141,8 @@ Csr build_csr(ThreadPool& pool, std::vector<Rec>& recs, int64_t nrows, int64_t r
   c.val.resize(nnz);
   pool.parallel_for(nnz, [&](int, int64_t b, int64_t e) {
     for (int64_t k = b; k < e; ++k) {
-      const int64_t pos = cnt[int64_t(recs[k].a) - row_base].fetch_add(1, std::memory_order_relaxed);
+      const int64_t pos =
+          cnt[int64_t(recs[k].a) - row_base].fetch_add(1, std::memory_order_relaxed);
       c.col[pos] = recs[k].b;
       c.val[pos] = recs[k].r;
     }
@@ -313,7 +316,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     });
   } else {
     std::vector<std::vector<Rec>> out(P);
-    for (int64_t k = 0; k < n; ++k) out[owner_of(items[k], P)].push_back({users[k], items[k], ratings[k]});
+    for (int64_t k = 0; k < n; ++k)
+      out[owner_of(items[k], P)].push_back({users[k], items[k], ratings[k]});
     recv1 = exchange(ctx, comm, out);
   }
   IdIndex item_idx;
@@ -357,7 +361,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   } else {
     std::vector<std::vector<Rec>> out(P);
     for (const Rec& x : recv2) {
-      const int q = int(std::upper_bound(I.off.begin(), I.off.end(), int64_t(x.b)) - I.off.begin()) - 1;
+      const int q =
+          int(std::upper_bound(I.off.begin(), I.off.end(), int64_t(x.b)) - I.off.begin()) - 1;
       out[q].push_back({x.b, x.a, x.r});
     }
     recv3 = exchange(ctx, comm, out);
@@ -435,7 +440,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       D.n_short = int64_t(sr.size());
       D.n_long = int64_t(lr.size());
       D.n_chunks = int64_t(cb.size());
-      D.partials = ctx.alloc(std::max<size_t>(size_t(D.n_chunks) * kern::als_partial_floats(r) * 4, 16));
+      D.partials =
+          ctx.alloc(std::max<size_t>(size_t(D.n_chunks) * kern::als_partial_floats(r) * 4, 16));
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
     upload_side(U, dU);

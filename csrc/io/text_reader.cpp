@@ -189,7 +189,8 @@ LibSvmText read_libsvm(const std::string& path, ThreadPool& pool) {
     out.labels.insert(out.labels.end(), piece[t].labels.begin(), piece[t].labels.end());
     out.indices.insert(out.indices.end(), piece[t].indices.begin(), piece[t].indices.end());
     out.values.insert(out.values.end(), piece[t].values.begin(), piece[t].values.end());
-    for (size_t i = 1; i < piece[t].indptr.size(); ++i) out.indptr.push_back(base + piece[t].indptr[i]);
+    for (size_t i = 1; i < piece[t].indptr.size(); ++i)
+      out.indptr.push_back(base + piece[t].indptr[i]);
     out.max_index = std::max(out.max_index, piece[t].max_index);
   }
   return out;

@@ -446,7 +446,8 @@ JNIEXPORT jobject JNICALL Java_org_apache_spark_ml_recommendation_ALSDALImpl_cSh
     std::memcpy(&key, out + 20 * i, 8);
     if (g_shuffle_keys.empty() || g_shuffle_keys.back() != key) g_shuffle_keys.push_back(key);
   }
-  if (!set_int(env, info, "ratingsNum", jint(n)) || !set_int(env, info, "csrRowNum", jint(distinct)))
+  if (!set_int(env, info, "ratingsNum", jint(n)) ||
+      !set_int(env, info, "csrRowNum", jint(distinct)))
     return nullptr;
   return env->NewDirectByteBuffer(g_shuffled, n * 20);
 }

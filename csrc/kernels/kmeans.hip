@@ -89,7 +89,8 @@ __global__ void oap_kmeans_accumulate_global(const T* x, int64_t n, int ld, int 
     if (b < 0 || b >= k) continue;
     if (f == 0) atomicAdd(&counts[b], 1ull);
     if (!sums) continue;
-    const long long q = static_cast<long long>(rintf(static_cast<float>(x[row * ld + f]) * scale[f]));
+    const long long q =
+        static_cast<long long>(rintf(static_cast<float>(x[row * ld + f]) * scale[f]));
     atomicAdd(&sums[size_t(b) * d + f], static_cast<u64>(q));
   }
 }

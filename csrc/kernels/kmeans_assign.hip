@@ -306,7 +306,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
   // Positions walk every tile, the seed's list of active tiles (one list, grid-strided), or —
   // seg_list — this workgroup's own segment of a deferral list (see defer_list below).
   const int64_t seg_cap = defer_segment(ntiles_all, gridDim.x);
-  const int32_t* list = a.tile_list ? a.tile_list + (a.seg_list ? blockIdx.x * seg_cap : 0) : nullptr;
+  const int32_t* list =
+      a.tile_list ? a.tile_list + (a.seg_list ? blockIdx.x * seg_cap : 0) : nullptr;
   const int64_t ntiles = rlist         ? (rcnt + 31) / 32
                          : !a.tile_list ? ntiles_all
                          : a.seg_list  ? int64_t(a.tile_count[blockIdx.x])
@@ -430,7 +431,8 @@ __global__ __launch_bounds__(kThreads, 2) void oap_kmeans_assign_mfma(KMeansAssi
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += __shfl_xor(nx2, 32, 64);
-      if (a.xnorm && !rlist) {  // per-tile max |x|^2 (the scan's margin: conservative for every row)
+      // per-tile max |x|^2 (the scan's margin: conservative for every row)
+      if (a.xnorm && !rlist) {
         float tmax = nx2;
 #pragma unroll
         for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));

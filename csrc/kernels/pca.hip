@@ -18,8 +18,8 @@
 // Workgroup = 4 waves on one 128x128 output tile (each wave 64x64 = 2x2 MFMA blocks); rows are
 // staged 32 at a time through LDS transposed to [feature][row] bf16 hi/lo planes (2 x 40 KB,
 // double buffered: chunk c+1 is loaded and converted while chunk c feeds the MFMAs, one barrier
-// per chunk), so A and B fragments are single 16-byte LDS reads.  Blocks are remapped so that all tiles of one
-// row split land on one XCD and share its L2.
+// per chunk), so A and B fragments are single 16-byte LDS reads.  Blocks are remapped so that
+// all tiles of one row split land on one XCD and share its L2.
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
@@ -430,7 +430,8 @@ __global__ void oap_pca_reduce(const double* __restrict__ part, const double* __
   for (int64_t f = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; f < d;
        f += int64_t(gridDim.x) * blockDim.x) {
     double s = 0.0;
-    for (int sp = 0; sp < splits; ++sp) s += cpart[(size_t(sp) * nb + f / kTile) * kTile + f % kTile];
+    for (int sp = 0; sp < splits; ++sp)
+      s += cpart[(size_t(sp) * nb + f / kTile) * kTile + f % kTile];
     colsum[f] = s;
   }
 }

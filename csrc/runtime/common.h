@@ -1,9 +1,9 @@
 // Core definitions shared by every native translation unit of the MI355X MLlib engine.
 //
-// Replaces the reference's exit()-on-error model (mllib-dal/src/main/native/error_handling.cpp:30-57,
-// which kills the executor JVM) with typed C++ exceptions that the Python bindings translate
-// into Python exceptions.  No global mutable state lives here; everything per-fit hangs off a
-// Context (runtime/context.h).
+// Replaces the reference's exit()-on-error model
+// (mllib-dal/src/main/native/error_handling.cpp:30-57, which kills the executor JVM) with typed
+// C++ exceptions that the Python bindings translate into Python exceptions.  No global mutable
+// state lives here; everything per-fit hangs off a Context (runtime/context.h).
 #pragma once
 
 #include <hip/hip_runtime.h>

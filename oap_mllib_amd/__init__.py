@@ -17,5 +17,6 @@ __version__ = "0.1.0"
 _loader.require_on_gpu_hosts()
 
 __all__ = ["Config", "get_config", "set_config", "DenseMatrix", "DenseVector", "Matrices",
-           "SparseVector", "Vectors", "KMeans", "KMeansModel", "KMeansSummary", "PCA", "PCAModel", "ALS", "ALSModel", "get_world",
+           "SparseVector", "Vectors", "KMeans", "KMeansModel", "KMeansSummary", "PCA", "PCAModel",
+           "ALS", "ALSModel", "get_world",
            "init_world", "shutdown_world", "__version__"]

@@ -51,7 +51,8 @@ def find_closest(x: np.ndarray, c: np.ndarray, measure: str = EUCLIDEAN,
         xs = x[s:s + chunk]
         if measure == EUCLIDEAN:
             # exact fp64 distances (no expansion) to match Spark's precise fallback
-            d = ((xs[:, None, :] - c[None, :, :]) ** 2).sum(-1) if c.shape[0] * xs.shape[1] <= 4096 \
+            small = c.shape[0] * xs.shape[1] <= 4096
+            d = ((xs[:, None, :] - c[None, :, :]) ** 2).sum(-1) if small \
                 else pairwise_cost(xs, c, measure)
         else:
             d = pairwise_cost(xs, c, measure)

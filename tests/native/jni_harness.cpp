@@ -234,8 +234,9 @@ int main() {
                                                                    X[9 + j]);
   }
   FakeObject* kres = make_obj("KMeansResult");
-  const jlong centers = Java_org_apache_spark_ml_clustering_KMeansDALImpl_cKMeansDALComputeWithInitCenters(
-      env, nullptr, xt, ct, 2, 1e-4, 10, 1, 1, kres);
+  const jlong centers =
+      Java_org_apache_spark_ml_clustering_KMeansDALImpl_cKMeansDALComputeWithInitCenters(
+          env, nullptr, xt, ct, 2, 1e-4, 10, 1, 1, kres);
   REQUIRE(g_errors.empty() && centers != 0);
   REQUIRE(kres->vals.at("iterationNum") >= 1);
   REQUIRE(std::fabs(kres->vals.at("totalCost") - 0.12) < 1e-9);

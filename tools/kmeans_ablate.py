@@ -24,14 +24,16 @@ out = {}
 for name, precise, ab in [("full", False, 0), ("no_accumulate", False, 1), ("no_cost", False, 2),
                           ("no_acc_no_cost", False, 3), ("no_distance", False, 8),
                           ("loads_only", False, 11), ("precise_full", True, 0),
-                          ("precise_no_acc_no_cost", True, 3), ("full_prefetch2", False, 16), ("full_tier3_only", False, 32)]:
+                          ("precise_no_acc_no_cost", True, 3), ("full_prefetch2", False, 16),
+                          ("full_tier3_only", False, 32)]:
     if only and name not in only:
         continue
     ms = N.kmeans_assign_timing(g, t, C, reps, precise, ab)
     out[name] = round(ms * 100e6 / rows, 3)  # normalised to 100M rows
 # bf16 rows (same data rounded), LDS-resident centroids
 tb = N.synth_blobs(g, rows, d, N.kmeans_ld(d, "bf16"), 0, k, 10.0, 1.0, 20240917, "bf16")
-for name, ab in [("bf16_full", 0), ("bf16_prefetch2", 16), ("bf16_no_acc_no_cost", 3), ("bf16_tier3_only", 32)]:
+for name, ab in [("bf16_full", 0), ("bf16_prefetch2", 16), ("bf16_no_acc_no_cost", 3),
+                 ("bf16_tier3_only", 32)]:
     if only and name not in only:
         continue
     out[name] = round(N.kmeans_assign_timing(g, tb, C, reps, False, ab) * 100e6 / rows, 3)

@@ -39,5 +39,6 @@ for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM", "SQ
         out[c + "_per_tile"] = round(vals[c] / tiles, 2)
 if "SQ_VALU_MFMA_BUSY_CYCLES" in vals and "GRBM_GUI_ACTIVE" in vals:
     # busy cycles summed over SIMDs (1024) against the GPU-active clock
-    out["mfma_busy_frac"] = round(vals["SQ_VALU_MFMA_BUSY_CYCLES"] / (vals["GRBM_GUI_ACTIVE"] * 1024), 4)
+    busy = vals["SQ_VALU_MFMA_BUSY_CYCLES"] / (vals["GRBM_GUI_ACTIVE"] * 1024)
+    out["mfma_busy_frac"] = round(busy, 4)
 print(json.dumps(out, indent=1))
