@@ -16,10 +16,12 @@ def _shard(X, rank, world):
     return X[lo: lo + base + (1 if rank < rem else 0)]
 
 
-def kmeans_native(n=4000, d=6, k=5, seed=7, device="cpu", use_rccl=True, init_mode="k-means||"):
+def kmeans_native(n=4000, d=6, k=5, seed=7, device="cpu", use_rccl=True, init_mode="k-means||",
+                  device_id=0):
     import oap_mllib_amd as O
 
-    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl, device_id=0))
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl,
+                                             device_id=device_id))
     X = _blobs(n, d, k, seed)
     local = _shard(X, w.rank, w.size)
     m = O.KMeans(k=k, seed=seed, maxIter=25, initMode=init_mode).fit(local)
@@ -78,10 +80,11 @@ def host_comm_collectives():
     return out
 
 
-def pca_native(n=3000, d=12, k=4, seed=5, device="cpu", use_rccl=True):
+def pca_native(n=3000, d=12, k=4, seed=5, device="cpu", use_rccl=True, device_id=0):
     import oap_mllib_amd as O
 
-    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl, device_id=0))
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl,
+                                             device_id=device_id))
     rng = np.random.default_rng(seed)
     X = rng.normal(size=(n, d)) @ rng.normal(size=(d, d)) + 50.0
     local = _shard(X, w.rank, w.size)
@@ -92,11 +95,12 @@ def pca_native(n=3000, d=12, k=4, seed=5, device="cpu", use_rccl=True):
     return out
 
 
-def als_native(seed=3, device="cpu", use_rccl=True, rank=3):
+def als_native(seed=3, device="cpu", use_rccl=True, rank=3, device_id=0):
     import oap_mllib_amd as O
     from test_als import gen_implicit
 
-    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl, device_id=0))
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl,
+                                             device_id=device_id))
     tr, _ = gen_implicit(30, 50, 2, 0.01, seed)
     mine = {k: v[w.rank::w.size] for k, v in tr.items()}  # a strided (non-range) partition
     m = O.ALS(rank=rank, maxIter=4, regParam=0.01, implicitPrefs=True, seed=0).fit(mine)
