@@ -10,6 +10,7 @@
 #include "bindings/bindings.h"
 #include "drivers/pca.h"
 #include "linalg/eigen.h"
+#include "linalg/eigen_gpu.h"
 
 namespace py = pybind11;
 using namespace oap;
@@ -28,10 +29,11 @@ void register_pca(py::module_& m) {
   m.def(
       "pca_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
-         int k, bool precise) {
+         int k, bool precise, bool gpu_eig) {
         PcaParams p;
         p.k = k;
         p.precise = precise;
+        p.gpu_eig = gpu_eig;
         PcaResult r;
         {
           py::gil_scoped_release rel;
@@ -47,10 +49,14 @@ void register_pca(py::module_& m) {
         out["allreduce_ms"] = r.allreduce_ms;
         out["eig_ms"] = r.eig_ms;
         out["total_ms"] = r.total_ms;
+        out["eig_on_gpu"] = r.eig_on_gpu;
+        out["eig_tridiag_ms"] = r.eig_tridiag_ms;
+        out["eig_host_ms"] = r.eig_host_ms;
+        out["eig_backtransform_ms"] = r.eig_backtransform_ms;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("k"),
-      py::arg("precise") = false);
+      py::arg("precise") = false, py::arg("gpu_eig") = true);
   m.def(
       "pca_covariance",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
@@ -89,4 +95,31 @@ void register_pca(py::module_& m) {
       },
       py::arg("a"), py::arg("k") = 0, py::arg("threads") = 4,
       "Eigen-decomposition of a symmetric matrix: (values sorted by |.| desc, vectors n x k).");
+  m.def(
+      "sym_eig_gpu",
+      [](std::shared_ptr<Context> ctx,
+         py::array_t<double, py::array::c_style | py::array::forcecast> a, int k) {
+        if (a.ndim() != 2 || a.shape(0) != a.shape(1))
+          throw ConfigError("sym_eig_gpu expects a square matrix");
+        const int n = static_cast<int>(a.shape(0));
+        if (k <= 0 || k > n) k = n;
+        SymEig e;
+        GpuEigTiming t;
+        {
+          py::gil_scoped_release rel;
+          hipStream_t s = ctx->compute();
+          Buffer da = ctx->alloc(sizeof(double) * size_t(n) * n);
+          ctx->copy_to_backend(da.data(), a.data(), sizeof(double) * size_t(n) * n, s);
+          e = sym_eig_topk_gpu(*ctx, da.as<double>(), n, k, s, &t);
+        }
+        py::dict tm;
+        tm["tridiag_ms"] = t.tridiag_ms;
+        tm["bisect_ms"] = t.bisect_ms;
+        tm["host_ms"] = t.host_ms;
+        tm["backtransform_ms"] = t.backtransform_ms;
+        return py::make_tuple(e.values, to_array(e.vectors, n, k), tm);
+      },
+      py::arg("ctx"), py::arg("a"), py::arg("k"),
+      "Device eigensolver (tridiagonalisation + back-transform on the GPU): (values, vectors, "
+      "timing).");
 }

@@ -6,6 +6,7 @@
 
 #include "kernels/kernels.h"
 #include "linalg/eigen.h"
+#include "linalg/eigen_gpu.h"
 #include "runtime/log.h"
 
 namespace oap {
@@ -153,7 +154,19 @@ PcaResult pca_fit(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p) {
   SymEig eg;
   {
     TraceRange tr(&ctx.metrics(), "pca/eigensolver");
-    eg = sym_eig_topk(cv.cov, d, p.k, &ctx.pool());
+    if (p.gpu_eig && sym_eig_gpu_supported(ctx, d, p.k)) {
+      hipStream_t s = ctx.compute();
+      Buffer dcov = ctx.alloc(sizeof(double) * size_t(d) * d);
+      ctx.copy_to_backend(dcov.data(), cv.cov.data(), sizeof(double) * cv.cov.size(), s);
+      GpuEigTiming t;
+      eg = sym_eig_topk_gpu(ctx, dcov.as<double>(), d, p.k, s, &t);
+      r.eig_on_gpu = true;
+      r.eig_tridiag_ms = t.tridiag_ms;
+      r.eig_host_ms = t.host_ms;
+      r.eig_backtransform_ms = t.backtransform_ms;
+    } else {
+      eg = sym_eig_topk(cv.cov, d, p.k, &ctx.pool());
+    }
   }
   r.eig_ms = ms_since(t1);
   r.eigenvalues = eg.values;

@@ -23,6 +23,7 @@ struct PcaParams {
   int k = 1;
   bool precise = false;  // 4-term bf16 split products (adds lo*lo); default 3-term
   int flush_rows = 4096; // rows accumulated in fp32 before the fp64 flush (GPU)
+  bool gpu_eig = true;   // device eigensolver (linalg/eigen_gpu.h) when the context is a GPU
 };
 
 struct PcaCovariance {
@@ -42,6 +43,8 @@ struct PcaResult {
   std::vector<double> eigenvalues;  // all d, |.|-descending
   std::vector<double> mean;
   double stats_ms = 0.0, allreduce_ms = 0.0, eig_ms = 0.0, total_ms = 0.0;
+  bool eig_on_gpu = false;
+  double eig_tridiag_ms = 0.0, eig_host_ms = 0.0, eig_backtransform_ms = 0.0;
 };
 
 PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p);

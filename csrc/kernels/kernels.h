@@ -282,5 +282,22 @@ void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
 void pca_reduce(const PcaPlan& p, const double* part, const double* cpart, int d, double* out,
                 double* colsum, hipStream_t s);
 
+// ----------------------------------------------------------------------------- eigensolver
+// Householder tridiagonalisation of a symmetric n x n fp64 matrix (device, row-major, full) by one
+// persistent cooperative kernel with the matrix LDS-resident across the CUs (eig.hip).  Outputs:
+// d[n], e[n] (e[n-2] last coupling; e[n-1] untouched), reflector rows vrows[n x n] and tau[n].
+// scratch: eig_tridiag_scratch_doubles(n, num_cus) doubles; bar: 2 zeroed-by-the-call unsigned.
+bool eig_tridiag_supported(int n, int num_cus);
+int eig_tridiag_grid(int n, int num_cus);
+size_t eig_tridiag_scratch_doubles(int n, int num_cus);
+void eig_tridiag(const double* a, int n, int num_cus, double* d, double* e, double* vrows,
+                 double* tau, double* scratch, unsigned* bar, hipStream_t s);
+// All n eigenvalues (ascending) of the symmetric tridiagonal (d, e) by multisection; [lo, hi)
+// must bracket the spectrum (Gershgorin), pivmin as LAPACK's.  Device pointers.
+void eig_bisect(const double* d, const double* e, int n, double lo, double hi, double pivmin,
+                double* out, hipStream_t s);
+// Z (n x k row-major, device) <- Q Z with the reflectors of eig_tridiag.
+void eig_apply_q(const double* vrows, const double* tau, int n, int k, double* z, hipStream_t s);
+
 }  // namespace kern
 }  // namespace oap

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <functional>
 #include <numeric>
 
 #include "runtime/common.h"
@@ -308,7 +309,8 @@ struct TriLU {
 // sel: eigenvalues in the order wanted.  Returns z (n x kk, column j for sel[j]) row-major.
 std::vector<double> tridiag_inverse_iteration(const std::vector<double>& d,
                                               const std::vector<double>& e, int n,
-                                              const std::vector<double>& sel) {
+                                              const std::vector<double>& sel,
+                                              ThreadPool* pool = nullptr) {
   const int kk = static_cast<int>(sel.size());
   double tnorm = 0.0;
   for (int i = 0; i < n; ++i)
@@ -317,46 +319,64 @@ std::vector<double> tridiag_inverse_iteration(const std::vector<double>& d,
   if (tnorm == 0.0) tnorm = 1.0;
   const double ortol = 1e-3 * tnorm, pert = 10.0 * DBL_EPSILON * tnorm;
   const double tiny = DBL_EPSILON * tnorm;
-  std::vector<std::vector<double>> zs(kk);
+  // clusters of close eigenvalues (exact multiples separated) first: the vectors of one cluster
+  // are orthogonalised in order, different clusters are independent (thread pool)
   std::vector<double> lam(sel);
-  TriLU lu;
-  std::vector<double> b(n);
-  int cluster_start = 0;
+  std::vector<int> cstart(kk, 0);
   for (int j = 0; j < kk; ++j) {
     if (j > 0 && std::fabs(lam[j] - lam[j - 1]) < ortol) {
       if (std::fabs(lam[j] - lam[j - 1]) < pert)  // separate exact multiples
         lam[j] = lam[j - 1] + (lam[j] <= lam[j - 1] ? -pert : pert);
+      cstart[j] = cstart[j - 1];
     } else {
-      cluster_start = j;
+      cstart[j] = j;
     }
-    lu.factor(d, e, n, lam[j], tiny);
-    uint64_t st = 0x9e3779b97f4a7c15ull * uint64_t(j + 1);
-    for (int i = 0; i < n; ++i) {  // deterministic start vector
-      st ^= st << 13;
-      st ^= st >> 7;
-      st ^= st << 17;
-      b[i] = double(st >> 11) * (1.0 / 9007199254740992.0) - 0.5;
-    }
-    for (int it = 0; it < 4; ++it) {
-      lu.solve(b, n);
-      for (int q = cluster_start; q < j; ++q) {  // MGS against the cluster's vectors
-        const std::vector<double>& z = zs[q];
-        double dot = 0.0;
-        for (int i = 0; i < n; ++i) dot += z[i] * b[i];
-        for (int i = 0; i < n; ++i) b[i] -= dot * z[i];
-      }
-      double nrm = 0.0;
-      for (int i = 0; i < n; ++i) nrm += b[i] * b[i];
-      nrm = std::sqrt(nrm);
-      if (nrm == 0.0) {
-        std::fill(b.begin(), b.end(), 0.0);
-        b[j % n] = 1.0;
-        continue;
-      }
-      for (int i = 0; i < n; ++i) b[i] /= nrm;
-    }
-    zs[j] = b;
   }
+  std::vector<int> heads;
+  for (int j = 0; j < kk; ++j)
+    if (cstart[j] == j) heads.push_back(j);
+  std::vector<std::vector<double>> zs(kk);
+  auto run_cluster = [&](int h) {
+    const int j0 = heads[h], j1 = h + 1 < int(heads.size()) ? heads[h + 1] : kk;
+    TriLU lu;
+    std::vector<double> b(n);
+    for (int j = j0; j < j1; ++j) {
+      lu.factor(d, e, n, lam[j], tiny);
+      uint64_t st = 0x9e3779b97f4a7c15ull * uint64_t(j + 1);
+      for (int i = 0; i < n; ++i) {  // deterministic start vector
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        b[i] = double(st >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+      }
+      for (int it = 0; it < 4; ++it) {
+        lu.solve(b, n);
+        for (int q = j0; q < j; ++q) {  // MGS against the cluster's vectors
+          const std::vector<double>& z = zs[q];
+          double dot = 0.0;
+          for (int i = 0; i < n; ++i) dot += z[i] * b[i];
+          for (int i = 0; i < n; ++i) b[i] -= dot * z[i];
+        }
+        double nrm = 0.0;
+        for (int i = 0; i < n; ++i) nrm += b[i] * b[i];
+        nrm = std::sqrt(nrm);
+        if (nrm == 0.0) {
+          std::fill(b.begin(), b.end(), 0.0);
+          b[j % n] = 1.0;
+          continue;
+        }
+        for (int i = 0; i < n; ++i) b[i] /= nrm;
+      }
+      zs[j] = b;
+    }
+  };
+  const int nh = static_cast<int>(heads.size());
+  if (pool && pool->size() > 1 && nh > 1 && int64_t(n) * kk > 20000)
+    pool->parallel_for(nh, [&](int, int64_t b, int64_t e2) {
+      for (int64_t h = b; h < e2; ++h) run_cluster(int(h));
+    });
+  else
+    for (int h = 0; h < nh; ++h) run_cluster(h);
   std::vector<double> z(size_t(n) * kk);
   for (int j = 0; j < kk; ++j)
     for (int i = 0; i < n; ++i) z[size_t(i) * kk + j] = zs[j][i];
@@ -386,6 +406,43 @@ void apply_q(const std::vector<Reflector>& refl, int n, std::vector<double>& z, 
   }
 }
 
+// sign: largest-magnitude component positive
+void normalize_signs(std::vector<double>& vecs, int n, int keep) {
+  for (int j = 0; j < keep; ++j) {
+    int big = 0;
+    for (int i = 1; i < n; ++i)
+      if (std::fabs(vecs[size_t(i) * keep + j]) > std::fabs(vecs[size_t(big) * keep + j])) big = i;
+    if (vecs[size_t(big) * keep + j] < 0.0)
+      for (int i = 0; i < n; ++i) vecs[size_t(i) * keep + j] = -vecs[size_t(i) * keep + j];
+  }
+}
+
+// Eigenvalues (QL, |lambda| descending) and the first `keep` eigenvectors of the tridiagonal by
+// inverse iteration, back-transformed by apply_q.
+SymEig tridiag_topk(const std::vector<double>& td, const std::vector<double>& te, int n, int keep,
+                    const std::function<void(std::vector<double>&, int)>& apply_q_fn,
+                    const std::vector<double>* eigvals = nullptr, ThreadPool* pool = nullptr) {
+  SymEig out;
+  out.n = n;
+  std::vector<double> diag = td, off = te;
+  if (eigvals)
+    diag = *eigvals;
+  else
+    tridiag_ql(diag, off, n, nullptr);
+  std::vector<int> perm(n);
+  std::iota(perm.begin(), perm.end(), 0);
+  std::stable_sort(perm.begin(), perm.end(),
+                   [&](int x, int y) { return std::fabs(diag[x]) > std::fabs(diag[y]); });
+  out.values.resize(n);
+  for (int j = 0; j < n; ++j) out.values[j] = diag[perm[j]];
+  std::vector<double> sel(out.values.begin(), out.values.begin() + keep);
+  std::vector<double> vecs = tridiag_inverse_iteration(td, te, n, sel, pool);
+  apply_q_fn(vecs, keep);
+  normalize_signs(vecs, n, keep);
+  out.vectors = std::move(vecs);
+  return out;
+}
+
 SymEig solve(const std::vector<double>& A, int n, int keep, ThreadPool* pool) {
   OAP_CHECK(n > 0 && A.size() == size_t(n) * n, "sym_eig: bad matrix size");
   keep = std::max(1, std::min(keep, n));
@@ -401,15 +458,9 @@ SymEig solve(const std::vector<double>& A, int n, int keep, ThreadPool* pool) {
   std::vector<double> vecs;  // n x keep, column j = eigenvector j (before sign normalisation)
   std::vector<double> vals(n);
   if (2 * keep <= n) {
-    tridiag_ql(diag, off, n, nullptr);
-    std::vector<int> perm(n);
-    std::iota(perm.begin(), perm.end(), 0);
-    std::stable_sort(perm.begin(), perm.end(),
-                     [&](int x, int y) { return std::fabs(diag[x]) > std::fabs(diag[y]); });
-    for (int j = 0; j < n; ++j) vals[j] = diag[perm[j]];
-    std::vector<double> sel(vals.begin(), vals.begin() + keep);
-    vecs = tridiag_inverse_iteration(td, te, n, sel);
-    apply_q(refl, n, vecs, keep, pool);
+    return tridiag_topk(
+        td, te, n, keep,
+        [&](std::vector<double>& z, int kk) { apply_q(refl, n, z, kk, pool); }, nullptr, pool);
   } else {
     // many vectors: QL with every rotation replayed on Q^T (rows i, i+1), column slices per
     // thread
@@ -442,19 +493,22 @@ SymEig solve(const std::vector<double>& A, int n, int keep, ThreadPool* pool) {
       for (int i = 0; i < n; ++i) vecs[size_t(i) * keep + j] = vt[size_t(perm[j]) * n + i];
   }
   out.values = vals;
-  // sign: largest-magnitude component positive
-  for (int j = 0; j < keep; ++j) {
-    int big = 0;
-    for (int i = 1; i < n; ++i)
-      if (std::fabs(vecs[size_t(i) * keep + j]) > std::fabs(vecs[size_t(big) * keep + j])) big = i;
-    if (vecs[size_t(big) * keep + j] < 0.0)
-      for (int i = 0; i < n; ++i) vecs[size_t(i) * keep + j] = -vecs[size_t(i) * keep + j];
-  }
+  normalize_signs(vecs, n, keep);
   out.vectors = std::move(vecs);
   return out;
 }
 
 }  // namespace
+
+SymEig sym_eig_from_tridiag(const std::vector<double>& d, const std::vector<double>& e, int n,
+                            int keep,
+                            const std::function<void(std::vector<double>&, int)>& apply_q_fn,
+                            const std::vector<double>* eigvals, ThreadPool* pool) {
+  OAP_CHECK(n > 0 && int(d.size()) == n && int(e.size()) == n, "sym_eig_from_tridiag: sizes");
+  OAP_CHECK(!eigvals || int(eigvals->size()) == n, "sym_eig_from_tridiag: eigenvalue count");
+  keep = std::max(1, std::min(keep, n));
+  return tridiag_topk(d, e, n, keep, apply_q_fn, eigvals, pool);
+}
 
 SymEig sym_eig(const std::vector<double>& A, int n, ThreadPool* pool) {
   return solve(A, n, n, pool);

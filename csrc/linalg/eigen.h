@@ -8,6 +8,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "runtime/thread_pool.h"
@@ -26,5 +27,16 @@ SymEig sym_eig(const std::vector<double>& A, int n, ThreadPool* pool);
 
 // Same, only the first `k` eigenvectors are kept (values still hold all n eigenvalues).
 SymEig sym_eig_topk(const std::vector<double>& A, int n, int k, ThreadPool* pool);
+
+// From an already tridiagonalised A = Q T Q^T (d: n diagonal, e: n off-diagonal, e[n-1] = 0):
+// all eigenvalues (QL, or the given `eigvals` in any order) and the first `keep` eigenvectors of
+// T (inverse iteration), which apply_q(z, keep) maps to eigenvectors of A in place (z: n x keep
+// row-major).  The GPU path (linalg/eigen_gpu.h) tridiagonalises, bisects and back-transforms on
+// the device around this.
+SymEig sym_eig_from_tridiag(const std::vector<double>& d, const std::vector<double>& e, int n,
+                            int keep,
+                            const std::function<void(std::vector<double>&, int)>& apply_q,
+                            const std::vector<double>* eigvals = nullptr,
+                            ThreadPool* pool = nullptr);
 
 }  // namespace oap
