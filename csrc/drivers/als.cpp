@@ -5,10 +5,12 @@
 #include <climits>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
-#include "kernels/rng.h"
+#include "kernels/als_setup.h"
 #include "kernels/kernels.h"
+#include "kernels/rng.h"
 #include "runtime/log.h"
 
 namespace oap {
@@ -306,79 +308,106 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   res.rank = r;
   auto t_setup = std::chrono::steady_clock::now();
 
-  // ---- 1. ratings -> item owners; dense item indices --------------------------------------
   Side U, I;
-  std::vector<Rec> recv1;
-  if (P == 1) {
-    recv1.resize(n);
-    ctx.pool().parallel_for(n, [&](int, int64_t b, int64_t e) {
-      for (int64_t k = b; k < e; ++k) recv1[k] = {users[k], items[k], ratings[k]};
-    });
-  } else {
-    std::vector<std::vector<Rec>> out(P);
-    for (int64_t k = 0; k < n; ++k)
-      out[owner_of(items[k], P)].push_back({users[k], items[k], ratings[k]});
-    recv1 = exchange(ctx, comm, out);
+  // ---- single rank on a GPU: re-indexing and both CSRs on the device (kernels/als_setup.hip)
+  kern::AlsDeviceSetup dev_setup;
+  bool on_device = false;
+  if (P == 1 && ctx.is_gpu() && !std::getenv("OAP_ALS_HOST_SETUP")) {
+    ctx.activate();
+    on_device = kern::als_device_setup(ctx, users, items, ratings, n, ctx.compute(), &dev_setup);
   }
-  IdIndex item_idx;
-  item_idx.build(ctx.pool(), recv1, false);
-  const std::vector<int32_t>& my_items = item_idx.ids;
-  I.cnt = allgather_i64(ctx, comm, {int64_t(my_items.size())});
-  I.off.assign(P + 1, 0);
-  for (int q = 0; q < P; ++q) I.off[q + 1] = I.off[q] + I.cnt[q];
-  I.n = I.off[P];
-  // ---- 2. -> user owners; dense user indices, user CSR (cols = global item index) ---------
-  std::vector<Rec> recv2;
-  if (P == 1) {
-    ctx.pool().parallel_for(int64_t(recv1.size()), [&](int, int64_t b, int64_t e) {
-      for (int64_t k = b; k < e; ++k) recv1[k].b = int32_t(item_idx.rank(recv1[k].b));
-    });
-    recv2.swap(recv1);
+  if (on_device) {
+    auto fill = [](Side& S, std::vector<int32_t>& ids, kern::AlsDeviceCsr& c) {
+      S.n = c.nrows;
+      S.cnt = {c.nrows};
+      S.off = {0, c.nrows};
+      S.ids = std::move(ids);
+      S.csr.ptr = c.ptr_h;  // (cols / values stay on the device)
+    };
+    fill(U, dev_setup.user_ids, dev_setup.users);
+    fill(I, dev_setup.item_ids, dev_setup.items);
+    res.nnz = n;
+    res.setup_ms = ms_since(t_setup);
+    ctx.metrics().add("als/setup", res.setup_ms * 1e3, n * int64_t(sizeof(Rec)) * 3);
+    if (Logger::instance().level() <= LogLevel::Info)
+      Logger::instance().log(LogLevel::Info, "als/device_setup",
+                             "\"upload_ms\":" + std::to_string(dev_setup.upload_ms) +
+                                 ",\"index_ms\":" + std::to_string(dev_setup.index_ms) +
+                                 ",\"sort_ms\":" + std::to_string(dev_setup.sort_ms));
   } else {
-    std::vector<std::vector<Rec>> out(P);
-    for (const Rec& x : recv1)
-      out[owner_of(x.a, P)].push_back({x.a, int32_t(I.off[me] + item_idx.rank(x.b)), x.r});
-    std::vector<Rec>().swap(recv1);
-    recv2 = exchange(ctx, comm, out);
-  }
-  IdIndex user_idx;
-  user_idx.build(ctx.pool(), recv2, true);
-  const std::vector<int32_t>& my_users = user_idx.ids;
-  U.cnt = allgather_i64(ctx, comm, {int64_t(my_users.size())});
-  U.off.assign(P + 1, 0);
-  for (int q = 0; q < P; ++q) U.off[q + 1] = U.off[q] + U.cnt[q];
-  U.n = U.off[P];
-  ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
-    for (int64_t k = b; k < e; ++k) recv2[k].a = int32_t(U.off[me] + user_idx.rank(recv2[k].a));
-  });
-  // ---- 3. (global user, global item) -> item owners: item CSR (cols = global user index) --
-  std::vector<Rec> recv3;
-  if (P == 1) {
-    recv3.resize(recv2.size());
-    ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
-      for (int64_t k = b; k < e; ++k) recv3[k] = {recv2[k].b, recv2[k].a, recv2[k].r};
-    });
-  } else {
-    std::vector<std::vector<Rec>> out(P);
-    for (const Rec& x : recv2) {
-      const int q =
-          int(std::upper_bound(I.off.begin(), I.off.end(), int64_t(x.b)) - I.off.begin()) - 1;
-      out[q].push_back({x.b, x.a, x.r});
+    // ---- 1. ratings -> item owners; dense item indices --------------------------------------
+    std::vector<Rec> recv1;
+    if (P == 1) {
+      recv1.resize(n);
+      ctx.pool().parallel_for(n, [&](int, int64_t b, int64_t e) {
+        for (int64_t k = b; k < e; ++k) recv1[k] = {users[k], items[k], ratings[k]};
+      });
+    } else {
+      std::vector<std::vector<Rec>> out(P);
+      for (int64_t k = 0; k < n; ++k)
+        out[owner_of(items[k], P)].push_back({users[k], items[k], ratings[k]});
+      recv1 = exchange(ctx, comm, out);
     }
-    recv3 = exchange(ctx, comm, out);
-  }
-  U.csr = build_csr(ctx.pool(), recv2, U.cnt[me], U.off[me]);
-  I.csr = build_csr(ctx.pool(), recv3, I.cnt[me], I.off[me]);
-  std::vector<Rec>().swap(recv2);
-  std::vector<Rec>().swap(recv3);
-  U.ids = allgatherv_i32(ctx, comm, my_users, U.cnt);
-  I.ids = allgatherv_i32(ctx, comm, my_items, I.cnt);
-  {
-    int64_t nn = int64_t(U.csr.col.size());
-    res.nnz = int64_t(comm_allreduce_scalar(ctx, comm, double(nn), ReduceOp::Sum));
-  }
-  res.setup_ms = ms_since(t_setup);
-  ctx.metrics().add("als/setup", res.setup_ms * 1e3, res.nnz * int64_t(sizeof(Rec)) * 3);
+    IdIndex item_idx;
+    item_idx.build(ctx.pool(), recv1, false);
+    const std::vector<int32_t>& my_items = item_idx.ids;
+    I.cnt = allgather_i64(ctx, comm, {int64_t(my_items.size())});
+    I.off.assign(P + 1, 0);
+    for (int q = 0; q < P; ++q) I.off[q + 1] = I.off[q] + I.cnt[q];
+    I.n = I.off[P];
+    // ---- 2. -> user owners; dense user indices, user CSR (cols = global item index) ---------
+    std::vector<Rec> recv2;
+    if (P == 1) {
+      ctx.pool().parallel_for(int64_t(recv1.size()), [&](int, int64_t b, int64_t e) {
+        for (int64_t k = b; k < e; ++k) recv1[k].b = int32_t(item_idx.rank(recv1[k].b));
+      });
+      recv2.swap(recv1);
+    } else {
+      std::vector<std::vector<Rec>> out(P);
+      for (const Rec& x : recv1)
+        out[owner_of(x.a, P)].push_back({x.a, int32_t(I.off[me] + item_idx.rank(x.b)), x.r});
+      std::vector<Rec>().swap(recv1);
+      recv2 = exchange(ctx, comm, out);
+    }
+    IdIndex user_idx;
+    user_idx.build(ctx.pool(), recv2, true);
+    const std::vector<int32_t>& my_users = user_idx.ids;
+    U.cnt = allgather_i64(ctx, comm, {int64_t(my_users.size())});
+    U.off.assign(P + 1, 0);
+    for (int q = 0; q < P; ++q) U.off[q + 1] = U.off[q] + U.cnt[q];
+    U.n = U.off[P];
+    ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k) recv2[k].a = int32_t(U.off[me] + user_idx.rank(recv2[k].a));
+    });
+    // ---- 3. (global user, global item) -> item owners: item CSR (cols = global user index) --
+    std::vector<Rec> recv3;
+    if (P == 1) {
+      recv3.resize(recv2.size());
+      ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
+        for (int64_t k = b; k < e; ++k) recv3[k] = {recv2[k].b, recv2[k].a, recv2[k].r};
+      });
+    } else {
+      std::vector<std::vector<Rec>> out(P);
+      for (const Rec& x : recv2) {
+        const int q =
+            int(std::upper_bound(I.off.begin(), I.off.end(), int64_t(x.b)) - I.off.begin()) - 1;
+        out[q].push_back({x.b, x.a, x.r});
+      }
+      recv3 = exchange(ctx, comm, out);
+    }
+    U.csr = build_csr(ctx.pool(), recv2, U.cnt[me], U.off[me]);
+    I.csr = build_csr(ctx.pool(), recv3, I.cnt[me], I.off[me]);
+    std::vector<Rec>().swap(recv2);
+    std::vector<Rec>().swap(recv3);
+    U.ids = allgatherv_i32(ctx, comm, my_users, U.cnt);
+    I.ids = allgatherv_i32(ctx, comm, my_items, I.cnt);
+    {
+      int64_t nn = int64_t(U.csr.col.size());
+      res.nnz = int64_t(comm_allreduce_scalar(ctx, comm, double(nn), ReduceOp::Sum));
+    }
+    res.setup_ms = ms_since(t_setup);
+    ctx.metrics().add("als/setup", res.setup_ms * 1e3, res.nnz * int64_t(sizeof(Rec)) * 3);
+  }  // host setup
 
   std::vector<float> Xh, Yh;  // final factors (host, [n][ld])
   auto t_train = std::chrono::steady_clock::now();
@@ -395,15 +424,21 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     } dU, dI;
     // rows longer than kLong ratings are split into kLong-sized chunks (partial Gramians)
     constexpr int64_t kLong = 4096;
-    auto upload_side = [&](Side& S, Dev& D) {
+    auto upload_side = [&](Side& S, Dev& D, kern::AlsDeviceCsr* dc) {
       D.f = ctx.alloc(std::max<size_t>(size_t(S.n) * ld * 4, 256));
-      D.ptr = ctx.alloc(S.csr.ptr.size() * 8);
-      D.col = ctx.alloc(std::max<size_t>(S.csr.col.size() * 4, 16));
-      D.val = ctx.alloc(std::max<size_t>(S.csr.val.size() * 4, 16));
-      ctx.copy_to_backend(D.ptr.data(), S.csr.ptr.data(), S.csr.ptr.size() * 8, s);
-      if (!S.csr.col.empty()) {
-        ctx.copy_to_backend(D.col.data(), S.csr.col.data(), S.csr.col.size() * 4, s);
-        ctx.copy_to_backend(D.val.data(), S.csr.val.data(), S.csr.val.size() * 4, s);
+      if (dc) {  // built on the device
+        D.ptr = std::move(dc->ptr);
+        D.col = std::move(dc->col);
+        D.val = std::move(dc->val);
+      } else {
+        D.ptr = ctx.alloc(S.csr.ptr.size() * 8);
+        D.col = ctx.alloc(std::max<size_t>(S.csr.col.size() * 4, 16));
+        D.val = ctx.alloc(std::max<size_t>(S.csr.val.size() * 4, 16));
+        ctx.copy_to_backend(D.ptr.data(), S.csr.ptr.data(), S.csr.ptr.size() * 8, s);
+        if (!S.csr.col.empty()) {
+          ctx.copy_to_backend(D.col.data(), S.csr.col.data(), S.csr.col.size() * 4, s);
+          ctx.copy_to_backend(D.val.data(), S.csr.val.data(), S.csr.val.size() * 4, s);
+        }
       }
       ctx.memset(D.f.data(), 0, size_t(S.n) * ld * 4);
       std::vector<int32_t> sr, lr;
@@ -444,8 +479,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
           ctx.alloc(std::max<size_t>(size_t(D.n_chunks) * kern::als_partial_floats(r) * 4, 16));
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
-    upload_side(U, dU);
-    upload_side(I, dI);
+    upload_side(U, dU, on_device ? &dev_setup.users : nullptr);
+    upload_side(I, dI, on_device ? &dev_setup.items : nullptr);
     {  // initial user factors from their ids (world-size independent), or the caller's
       Buffer ids = ctx.alloc(std::max<size_t>(U.ids.size() * 4, 16));
       if (!U.ids.empty()) ctx.copy_to_backend(ids.data(), U.ids.data(), U.ids.size() * 4, s);

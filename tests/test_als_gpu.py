@@ -66,3 +66,23 @@ def test_api_gpu_engine(gpu_world):
     assert len(recs) == 30 and all(len(x) == 4 for x in recs["recommendations"])
     pred = m.transform(data)["prediction"].to_numpy()
     assert np.all(np.isfinite(pred))
+
+
+def test_device_setup_matches_host_setup(native, gpu_world, monkeypatch):
+    """The GPU re-indexing + radix-sort CSR build (kernels/als_setup.hip) gives the host
+    setup's ids and factors; sparse ids (range >> ratings) fall back to the host setup."""
+    u, i, r = _data(300, 200, 20000, 11)
+    dev = native.als_fit(gpu_world.ctx, gpu_world.comm, u, i, r, 12, 2, 0.1, 3.0, True, 3)
+    monkeypatch.setenv("OAP_ALS_HOST_SETUP", "1")
+    host = native.als_fit(gpu_world.ctx, gpu_world.comm, u, i, r, 12, 2, 0.1, 3.0, True, 3)
+    monkeypatch.delenv("OAP_ALS_HOST_SETUP")
+    assert np.array_equal(dev["user_ids"], host["user_ids"])
+    assert np.array_equal(dev["item_ids"], host["item_ids"])
+    assert dev["nnz"] == host["nnz"] == len(r)
+    np.testing.assert_allclose(dev["user_factors"], host["user_factors"], rtol=0,
+                               atol=1e-4 * np.abs(host["user_factors"]).max())
+    # sparse ids: (the dense index would need a 2^30-wide range)
+    us = (u.astype(np.int64) * 3_000_000 % (1 << 30)).astype(np.int32)
+    sp = native.als_fit(gpu_world.ctx, gpu_world.comm, us, i, r, 12, 2, 0.1, 3.0, True, 3)
+    assert len(sp["user_ids"]) == len(np.unique(us))
+    assert sp["failed_rows"] == 0
