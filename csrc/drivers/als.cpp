@@ -417,10 +417,16 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     ctx.activate();
     hipStream_t s = ctx.compute();
     const int cus = ctx.info().cu_count;
+    // Multi-rank: each half solves its owned rows in C row-range chunks; chunk c of every rank
+    // is broadcast (root = owner, straight into the replicated factor slab) on the comm stream
+    // while chunk c+1 solves on the compute stream.
+    const int C = P > 1 ? 4 : 1;
     struct Dev {
       Buffer f, ptr, col, val;
       Buffer short_rows, long_rows, long_chunk_ptr, chunk_begin, chunk_end, partials;
-      int64_t n_short = 0, n_long = 0, n_chunks = 0;
+      // per row-range chunk c: [sr_off[c], sr_off[c+1]) of short_rows, [lr_off[c], ...) of
+      // long_rows (long_chunk_ptr segment at lr_off[c] + c), [cb_off[c], ...) of chunk_begin/end
+      std::vector<int64_t> sr_off, lr_off, cb_off;
     } dU, dI;
     // rows longer than kLong ratings are split into kLong-sized chunks (partial Gramians)
     constexpr int64_t kLong = 4096;
@@ -442,26 +448,37 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       }
       ctx.memset(D.f.data(), 0, size_t(S.n) * ld * 4);
       std::vector<int32_t> sr, lr;
-      std::vector<int64_t> lcp{0}, cb, ce;
+      std::vector<int64_t> lcp, cb, ce;
       const int64_t nloc = int64_t(S.csr.ptr.size()) - 1;
-      // longest rows first: they start early and the short ones fill in behind them
-      std::vector<std::pair<int64_t, int32_t>> order;
-      order.reserve(nloc);
-      for (int64_t i = 0; i < nloc; ++i)
-        order.push_back({S.csr.ptr[i + 1] - S.csr.ptr[i], int32_t(i)});
-      std::stable_sort(order.begin(), order.end(),
-                       [](const auto& x, const auto& y) { return x.first > y.first; });
-      for (const auto& [len, i] : order) {
-        if (len > kLong) {
-          lr.push_back(i);
-          for (int64_t p0 = S.csr.ptr[i]; p0 < S.csr.ptr[i + 1]; p0 += kLong) {
-            cb.push_back(p0);
-            ce.push_back(std::min(p0 + kLong, S.csr.ptr[i + 1]));
+      D.sr_off.assign(1, 0);
+      D.lr_off.assign(1, 0);
+      D.cb_off.assign(1, 0);
+      for (int c = 0; c < C; ++c) {
+        const int64_t lo = nloc * c / C, hi = nloc * (c + 1) / C;
+        // longest rows first: they start early and the short ones fill in behind them
+        std::vector<std::pair<int64_t, int32_t>> order;
+        order.reserve(hi - lo);
+        for (int64_t i = lo; i < hi; ++i)
+          order.push_back({S.csr.ptr[i + 1] - S.csr.ptr[i], int32_t(i)});
+        std::stable_sort(order.begin(), order.end(),
+                         [](const auto& x, const auto& y) { return x.first > y.first; });
+        const int64_t cb0 = int64_t(cb.size());
+        lcp.push_back(0);
+        for (const auto& [len, i] : order) {
+          if (len > kLong) {
+            lr.push_back(i);
+            for (int64_t p0 = S.csr.ptr[i]; p0 < S.csr.ptr[i + 1]; p0 += kLong) {
+              cb.push_back(p0);
+              ce.push_back(std::min(p0 + kLong, S.csr.ptr[i + 1]));
+            }
+            lcp.push_back(int64_t(cb.size()) - cb0);
+          } else {
+            sr.push_back(i);
           }
-          lcp.push_back(int64_t(cb.size()));
-        } else {
-          sr.push_back(i);
         }
+        D.sr_off.push_back(int64_t(sr.size()));
+        D.lr_off.push_back(int64_t(lr.size()));
+        D.cb_off.push_back(int64_t(cb.size()));
       }
       auto up = [&](Buffer& b, const void* h, size_t bytes) {
         b = ctx.alloc(std::max<size_t>(bytes, 16));
@@ -472,11 +489,11 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       up(D.long_chunk_ptr, lcp.data(), lcp.size() * 8);
       up(D.chunk_begin, cb.data(), cb.size() * 8);
       up(D.chunk_end, ce.data(), ce.size() * 8);
-      D.n_short = int64_t(sr.size());
-      D.n_long = int64_t(lr.size());
-      D.n_chunks = int64_t(cb.size());
+      int64_t max_chunks = 1;
+      for (int c = 0; c < C; ++c)
+        max_chunks = std::max(max_chunks, D.cb_off[c + 1] - D.cb_off[c]);
       D.partials =
-          ctx.alloc(std::max<size_t>(size_t(D.n_chunks) * kern::als_partial_floats(r) * 4, 16));
+          ctx.alloc(std::max<size_t>(size_t(max_chunks) * kern::als_partial_floats(r) * 4, 16));
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
     upload_side(U, dU, on_device ? &dev_setup.users : nullptr);
@@ -499,22 +516,19 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     Buffer gram64 = ctx.alloc((size_t(r) * r + r) * 8), gram32 = ctx.alloc(size_t(r) * r * 4);
     Buffer zshift = ctx.alloc(size_t(ld + 128) * 4);
     ctx.memset(zshift.data(), 0, size_t(ld + 128) * 4);
-    int64_t maxu = 0, maxi = 0;
-    for (int q = 0; q < P; ++q) {
-      maxu = std::max(maxu, U.cnt[q]);
-      maxi = std::max(maxi, I.cnt[q]);
-    }
-    const int64_t maxrows = std::max<int64_t>(1, std::max(maxu, maxi));
-    Buffer stage, gathered;
-    if (P > 1) {
-      stage = ctx.alloc(size_t(maxrows) * ld * 4);
-      gathered = ctx.alloc(size_t(maxrows) * ld * 4 * P);
-    }
-    // one half-iteration: dst rows of side D from source side S
-    auto half = [&](Side& Dst, Dev& dD, Side& Src, Dev& dS) {
+    hipStream_t cs = ctx.comm_stream() ? ctx.comm_stream() : s;
+    const bool dev_comm = P > 1 && comm.on_device();
+    struct HalfEvents {
       Event e0, e1, e2, e3;
-      e0.record(s);
-      // Gramian of the source factors: owned slice -> allreduce
+      std::vector<Event> solved;  // per chunk (compute stream -> comm stream)
+      Event gram_in, gram_out, gathered;
+    };
+    std::vector<HalfEvents> hev(2);
+    // one half-iteration: dst rows of side D from source side S
+    auto half = [&](HalfEvents& E, Side& Dst, Dev& dD, Side& Src, Dev& dS) {
+      E.e0.record(s);
+      // Gramian of the source factors: owned slice -> allreduce (on the comm stream, after the
+      // previous half's broadcasts: every collective of this communicator is issued in one order)
       if (p.implicit) {
         const int64_t cnt = Src.cnt[me];
         const kern::PcaPlan plan = kern::pca_syrk_plan(cnt, r, cus);
@@ -523,22 +537,22 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
                        part.as<double>(), cpart.as<double>(), false, 4096, s);
         kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), r, gram64.as<double>(),
                          gram64.as<double>() + size_t(r) * r, s);
-        comm_allreduce(ctx, comm, gram64.data(), size_t(r) * r, DType::F64, ReduceOp::Sum, s);
+        if (dev_comm) {
+          E.gram_in.record(s);
+          E.gram_in.wait_on(cs);
+          comm.allreduce(gram64.data(), size_t(r) * r, DType::F64, ReduceOp::Sum, cs);
+          E.gram_out.record(cs);
+          E.gram_out.wait_on(s);
+        } else {
+          comm_allreduce(ctx, comm, gram64.data(), size_t(r) * r, DType::F64, ReduceOp::Sum, s);
+        }
         kern::f64_to_f32(gram64.as<double>(), gram32.as<float>(), int64_t(r) * r, s);
       }
-      e1.record(s);
+      E.e1.record(s);
       kern::AlsSolveArgs a;
       a.rowptr = dD.ptr.as<int64_t>();
       a.cols = dD.col.as<int32_t>();
       a.vals = dD.val.as<float>();
-      a.short_rows = dD.short_rows.as<int32_t>();
-      a.n_short = dD.n_short;
-      a.long_rows = dD.long_rows.as<int32_t>();
-      a.n_long = dD.n_long;
-      a.long_chunk_ptr = dD.long_chunk_ptr.as<int64_t>();
-      a.chunk_begin = dD.chunk_begin.as<int64_t>();
-      a.chunk_end = dD.chunk_end.as<int64_t>();
-      a.n_chunks = dD.n_chunks;
       a.partials = dD.partials.as<float>();
       a.src = dS.f.as<float>();
       a.ld = ld;
@@ -547,36 +561,64 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       a.alpha = float(p.alpha);
       a.lambda = float(p.reg);
       a.implicit = p.implicit;
-      a.dst = P == 1 ? dD.f.as<float>() : stage.as<float>();
+      a.dst = dD.f.as<float>() + Dst.off[me] * ld;  // owned rows, in place in the slab
       a.queue = ctr.as<unsigned long long>();
       a.fail = ctr.as<unsigned long long>() + 2;
-      kern::als_solve(a, cus, s);
-      e2.record(s);
-      if (P > 1) {
-        comm_allgather(ctx, comm, stage.data(), gathered.data(), size_t(maxrows) * ld,
-                       DType::F32, s);
-        for (int q = 0; q < P; ++q)
-          if (Dst.cnt[q])
-            OAP_HIP_CHECK(hipMemcpyAsync(dD.f.as<float>() + Dst.off[q] * ld,
-                                         gathered.as<float>() + size_t(q) * maxrows * ld,
-                                         size_t(Dst.cnt[q]) * ld * 4, hipMemcpyDeviceToDevice, s));
-        if (comm.on_device()) comm.wait(s);
+      if (int(E.solved.size()) != C) E.solved = std::vector<Event>(C);
+      for (int c = 0; c < C; ++c) {
+        a.short_rows = dD.short_rows.as<int32_t>() + dD.sr_off[c];
+        a.n_short = dD.sr_off[c + 1] - dD.sr_off[c];
+        a.long_rows = dD.long_rows.as<int32_t>() + dD.lr_off[c];
+        a.n_long = dD.lr_off[c + 1] - dD.lr_off[c];
+        a.long_chunk_ptr = dD.long_chunk_ptr.as<int64_t>() + dD.lr_off[c] + c;
+        a.chunk_begin = dD.chunk_begin.as<int64_t>() + dD.cb_off[c];
+        a.chunk_end = dD.chunk_end.as<int64_t>() + dD.cb_off[c];
+        a.n_chunks = dD.cb_off[c + 1] - dD.cb_off[c];
+        kern::als_solve(a, cus, s);
+        if (P == 1) continue;
+        // chunk c of every rank's rows -> every rank (root = owner; in place in the slab)
+        auto bcast_chunk = [&](hipStream_t st) {
+          if (comm.name() == std::string("rccl")) static_cast<RcclComm&>(comm).group_start();
+          for (int q = 0; q < P; ++q) {
+            const int64_t lo = Dst.cnt[q] * c / C, hi = Dst.cnt[q] * (c + 1) / C;
+            if (hi > lo)
+              comm_bcast(ctx, comm, dD.f.as<float>() + (Dst.off[q] + lo) * ld,
+                         size_t(hi - lo) * ld, DType::F32, q, st);
+          }
+          if (comm.name() == std::string("rccl")) static_cast<RcclComm&>(comm).group_end();
+        };
+        if (dev_comm) {
+          E.solved[c].record(s);
+          E.solved[c].wait_on(cs);
+          bcast_chunk(cs);
+        } else {
+          bcast_chunk(s);
+        }
       }
-      e3.record(s);
-      e3.sync();
-      res.gram_ms += Event::elapsed_ms(e0, e1);
-      res.solve_ms += Event::elapsed_ms(e1, e2);
-      res.comm_ms += Event::elapsed_ms(e2, e3);
+      E.e2.record(s);
+      if (dev_comm) {  // the next half reads every rank's rows
+        E.gathered.record(cs);
+        E.gathered.wait_on(s);
+      }
+      E.e3.record(s);
     };
     for (int it = 0; it < p.max_iter; ++it) {
       auto t0 = std::chrono::steady_clock::now();
       {
         TraceRange tr(&ctx.metrics(), "als/half_items");
-        half(I, dI, U, dU);
+        half(hev[0], I, dI, U, dU);
       }
       {
         TraceRange tr(&ctx.metrics(), "als/half_users");
-        half(U, dU, I, dI);
+        half(hev[1], U, dU, I, dI);
+      }
+      // one host wait per iteration (both halves queued back to back)
+      if (dev_comm) comm.wait(s);
+      hev[1].e3.sync();
+      for (HalfEvents& E : hev) {
+        res.gram_ms += Event::elapsed_ms(E.e0, E.e1);
+        res.solve_ms += Event::elapsed_ms(E.e1, E.e2);
+        res.comm_ms += Event::elapsed_ms(E.e2, E.e3);  // exposed (not overlapped) gather time
       }
       res.iter_ms.push_back(ms_since(t0));
       maybe_inject_fault(me, "als_iter", it);

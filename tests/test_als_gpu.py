@@ -86,3 +86,23 @@ def test_device_setup_matches_host_setup(native, gpu_world, monkeypatch):
     sp = native.als_fit(gpu_world.ctx, gpu_world.comm, us, i, r, 12, 2, 0.1, 3.0, True, 3)
     assert len(sp["user_ids"]) == len(np.unique(us))
     assert sp["failed_rows"] == 0
+
+
+def test_gpu_two_ranks_host_comm_matches_single():
+    """Two ranks on GPU 0 over host (gloo) collectives: the chunked solve + per-chunk owner
+    broadcasts into the replicated factor slab (the overlapped multi-rank path) give the
+    single-rank factors."""
+    from mp_util import run_world
+
+    from dist_workers import als_native
+
+    rc, outs = run_world("dist_workers", "als_native", nproc=2, device="gpu", use_rccl=False)
+    assert rc == 0, outs
+    O.shutdown_world()
+    ref = als_native(device="gpu")
+    O.shutdown_world()
+    for o in outs:
+        assert o["engine"] == "gpu"
+        assert o["uid"] == ref["uid"]
+        np.testing.assert_allclose(o["uf"], ref["uf"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(o["if"], ref["if"], rtol=1e-4, atol=1e-5)
