@@ -455,13 +455,29 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       D.cb_off.assign(1, 0);
       for (int c = 0; c < C; ++c) {
         const int64_t lo = nloc * c / C, hi = nloc * (c + 1) / C;
-        // longest rows first: they start early and the short ones fill in behind them
+        // longest rows first: they start early and the short ones fill in behind them (a
+        // counting sort by length: O(rows), rows longer than kLong by a comparison sort)
         std::vector<std::pair<int64_t, int32_t>> order;
         order.reserve(hi - lo);
-        for (int64_t i = lo; i < hi; ++i)
-          order.push_back({S.csr.ptr[i + 1] - S.csr.ptr[i], int32_t(i)});
-        std::stable_sort(order.begin(), order.end(),
-                         [](const auto& x, const auto& y) { return x.first > y.first; });
+        {
+          std::vector<int64_t> bucket(kLong + 2, 0);
+          std::vector<std::pair<int64_t, int32_t>> longs;
+          for (int64_t i = lo; i < hi; ++i) {
+            const int64_t len = S.csr.ptr[i + 1] - S.csr.ptr[i];
+            if (len > kLong) longs.push_back({len, int32_t(i)});
+            else ++bucket[kLong - len + 1];
+          }
+          std::stable_sort(longs.begin(), longs.end(),
+                           [](const auto& x, const auto& y) { return x.first > y.first; });
+          order = longs;
+          for (int64_t b = 1; b <= kLong + 1; ++b) bucket[b] += bucket[b - 1];
+          const size_t base = order.size();
+          order.resize(base + size_t(bucket[kLong + 1]));
+          for (int64_t i = lo; i < hi; ++i) {  // stable within a length (ascending row)
+            const int64_t len = S.csr.ptr[i + 1] - S.csr.ptr[i];
+            if (len <= kLong) order[base + size_t(bucket[kLong - len]++)] = {len, int32_t(i)};
+          }
+        }
         const int64_t cb0 = int64_t(cb.size());
         lcp.push_back(0);
         for (const auto& [len, i] : order) {

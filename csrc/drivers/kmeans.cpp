@@ -14,6 +14,7 @@
 #include <unordered_map>
 
 #include "kernels/kernels.h"
+#include "kernels/kmeans_wide.h"
 
 namespace oap {
 
@@ -344,6 +345,37 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
     kern::kmeans_exact_rows(b, grid, s);
     return a.cost_slab ? 2 * grid : 0;
+  }
+  if (x.cols > 128 && x.rows > 0 && req.fast1 && !req.precise && !req.mindist_seeded &&
+      !req.delta && kern::kmeans_wide_supported(x.cols, g.k) &&
+      !std::getenv("OAP_KMEANS_NO_WIDE")) {
+    // ---- wide rows on MFMA (kmeans_wide.hip): tier-1 labels + exact re-decision, then the
+    // label-driven accumulation and (when asked) the per-row cost
+    Buffer lab, dbuf;
+    int32_t* labels = req.labels;
+    if (!labels) {
+      lab = ctx.alloc(sizeof(int32_t) * size_t(x.rows));
+      labels = lab.as<int32_t>();
+    }
+    a.labels = labels;
+    dbuf = ctx.alloc(sizeof(int32_t) * size_t(x.rows) + 64);
+    unsigned* dcount = reinterpret_cast<unsigned*>(dbuf.as<int32_t>() + x.rows);
+    kern::kmeans_wide_assign(a, ctx.info().cu_count, dbuf.as<int32_t>(), dcount, s);
+    if (req.accumulate)
+      kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows, int(x.ld), x.cols,
+                              labels, g.k, req.scale, req.sums_too ? req.sums : nullptr,
+                              req.counts, s);
+    if (req.cost_slab)
+      return kern::kmeans_wide_cost(a, req.cost_slab, kern::kmeans_cost_slab_size(
+                                                          ctx.info().cu_count), s);
+    if (req.mindist) {
+      Buffer tmp = ctx.alloc(sizeof(double) * size_t(kern::kmeans_cost_slab_size(
+                                                  ctx.info().cu_count)));
+      kern::kmeans_wide_cost(a, tmp.as<double>(), kern::kmeans_cost_slab_size(
+                                                      ctx.info().cu_count), s);
+      OAP_HIP_CHECK(hipStreamSynchronize(s));  // (tmp is freed on return)
+    }
+    return 0;
   }
   if (x.cols > 128 || g.kpad <= kmax || kmax == 0) {
     if (req.delta) {

@@ -337,3 +337,32 @@ def test_lean_variants_agree(native, variant):
         native.kmeans_set_lean_variant(0)
     assert np.array_equal(r["centers"], ref["centers"])
     assert r["deferred_rows"] == ref["deferred_rows"]
+
+
+@pytest.mark.parametrize("d,k,sigma,dtype", [(784, 256, 0.3, "f32"), (300, 40, 3.0, "f32"),
+                                             (200, 100, 1.0, "bf16")])
+def test_wide_mfma_path_bitwise_equals_generic_and_cpu(native, monkeypatch, d, k, sigma, dtype):
+    """d > 128 on the matrix cores (kmeans_wide.hip: fp16 tier 1 over 128-feature chunks + exact
+    re-decision) gives the generic VALU kernel's labels, hence bitwise its centers, and the CPU
+    engine's."""
+    rng = np.random.default_rng(d + k)
+    C = rng.uniform(-1, 1, size=(k, d))
+    X = C[rng.integers(0, k, 8000)] + rng.normal(0, sigma / np.sqrt(d), size=(8000, d))
+    X = X.astype(np.float32).astype(np.float64)
+    if dtype == "bf16":
+        X = bf16_round(X)
+    init = X[rng.choice(len(X), k, replace=False)]
+    g = native.Context(0, 0.5, 0)
+    tg = native.upload_dense(g, X, dtype, native.kmeans_ld(d, dtype))
+    rw = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, 4, -1.0)
+    monkeypatch.setenv("OAP_KMEANS_NO_WIDE", "1")
+    rgen = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, 4, -1.0)
+    monkeypatch.delenv("OAP_KMEANS_NO_WIDE")
+    assert rw["last_counts"] == rgen["last_counts"]
+    assert np.array_equal(rw["centers"], rgen["centers"])
+    np.testing.assert_allclose(rw["cost"], rgen["cost"], rtol=1e-6)
+    if dtype == "f32":
+        c = native.Context(-1)
+        tc = native.upload_dense(c, X, "f64", d)
+        rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, 4, -1.0)
+        assert np.array_equal(rw["centers"], rc["centers"])
