@@ -1455,7 +1455,7 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
   if (ablate & 64) {  // the Lloyd fit's path: lean tier-1 pass + exact re-decision of its rows
     AssignReq req;
     req.accumulate = true;
-    req.ablate = ablate & 11;
+    req.ablate = ablate & 59;
     req.scale = scale.as<float>();
     req.sums = a.sums;
     req.counts = a.counts;

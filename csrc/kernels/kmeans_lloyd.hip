@@ -47,6 +47,8 @@ namespace {
 using namespace kmdev;
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr float kBiasUnit = 16.f;  // bias features' unit (2^4)
 
@@ -72,7 +74,8 @@ struct LeanArgs {
   int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
   int accumulate, sums_too, delta;
-  int ablate;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance work
+  int ablate;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance, 16 no loads,
+               // 32 minimal epilogue
 };
 
 struct LeanSmem {
@@ -206,6 +209,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     return tl < 0 ? 0 : (tl < ntiles_all ? tl : ntiles_all - 1);
   };
   auto load_row = [&](int64_t row, F& dst) {
+    if (a.ablate & 16) {  // timing ablation: no row loads (synthetic values)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          uint32_t hsh = uint32_t(row) * 2654435761u ^ uint32_t(16 * s + j) * 2246822519u;
+          hsh ^= hsh >> 15;
+          hsh *= 2654435761u;
+          const float v = float(hsh >> 8) * (20.f / 16777216.f) - 10.f;
+          if constexpr (XB)
+            dst.v[s][j] = static_cast<__bf16>(v);
+          else
+            dst.v[s][j] = v;
+        }
+      return;
+    }
     if constexpr (XB) {
       const __bf16* p = static_cast<const __bf16*>(a.x) + row * a.ld + 8 * h;
 #pragma unroll
@@ -315,7 +334,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       for (int s = 0; s < KS; ++s) {
         f16x8 v;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = static_cast<_Float16>(alpha * x.at(s, j));
+        for (int j = 0; j < 8; j += 2) {  // v_pk_mul_f32 + v_cvt_pk_f16_f32 (RNE): 1 op / value
+          const f32x2 p = f32x2{x.at(s, j), x.at(s, j + 1)} * alpha;
+          const f16x2 q = __builtin_convertvector(p, f16x2);
+          v[j] = q[0];
+          v[j + 1] = q[1];
+        }
         if (s == KS - 1) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -348,6 +372,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       }
     };
     auto epilogue = [&](int c0, const f32x16& acc) {
+      if (a.ablate & 32) {  // timing ablation: consume the accumulators with one op per chunk
+        k1 = min(k1, (__float_as_int(acc[0]) & ~0x3ff) | (c0 + 4 * h));
+        return;
+      }
       int t1[4], t2[4];
       // padded centers carry the largest finite bias: they never win, so no chunk needs a
       // branch for them
