@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       for (int j = 0; j < 16; ++j) {
         const float piv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), j));
         ok = ok && (piv > 0.f);
-        const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = 1.f / dj;
+        const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
         t[j] = (lane > j) ? t[j] * inv : (lane == j ? dj : t[j]);
         const float lij = (lane > j) ? t[j] : 0.f;
 #pragma unroll
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
           float s = x[cc];
 #pragma unroll
           for (int m = 0; m < cc; ++m) s = fmaf(-x[m], lrow[m], s);
-          x[cc] = s / lrow[cc];
+          x[cc] = s * __builtin_amdgcn_rcpf(lrow[cc]);
         }
 #pragma unroll
         for (int m = 0; m < 16; m += 4)
@@ -378,7 +378,9 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       float z[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const float zl = vd / t[j];  // meaningful at lane base + j (t[j] = L_jj there)
+        // meaningful at lane base + j (t[j] = L_jj there); v_rcp_f32 (1 ulp) instead of the
+        // ~10-instruction IEEE division
+        const float zl = vd * __builtin_amdgcn_rcpf(t[j]);
         z[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), base + j));
         if (rl == j) vd = z[j];
         else if (mine && rl > j) vd = fmaf(-t[j], z[j], vd);
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi(o + mm, o + cp)];
 #pragma unroll
       for (int j = 15; j >= 0; --j) {
-        const float xl = vd / c[j];  // meaningful at lane base + j
+        const float xl = vd * __builtin_amdgcn_rcpf(c[j]);  // meaningful at lane base + j
         const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), base + j));
         if (rl == j) vd = xj;
         else if (mine && rl < j) vd = fmaf(-c[j], xj, vd);
