@@ -442,6 +442,45 @@ PYBIND11_MODULE(_native, m) {
       py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1,
       py::arg("precise") = false, py::arg("prune") = true, py::arg("delta") = true);
   m.def(
+      "kmeans_fit_streamed",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,
+         py::array_t<float, py::array::c_style | py::array::forcecast> x, py::object init_centers,
+         int max_iter, double tol, int64_t chunk_rows, bool precise) {
+        if (x.ndim() != 2) throw ConfigError("kmeans_fit_streamed expects a 2-D array");
+        auto a = py::array_t<double, py::array::c_style | py::array::forcecast>(init_centers);
+        std::vector<double> init(a.data(), a.data() + a.size());
+        KMeansParams p;
+        p.precise = precise;
+        p.max_iter = max_iter;
+        p.tol = tol;
+        p.init = KMeansInit::Given;
+        p.k = static_cast<int>(init.size() / std::max<int64_t>(x.shape(1), 1));
+        KMeansResult r;
+        {
+          py::gil_scoped_release rel;
+          r = kmeans_fit_streamed(*ctx, *comm, x.data(), x.shape(0), static_cast<int>(x.shape(1)),
+                                  init, p, chunk_rows);
+        }
+        py::dict out;
+        py::array_t<double> c({int64_t(r.k), int64_t(r.d)});
+        if (!r.centers.empty())
+          std::memcpy(c.mutable_data(), r.centers.data(), r.centers.size() * 8);
+        out["centers"] = c;
+        out["cost"] = r.cost;
+        out["num_iter"] = r.num_iter;
+        out["converged"] = r.converged;
+        out["cost_history"] = r.cost_history;
+        out["shift_history"] = r.shift_history;
+        out["last_counts"] = r.last_counts;
+        out["iter_seconds"] = r.iter_seconds;
+        out["global_rows"] = r.global_rows;
+        return out;
+      },
+      py::arg("ctx"), py::arg("comm"), py::arg("x"), py::arg("init_centers"),
+      py::arg("max_iter") = 20, py::arg("tol") = 1e-4, py::arg("chunk_rows") = 1 << 22,
+      py::arg("precise") = false,
+      "Out-of-core K-Means: host rows streamed through HBM chunk buffers every iteration.");
+  m.def(
       "kmeans_init",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
          int k, const std::string& init_mode, int init_steps, uint64_t seed) {

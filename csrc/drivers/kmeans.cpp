@@ -1406,6 +1406,165 @@ void kmeans_predict(Context& ctx, const DenseTable& x, const std::vector<double>
   }
 }
 
+// ---------------------------------------------------------------- streamed (out-of-core) fit
+KMeansResult kmeans_fit_streamed(Context& ctx, Comm& comm, const float* host, int64_t rows,
+                                 int d, const std::vector<double>& init_centers,
+                                 const KMeansParams& p, int64_t chunk_rows) {
+  OAP_CHECK(ctx.is_gpu(), "kmeans_fit_streamed needs a GPU context");
+  OAP_CHECK(d >= 1 && !init_centers.empty() && init_centers.size() % size_t(d) == 0,
+            "kmeans_fit_streamed: initial centers must be k x d");
+  OAP_CHECK(chunk_rows >= 32, "kmeans_fit_streamed: chunk_rows must be >= 32");
+  ctx.activate();
+  const int k = static_cast<int>(init_centers.size() / d);
+  const size_t kd = size_t(k) * d;
+  KMeansResult res;
+  res.d = d;
+  res.k = k;
+  std::vector<double> centers = init_centers;
+  hipStream_t s = ctx.compute(), hs = ctx.h2d() ? ctx.h2d() : s;
+  // global rows and per-column |x| max (host pass over the rows, thread pool)
+  const int64_t g_rows = static_cast<int64_t>(
+      comm_allreduce_scalar(ctx, comm, double(rows), ReduceOp::Sum));
+  const int64_t max_local = static_cast<int64_t>(
+      comm_allreduce_scalar(ctx, comm, double(rows), ReduceOp::Max));
+  res.global_rows = g_rows;
+  std::vector<double> absmax(d, 0.0);
+  {
+    const int nt = ctx.pool().size();
+    std::vector<std::vector<double>> part(nt, std::vector<double>(d, 0.0));
+    ctx.pool().parallel_for(rows, [&](int ci, int64_t b, int64_t e) {
+      std::vector<double>& m = part[ci];
+      for (int64_t i = b; i < e; ++i)
+        for (int f = 0; f < d; ++f)
+          m[f] = std::max(m[f], std::fabs(double(host[size_t(i) * d + f])));
+    });
+    for (const auto& m : part)
+      for (int f = 0; f < d; ++f) absmax[f] = std::max(absmax[f], m[f]);
+    comm_allreduce_host(ctx, comm, absmax.data(), size_t(d), DType::F64, ReduceOp::Max);
+  }
+  FixedPoint fp = fixed_point_scales(absmax, g_rows, max_local);
+  auto t_iter = std::chrono::steady_clock::now();
+
+  // two device chunk buffers, filled by pitched DMA from the (registered) host rows on the H2D
+  // stream while the other chunk is assigned on the compute stream
+  const int64_t ld = kern::kmeans_ld(d);
+  const int64_t cr = std::min<int64_t>(chunk_rows, std::max<int64_t>(rows, 1));
+  Buffer dev[2] = {ctx.alloc(size_t(cr) * ld * 4), ctx.alloc(size_t(cr) * ld * 4)};
+  for (auto& b : dev) OAP_HIP_CHECK(hipMemsetAsync(b.data(), 0, size_t(cr) * ld * 4, s));
+  bool registered = false;
+  if (rows > 0)
+    registered = hipHostRegister(const_cast<float*>(host), size_t(rows) * d * 4,
+                                 hipHostRegisterDefault) == hipSuccess;
+  (void)hipGetLastError();  // (a refused registration leaves pageable DMA)
+  Event loaded[2], used[2];
+  used[0].record(s);
+  used[1].record(s);
+
+  GpuCenters g = alloc_centers(ctx, k, d);
+  Buffer c64 = ctx.alloc(sizeof(double) * kd);
+  Buffer stats = ctx.alloc(sizeof(u64) * (kd + k));
+  const int nslab = kern::kmeans_cost_slab_size(ctx.info().cu_count);
+  Buffer slab = ctx.alloc(sizeof(double) * nslab);
+  const int64_t nchunks = (rows + cr - 1) / cr;
+  Buffer costs = ctx.alloc(sizeof(double) * size_t(std::max<int64_t>(nchunks, 1)) + 8);
+  Buffer cost_d = ctx.alloc(sizeof(double));
+  Buffer scale = ctx.alloc(sizeof(float) * (round_up(d, 4) + 4));
+  Buffer inv_scale = ctx.alloc(sizeof(double) * d);
+  Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags));
+  Buffer fin_scratch = ctx.alloc(sizeof(double) * 2 * std::max(k, 1));
+  ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4), s);
+  ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * kd, s);
+  ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d, s);
+  ctx.copy_to_backend(inv_scale.data(), fp.inv_scale.data(), sizeof(double) * d, s);
+  kern::kmeans_prepare_centers(c64.as<double>(), k, d, g.dp, g.c32.as<float>(),
+                               g.cnorm.as<float>(), g.cstat.as<float>(), g.kpad, s);
+  u64* sums = stats.as<u64>();
+  u64* counts = sums + kd;
+  kern::KMeansFinalizeArgs fa;
+  fa.sums = sums;
+  fa.counts = counts;
+  fa.inv_scale = inv_scale.as<double>();
+  fa.centers64 = c64.as<double>();
+  fa.centers32 = g.c32.as<float>();
+  fa.cnorm = g.cnorm.as<float>();
+  fa.cstat = g.cstat.as<float>();
+  fa.k = k;
+  fa.d = d;
+  fa.dp = g.dp;
+  fa.tol = p.tol;
+  fa.cost_in = cost_d.as<double>();
+  fa.flags = flags_d.data();
+  fa.scratch = fin_scratch.as<double>();
+  kern::KMeansFlags fl{};
+  for (int it = 0; it < p.max_iter; ++it) {
+    maybe_inject_fault(comm.rank(), "kmeans_iter", it);
+    TraceRange tr(&ctx.metrics(), "kmeans/iteration_streamed");
+    OAP_HIP_CHECK(hipMemsetAsync(stats.data(), 0, sizeof(u64) * (kd + k), s));
+    for (int64_t c = 0; c < nchunks; ++c) {
+      const int b = int(c & 1);
+      const int64_t r0 = c * cr, nr = std::min(cr, rows - r0);
+      used[b].wait_on(hs);  // the chunk that last used this buffer is assigned
+      OAP_HIP_CHECK(hipMemcpy2DAsync(dev[b].data(), size_t(ld) * 4, host + size_t(r0) * d,
+                                     size_t(d) * 4, size_t(d) * 4, size_t(nr),
+                                     hipMemcpyHostToDevice, hs));
+      loaded[b].record(hs);
+      loaded[b].wait_on(s);
+      DenseTable view;
+      view.rows = nr;
+      view.cols = d;
+      view.ld = ld;
+      view.dtype = DType::F32;
+      view.backend = Backend::GPU;
+      view.data = Buffer::view(dev[b].data(), size_t(nr) * ld * 4);
+      view.global_offset = r0;
+      view.global_rows = g_rows;
+      AssignReq req;
+      req.accumulate = true;
+      req.sums_too = true;
+      req.precise = p.precise;
+      req.scale = scale.as<float>();
+      req.sums = sums;
+      req.counts = counts;
+      req.cost_slab = slab.as<double>();
+      const int nb = gpu_assign(ctx, view, g, req, s);
+      if (nb > 0)
+        kern::sum_f64(slab.as<double>(), nb, costs.as<double>() + c, s);
+      else
+        OAP_HIP_CHECK(hipMemsetAsync(costs.as<double>() + c, 0, sizeof(double), s));
+      used[b].record(s);
+    }
+    // chunk costs in chunk order (deterministic), then one grouped allreduce + finalize
+    if (nchunks > 0)
+      kern::sum_f64(costs.as<double>(), int(nchunks), cost_d.as<double>(), s);
+    else
+      OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+    if (comm.size() > 1) {
+      comm_allreduce(ctx, comm, stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
+      comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+      if (comm.on_device()) comm.wait(s);
+    }
+    kern::kmeans_finalize(fa, s);
+    ctx.copy_to_host(&fl, flags_d.data(), sizeof(fl), s);
+    res.cost = fl.cost;
+    res.cost_history.push_back(fl.cost);
+    res.shift_history.push_back(std::sqrt(std::max(fl.max_shift2, 0.0)));
+    res.num_iter = it + 1;
+    if (fl.converged && p.tol >= 0) {
+      res.converged = true;
+      break;
+    }
+  }
+  OAP_HIP_CHECK(hipStreamSynchronize(s));
+  if (registered) (void)hipHostUnregister(const_cast<float*>(host));
+  res.centers.resize(kd);
+  ctx.copy_to_host(res.centers.data(), c64.data(), sizeof(double) * kd, s);
+  std::vector<u64> cnt(k);
+  ctx.copy_to_host(cnt.data(), counts, sizeof(u64) * k, s);
+  res.last_counts.assign(cnt.begin(), cnt.end());
+  res.iter_seconds = seconds_since(t_iter);
+  return res;
+}
+
 }  // namespace oap
 
 namespace oap {

@@ -68,6 +68,15 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
                                         const KMeansParams& params, int* k_eff);
 
 // Full fit: init (unless params.init == Given, in which case init_centers is used) + Lloyd.
+// Out-of-core fit (SURVEY.md §5 scale axis): the rank's rows stay in host memory (row-major
+// f32, `rows` x `d`, page-locked for the duration when the driver allows) and every Lloyd
+// iteration streams them through two HBM chunk buffers — pitched DMA of chunk c+1 on the H2D
+// stream while chunk c is assigned and accumulated on the compute stream.  Given initial centers;
+// the same fixed-point statistics as the resident fit, so the centers are bitwise equal to it.
+KMeansResult kmeans_fit_streamed(Context& ctx, Comm& comm, const float* host, int64_t rows,
+                                 int d, const std::vector<double>& init_centers,
+                                 const KMeansParams& p, int64_t chunk_rows);
+
 KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                         const std::vector<double>& init_centers, const KMeansParams& params);
 

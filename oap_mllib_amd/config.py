@@ -45,6 +45,11 @@ class Config:
     pca_max_features: int = 65535
     #: rows per pinned staging chunk during ingestion
     ingest_chunk_rows: int = 1 << 18
+    #: K-Means rows per rank beyond which the fit streams them from host memory through HBM
+    #: chunk buffers every iteration (0 = automatic: 60% of the device's total memory)
+    hbm_budget_bytes: int = 0
+    #: rows per HBM chunk of the streamed (out-of-core) K-Means fit
+    stream_chunk_rows: int = 1 << 22
     log_level: str = "warn"
     log_file: str = ""
     #: directory for periodic training snapshots ("" = off; the sc.checkpointDir analogue)

@@ -119,6 +119,10 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
                             self.getOrDefault("distanceMeasure"), weights, None, allreduce)
             centers, cost, n_iter = r.centers, r.cost, r.num_iter
             extra = {"engine": "vanilla"}
+        elif engine == "gpu" and _streamed(w, X):
+            r, centers, cost, n_iter = self._fit_streamed(w, X, k, max_iter, tol, seed)
+            extra = {"engine": engine, "streamed": True, "init_seconds": r["init_seconds"],
+                     "iter_seconds": r["iter_seconds"], "global_rows": r["global_rows"]}
         else:
             N = _loader.load()
             table = upload_table(w, X)
@@ -149,6 +153,27 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
         return model
 
 
+    def _fit_streamed(self, w, X, k, max_iter, tol, seed):
+        """Rows beyond the HBM budget: k-means|| (or random) init on a uniform sample uploaded to
+        HBM, then Lloyd with the rows streamed from host memory each iteration
+        (drivers/kmeans.cpp kmeans_fit_streamed)."""
+        N = _loader.load()
+        t0 = time.time()
+        rng = np.random.default_rng(seed)
+        m = min(len(X), max(64 * k, 1 << 20))
+        sample = X[np.sort(rng.choice(len(X), m, replace=False))] if m < len(X) else X
+        st = upload_table(w, np.ascontiguousarray(sample))
+        init = N.kmeans_init(w.ctx, w.comm, st, k, self.getOrDefault("initMode"),
+                             self.getOrDefault("initSteps"), seed)
+        del st
+        init_s = time.time() - t0
+        r = N.kmeans_fit_streamed(w.ctx, w.comm, np.ascontiguousarray(X, dtype=np.float32),
+                                  np.asarray(init), max_iter, tol,
+                                  int(w.config.stream_chunk_rows))
+        r = dict(r)
+        r["init_seconds"] = init_s
+        return r, r["centers"], r["cost"], r["num_iter"]
+
     def _fit_segmented(self, N, w, table, ck, k, max_iter, tol, seed):
         """Lloyd in checkpoint_interval-sized segments, resuming from a saved state."""
         interval = max(1, int(w.config.checkpoint_interval))
@@ -176,6 +201,18 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
                 break
             k = centers.shape[0]
         return r, centers, cost, done
+
+
+def _streamed(w, X: np.ndarray) -> bool:
+    """K-Means rows of this rank exceed the HBM budget (Config.hbm_budget_bytes, automatic:
+    60% of the device memory): stream them from host memory instead of uploading."""
+    if X.ndim != 2 or w.config.storage_dtype != "f32":
+        return False
+    budget = int(w.config.hbm_budget_bytes)
+    if budget <= 0:
+        budget = int(0.6 * w.ctx.info["total_mem"])
+    ld = (X.shape[1] + 3) // 4 * 4
+    return X.shape[0] * ld * 4 > budget
 
 
 def upload_table(w, X: np.ndarray, layout: str = "kmeans"):
@@ -234,6 +271,14 @@ class KMeansModel(_KMeansParams, Model, HasTrainingSummary, MLWritable, MLReadab
         if engine == "vanilla" or len(X) == 0 or self._centers.shape[0] == 0:
             return vanilla.find_closest(X, self._centers, self.getOrDefault("distanceMeasure"))
         N = _loader.load()
+        if engine == "gpu" and _streamed(w, X):  # beyond the HBM budget: predict in row chunks
+            step = max(1, int(w.config.stream_chunk_rows))
+            labs, costs = [], []
+            for r0 in range(0, len(X), step):
+                lb, cs = N.kmeans_predict(w.ctx, upload_table(w, X[r0:r0 + step]), self._centers)
+                labs.append(np.asarray(lb))
+                costs.append(np.asarray(cs))
+            return np.concatenate(labs), np.concatenate(costs)
         table = upload_table(w, X)
         return N.kmeans_predict(w.ctx, table, self._centers)
 

@@ -366,3 +366,29 @@ def test_wide_mfma_path_bitwise_equals_generic_and_cpu(native, monkeypatch, d, k
         tc = native.upload_dense(c, X, "f64", d)
         rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, 4, -1.0)
         assert np.array_equal(rw["centers"], rc["centers"])
+
+
+def test_streamed_out_of_core_fit_bitwise_equals_resident(native):
+    """Rows streamed from host memory through two HBM chunk buffers each iteration (the
+    out-of-core path for shards beyond the HBM budget) give the resident fit's centers."""
+    rng = np.random.default_rng(5)
+    C = rng.uniform(-5, 5, size=(16, 24))
+    X = (C[rng.integers(0, 16, 70001)] + rng.normal(0, 1.5, size=(70001, 24))).astype(np.float32)
+    init = X[:16].astype(np.float64)
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X.astype(np.float64), "f32", native.kmeans_ld(24))
+    rr = native.kmeans_fit(g, native.LocalComm(True), t, init, 16, 6, -1.0)
+    rs = native.kmeans_fit_streamed(g, native.LocalComm(True), X, init, 6, -1.0, 8192)
+    assert rs["last_counts"] == rr["last_counts"]
+    assert np.array_equal(rs["centers"], rr["centers"])
+    np.testing.assert_allclose(rs["cost"], rr["cost"], rtol=1e-9)
+
+
+def test_estimator_streams_beyond_budget(gpu_world, monkeypatch):
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(50000, 8)) + rng.integers(0, 4, (50000, 1)) * 6.0
+    monkeypatch.setattr(gpu_world.config, "hbm_budget_bytes", 1 << 20)
+    monkeypatch.setattr(gpu_world.config, "stream_chunk_rows", 10000)
+    m = O.KMeans(k=4, seed=1, maxIter=10).fit(X)
+    assert m.fit_info.get("streamed") and m.fit_info["engine"] == "gpu"
+    assert len(m.summary.clusterSizes) == 4 and sum(m.summary.clusterSizes) == len(X)
