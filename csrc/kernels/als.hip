@@ -18,6 +18,8 @@
 //    reads) and is factored by a right-looking blocked Cholesky with 16-wide panels: the
 //    diagonal block in registers (lane-per-row, cross-lane broadcasts), the panel TRSM
 //    lane-per-row against broadcast LDS rows, and the trailing SYRK update on MFMA.
+#include <cstdlib>
+
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
@@ -57,6 +59,8 @@ struct SolveArgs {
   float* dst;                // [*][ld], indexed by row id
   unsigned long long* queue;
   unsigned long long* fail;
+  int ablate;  // timing ablations (OAP_ALS_ABLATE): 1 no Gramian, 2 no Cholesky, 4 no solves,
+               // 8 no YtY loads
 };
 
 struct PartialArgs {
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         for (int f = 0; f < NB; ++f) bacc[f] += pp[NT * 256 + f * 64 + lane];
         nexp += static_cast<int>(pp[NT * 256 + NB * 64 + lane]);
       }
-    } else {
+    } else if (!(a.ablate & 1)) {
       accumulate<NB>(a.cols, a.vals, a.rowptr[row], a.rowptr[row + 1], a.src, a.ld, a.alpha,
                      a.implicit != 0, acc, bacc, nexp);
     }
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
             float v;
             if (i < r && j < r) {
               v = acc[t][e];
-              if (a.yty) v += a.yty[i * r + j];
+              if (a.yty && !(a.ablate & 8)) v += a.yty[i * r + j];
               if (i == j) v += lam;
             } else {
               v = (i == j) ? 1.f : 0.f;
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
 
     // ---- blocked right-looking Cholesky, 16-wide panels
     bool spd = true;
-    for (int jb = 0; jb < NB; ++jb) {
+    for (int jb = (a.ablate & 2) ? NB : 0; jb < NB; ++jb) {
       const int o = 16 * jb;
       // (1) diagonal block: lanes 0..15 own its rows, in registers
       float t[16];
@@ -359,9 +363,10 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
     // steps, readlane broadcasts), the off-diagonal part is one lane-parallel update — instead
     // of r sequential LDS round trips per direction.
     float v0 = bv[lane], v1 = (lane + 64 < RP) ? bv[lane + 64] : 0.f;
+    const int nsolve = (a.ablate & 4) ? 0 : NB;
     // forward: L z = b
 #pragma unroll
-    for (int jb = 0; jb < NB; ++jb) {
+    for (int jb = 0; jb < nsolve; ++jb) {
       const int o = 16 * jb, base = o & 63, rl = lane - base;
       const bool mine = rl >= 0 && rl < 16;
       const int rr = mine ? rl : 0;
@@ -409,7 +414,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
     }
     // backward: L^T x = z
 #pragma unroll
-    for (int jb = NB - 1; jb >= 0; --jb) {
+    for (int jb = nsolve - 1; jb >= 0; --jb) {
       const int o = 16 * jb, base = o & 63, rl = lane - base;
       const bool mine = rl >= 0 && rl < 16;
       float vd = (o < 64) ? v0 : v1;
@@ -484,6 +489,11 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
   a.implicit = s.implicit ? 1 : 0;
   a.dst = s.dst;
   a.fail = s.fail;
+  static const int ablate = [] {
+    const char* e = std::getenv("OAP_ALS_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.ablate = ablate;
   if (s.n_short > 0) {
     OAP_HIP_CHECK(hipMemsetAsync(s.queue, 0, sizeof(unsigned long long), st));
     a.rows = s.short_rows;
