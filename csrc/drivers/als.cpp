@@ -1,6 +1,7 @@
 #include "drivers/als.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <climits>
 #include <chrono>
@@ -11,6 +12,7 @@
 #include "kernels/als_setup.h"
 #include "kernels/kernels.h"
 #include "kernels/rng.h"
+#include "linalg/eigen.h"
 #include "runtime/log.h"
 
 namespace oap {
@@ -421,9 +423,19 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     // is broadcast (root = owner, straight into the replicated factor slab) on the comm stream
     // while chunk c+1 solves on the compute stream.
     const int C = P > 1 ? 4 : 1;
+    // implicit rows with <= 64 ratings: low-rank (Woodbury) solve in the eigenbasis of Y^T Y
+    // (kernels/als_lowrank.hip); OAP_ALS_LOWRANK=0 sends every row to the direct r x r solve
+    const bool lowrank = [] {
+      const char* e = std::getenv("OAP_ALS_LOWRANK");
+      return !e || std::atoi(e) != 0;
+    }();
     struct Dev {
       Buffer f, ptr, col, val;
       Buffer short_rows, long_rows, long_chunk_ptr, chunk_begin, chunk_end, partials;
+      // low-rank path: per chunk, lr offsets into the chunk's short rows (AlsSolveArgs::lr_off);
+      // rot: this side's factors in the eigenbasis of their Gramian (when it is a source)
+      std::vector<std::array<int64_t, 5>> lro;
+      Buffer rot, lr_scratch;
       // per row-range chunk c: [sr_off[c], sr_off[c+1]) of short_rows, [lr_off[c], ...) of
       // long_rows (long_chunk_ptr segment at lr_off[c] + c), [cb_off[c], ...) of chunk_begin/end
       std::vector<int64_t> sr_off, lr_off, cb_off;
@@ -480,6 +492,22 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         }
         const int64_t cb0 = int64_t(cb.size());
         lcp.push_back(0);
+        // low-rank classes: the short rows come by decreasing length, so each class
+        // (<= 64, 48, 32, 16 ratings) is a contiguous tail of the chunk's short rows
+        std::array<int64_t, 5> lo5{};
+        {
+          int64_t nsh = 0;
+          std::array<int64_t, 4> above{};  // short rows longer than 64, 48, 32, 16
+          for (const auto& [len, i] : order) {
+            if (len > kLong) continue;
+            ++nsh;
+            for (int j = 0; j < 4; ++j) above[j] += len > 16 * (4 - j) ? 1 : 0;
+          }
+          const bool use = lowrank && p.implicit;
+          for (int j = 0; j < 4; ++j) lo5[j] = use ? above[j] : nsh;
+          lo5[4] = nsh;
+        }
+        D.lro.push_back(lo5);
         for (const auto& [len, i] : order) {
           if (len > kLong) {
             lr.push_back(i);
@@ -510,6 +538,9 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         max_chunks = std::max(max_chunks, D.cb_off[c + 1] - D.cb_off[c]);
       D.partials =
           ctx.alloc(std::max<size_t>(size_t(max_chunks) * kern::als_partial_floats(r) * 4, 16));
+      int64_t max_lr = 0;
+      for (const auto& o : D.lro) max_lr = std::max(max_lr, o[4] - o[0]);
+      if (max_lr > 0) D.lr_scratch = ctx.alloc(size_t(max_lr) * ld * 4);
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
     upload_side(U, dU, on_device ? &dev_setup.users : nullptr);
@@ -527,8 +558,13 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         OAP_HIP_CHECK(hipStreamSynchronize(s));
       }
     }
-    Buffer ctr = ctx.alloc(32);
-    ctx.memset(ctr.data(), 0, 32);
+    Buffer ctr = ctx.alloc(64);
+    ctx.memset(ctr.data(), 0, 64);
+    // low-rank path state: eigenbasis of the source Gramian (host, then device)
+    Buffer lrQ = ctx.alloc(size_t(ld) * ld * 4), lrQT = ctx.alloc(size_t(ld) * ld * 4),
+           lrEig = ctx.alloc(size_t(ld) * 4);
+    std::vector<float> hQ(size_t(ld) * ld), hQT(size_t(ld) * ld), hEig(ld);
+    std::vector<double> hG(size_t(r) * r);
     Buffer gram64 = ctx.alloc((size_t(r) * r + r) * 8), gram32 = ctx.alloc(size_t(r) * r * 4);
     Buffer zshift = ctx.alloc(size_t(ld + 128) * 4);
     ctx.memset(zshift.data(), 0, size_t(ld + 128) * 4);
@@ -564,6 +600,32 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         }
         kern::f64_to_f32(gram64.as<double>(), gram32.as<float>(), int64_t(r) * r, s);
       }
+      // low-rank path: Y^T Y = Q Lambda Q^T on the host (fp64, identical on every rank), the
+      // source factors rotated once into that basis
+      bool lr_on = false;
+      for (const auto& o : dD.lro) lr_on = lr_on || o[4] > o[0];
+      if (lr_on) {
+        if (dev_comm) comm.wait(s);  // the Gramian allreduce, under the collective watchdog
+        ctx.copy_to_host(hG.data(), gram64.data(), hG.size() * 8, s);
+        const SymEig eg = sym_eig(hG, r, &ctx.pool());
+        std::fill(hQ.begin(), hQ.end(), 0.f);
+        std::fill(hQT.begin(), hQT.end(), 0.f);
+        for (int k = 0; k < ld; ++k) {
+          hEig[k] = k < r ? float(std::max(eg.values[k], 0.0)) : 1.f;
+          for (int j = 0; j < ld; ++j) {
+            const float v = (k < r && j < r) ? float(eg.vectors[size_t(k) * r + j])
+                                             : (k == j ? 1.f : 0.f);
+            hQ[size_t(k) * ld + j] = v;
+            hQT[size_t(j) * ld + k] = v;
+          }
+        }
+        ctx.copy_to_backend(lrQ.data(), hQ.data(), hQ.size() * 4, s);
+        ctx.copy_to_backend(lrQT.data(), hQT.data(), hQT.size() * 4, s);
+        ctx.copy_to_backend(lrEig.data(), hEig.data(), hEig.size() * 4, s);
+        if (!dS.rot.data()) dS.rot = ctx.alloc(std::max<size_t>(size_t(Src.n) * ld * 4, 256));
+        kern::als_rotate(dS.f.as<float>(), nullptr, dS.rot.as<float>(), nullptr, Src.n,
+                         lrQ.as<float>(), ld, cus, s);
+      }
       E.e1.record(s);
       kern::AlsSolveArgs a;
       a.rowptr = dD.ptr.as<int64_t>();
@@ -590,6 +652,13 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         a.chunk_begin = dD.chunk_begin.as<int64_t>() + dD.cb_off[c];
         a.chunk_end = dD.chunk_end.as<int64_t>() + dD.cb_off[c];
         a.n_chunks = dD.cb_off[c + 1] - dD.cb_off[c];
+        for (int j = 0; j < 5; ++j) a.lr_off[j] = dD.lro[c][j];
+        if (lr_on) {
+          a.lr_src = dS.rot.as<float>();
+          a.lr_eig = lrEig.as<float>();
+          a.lr_back = lrQT.as<float>();
+          a.lr_scratch = dD.lr_scratch.as<float>();
+        }
         kern::als_solve(a, cus, s);
         if (P == 1) continue;
         // chunk c of every rank's rows -> every rank (root = owner; in place in the slab)

@@ -20,6 +20,7 @@
 //    lane-per-row against broadcast LDS rows, and the trailing SYRK update on MFMA.
 #include <cstdlib>
 
+#include "kernels/als_chol.h"
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
@@ -30,18 +31,11 @@ namespace kern {
 namespace {
 
 constexpr int kAlsThreads = 64;
-typedef float f4 __attribute__((ext_vector_type(4)));
+using als::f4;
 
-// LDS image of the row's matrix: only the lower 16x16 blocks, packed (block (bi, bj), bi >= bj, at
-// bi (bi + 1) / 2 + bj), dense 16-float rows and a 16-byte pad per block (consecutive blocks start
-// on different banks).  28 blocks at rank 100 = 29 KB per row instead of 52 KB for the full
-// square: 5 rows per CU.  Occupancy beats bank conflicts here: 20-float (conflict-free) rows fit
-// only 4 rows per CU and ran 15% slower (0.200 vs 0.173 s/iter, 50M ratings, rank 100).
-constexpr int kBS = 16, kBlkF = 16 * kBS + 4;
-__device__ inline int mi(int i, int j) {
-  const int bi = i >> 4, bj = j >> 4;
-  return (bi * (bi + 1) / 2 + bj) * kBlkF + (i & 15) * kBS + (j & 15);
-}
+using als::kBlkF;
+using als::kBS;
+using als::mi;
 
 struct SolveArgs {
   const int64_t* rowptr;
@@ -252,105 +246,8 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
     }
     __syncthreads();
 
-    // ---- blocked right-looking Cholesky, 16-wide panels
-    bool spd = true;
-    for (int jb = (a.ablate & 2) ? NB : 0; jb < NB; ++jb) {
-      const int o = 16 * jb;
-      // (1) diagonal block: lanes 0..15 own its rows, in registers
-      float t[16];
-      {
-        const int rl = lane & 15;
-#pragma unroll
-        for (int m = 0; m < 16; m += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + rl, o + m)]);
-          t[m] = v.x;
-          t[m + 1] = v.y;
-          t[m + 2] = v.z;
-          t[m + 3] = v.w;
-        }
-      }
-      bool ok = true;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const float piv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), j));
-        ok = ok && (piv > 0.f);
-        const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
-        t[j] = (lane > j) ? t[j] * inv : (lane == j ? dj : t[j]);
-        const float lij = (lane > j) ? t[j] : 0.f;
-#pragma unroll
-        for (int k = j + 1; k < 16; ++k) {
-          const float lkj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), k));
-          t[k] = fmaf(-lij, lkj, t[k]);
-        }
-      }
-      if (!ok) {
-        spd = false;
-        break;
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int m = 0; m < 16; m += 4)
-          *reinterpret_cast<float4*>(&M[mi(o + lane, o + m)]) =
-              make_float4(t[m], t[m + 1], t[m + 2], t[m + 3]);
-      }
-      __syncthreads();
-      if (jb + 1 == NB) break;
-      // (2) panel TRSM: rows below solve x L_jj^T = a, lane-per-row, L_jj rows broadcast
-      for (int i = o + 16 + lane; i < RP; i += 64) {
-        float x[16];
-#pragma unroll
-        for (int m = 0; m < 16; m += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
-          x[m] = v.x;
-          x[m + 1] = v.y;
-          x[m + 2] = v.z;
-          x[m + 3] = v.w;
-        }
-#pragma unroll
-        for (int cc = 0; cc < 16; ++cc) {
-          float lrow[16];
-#pragma unroll
-          for (int m = 0; m < 16; m += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + cc, o + m)]);
-            lrow[m] = v.x;
-            lrow[m + 1] = v.y;
-            lrow[m + 2] = v.z;
-            lrow[m + 3] = v.w;
-          }
-          float s = x[cc];
-#pragma unroll
-          for (int m = 0; m < cc; ++m) s = fmaf(-x[m], lrow[m], s);
-          x[cc] = s * __builtin_amdgcn_rcpf(lrow[cc]);
-        }
-#pragma unroll
-        for (int m = 0; m < 16; m += 4)
-          *reinterpret_cast<float4*>(&M[mi(i, o + m)]) =
-              make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
-      }
-      __syncthreads();
-      // (3) trailing update T[ib][kb] -= P_ib P_kb^T on MFMA (fragments straight from LDS)
-      {
-        const int kk = lane >> 4, c = lane & 15;
-        for (int ib = jb + 1; ib < NB; ++ib) {
-          float pa[4];
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[mi(16 * ib + c, o + 4 * s4 + kk)];
-          for (int kb = jb + 1; kb <= ib; ++kb) {
-            f4 cacc;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) cacc[e] = M[mi(16 * ib + 4 * kk + e, 16 * kb + c)];
-#pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) {
-              const float pb = M[mi(16 * kb + c, o + 4 * s4 + kk)];
-              cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s4], pb, cacc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) M[mi(16 * ib + 4 * kk + e, 16 * kb + c)] = cacc[e];
-          }
-        }
-      }
-      __syncthreads();
-    }
+    // ---- blocked right-looking Cholesky, 16-wide panels (kernels/als_chol.h)
+    const bool spd = als::chol_factor<NB>(M, (a.ablate & 2) ? NB : 0);
     float* out = a.dst + row * a.ld;
     if (!spd) {
       if (lane == 0) atomicAdd(a.fail, 1ull);
@@ -363,90 +260,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
     // steps, readlane broadcasts), the off-diagonal part is one lane-parallel update — instead
     // of r sequential LDS round trips per direction.
     float v0 = bv[lane], v1 = (lane + 64 < RP) ? bv[lane + 64] : 0.f;
-    const int nsolve = (a.ablate & 4) ? 0 : NB;
-    // forward: L z = b
-#pragma unroll
-    for (int jb = 0; jb < nsolve; ++jb) {
-      const int o = 16 * jb, base = o & 63, rl = lane - base;
-      const bool mine = rl >= 0 && rl < 16;
-      const int rr = mine ? rl : 0;
-      float t[16];
-#pragma unroll
-      for (int m = 0; m < 16; m += 4) {
-        const float4 q = *reinterpret_cast<const float4*>(&M[mi(o + rr, o + m)]);
-        t[m] = q.x;
-        t[m + 1] = q.y;
-        t[m + 2] = q.z;
-        t[m + 3] = q.w;
-      }
-      float vd = (o < 64) ? v0 : v1;
-      float z[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        // meaningful at lane base + j (t[j] = L_jj there); v_rcp_f32 (1 ulp) instead of the
-        // ~10-instruction IEEE division
-        const float zl = vd * __builtin_amdgcn_rcpf(t[j]);
-        z[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), base + j));
-        if (rl == j) vd = z[j];
-        else if (mine && rl > j) vd = fmaf(-t[j], z[j], vd);
-      }
-      if (o < 64) v0 = vd;
-      else v1 = vd;
-      if (jb + 1 < NB) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int i = lane + 64 * h;
-          if (i >= o + 16 && i < RP) {
-            float acc2 = 0.f;
-#pragma unroll
-            for (int m = 0; m < 16; m += 4) {
-              const float4 q = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
-              acc2 = fmaf(q.x, z[m], acc2);
-              acc2 = fmaf(q.y, z[m + 1], acc2);
-              acc2 = fmaf(q.z, z[m + 2], acc2);
-              acc2 = fmaf(q.w, z[m + 3], acc2);
-            }
-            if (h == 0) v0 -= acc2;
-            else v1 -= acc2;
-          }
-        }
-      }
-    }
-    // backward: L^T x = z
-#pragma unroll
-    for (int jb = nsolve - 1; jb >= 0; --jb) {
-      const int o = 16 * jb, base = o & 63, rl = lane - base;
-      const bool mine = rl >= 0 && rl < 16;
-      float vd = (o < 64) ? v0 : v1;
-      if (jb + 1 < NB) {
-        // z_{o+m} -= sum_{i >= o+16} L[i][o+m] x_i: x staged in LDS, 4 row groups per column
-        bv[lane] = v0;
-        if (lane + 64 < RP) bv[lane + 64] = v1;
-        __syncthreads();
-        const int m = lane & 15, g = lane >> 4;
-        float part = 0.f;
-        for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[mi(i, o + m)], bv[i], part);
-        part += __shfl_xor(part, 16, 64);
-        part += __shfl_xor(part, 32, 64);
-        const float sub = __shfl(part, (lane - base) & 15, 64);
-        if (mine) vd -= sub;
-        __syncthreads();
-      }
-      // diagonal block: lane base + p holds column p of L_jj
-      float c[16];
-      const int cp = mine ? rl : 0;
-#pragma unroll
-      for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi(o + mm, o + cp)];
-#pragma unroll
-      for (int j = 15; j >= 0; --j) {
-        const float xl = vd * __builtin_amdgcn_rcpf(c[j]);  // meaningful at lane base + j
-        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), base + j));
-        if (rl == j) vd = xj;
-        else if (mine && rl < j) vd = fmaf(-c[j], xj, vd);
-      }
-      if (o < 64) v0 = vd;
-      else v1 = vd;
-    }
+    als::chol_solve<NB>(M, bv, v0, v1, (a.ablate & 4) ? 0 : NB);
     if (lane < a.ld) out[lane] = lane < r ? v0 : 0.f;
     if (lane + 64 < a.ld) out[lane + 64] = lane + 64 < r ? v1 : 0.f;
     for (int i = lane + 128; i < a.ld; i += 64) out[i] = 0.f;
@@ -456,7 +270,8 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
 
 template <int NB>
 size_t solve_lds() {
-  return (size_t(NB * (NB + 1) / 2) * kBlkF + 16 * NB) * sizeof(float);
+  // bv: the backward solve stages all 64 lanes (at least 128 floats)
+  return (size_t(NB * (NB + 1) / 2) * kBlkF + std::max(16 * NB, 128)) * sizeof(float);
 }
 
 template <int NB, bool LONG>
@@ -494,13 +309,16 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     return e ? std::atoi(e) : 0;
   }();
   a.ablate = ablate;
-  if (s.n_short > 0) {
+  // rows of the low-rank path (the tail of short_rows) are solved by als_solve_lowrank
+  const int64_t n_direct = (s.lr_off[4] > s.lr_off[0]) ? s.lr_off[0] : s.n_short;
+  if (n_direct > 0) {
     OAP_HIP_CHECK(hipMemsetAsync(s.queue, 0, sizeof(unsigned long long), st));
     a.rows = s.short_rows;
-    a.nrows = s.n_short;
+    a.nrows = n_direct;
     a.queue = s.queue;
-    launch_solve<NB, false>(a, int(std::min<int64_t>(s.n_short, int64_t(num_cus) * per_cu)), st);
+    launch_solve<NB, false>(a, int(std::min<int64_t>(n_direct, int64_t(num_cus) * per_cu)), st);
   }
+  als_solve_lowrank(s, num_cus, st);
   if (s.n_long > 0) {
     PartialArgs pa{};
     pa.cols = s.cols;

@@ -1,0 +1,232 @@
+// One-wave blocked Cholesky factorisation and triangular solves of a small SPD matrix held in LDS
+// as packed lower 16x16 blocks.  Shared by the ALS normal-equation solve (kernels/als.hip, the
+// r x r system of a long row) and the low-rank Woodbury solve (kernels/als_lowrank.hip, the
+// n x n capacitance system of a short row).
+#pragma once
+
+#include "kernels/device_utils.h"
+
+namespace oap {
+namespace kern {
+namespace als {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// LDS image: only the lower 16x16 blocks, packed (block (bi, bj), bi >= bj, at bi (bi + 1) / 2 +
+// bj), dense 16-float rows and a 16-byte pad per block (consecutive blocks start on different
+// banks).  28 blocks at rank 100 = 29 KB per row instead of 52 KB for the full square: 5 rows per
+// CU.  Occupancy beats bank conflicts here: 20-float (conflict-free) rows fit only 4 rows per CU
+// and ran 15% slower (0.200 vs 0.173 s/iter, 50M ratings, rank 100).
+constexpr int kBS = 16, kBlkF = 16 * kBS + 4;
+__device__ inline int mi(int i, int j) {
+  const int bi = i >> 4, bj = j >> 4;
+  return (bi * (bi + 1) / 2 + bj) * kBlkF + (i & 15) * kBS + (j & 15);
+}
+template <int NB>
+constexpr int packed_floats() {
+  return NB * (NB + 1) / 2 * kBlkF;
+}
+
+// Right-looking blocked Cholesky, 16-wide panels: the diagonal block in registers (lane-per-row,
+// cross-lane broadcasts), the panel TRSM lane-per-row against broadcast LDS rows, the trailing
+// SYRK update on v_mfma_f32_16x16x4_f32 with fragments straight from LDS.  Returns false (and
+// stops) at the first non-positive pivot.  `first` > 0 skips panels (timing ablation).
+template <int NB>
+__device__ inline bool chol_factor(float* M, int first = 0) {
+  constexpr int RP = 16 * NB;
+  const int lane = threadIdx.x;
+  for (int jb = first; jb < NB; ++jb) {
+    const int o = 16 * jb;
+    // (1) diagonal block: lanes 0..15 own its rows, in registers
+    float t[16];
+    {
+      const int rl = lane & 15;
+#pragma unroll
+      for (int m = 0; m < 16; m += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + rl, o + m)]);
+        t[m] = v.x;
+        t[m + 1] = v.y;
+        t[m + 2] = v.z;
+        t[m + 3] = v.w;
+      }
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float piv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), j));
+      ok = ok && (piv > 0.f);
+      const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
+      t[j] = (lane > j) ? t[j] * inv : (lane == j ? dj : t[j]);
+      const float lij = (lane > j) ? t[j] : 0.f;
+#pragma unroll
+      for (int k = j + 1; k < 16; ++k) {
+        const float lkj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), k));
+        t[k] = fmaf(-lij, lkj, t[k]);
+      }
+    }
+    if (!ok) return false;
+    if (lane < 16) {
+#pragma unroll
+      for (int m = 0; m < 16; m += 4)
+        *reinterpret_cast<float4*>(&M[mi(o + lane, o + m)]) =
+            make_float4(t[m], t[m + 1], t[m + 2], t[m + 3]);
+    }
+    __syncthreads();
+    if (jb + 1 == NB) break;
+    // (2) panel TRSM: rows below solve x L_jj^T = a, lane-per-row, L_jj rows broadcast
+    for (int i = o + 16 + lane; i < RP; i += 64) {
+      float x[16];
+#pragma unroll
+      for (int m = 0; m < 16; m += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
+        x[m] = v.x;
+        x[m + 1] = v.y;
+        x[m + 2] = v.z;
+        x[m + 3] = v.w;
+      }
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc) {
+        float lrow[16];
+#pragma unroll
+        for (int m = 0; m < 16; m += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + cc, o + m)]);
+          lrow[m] = v.x;
+          lrow[m + 1] = v.y;
+          lrow[m + 2] = v.z;
+          lrow[m + 3] = v.w;
+        }
+        float s = x[cc];
+#pragma unroll
+        for (int m = 0; m < cc; ++m) s = fmaf(-x[m], lrow[m], s);
+        x[cc] = s * __builtin_amdgcn_rcpf(lrow[cc]);
+      }
+#pragma unroll
+      for (int m = 0; m < 16; m += 4)
+        *reinterpret_cast<float4*>(&M[mi(i, o + m)]) =
+            make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
+    }
+    __syncthreads();
+    // (3) trailing update T[ib][kb] -= P_ib P_kb^T on MFMA (fragments straight from LDS)
+    {
+      const int kk = lane >> 4, c = lane & 15;
+      for (int ib = jb + 1; ib < NB; ++ib) {
+        float pa[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[mi(16 * ib + c, o + 4 * s4 + kk)];
+        for (int kb = jb + 1; kb <= ib; ++kb) {
+          f4 cacc;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cacc[e] = M[mi(16 * ib + 4 * kk + e, 16 * kb + c)];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const float pb = M[mi(16 * kb + c, o + 4 * s4 + kk)];
+            cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s4], pb, cacc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) M[mi(16 * ib + 4 * kk + e, 16 * kb + c)] = cacc[e];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  return true;
+}
+
+// L L^T x = b with the factor from chol_factor.  Right-hand side in registers: lane l holds rows
+// l and l + 64 (v0, v1; v1 only when NB > 4).  Per 16-row block the diagonal solve runs in
+// registers (16 sequential steps, readlane broadcasts) and the off-diagonal part is one
+// lane-parallel update — instead of r sequential LDS round trips per direction.  `bv`: RP floats
+// of LDS scratch.  `nsolve` < NB skips blocks (timing ablation).
+template <int NB>
+__device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v1,
+                                  int nsolve = NB) {
+  constexpr int RP = 16 * NB;
+  const int lane = threadIdx.x;
+  // forward: L z = b
+#pragma unroll
+  for (int jb = 0; jb < nsolve; ++jb) {
+    const int o = 16 * jb, base = o & 63, rl = lane - base;
+    const bool mine = rl >= 0 && rl < 16;
+    const int rr = mine ? rl : 0;
+    float t[16];
+#pragma unroll
+    for (int m = 0; m < 16; m += 4) {
+      const float4 q = *reinterpret_cast<const float4*>(&M[mi(o + rr, o + m)]);
+      t[m] = q.x;
+      t[m + 1] = q.y;
+      t[m + 2] = q.z;
+      t[m + 3] = q.w;
+    }
+    float vd = (o < 64) ? v0 : v1;
+    float z[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      // meaningful at lane base + j (t[j] = L_jj there); v_rcp_f32 (1 ulp) instead of the
+      // ~10-instruction IEEE division
+      const float zl = vd * __builtin_amdgcn_rcpf(t[j]);
+      z[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), base + j));
+      if (rl == j) vd = z[j];
+      else if (mine && rl > j) vd = fmaf(-t[j], z[j], vd);
+    }
+    if (o < 64) v0 = vd;
+    else v1 = vd;
+    if (jb + 1 < NB) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = lane + 64 * h;
+        if (i >= o + 16 && i < RP) {
+          float acc2 = 0.f;
+#pragma unroll
+          for (int m = 0; m < 16; m += 4) {
+            const float4 q = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
+            acc2 = fmaf(q.x, z[m], acc2);
+            acc2 = fmaf(q.y, z[m + 1], acc2);
+            acc2 = fmaf(q.z, z[m + 2], acc2);
+            acc2 = fmaf(q.w, z[m + 3], acc2);
+          }
+          if (h == 0) v0 -= acc2;
+          else v1 -= acc2;
+        }
+      }
+    }
+  }
+  // backward: L^T x = z
+#pragma unroll
+  for (int jb = nsolve - 1; jb >= 0; --jb) {
+    const int o = 16 * jb, base = o & 63, rl = lane - base;
+    const bool mine = rl >= 0 && rl < 16;
+    float vd = (o < 64) ? v0 : v1;
+    if (jb + 1 < NB) {
+      // z_{o+m} -= sum_{i >= o+16} L[i][o+m] x_i: x staged in LDS, 4 row groups per column
+      bv[lane] = v0;
+      if (lane + 64 < RP) bv[lane + 64] = v1;
+      __syncthreads();
+      const int m = lane & 15, g = lane >> 4;
+      float part = 0.f;
+      for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[mi(i, o + m)], bv[i], part);
+      part += __shfl_xor(part, 16, 64);
+      part += __shfl_xor(part, 32, 64);
+      const float sub = __shfl(part, (lane - base) & 15, 64);
+      if (mine) vd -= sub;
+      __syncthreads();
+    }
+    // diagonal block: lane base + p holds column p of L_jj
+    float c[16];
+    const int cp = mine ? rl : 0;
+#pragma unroll
+    for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi(o + mm, o + cp)];
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+      const float xl = vd * __builtin_amdgcn_rcpf(c[j]);  // meaningful at lane base + j
+      const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), base + j));
+      if (rl == j) vd = xj;
+      else if (mine && rl < j) vd = fmaf(-c[j], xj, vd);
+    }
+    if (o < 64) v0 = vd;
+    else v1 = vd;
+  }
+}
+
+}  // namespace als
+}  // namespace kern
+}  // namespace oap

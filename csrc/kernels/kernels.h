@@ -268,12 +268,26 @@ struct AlsSolveArgs {
   float alpha = 1.f, lambda = 0.f;
   bool implicit = true;
   float* dst = nullptr;             // [nrows][ld], indexed by destination row
-  unsigned long long* queue = nullptr;  // device scratch: 2 counters
+  unsigned long long* queue = nullptr;  // device scratch: 8 counters (2 and 3 unused)
   unsigned long long* fail = nullptr;   // device counter of non-SPD rows
+  // Low-rank (Woodbury) path for implicit rows with <= als_lowrank_max_len() ratings
+  // (kernels/als_lowrank.hip): short_rows[lr_off[0], lr_off[4]) are those rows by decreasing
+  // length, [lr_off[j], lr_off[j+1]) holding 16 (3 - j) + 1 .. 16 (4 - j) ratings; the direct
+  // kernel solves short_rows[0, lr_off[0]).  lr_off[0] = n_short disables the path.
+  int64_t lr_off[5] = {0, 0, 0, 0, 0};
+  const float* lr_src = nullptr;   // source factors in the eigenbasis of Y^T Y: [n_src][ld]
+  const float* lr_eig = nullptr;   // [ld] eigenvalues of Y^T Y (padding 1)
+  const float* lr_back = nullptr;  // [ld][ld] Q^T (row vectors x^T = x_q^T Q^T)
+  float* lr_scratch = nullptr;     // [lr_off[4] - lr_off[0]][ld]
 };
 size_t als_partial_floats(int r);
 int als_max_rank();
 void als_solve(const AlsSolveArgs& a, int num_cus, hipStream_t s);
+int als_lowrank_max_len();
+void als_solve_lowrank(const AlsSolveArgs& a, int num_cus, hipStream_t s);
+// out[out_rows ? out_rows[i] : i] = in[in_rows ? in_rows[i] : i] R for n rows (R: ld x ld)
+void als_rotate(const float* in, const int32_t* in_rows, float* out, const int32_t* out_rows,
+                int64_t n, const float* R, int ld, int num_cus, hipStream_t s);
 void als_init_factors(const int32_t* ids, int64_t n, int r, int ld, uint64_t seed, float* out,
                       hipStream_t s);
 void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);

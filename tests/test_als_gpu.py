@@ -106,3 +106,28 @@ def test_gpu_two_ranks_host_comm_matches_single():
         assert o["uid"] == ref["uid"]
         np.testing.assert_allclose(o["uf"], ref["uf"], rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(o["if"], ref["if"], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("rank", [7, 33, 100])
+def test_lowrank_path_matches_direct_and_oracle(native, gpu_world, monkeypatch, rank):
+    """Rows with <= 64 ratings are solved by the Woodbury path in the eigenbasis of Y^T Y
+    (kernels/als_lowrank.hip); it must agree with the direct r x r Cholesky and the fp64 oracle,
+    across all four row classes (1-16, 17-32, 33-48, 49-64 ratings), rows above 64, and zero /
+    negative ratings."""
+    rng = np.random.default_rng(rank)
+    lens = rng.integers(1, 91, 300)
+    u = np.repeat(np.arange(300), lens).astype(np.int32)
+    i = rng.integers(0, 250, len(u)).astype(np.int32)
+    r = rng.integers(-1, 6, len(u)).astype(np.float32)
+    args = (u, i, r, rank, 2, 0.05, 8.0, True, 4)
+    monkeypatch.setenv("OAP_ALS_LOWRANK", "1")
+    lr = native.als_fit(gpu_world.ctx, gpu_world.comm, *args)
+    monkeypatch.setenv("OAP_ALS_LOWRANK", "0")
+    direct = native.als_fit(gpu_world.ctx, gpu_world.comm, *args)
+    monkeypatch.delenv("OAP_ALS_LOWRANK")
+    ref = als_vanilla.fit(u, i, r, rank, 2, 0.05, True, 8.0, False, 4)
+    assert lr["failed_rows"] == 0 and direct["failed_rows"] == 0
+    for key, rk in (("user_factors", ref.user_factors), ("item_factors", ref.item_factors)):
+        scale = np.abs(rk).max()
+        np.testing.assert_allclose(lr[key], direct[key], atol=1e-3 * scale)
+        np.testing.assert_allclose(lr[key], rk, atol=2e-3 * scale)
