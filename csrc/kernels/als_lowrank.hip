@@ -107,7 +107,8 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
           okd = okd && d4[e] > 0.f;
           o4[e] = __builtin_amdgcn_rsqf(fmaxf(d4[e], 1e-30f));
         }
-        *reinterpret_cast<float4*>(dhs + 16 * qb + 4 * kk) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+        *reinterpret_cast<float4*>(dhs + 16 * qb + 4 * kk) =
+            make_float4(o4[0], o4[1], o4[2], o4[3]);
       }
     }
     const bool fail_d = __ballot(!okd) != 0;
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) xv[e] = dv[e] * (gv[e] - dv[e] * xor_sum16(t[qb][e]));
       if (c == 0)
-        *reinterpret_cast<float4*>(out + 16 * qb + 4 * kk) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+        *reinterpret_cast<float4*>(out + 16 * qb + 4 * kk) =
+            make_float4(xv[0], xv[1], xv[2], xv[3]);
     }
     __syncthreads();
   }
@@ -387,7 +389,8 @@ void als_solve_lowrank(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
 void als_rotate(const float* in, const int32_t* in_rows, float* out, const int32_t* out_rows,
                 int64_t n, const float* R, int ld, int num_cus, hipStream_t s) {
   if (n <= 0) return;
-  OAP_CHECK(ld % 16 == 0 && ld >= 16 && ld <= 128, "als_rotate: ld must be 16..128, multiple of 16");
+  OAP_CHECK(ld % 16 == 0 && ld >= 16 && ld <= 128,
+            "als_rotate: ld must be 16..128, multiple of 16");
   switch (ld / 16) {
     case 1: launch_rotate<4>(in, in_rows, out, out_rows, n, R, num_cus, s); break;
     case 2: launch_rotate<8>(in, in_rows, out, out_rows, n, R, num_cus, s); break;

@@ -124,8 +124,8 @@ bool als_device_setup(Context& ctx, const int32_t* users, const int32_t* items,
   ctx.copy_to_backend(dr.data(), ratings, size_t(n) * 4, s);
   Buffer mmb = ctx.alloc(64);
   hipLaunchKernelGGL(oap_als_init_mm, dim3(1), dim3(1), 0, s, mmb.as<int>());
-  hipLaunchKernelGGL(oap_als_minmax, dim3(std::min(grid_of(n), 2048)), dim3(kThreads), 0, s, du.as<int32_t>(),
-                     di.as<int32_t>(), n, mmb.as<int>());
+  hipLaunchKernelGGL(oap_als_minmax, dim3(std::min(grid_of(n), 2048)), dim3(kThreads), 0, s,
+                     du.as<int32_t>(), di.as<int32_t>(), n, mmb.as<int>());
   OAP_HIP_CHECK(hipGetLastError());
   int mm[4];
   ctx.copy_to_host(mm, mmb.data(), sizeof(mm), s);

@@ -33,6 +33,9 @@ for st in $STEPS; do
     alsprof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/alsprof_$T -o run -- python3 $R/benchmarks/bench_als.py --ratings 20000000 --users 1000000 --items 100000 --iters 2 > $R/gpurun_out/alsprof_$T.log 2>&1)
       rc=$?; echo alsprof_rc=$rc; fatal $rc alsprof;;
+    alsprof1b)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/alsprof1b_$T -o run -- python3 $R/benchmarks/bench_als.py --iters 2 > $R/gpurun_out/alsprof1b_$T.log 2>&1)
+      rc=$?; echo alsprof1b_rc=$rc; fatal $rc alsprof1b;;
     pcaprof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/pcaprof_$T -o run -- python3 $R/benchmarks/bench_pca.py --reps 2 > $R/gpurun_out/pcaprof_$T.log 2>&1)
       rc=$?; echo pcaprof_rc=$rc; fatal $rc pcaprof;;
