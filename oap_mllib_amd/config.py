@@ -56,6 +56,10 @@ class Config:
     checkpoint_dir: str = ""
     #: K-Means iterations between snapshots (ALS uses its checkpointInterval param)
     checkpoint_interval: int = 10
+    #: Spark version written into saved models' metadata (and PMML headers); "" = the
+    #: installed pyspark's, else 3.1.1.  The reference builds one jar per Spark profile
+    #: (3.0.0, 3.0.1, 3.0.2, 3.1.1, mllib-dal/pom.xml:151-224); here it is one knob.
+    spark_version: str = ""
 
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)

@@ -321,8 +321,11 @@ class KMeansModel(_KMeansParams, Model, HasTrainingSummary, MLWritable, MLReadab
 
         meta = sf.read_metadata(path, cls._spark_class)
         t = sf.read_parquet_dir(os.path.join(path, "data")).to_pylist()
-        t.sort(key=lambda r: r["clusterIdx"])
-        centers = np.array([sf.vector_from_struct(r["clusterCenter"]) for r in t])
+        if sf.major_version(meta.get("sparkVersion", "3.1.1")) >= 2:
+            t.sort(key=lambda r: r["clusterIdx"])
+            centers = np.array([sf.vector_from_struct(r["clusterCenter"]) for r in t])
+        else:  # Spark <= 1.6: one row holding every center (KMeans.scala:253-257)
+            centers = np.array([sf.vector_from_struct(v) for v in t[0]["clusterCenters"]])
         m = cls(uid=meta["uid"], centers=centers)
         for k, v in meta.get("paramMap", {}).items():
             if m.hasParam(k):
@@ -342,7 +345,7 @@ def write_pmml(model: KMeansModel, path: str) -> None:
     lines = ['<?xml version="1.0" encoding="UTF-8" standalone="yes"?>',
              '<PMML version="4.2" xmlns="http://www.dmg.org/PMML-4_2">',
              '    <Header description="k-means clustering">',
-             f'        <Application name="Apache Spark MLlib" version="{sf.SPARK_VERSION}"/>',
+             f'        <Application name="Apache Spark MLlib" version="{sf.spark_version()}"/>',
              f'        <Timestamp>{escape(ts)}</Timestamp>', '    </Header>',
              f'    <DataDictionary numberOfFields="{d}">']
     lines += [f'        <DataField name="{f}" optype="continuous" dataType="double"/>'

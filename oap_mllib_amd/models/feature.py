@@ -141,7 +141,10 @@ class PCAModel(_PCAParams, Model, MLWritable, MLReadable):
         meta = sf.read_metadata(path, cls._spark_class)
         rows = sf.read_parquet_dir(os.path.join(path, "data")).to_pylist()
         pc = sf.matrix_from_struct(rows[0]["pc"])
-        ev = sf.vector_from_struct(rows[0]["explainedVariance"])
+        if sf.major_version(meta.get("sparkVersion", "3.1.1")) >= 2:
+            ev = sf.vector_from_struct(rows[0]["explainedVariance"])
+        else:  # Spark <= 1.6 stored no explained variance (PCA.scala:234-245)
+            ev = np.zeros(0)
         m = cls(uid=meta["uid"], pc=DenseMatrix.from_array(pc), explainedVariance=DenseVector(ev))
         for k, v in meta.get("paramMap", {}).items():
             if m.hasParam(k):

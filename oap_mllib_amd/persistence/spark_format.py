@@ -27,7 +27,33 @@ import numpy as np
 import pyarrow as pa
 import pyarrow.parquet as pq
 
-SPARK_VERSION = "3.1.1"
+SPARK_VERSION = "3.1.1"  # default unless Config.spark_version or pyspark says otherwise
+#: Spark versions the reference ships shadow sources for (mllib-dal/pom.xml:151-224)
+SUPPORTED_SPARK_VERSIONS = ("3.0.0", "3.0.1", "3.0.2", "3.1.1")
+
+
+def spark_version() -> str:
+    """Version stamped into written models: Config.spark_version, else pyspark's, else 3.1.1."""
+    from ..config import get_config
+
+    v = get_config().spark_version
+    if v:
+        return v
+    try:
+        import pyspark
+
+        return str(pyspark.__version__)
+    except ImportError:
+        return SPARK_VERSION
+
+
+def major_version(v: str) -> int:
+    """Spark's VersionUtils.majorVersion ("1.6.3" -> 1); used by the readers to pick the
+    on-disk layout (Spark <= 1.6 stored K-Means centers in one row, PCA without variances)."""
+    try:
+        return int(str(v).split(".")[0])
+    except ValueError as e:
+        raise ValueError(f"Spark version {v!r} is not of the form major.minor[.patch]") from e
 ROW_METADATA_KEY = b"org.apache.spark.sql.parquet.row.metadata"
 
 VECTOR_SQL = {"type": "struct", "fields": [
@@ -133,7 +159,7 @@ def prepare_dir(path: str, overwrite: bool) -> None:
 def write_metadata(path: str, class_name: str, uid: str, param_map: dict, default_map: dict,
                    extra: dict | None = None) -> dict:
     meta = {"class": class_name, "timestamp": int(time.time() * 1000),
-            "sparkVersion": SPARK_VERSION, "uid": uid,
+            "sparkVersion": spark_version(), "uid": uid,
             "paramMap": {k: _json_value(v) for k, v in param_map.items()},
             "defaultParamMap": {k: _json_value(v) for k, v in default_map.items()}}
     if extra:
@@ -159,7 +185,7 @@ def write_parquet(dir_path: str, table: pa.Table, spark_schema: dict) -> str:
     os.makedirs(dir_path, exist_ok=True)
     md = dict(table.schema.metadata or {})
     md[ROW_METADATA_KEY] = json.dumps(spark_schema, separators=(",", ":")).encode()
-    md[b"org.apache.spark.version"] = SPARK_VERSION.encode()
+    md[b"org.apache.spark.version"] = spark_version().encode()
     table = table.replace_schema_metadata(md)
     fname = f"part-00000-{uuid.uuid4()}-c000.snappy.parquet"
     pq.write_table(table, os.path.join(dir_path, fname), compression="snappy")

@@ -11,9 +11,12 @@ hopes all of them are scheduled together (no barrier mode).  He
 * every task derives RANK / WORLD_SIZE / LOCAL_RANK from the BarrierTaskContext, rank 0
   publishes a free port through ``allGather``, and ``init_world`` forms the gloo rendezvous
   plus the RCCL communicator (unique id broadcast) — no ports are guessed in advance;
-* the local partition is converted to a numpy matrix (or rating columns) and the estimator's
-  normal ``fit`` runs on it; rank 0 returns the fitted model as ``.npy`` payloads (loaded on
-  the driver with ``allow_pickle=False``).
+* only the input columns are shuffled; on Spark >= 3.5 the stage is ``mapInArrow(...,
+  barrier=True)`` and each partition arrives as Arrow record batches that become the numpy
+  matrix (or rating columns) column-at-a-time (``vectors_from_arrow``); older Spark uses the
+  RDD barrier path with one numpy pass per column;
+* the estimator's normal ``fit`` runs on it; rank 0 returns the fitted model as ``.npy``
+  payloads (loaded on the driver with ``allow_pickle=False``).
 
 pyspark is optional: everything except ``fit`` is importable and testable without it.
 """
@@ -113,18 +116,106 @@ def import_model(payload: dict[str, bytes]):
     return m
 
 
-def _partition_to_input(estimator, rows: list):
-    """Spark Rows of this partition -> what estimator.fit accepts."""
+def _input_columns(estimator) -> list[str]:
+    """The DataFrame columns a fit reads (only these are shuffled into the barrier stage)."""
     from ..models.recommendation import ALS
 
     if isinstance(estimator, ALS):
-        u, i, r = (estimator.getOrDefault(c) for c in ("userCol", "itemCol", "ratingCol"))
-        return {"user": [row[u] for row in rows], "item": [row[i] for row in rows],
-                "rating": [row[r] for row in rows] if r else [1.0] * len(rows)}
-    col = (estimator.getOrDefault("inputCol") if estimator.hasParam("inputCol")
-           else estimator.getOrDefault("featuresCol"))
-    vecs = [row[col] for row in rows]
-    return np.array([v.toArray() for v in vecs], dtype=np.float64) if vecs else np.zeros((0, 0))
+        cols = [estimator.getOrDefault("userCol"), estimator.getOrDefault("itemCol")]
+        r = estimator.getOrDefault("ratingCol")
+        return cols + ([r] if r else [])
+    return [estimator.getOrDefault("inputCol") if estimator.hasParam("inputCol")
+            else estimator.getOrDefault("featuresCol")]
+
+
+def vectors_from_arrow(col) -> np.ndarray:
+    """A VectorUDT column in Arrow form (struct<type: int8, size: int32, indices: list<int32>,
+    values: list<double>>, how Spark ships ml.linalg vectors to Python) -> dense float64 matrix.
+    Column-at-a-time: dense rows are one reshape of the flattened values, sparse rows one
+    scatter — no per-row Python objects (the reference coalesces partitions in the JVM and
+    copies rows into oneDAL tables one by one, OneDAL.scala:69-101)."""
+    import pyarrow as pa
+
+    if isinstance(col, pa.ChunkedArray):
+        col = col.combine_chunks()
+    n = len(col)
+    if n == 0:
+        return np.zeros((0, 0))
+    typ = col.field("type").to_numpy(zero_copy_only=False)
+    vals = col.field("values")
+    lens = vals.value_lengths().fill_null(0).to_numpy(zero_copy_only=False).astype(np.int64)
+    flat = vals.flatten().to_numpy(zero_copy_only=False).astype(np.float64, copy=False)
+    dense = typ == 1
+    if dense.all():
+        d = int(lens[0])
+        if not np.all(lens == d):
+            raise ValueError("dense vectors of different sizes in one column")
+        return flat.reshape(n, d)
+    size = col.field("size").fill_null(0).to_numpy(zero_copy_only=False).astype(np.int64)
+    d = int(max(np.where(dense, lens, size).max(), 0))
+    out = np.zeros((n, d))
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    if dense.any():
+        dl = lens[dense]
+        if not np.all(dl == d):
+            raise ValueError("dense vectors of different sizes in one column")
+        idx = starts[dense][:, None] + np.arange(d)[None, :]
+        out[dense] = flat[idx]
+    sp = ~dense
+    ind = col.field("indices")
+    ilens = ind.value_lengths().fill_null(0).to_numpy(zero_copy_only=False).astype(np.int64)
+    iflat = ind.flatten().to_numpy(zero_copy_only=False)
+    istarts = np.concatenate([[0], np.cumsum(ilens)[:-1]])
+    rows_sp = np.nonzero(sp)[0]
+    cnt = ilens[rows_sp]
+    r_rep = np.repeat(rows_sp, cnt)
+    off = np.arange(cnt.sum()) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    out[r_rep, iflat[np.repeat(istarts[rows_sp], cnt) + off]] = \
+        flat[np.repeat(starts[rows_sp], cnt) + off]
+    return out
+
+
+def table_to_input(estimator, table):
+    """An Arrow table of this partition's input columns -> what estimator.fit accepts."""
+    from ..models.recommendation import ALS
+
+    cols = _input_columns(estimator)
+    if isinstance(estimator, ALS):
+        get = lambda c: table.column(c).to_numpy()  # noqa: E731
+        n = table.num_rows
+        return {"user": get(cols[0]), "item": get(cols[1]),
+                "rating": get(cols[2]) if len(cols) > 2 else np.ones(n)}
+    return vectors_from_arrow(table.column(cols[0]))
+
+
+def _partition_to_input(estimator, rows: list):
+    """Spark Rows of this partition (the pre-3.5 RDD barrier path) -> what estimator.fit
+    accepts, column-wise through numpy (one pass over the rows per column)."""
+    from ..models.recommendation import ALS
+
+    cols = _input_columns(estimator)
+    n = len(rows)
+    if isinstance(estimator, ALS):
+        u = np.fromiter((row[cols[0]] for row in rows), dtype=np.int64, count=n)
+        i = np.fromiter((row[cols[1]] for row in rows), dtype=np.int64, count=n)
+        r = (np.fromiter((row[cols[2]] for row in rows), dtype=np.float64, count=n)
+             if len(cols) > 2 else np.ones(n))
+        return {"user": u, "item": i, "rating": r}
+    if n == 0:
+        return np.zeros((0, 0))
+    first = rows[0][cols[0]]
+    out = np.empty((n, first.size))
+    for j, row in enumerate(rows):
+        out[j] = row[cols[0]].toArray()
+    return out
+
+
+def _arrow_barrier_supported(df) -> bool:
+    """mapInArrow(..., barrier=True) exists from pyspark 3.5 on."""
+    import inspect
+
+    f = getattr(df, "mapInArrow", None)
+    return f is not None and "barrier" in inspect.signature(f).parameters
 
 
 def fit(estimator, df, num_ranks: int, spark_conf: dict | None = None):
@@ -138,7 +229,9 @@ def fit(estimator, df, num_ranks: int, spark_conf: dict | None = None):
     est_uid = estimator.uid
     conf = dict(spark_conf or {})
 
-    def task(it):
+    def run_rank(make_input):
+        """Rendezvous through the barrier context, fit this rank's shard, return rank 0's
+        payload (None elsewhere)."""
         import os
 
         ctx = BarrierTaskContext.get()
@@ -156,14 +249,36 @@ def fit(estimator, df, num_ranks: int, spark_conf: dict | None = None):
         O.init_world(resolve(spark_conf=conf))
         est = est_cls(uid=est_uid)
         est._set(**est_params)
-        model = est.fit(_partition_to_input(est, list(it)))
+        model = est.fit(make_input(est))
         payload = export_model(model) if rank == 0 else None
         O.shutdown_world()
         ctx.barrier()
+        return payload
+
+    def task(it):  # RDD barrier path: Row objects
+        rows = list(it)
+        payload = run_rank(lambda est: _partition_to_input(est, rows))
         if payload is not None:
             yield payload
 
-    payloads = df.repartition(num_ranks).rdd.barrier().mapPartitions(task).collect()
+    def arrow_task(batches):  # Arrow barrier path: record batches
+        import pyarrow as pa
+
+        table = pa.Table.from_batches(list(batches))
+        payload = run_rank(lambda est: table_to_input(est, table))
+        if payload is not None:
+            keys = list(payload)
+            yield pa.RecordBatch.from_arrays(
+                [pa.array(keys), pa.array([payload[k] for k in keys], type=pa.binary())],
+                names=["key", "value"])
+
+    src = df.select(*_input_columns(estimator)).repartition(num_ranks)
+    if _arrow_barrier_supported(src):
+        # Spark >= 3.5: partitions arrive as Arrow record batches (no Row objects at all)
+        rows = src.mapInArrow(arrow_task, "key string, value binary", barrier=True).collect()
+        payloads = [{r["key"]: bytes(r["value"]) for r in rows}]
+    else:
+        payloads = src.rdd.barrier().mapPartitions(task).collect()
     model = import_model(payloads[0])
     model.setParent(estimator)
     return model

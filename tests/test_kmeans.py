@@ -244,3 +244,65 @@ def test_spark_parquet_layout(cpu_world, tmp_path):
     assert row_md["fields"][1]["type"]["class"] == "org.apache.spark.ml.linalg.VectorUDT"
     first = t.to_pylist()[0]["clusterCenter"]
     assert first["type"] == 1 and first["size"] is None and len(first["values"]) == 3
+
+
+@pytest.mark.parametrize("version", ["3.0.0", "3.0.2", "3.1.1"])
+def test_spark_version_knob(cpu_world, tmp_path, version):
+    """Config.spark_version is what saved models carry (the reference's per-Spark-profile jars,
+    pom.xml:151-224, collapse into one knob); the reader accepts every 3.x layout."""
+    import json
+
+    from oap_mllib_amd.persistence import spark_format as sf
+
+    old = cpu_world.config.spark_version
+    O.set_config(spark_version=version)
+    try:
+        m = KMeans(k=2, seed=1).fit(generate_kmeans_data())
+        p = str(tmp_path / "m")
+        m.write().save(p)
+        meta = json.loads(open(p + "/metadata/part-00000").read())
+        assert meta["sparkVersion"] == version and sf.spark_version() == version
+        np.testing.assert_array_equal(np.array(KMeansModel.load(p).clusterCenters()),
+                                      np.array(m.clusterCenters()))
+    finally:
+        O.set_config(spark_version=old)
+
+
+def test_load_spark_1x_layouts(cpu_world, tmp_path):
+    """Models saved by Spark <= 1.6 (majorVersion < 2): K-Means centers in one row's
+    `clusterCenters` array, PCA without `explainedVariance` (KMeans.scala:253-257,
+    PCA.scala:234-245)."""
+    import json
+    import os
+
+    import pyarrow as pa
+
+    from oap_mllib_amd.models.feature import PCAModel
+    from oap_mllib_amd.persistence import spark_format as sf
+
+    def meta(path, cls):
+        os.makedirs(path + "/metadata")
+        with open(path + "/metadata/part-00000", "w") as f:
+            f.write(json.dumps({"class": cls, "timestamp": 0, "sparkVersion": "1.6.3",
+                                "uid": "old_uid", "paramMap": {"k": 2}}))
+
+    centers = np.array([[1.0, 2.0], [3.0, -4.0]])
+    p = str(tmp_path / "km16")
+    meta(p, "org.apache.spark.ml.clustering.KMeansModel")
+    t = pa.table({"clusterCenters": pa.array(
+        [[sf.dense_vector_struct(c) for c in centers]], type=pa.list_(sf.VECTOR_ARROW))})
+    sf.write_parquet(p + "/data", t, sf.spark_schema(
+        [("clusterCenters", {"type": "array", "elementType": sf.VECTOR_UDT,
+                             "containsNull": True}, True)]))
+    m = KMeansModel.load(p)
+    assert m.uid == "old_uid" and m.getK() == 2
+    np.testing.assert_array_equal(np.array(m.clusterCenters()), centers)
+
+    pc = np.array([[0.6, 0.8], [0.8, -0.6]])
+    p = str(tmp_path / "pca16")
+    meta(p, "org.apache.spark.ml.feature.PCAModel")
+    t = pa.table({"pc": pa.array([sf.dense_matrix_struct(pc)], type=sf.MATRIX_ARROW)})
+    sf.write_parquet(p + "/data", t, sf.spark_schema([("pc", sf.MATRIX_UDT, True)]))
+    pm = PCAModel.load(p)
+    np.testing.assert_allclose(pm.pc.toArray(), pc)
+    assert pm.explainedVariance.toArray().shape == (0,)

@@ -38,7 +38,39 @@ def test_partition_conversion():
     X = S._partition_to_input(O.KMeans(), rows)
     np.testing.assert_array_equal(X, [[1, 2], [3, 4]])
     r = S._partition_to_input(O.ALS(), [Row(user=1, item=2, rating=3.0)])
-    assert r == {"user": [1], "item": [2], "rating": [3.0]}
+    assert r["user"].tolist() == [1] and r["item"].tolist() == [2]
+    assert r["rating"].tolist() == [3.0]
+
+
+def test_arrow_vector_column_to_matrix():
+    """VectorUDT columns as Spark ships them to Python in Arrow form: dense, sparse and mixed
+    chunks become one dense matrix without per-row objects."""
+    import pyarrow as pa
+
+    from oap_mllib_amd.persistence.spark_format import VECTOR_ARROW
+
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(7, 5))
+    X[X < 0.3] = 0.0
+    recs = []
+    for j, x in enumerate(X):
+        if j % 2:  # sparse
+            nz = np.nonzero(x)[0]
+            recs.append({"type": 0, "size": 5, "indices": nz.tolist(), "values": x[nz].tolist()})
+        else:
+            recs.append({"type": 1, "size": None, "indices": None, "values": x.tolist()})
+    col = pa.chunked_array([pa.array(recs[:3], type=VECTOR_ARROW),
+                            pa.array(recs[3:], type=VECTOR_ARROW)])
+    np.testing.assert_array_equal(S.vectors_from_arrow(col), X)
+    dense = pa.array([{"type": 1, "size": None, "indices": None, "values": x.tolist()}
+                      for x in X], type=VECTOR_ARROW)
+    np.testing.assert_array_equal(S.vectors_from_arrow(dense), X)
+    tbl = pa.table({"features": dense})
+    np.testing.assert_array_equal(S.table_to_input(O.KMeans(), tbl), X)
+    als_tbl = pa.table({"user": [1, 2], "item": [3, 4], "rating": [0.5, 2.0]})
+    r = S.table_to_input(O.ALS(), als_tbl)
+    assert r["user"].tolist() == [1, 2] and r["rating"].tolist() == [0.5, 2.0]
+    assert S._input_columns(O.PCA(inputCol="v")) == ["v"]
 
 
 @pytest.mark.skipif(not S.spark_available(), reason="pyspark not installed")
