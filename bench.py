@@ -121,6 +121,17 @@ def bench_kmeans(args, w):
     samples = rows_total * args.steps / el_max
     flops = 2.0 * rows_total * k * d
     comm_name = getattr(w.comm, "name", "none") if w.comm is not None else "none"
+    kpad = -(-k // 32) * 32
+    if args.precise:
+        path = "fp32-exact MFMA"
+    elif d <= 128 and kpad > N.kmeans_lds_kmax(d, False):
+        path = ("chunked large-k passes: tiered bf16 MFMA distances per centroid chunk (merge "
+                "mode, exact-fp32 re-decision of near ties; assignments identical to exact fp32), "
+                "label-driven binned accumulation")
+    else:
+        path = ("lean pass: one fp16 MFMA product per k-step (v_mfma_f32_32x32x16_f16) with a "
+                "rigorous error bound; rows inside it re-decided by the exact fp32 MFMA argmin "
+                "(assignments identical to exact fp32); delta accumulation of moved rows")
     extra = {"fit_wall_s_end_to_end": fit_s, "fit_iters": fit_iters,
              "init_kmeans_parallel_s": init_s, "ingest_synth_s": ingest_s,
              "data_sigma": args.sigma, "data_box": args.box,
@@ -148,10 +159,7 @@ def bench_kmeans(args, w):
              "comm": comm_name,
              "rccl_ranks": w.size if comm_name == "rccl" else 0,
              "world_size": w.size,
-             "distance_path": "fp32-exact MFMA" if args.precise else
-             ("lean pass: one fp16 MFMA product per k-step (v_mfma_f32_32x32x16_f16) with a "
-              "rigorous error bound; rows inside it re-decided by the exact fp32 MFMA argmin "
-              "(assignments identical to exact fp32); delta accumulation of moved rows"),
+             "distance_path": path,
              "cost": r["cost"]}
     del table
     if args.separable_extra and args.sigma != 1.0:

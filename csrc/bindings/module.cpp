@@ -386,6 +386,10 @@ PYBIND11_MODULE(_native, m) {
       [](int d, const std::string& dtype) { return kern::kmeans_ld(d, dtype == "bf16"); },
       py::arg("d"), py::arg("dtype") = "f32");
   m.def(
+      "kmeans_lds_kmax", [](int d, bool precise) { return kern::kmeans_lds_kmax(d, precise); },
+      py::arg("d"), py::arg("precise") = false,
+      "largest k whose centroid plane one LDS plan holds (larger k: chunked passes)");
+  m.def(
       "kmeans_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
          py::object init_centers, int k, int max_iter, double tol, const std::string& init_mode,

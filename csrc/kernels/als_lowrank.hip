@@ -60,7 +60,9 @@ __device__ inline float xor_sum16(float v) {  // sum over the 16 lanes of a row 
   return v;
 }
 
-template <int NBR, int NBN>
+// KEEPW: W stays in registers through the Cholesky (no second gather of the factor rows) when
+// the register budget allows it; otherwise the rows are re-read for W^T S s.
+template <int NBR, int NBN, bool KEEPW>
 __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* M = lds;                                 // n x n, packed lower blocks
@@ -216,15 +218,22 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
     for (int bi = 0; bi < NBN; ++bi) {
       const int i = 16 * bi + c;
       const float s_i = __shfl(ss, i, 64);
-      const int item = __shfl(it, i, 64);
-      const float* yrow = a.src + static_cast<int64_t>(item) * ld + 4 * kk;
+      if constexpr (KEEPW) {
 #pragma unroll
-      for (int qb = 0; qb < NBR; ++qb) {
-        const float4 y = *reinterpret_cast<const float4*>(yrow + 16 * qb);
-        t[qb][0] = fmaf(y.x, s_i, t[qb][0]);
-        t[qb][1] = fmaf(y.y, s_i, t[qb][1]);
-        t[qb][2] = fmaf(y.z, s_i, t[qb][2]);
-        t[qb][3] = fmaf(y.w, s_i, t[qb][3]);
+        for (int qb = 0; qb < NBR; ++qb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) t[qb][e] = fmaf(W[bi][qb][e], s_i, t[qb][e]);
+      } else {
+        const int item = __shfl(it, i, 64);
+        const float* yrow = a.src + static_cast<int64_t>(item) * ld + 4 * kk;
+#pragma unroll
+        for (int qb = 0; qb < NBR; ++qb) {
+          const float4 y = *reinterpret_cast<const float4*>(yrow + 16 * qb);
+          t[qb][0] = fmaf(y.x, s_i, t[qb][0]);
+          t[qb][1] = fmaf(y.y, s_i, t[qb][1]);
+          t[qb][2] = fmaf(y.z, s_i, t[qb][2]);
+          t[qb][3] = fmaf(y.w, s_i, t[qb][3]);
+        }
       }
     }
 #pragma unroll
@@ -235,7 +244,8 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
       const float4 gq = *reinterpret_cast<const float4*>(gs + 16 * qb + 4 * kk);
       const float gv[4] = {gq.x, gq.y, gq.z, gq.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e) xv[e] = dv[e] * (gv[e] - dv[e] * xor_sum16(t[qb][e]));
+      for (int e = 0; e < 4; ++e)  // KEEPW: t already carries D^{-1/2} (W = Yq_u D^{-1/2})
+        xv[e] = dv[e] * (gv[e] - (KEEPW ? 1.f : dv[e]) * xor_sum16(t[qb][e]));
       if (c == 0)
         *reinterpret_cast<float4*>(out + 16 * qb + 4 * kk) =
             make_float4(xv[0], xv[1], xv[2], xv[3]);
@@ -246,10 +256,11 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
 
 template <int NBR, int NBN>
 void launch_lowrank(const LowRankArgs& a, int num_cus, hipStream_t s) {
+  constexpr bool kKeepW = NBN * NBR <= 21;  // above: spills at 2 waves per SIMD (reload instead)
   constexpr size_t lds = (als::packed_floats<NBN>() + 64 + 32 * NBR) * sizeof(float);
   const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 512))));
   const int grid = int(std::min<int64_t>(a.nrows, int64_t(num_cus) * per_cu));
-  hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN>), dim3(grid), dim3(64), lds, s, a);
+  hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN, kKeepW>), dim3(grid), dim3(64), lds, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
