@@ -262,6 +262,16 @@ bool lean_applies(const DenseTable& x, int k, int kpad, const AssignReq& req) {
          !(req.bounds && req.drift && !req.delta);  // the in-kernel pruning test: general kernel
 }
 
+// Whether the centroid-chunked lean pass applies: k too large for one LDS plan of the general
+// kernel, but small enough for 10-bit key indices; no pruning state (full passes).
+bool lean_chunked_applies(const DenseTable& x, const GpuCenters& g, const AssignReq& req,
+                          int kmax) {
+  const bool off = std::getenv("OAP_KMEANS_NO_LEAN_CHUNKED") != nullptr;
+  return !off && req.lean && req.fast1 && !req.precise && !req.mindist_seeded && !req.bounds &&
+         !req.delta && x.cols <= 128 && g.kpad > kmax && g.kpad <= 1024 &&
+         kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
+}
+
 size_t lean_defer_bytes(int64_t rows, int num_cus, int* grid, int64_t* cap) {
   *grid = kern::kmeans_lloyd_grid(rows, num_cus);
   *cap = kern::kmeans_lloyd_seg_cap(rows, *grid, kern::kmeans_lloyd_waves(lean_variant()));
@@ -388,6 +398,86 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     return kern::kmeans_assign(a, ctx.info().cu_count, s);
   }
   OAP_CHECK(!req.delta, "kmeans delta accumulation is single-launch only");
+  if (x.rows > 0 && lean_chunked_applies(x, g, req, kmax)) {
+    // ---- centroid-chunked lean pass: the lean tier-1 kernel walks chunks of the fp16 centroid
+    // plane carrying each row's top-2 keys (global indices) between launches; the last chunk
+    // finishes the sure rows and defers the near ties; the exact re-decision walks chunks of
+    // fp32 centers carrying (best, index); labels drive the binned accumulation.
+    const int lk = kern::kmeans_lloyd_chunk_kmax(x.cols);
+    const int ek = kern::kmeans_exact_chunk_kmax(x.cols);
+    auto split = [&](int cap, int* n) {
+      *n = (g.k + cap - 1) / cap;
+      return static_cast<int>(round_up((g.k + *n - 1) / *n, 32));
+    };
+    int nl = 0, ne = 0;
+    const int lsz = split(lk, &nl), esz = split(ek, &ne);
+    int grid = 0;
+    int64_t cap = 0;
+    Buffer dbuf = ctx.alloc(lean_defer_bytes(x.rows, ctx.info().cu_count, &grid, &cap));
+    int32_t* drows = dbuf.as<int32_t>();
+    unsigned* dcnt = reinterpret_cast<unsigned*>(drows + size_t(grid) * size_t(cap));
+    Buffer keys = ctx.alloc(sizeof(int32_t) * 2 * size_t(x.rows));
+    Buffer xstate = ctx.alloc(sizeof(float) * 2 * size_t(grid) * size_t(cap));
+    Buffer lab;
+    int32_t* labels = req.labels;
+    if (!labels && req.accumulate) {
+      lab = ctx.alloc(sizeof(int32_t) * size_t(x.rows));
+      labels = lab.as<int32_t>();
+    }
+    a.labels = labels;
+    a.accumulate = false;
+    a.defer_rows = drows;
+    a.defer_row_count = dcnt;
+    a.row_seg_cap = cap;
+    a.lean_keys = keys.as<int32_t>();
+    a.xstate = xstate.as<float>();
+    a.centers_all = g.c32.as<float>();
+    a.kglob = g.k;
+    auto chunk = [&](kern::KMeansAssignArgs& b, int c, int size, int ci, int n) {
+      const int kc = std::min(size, g.k - c);
+      b.centers = g.c32.as<float>() + size_t(c) * g.dp;
+      b.cnorm = g.cnorm.as<float>() + c;
+      b.k = kc;
+      b.kpad = static_cast<int>(round_up(kc, 32));
+      b.base = c;
+      b.chunk_mode = n == 1 ? 0 : (ci == 0 ? 1 : (ci == n - 1 ? 3 : 2));
+      if (b.chunk_mode == 1 || b.chunk_mode == 2) {  // running state only
+        b.labels = nullptr;
+        b.mindist = nullptr;
+        b.cost_slab = nullptr;
+        b.deferred_rows = nullptr;
+      }
+    };
+    for (int ci = 0; ci < nl; ++ci) {
+      kern::KMeansAssignArgs b = a;
+      b.deferred_rows = req.deferred_rows;
+      chunk(b, ci * lsz, lsz, ci, nl);
+      kern::kmeans_lloyd(b, grid, lean_variant(), s);
+    }
+    for (int ci = 0; ci < ne; ++ci) {
+      kern::KMeansAssignArgs b = a;
+      b.defer_rows = nullptr;
+      b.defer_row_count = nullptr;
+      b.deferred_rows = nullptr;
+      b.row_list = drows;
+      b.row_count = dcnt;
+      b.row_subs = kern::kmeans_lloyd_waves(lean_variant());
+      b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
+      chunk(b, ci * esz, esz, ci, ne);
+      kern::kmeans_exact_rows(b, grid, s);
+    }
+    if (req.accumulate) {
+      Buffer bins = ctx.alloc(kern::kmeans_bin_scratch_bytes(x.rows, g.k));
+      if (!kern::kmeans_accumulate_binned(x.data.data(), x.dtype == DType::BF16, x.rows,
+                                          static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
+                                          req.sums_too ? req.sums : nullptr, req.counts,
+                                          bins.data(), s))
+        kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
+                                static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
+                                req.sums_too ? req.sums : nullptr, req.counts, s);
+    }
+    return a.cost_slab ? 2 * grid : 0;
+  }
   // ---- chunked path (more centroids than one LDS plan holds)
   Buffer lab, dist;
   int32_t* labels = req.labels;
@@ -996,6 +1086,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   req.counts = counts;
   req.cost_slab = slab.as<double>();
   req.refine_tiles = refine_d.as<u64>();
+  if (const char* e = std::getenv("OAP_KMEANS_CHUNK_DEFER")) req.defer = std::atoi(e) != 0;
   // chunked (large-k) path: labels/mindist persist across iterations to seed the merge passes
   Buffer lab_keep, mind_keep;
   const bool chunked = x.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x.cols, p.precise);
@@ -1005,8 +1096,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     req.labels = lab_keep.as<int32_t>();
     req.mindist = mind_keep.as<float>();
   }
+  // the centroid-chunked lean pass runs full passes (no pruning state)
+  const bool lean_chunked =
+      chunked && !p.precise && g.kpad <= 1024 && !std::getenv("OAP_KMEANS_NO_LEAN_CHUNKED") &&
+      kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
   // pruning: per-row bounds (+ labels) persist across iterations, finalize reports the drift
-  const bool prune = p.prune && !p.precise && x.cols <= 128 && x.rows > 0;
+  const bool prune = p.prune && !p.precise && x.cols <= 128 && x.rows > 0 && !lean_chunked;
   Buffer bounds_b, drift_b, pruned_d, tiles_b;
   if (prune) {
     bounds_b = ctx.alloc(sizeof(float) * 2 * x.rows);
@@ -1074,6 +1169,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     ldefer_b = ctx.alloc(lean_defer_bytes(x.rows, ctx.info().cu_count, &lg, &lcap));
     req.defer_rows = ldefer_b.as<int32_t>();
     req.defer_count = reinterpret_cast<unsigned*>(req.defer_rows + size_t(lg) * size_t(lcap));
+  }
+  if (x.rows > 0 && (req.defer_rows || lean_chunked)) {
     ldstat_b = ctx.alloc(2 * sizeof(u64));  // [deferred rows, moved rows staged]
     ldstat_h = ctx.alloc_pinned(2 * sizeof(u64));
     ctx.memset(ldstat_b.data(), 0, 2 * sizeof(u64), s);

@@ -125,6 +125,18 @@ struct KMeansAssignArgs {
   int32_t* exact_rows = nullptr;
   unsigned* exact_count = nullptr;
   int64_t exact_sub_cap = 0;
+  // Centroid-chunked lean pass (kmeans_lloyd / kmeans_exact_rows, k too large for one LDS plan,
+  // k <= 1024): a launch sees centers / cnorm / k / kpad of ONE chunk whose first center has
+  // global index `base`.  chunk_mode 1 = first, 2 = middle chunk (only the running state is
+  // written), 3 = last chunk (the outputs), 0 = not chunked.  lean_keys: the lean kernel's
+  // running top-2 keys per row ([n][2]); xstate: the exact kernel's running (best, index) per
+  // deferral-list slot ([grid * row_seg_cap][2]; no bounds in this mode); centers_all / kglob:
+  // every center (the chosen center's exact cost) and the global k.
+  int chunk_mode = 0;
+  int kglob = 0;
+  int32_t* lean_keys = nullptr;
+  float* xstate = nullptr;
+  const float* centers_all = nullptr;
 };
 // Lean tier-1 Lloyd kernel (kmeans_lloyd.hip): applicable when the centroid hi plane + the
 // fixed-point accumulator fit LDS and d + 4 bias features fit the padded width.
@@ -139,6 +151,10 @@ int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves);
 // selects the workgroup shape (0: 16 waves; tuning: 1-3).  Writes `grid`
 // cost partials.
 int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s);
+// Largest centroid chunks (multiples of 32) of the chunked lean pass at dimension d: the lean
+// kernel's fp16 plane and the exact kernel's fp32 centers (0: d not supported).
+int kmeans_lloyd_chunk_kmax(int d);
+int kmeans_exact_chunk_kmax(int d);
 // The general fused kernel over the rows kmeans_lloyd deferred (a.row_list / row_count /
 // row_seg_cap from its defer outputs), on the same `grid`.
 void kmeans_assign_rows(const KMeansAssignArgs& a, int grid, hipStream_t s);

@@ -76,6 +76,11 @@ struct LeanArgs {
   int accumulate, sums_too, delta;
   int ablate;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance, 16 no loads,
                // 32 minimal epilogue
+  // centroid-chunked pass (KMeansAssignArgs::chunk_mode): running top-2 keys per row, the
+  // chunk's first global center, the global k, every center (the final chunk's exact cost)
+  int2* keys;
+  const float* centers_all;
+  int kbase, kglob, chunk_mode;
 };
 
 struct LeanSmem {
@@ -133,6 +138,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
+  // chunked passes: keys carry global center indices (kbase + in-chunk offset, < 1024); the
+  // first and middle chunks only merge into the running keys, the last one finishes the rows
+  const int kglob = a.chunk_mode ? a.kglob : k, kbase = a.chunk_mode ? a.kbase : 0;
+  const float* cen_all = a.chunk_mode ? a.centers_all : a.centers;
+  const bool keys_in = a.chunk_mode >= 2, keys_out = a.chunk_mode == 1 || a.chunk_mode == 2;
   const bool accumulate = a.accumulate != 0;
   const bool do_acc = accumulate && !(a.ablate & 1);
   const bool do_cost = !(a.ablate & 2);
@@ -355,6 +365,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     // ---- tier 1: one fp16 product per k-step; top-2 on integer keys (the distance's bits with
     // the low 10 mantissa bits replaced by the in-chunk offset; value order, lowest index first)
     int k1 = 0x7fffffff, k2 = 0x7fffffff;
+    if (keys_in && h == 0 && valid) {  // one half starts from the running pair (no duplicate)
+      const int2 kv = a.keys[row];
+      k1 = kv.x;
+      k2 = kv.y;
+    }
     auto mfma_chunk = [&](int c0, f32x16& acc) {
       const _Float16* ap = ph + size_t(c0 + r) * sb + 8 * h;
       f16x8 av[KS];
@@ -399,7 +414,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       merge2(t1[0], t2[0], t1[1], t2[1]);
       merge2(t1[2], t2[2], t1[3], t2[3]);
       merge2(t1[0], t2[0], t1[2], t2[2]);
-      const int base = c0 + 4 * h;  // disjoint from every in-chunk offset's bits
+      const int base = c0 + 4 * h + kbase;  // disjoint from every in-chunk offset's bits
       const int i1 = t1[0] | base, i2 = t2[0] | base;
       k2 = min(max(k1, i1), min(k2, i2));
       k1 = min(k1, i1);
@@ -460,6 +475,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
       k2 = min(max(k1, o1), min(k2, o2));
       k1 = min(k1, o1);
+      if (keys_out) {  // not the last chunk: carry the pair to the next one
+        if (h == 0 && valid) a.keys[row] = make_int2(k1, k2);
+        return;
+      }
       b1 = __int_as_float(k1 & ~0x3ff);
       b2 = __int_as_float(k2 & ~0x3ff);
       tt = fmaf(thr_c, sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
@@ -479,7 +498,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
     const bool done = valid && !unsure;
     int b = k1 & 0x3ff;
-    b = (b < k) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
+    b = (b < kglob) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
     const bool acc_row = done && do_acc && (!a.delta || (old >= 0 && old != b));
     if (a.delta) {  // stage moved rows (wave-private slots, in row order)
       const unsigned long long mm = __ballot(acc_row && h == 0);
@@ -500,7 +519,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       const F& xr = (PF == 2) ? xr_buf : x;
       float cb[KS][8];
       if (do_cost) {
-        load_row8<KS>(a.centers + size_t(b) * DP + 8 * h, cb);  // L2-resident; lands under adds
+        load_row8<KS>(cen_all + size_t(b) * DP + 8 * h, cb);  // L2-resident; lands under adds
       } else {
 #pragma unroll
         for (int s = 0; s < KS; ++s)
@@ -720,6 +739,11 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
   using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int k = a.k, d = a.d, kpad = a.kpad;
+  // chunked passes: the running (best, second, index) of each deferred row lives in xstate
+  // between the chunk launches; the last chunk finishes the rows against every center
+  const int kglob = a.chunk_mode ? a.kglob : k;
+  const bool st_in = a.chunk_mode >= 2, st_out = a.chunk_mode == 1 || a.chunk_mode == 2;
+  float2* xst = reinterpret_cast<float2*>(a.xstate);  // (best, index): no bounds when chunked
   const bool accumulate = a.accumulate;
   const ExactSmem L = exact_plan(kpad, k, d, accumulate, a.sums_too);
   float* ct = reinterpret_cast<float*>(smem + L.ct);
@@ -760,11 +784,14 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
   const float mrel = 4e-7f * float(d + 8);
   const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);
   const int64_t ngroups = (int64_t(total) + 31) / 32;
-  auto row_at = [&](int64_t i) -> int64_t {  // i-th deferred row of this workgroup (clamped)
+  auto slot_at = [&](int64_t i) -> int64_t {  // list slot of this workgroup's i-th row (clamped)
     i = i < int64_t(total) ? i : int64_t(total) - 1;
     int w = 0;
     while (w + 1 < a.row_subs && int64_t(pref[w + 1]) <= i) ++w;
-    return int64_t(a.row_list[int64_t(blockIdx.x) * a.row_seg_cap + w * sub + (i - pref[w])]);
+    return int64_t(blockIdx.x) * a.row_seg_cap + w * sub + (i - pref[w]);
+  };
+  auto row_at = [&](int64_t i) -> int64_t {  // i-th deferred row of this workgroup (clamped)
+    return int64_t(a.row_list[slot_at(i)]);
   };
   auto load_rows = [&](int64_t g, F& dst) {
     const int64_t row = row_at(g * 32 + r);
@@ -827,6 +854,12 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
     // exact argmin with the best and second-best exact distances (the second for the bounds)
     float best = INFINITY, second = INFINITY;
     int bidx = 0x7fffffff;
+    const int64_t slot = slot_at(i);
+    if (st_in && h == 0 && valid) {  // one half starts from the running state (no duplicate)
+      const float2 st = xst[slot];
+      best = st.x;
+      bidx = __float_as_int(st.y);
+    }
     for (int c0 = 0; c0 < kpad; c0 += 32) {
       f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       const float* cp = ct + size_t(c0 + r) * CS + 8 * h;
@@ -852,7 +885,7 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
           if (dist < best) {
             second = best;
             best = dist;
-            bidx = c0 + 8 * gq + 4 * h + q;
+            bidx = a.base + c0 + 8 * gq + 4 * h + q;
           } else if (dist < second) {
             second = dist;
           }
@@ -869,12 +902,18 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
         bidx = oi;
       }
     }
-    const int b = (bidx >= 0 && bidx < k) ? bidx : 0;
+    if (st_out) {  // not the last chunk: carry the state to the next one
+      if (valid && h == 0) xst[slot] = make_float2(best, __int_as_float(bidx));
+      xa = xb;
+      continue;
+    }
+    const int b = (bidx >= 0 && bidx < kglob) ? bidx : 0;
     int old = -1;
     if (a.delta && valid) old = a.labels[row];
     // exact cost and |x|^2 in the assign kernels' lane order
     float part = 0.f, px = 0.f;
-    const float* cb = ct + size_t(b) * CS + 8 * h;
+    const float* cb = a.chunk_mode ? a.centers_all + size_t(b) * DP + 8 * h
+                                   : ct + size_t(b) * CS + 8 * h;
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -1039,6 +1078,23 @@ bool kmeans_lloyd_supported(int d, int k, bool accumulate, bool sums_too) {
          exact_plan(kpad, k, d, accumulate, sums_too).total <= kLdsLimit;
 }
 
+int kmeans_lloyd_chunk_kmax(int d) {
+  if (d + 4 > 128) return 0;
+  const int dp = (d + 4 + 15) / 16 * 16;
+  if (dp != kmeans_dp(d)) return 0;
+  int best = 0;
+  for (int kp = 32; kp <= 1024; kp += 32)
+    if (lean_plan(dp, kp, kp, d, false, false, 16, false).total <= kLdsLimit) best = kp;
+  return best;
+}
+
+int kmeans_exact_chunk_kmax(int d) {
+  int best = 0;
+  for (int kp = 32; kp <= 1024; kp += 32)
+    if (exact_plan(kp, kp, d, false, false).total <= kLdsLimit) best = kp;
+  return best;
+}
+
 int kmeans_lloyd_grid(int64_t n, int num_cus) {
   const int64_t tiles = (n + 31) / 32;
   const int64_t cap = num_cus > 256 ? num_cus : 256;
@@ -1060,7 +1116,14 @@ int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
 }
 
 int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s) {
-  OAP_CHECK(kmeans_lloyd_supported(a.d, a.k, a.accumulate, a.sums_too) && !a.precise &&
+  // the chunked driver (centers_all set) pairs this pass with a chunked exact pass, so only the
+  // lean plane has to fit (a single lean chunk runs as chunk_mode 0)
+  const bool chunk_ok = !a.centers_all
+                            ? kmeans_lloyd_supported(a.d, a.k, a.accumulate, a.sums_too)
+                            : (a.kpad <= kmeans_lloyd_chunk_kmax(a.d) && !a.accumulate &&
+                               !a.delta && (a.chunk_mode == 0 || a.lean_keys) &&
+                               a.base + a.kpad <= 1024 && a.base % 32 == 0);
+  OAP_CHECK(chunk_ok && !a.precise &&
                 !a.merge && a.cstat && a.defer_rows && a.defer_row_count &&
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, kmeans_lloyd_waves(variant)) &&
                 a.ld == kmeans_ld(a.d, a.xbf16),
@@ -1097,6 +1160,11 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.sums_too = a.sums_too;
   l.delta = a.delta;
   l.ablate = a.ablate;
+  l.keys = reinterpret_cast<int2*>(a.lean_keys);
+  l.centers_all = a.centers_all;
+  l.kbase = a.base;
+  l.kglob = a.kglob;
+  l.chunk_mode = a.chunk_mode;
   // the exact per-row cost is computed when a cost or mindist is asked for
   const bool cost = a.cost_slab != nullptr || a.mindist != nullptr;
   if (a.xbf16)
@@ -1114,6 +1182,9 @@ void kmeans_exact_rows(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   if (a.n == 0) return;
   OAP_CHECK(exact_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too).total <= kLdsLimit,
             "kmeans_exact_rows: centers exceed LDS");
+  OAP_CHECK(a.chunk_mode == 0 ||
+                (a.xstate && a.centers_all && !a.accumulate && !a.delta && !a.bounds),
+            "kmeans_exact_rows: chunked pass needs its running state and every center");
   if (a.xbf16)
     launch_exact_xb<true>(a, grid, s);
   else

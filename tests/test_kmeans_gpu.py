@@ -258,9 +258,11 @@ def test_batched_iterations_match_stepwise(native):
 @pytest.mark.parametrize("d,k,dtype,n", [(50, 200, "f32", 200000), (20, 16, "f32", 100000),
                                          (50, 1500, "f32", 60000), (100, 1000, "bf16", 60000),
                                          (100, 60, "bf16", 100000), (128, 40, "f32", 50000)])
-def test_pruning_is_exact(native, d, k, dtype, n):
+def test_pruning_is_exact(native, monkeypatch, d, k, dtype, n):
     """Bound-based pruning skips distance work but never changes a label: centers, cost history
-    and counts are bitwise those of the unpruned fit (single-launch and chunked large-k paths)."""
+    and counts are bitwise those of the unpruned fit (single-launch and chunked large-k paths;
+    k <= 1024 large-k fits otherwise take the centroid-chunked lean pass, without pruning)."""
+    monkeypatch.setenv("OAP_KMEANS_NO_LEAN_CHUNKED", "1")
     rng = np.random.default_rng(d * 7 + k)
     C = rng.uniform(-10, 10, size=(k, d))
     X = C[rng.integers(0, k, n)] + rng.normal(0, 1.0, size=(n, d))
@@ -392,3 +394,38 @@ def test_estimator_streams_beyond_budget(gpu_world, monkeypatch):
     m = O.KMeans(k=4, seed=1, maxIter=10).fit(X)
     assert m.fit_info.get("streamed") and m.fit_info["engine"] == "gpu"
     assert len(m.summary.clusterSizes) == 4 and sum(m.summary.clusterSizes) == len(X)
+
+
+@pytest.mark.parametrize("d,k,sigma,dtype", [(100, 1000, 8.0, "bf16"), (60, 1000, 6.0, "f32"),
+                                             (100, 700, 1.0, "bf16")])
+def test_lean_chunked_large_k_bitwise(native, monkeypatch, d, k, sigma, dtype):
+    """k beyond one LDS plan (<= 1024): the lean tier-1 kernel walks fp16 centroid chunks carrying
+    each row's top-2 keys, the exact re-decision walks fp32 chunks carrying (best, index), labels
+    drive the binned accumulation.  Bitwise the exact-fp32 fit, the previous chunked path and the
+    CPU engine."""
+    n = 60000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d, dtype), 0, k, 10.0, sigma, 5, dtype)
+    init = t.to_numpy(g, 0, k) + 0.25
+    if dtype == "bf16":
+        init = bf16_round(init)
+    comm = native.LocalComm(True)
+    rl = native.kmeans_fit(g, comm, t, init, k, 3, -1.0)
+    rp = native.kmeans_fit(g, comm, t, init, k, 3, -1.0, precise=True)
+    monkeypatch.setenv("OAP_KMEANS_NO_LEAN_CHUNKED", "1")
+    ro = native.kmeans_fit(g, comm, t, init, k, 3, -1.0)
+    monkeypatch.delenv("OAP_KMEANS_NO_LEAN_CHUNKED")
+    c = native.Context(-1)
+    X = t.to_numpy(g)
+    rc = native.kmeans_fit(c, native.LocalComm(False), native.upload_dense(c, X, "f64", d), init,
+                           k, 3, -1.0)
+    if sigma > 2:
+        assert rl["deferred_rows"] > 0  # near ties went through the chunked exact pass
+    for r in (rp, ro, rc):
+        assert r["last_counts"] == rl["last_counts"]
+        assert np.array_equal(r["centers"], rl["centers"])
+    assert abs(rl["cost"] - rp["cost"]) <= 1e-9 * rp["cost"]
+    lab, dist = native.kmeans_predict(g, t, rl["centers"])
+    ref_lab, ref_d = vanilla.find_closest(X, rl["centers"])
+    assert (lab == ref_lab).mean() > 0.9999
+
