@@ -88,7 +88,7 @@ __device__ inline void accumulate(const int32_t* __restrict__ cols, const float*
                                   float alpha, bool implicit, f4 (&acc)[NB * (NB + 1) / 2],
                                   float (&bacc)[NB], int& nexp) {
   constexpr int kSteps = 2, kBlock = 4 * kSteps;
-  const int lane = threadIdx.x, kk = lane >> 4, c = lane & 15;
+  const int lane = als::fresh_lane(), kk = lane >> 4, c = lane & 15;
   auto fetch = [&](int64_t p, int& it, float& rv) {
     const int64_t q = p + (c & (kBlock - 1));
     const bool ok = q < p1;

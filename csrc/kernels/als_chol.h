@@ -31,10 +31,20 @@ constexpr int packed_floats() {
 // cross-lane broadcasts), the panel TRSM lane-per-row against broadcast LDS rows, the trailing
 // SYRK update on v_mfma_f32_16x16x4_f32 with fragments straight from LDS.  Returns false (and
 // stops) at the first non-positive pivot.  `first` > 0 skips panels (timing ablation).
+// The lane id laundered through an empty asm: the lane masks derived from it (lane > j, lane ==
+// j, ... for every unrolled j) are then recomputed where they are used instead of being hoisted
+// out of the caller's row loop into hundreds of SGPR pairs (spilled to VGPR lanes and read back
+// with v_readlane + hazard nops on every use).
+__device__ inline int fresh_lane() {
+  int lane = static_cast<int>(threadIdx.x);
+  asm volatile("" : "+v"(lane));
+  return lane;
+}
+
 template <int NB>
 __device__ inline bool chol_factor(float* M, int first = 0) {
   constexpr int RP = 16 * NB;
-  const int lane = threadIdx.x;
+  const int lane = fresh_lane();
   for (int jb = first; jb < NB; ++jb) {
     const int o = 16 * jb;
     // (1) diagonal block: lanes 0..15 own its rows, in registers
@@ -141,7 +151,7 @@ template <int NB>
 __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v1,
                                   int nsolve = NB) {
   constexpr int RP = 16 * NB;
-  const int lane = threadIdx.x;
+  const int lane = fresh_lane();
   // forward: L z = b
 #pragma unroll
   for (int jb = 0; jb < nsolve; ++jb) {

@@ -52,11 +52,17 @@ struct LowRankArgs {
   unsigned long long* fail;
 };
 
-__device__ inline float xor_sum16(float v) {  // sum over the 16 lanes of a row group (c)
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+template <int CTRL>
+__device__ inline float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// sum over the 16 lanes of a row group (c), every lane gets it (bitwise the same): DPP
+// quad_perm xor 1, xor 2, row_half_mirror, row_mirror — four VALU adds, no LDS crossbar
+__device__ inline float xor_sum16(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
   return v;
 }
 
@@ -69,10 +75,11 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
   float* bv = lds + als::packed_floats<NBN>();    // 64 floats (the backward solve stages 64 lanes)
   float* gs = bv + 64;                            // 16 NBR floats: g while W is not resident
   float* dhs = gs + 16 * NBR;                     // 16 NBR floats: D^{-1/2}
-  const int lane = threadIdx.x, kk = lane >> 4, c = lane & 15;
   const int ld = a.ld;
 
   while (true) {
+    // lane masks recomputed per row (kernels/als_chol.h: fresh_lane)
+    const int lane = als::fresh_lane(), kk = lane >> 4, c = lane & 15;
     unsigned long long q_u = 0;
     if (lane == 0) q_u = atomicAdd(a.queue, 1ull);
     const int64_t q = static_cast<int64_t>(__shfl(q_u, 0, 64));
