@@ -144,6 +144,95 @@ __device__ inline void accumulate(const int32_t* __restrict__ cols, const float*
   }
 }
 
+// accumulate() for long-row chunks: the factor rows of block p + 1 are loaded while block p's
+// MFMAs run (one block ahead, double-buffered), the (item, rating) pairs two blocks ahead.  The
+// unpipelined loop waited for every block's rows before its first MFMA: at one wave per SIMD
+// (the partial kernel keeps 28 accumulator tiles) it stalled most of the time.
+template <int NB, int kSteps>
+__device__ inline void accumulate_pipe(const int32_t* __restrict__ cols,
+                                       const float* __restrict__ vals, int64_t p0, int64_t p1,
+                                       const float* __restrict__ src, int ld, float alpha,
+                                       bool implicit, f4 (&acc)[NB * (NB + 1) / 2],
+                                       float (&bacc)[NB], int& nexp) {
+  constexpr int kBlock = 4 * kSteps;
+  static_assert(kBlock <= 16, "pairs of one block are fetched by 16 lanes");
+  const int lane = threadIdx.x, kk = lane >> 4, c = lane & 15;
+  auto fetch = [&](int64_t p, int& it, float& rv) {
+    const int64_t q = p + (c & (kBlock - 1));
+    const bool ok = q < p1;
+    it = ok ? cols[q] : -1;
+    rv = ok ? vals[q] : 0.f;
+  };
+  auto load = [&](int it_l, float rv_l, float (&yv)[kSteps][NB], float (&rvs)[kSteps],
+                  bool (&oks)[kSteps]) {
+#pragma unroll
+    for (int s4 = 0; s4 < kSteps; ++s4) {
+      const int item = __shfl(it_l, 4 * s4 + kk, 64);
+      rvs[s4] = __shfl(rv_l, 4 * s4 + kk, 64);
+      oks[s4] = item >= 0;
+      const float* yrow = src + static_cast<int64_t>(oks[s4] ? item : 0) * ld + c;
+#pragma unroll
+      for (int f = 0; f < NB; ++f) yv[s4][f] = yrow[16 * f];
+    }
+  };
+  if (p0 >= p1) return;
+  int it_b = -1;
+  float rv_b = 0.f;
+  fetch(p0, it_b, rv_b);
+  float yc[kSteps][NB], rc[kSteps];
+  bool oc[kSteps];
+  load(it_b, rv_b, yc, rc, oc);
+  if (p0 + kBlock < p1) fetch(p0 + kBlock, it_b, rv_b);
+  for (int64_t p = p0; p < p1; p += kBlock) {
+    float yn[kSteps][NB], rn[kSteps];
+    bool on[kSteps];
+    const bool more = p + kBlock < p1;  // wave-uniform
+    if (more) load(it_b, rv_b, yn, rn, on);
+    if (p + 2 * kBlock < p1) fetch(p + 2 * kBlock, it_b, rv_b);
+#pragma unroll
+    for (int s4 = 0; s4 < kSteps; ++s4) {
+      const bool ok = oc[s4];
+      const float rv = rc[s4];
+      float wa, wb;
+      if (implicit) {
+        const float c1 = alpha * fabsf(rv);
+        wa = ok ? c1 : 0.f;
+        wb = (ok && rv > 0.f) ? 1.f + c1 : 0.f;
+        nexp += (ok && rv > 0.f && c == 0) ? 1 : 0;
+      } else {
+        wa = ok ? 1.f : 0.f;
+        wb = ok ? rv : 0.f;
+        nexp += (ok && c == 0) ? 1 : 0;
+      }
+      float av[NB];
+#pragma unroll
+      for (int f = 0; f < NB; ++f) {
+        av[f] = wa * yc[s4][f];
+        bacc[f] = fmaf(wb, yc[s4][f], bacc[f]);
+      }
+      int t = 0;
+#pragma unroll
+      for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+        for (int bj = 0; bj <= bi; ++bj, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[bi], yc[s4][bj], acc[t], 0, 0, 0);
+    }
+    if (more) {
+#pragma unroll
+      for (int s4 = 0; s4 < kSteps; ++s4) {
+        rc[s4] = rn[s4];
+        oc[s4] = on[s4];
+#pragma unroll
+        for (int f = 0; f < NB; ++f) yc[s4][f] = yn[s4][f];
+      }
+    }
+  }
+}
+
+// Partial Gramian of one long-row chunk, pipelined accumulation at one wave per SIMD (all 512
+// registers: the 28 accumulator tiles plus two blocks of factor rows in flight; 2 waves/SIMD with
+// 256 registers each measured slower, 170 -> 199 ms/iter; 1 wave/SIMD without the pipeline 170;
+// this form 140 at 1B ratings).
 template <int NB>
 __global__ __launch_bounds__(kAlsThreads) void oap_als_partial(PartialArgs a) {
   constexpr int NT = NB * (NB + 1) / 2;
@@ -156,8 +245,8 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_partial(PartialArgs a) {
 #pragma unroll
     for (int f = 0; f < NB; ++f) bacc[f] = 0.f;
     int nexp = 0;
-    accumulate<NB>(a.cols, a.vals, a.chunk_begin[q], a.chunk_end[q], a.src, a.ld, a.alpha,
-                   a.implicit != 0, acc, bacc, nexp);
+    accumulate_pipe<NB, 4>(a.cols, a.vals, a.chunk_begin[q], a.chunk_end[q], a.src, a.ld, a.alpha,
+                           a.implicit != 0, acc, bacc, nexp);
     float* out = a.partials + q * partial_floats<NB>();
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -332,7 +421,7 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     pa.implicit = s.implicit ? 1 : 0;
     pa.partials = s.partials;
     hipLaunchKernelGGL(oap_als_partial<NB>,
-                       dim3(int(std::min<int64_t>(s.n_chunks, int64_t(num_cus) * 8))),
+                       dim3(int(std::min<int64_t>(s.n_chunks, int64_t(num_cus) * 4))),
                        dim3(kAlsThreads), 0, st, pa);
     OAP_HIP_CHECK(hipGetLastError());
     OAP_HIP_CHECK(hipMemsetAsync(s.queue + 1, 0, sizeof(unsigned long long), st));
