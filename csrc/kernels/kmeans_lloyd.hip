@@ -190,7 +190,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   // 2 x 2 x 2^-10 |alpha c||alpha x| (fp16 products), fp16 subnormals d 2^-14, the bias pairs
   // 2^-21 (|c|^2 + |x|^2), fp32 accumulation 4e-5 (cmax^2 + |x|^2), plus the key truncation
   const float cm_s = alpha * cmax;
-  const float thr_c = 0.0040f * cm_s;
+  // bf16 rows are exact in fp16 (8 significant bits, alpha a power of two; subnormal and
+  // out-of-range rows are covered by thr_k / deferred), so only the centers' fp16 rounding
+  // enters the cross term: half the f32-row coefficient (2 x 2^-10 instead of 2 x 2 x 2^-10)
+  const float thr_c = (XB ? 0.0020f : 0.0040f) * cm_s;
   const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
   const float mrel = 4e-7f * float(d + 8);                // fp32 evaluation margin (bounds)
   const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);  // direct-form |x - c|^2 rounding
