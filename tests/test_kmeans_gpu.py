@@ -336,7 +336,7 @@ def test_lean_variants_agree(native, variant):
         native.kmeans_set_lean_variant(variant)
         r = native.kmeans_fit(g, native.LocalComm(True), t, init, 100, 4, -1.0, prune=False)
     finally:
-        native.kmeans_set_lean_variant(0)
+        native.kmeans_set_lean_variant(-1)  # back to the width rule
     assert np.array_equal(r["centers"], ref["centers"])
     assert r["deferred_rows"] == ref["deferred_rows"]
 
