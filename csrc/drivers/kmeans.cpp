@@ -244,6 +244,12 @@ struct AssignReq {
   unsigned* defer_count = nullptr;
   u64* deferred_rows = nullptr;
   int ablate = 0;  // timing ablations (kern::KMeansAssignArgs::ablate)
+  // centroid-chunked lean pass: sums / counts persist across iterations (local statistics);
+  // with prev_labels (the previous iteration's labels, a separate buffer) only the moved rows
+  // are accumulated, otherwise the statistics are recounted from zero
+  bool stats_persist = false;
+  const int32_t* prev_labels = nullptr;
+  int64_t* moved_rows = nullptr;  // host counter of the rows the delta accumulated
 };
 
 int& lean_variant_ref() {  // -1: by width (below)
@@ -473,14 +479,34 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
       kern::kmeans_exact_rows(b, grid, s);
     }
     if (req.accumulate) {
-      Buffer bins = ctx.alloc(kern::kmeans_bin_scratch_bytes(x.rows, g.k));
-      if (!kern::kmeans_accumulate_binned(x.data.data(), x.dtype == DType::BF16, x.rows,
-                                          static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
-                                          req.sums_too ? req.sums : nullptr, req.counts,
-                                          bins.data(), s))
-        kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
-                                static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
-                                req.sums_too ? req.sums : nullptr, req.counts, s);
+      // the pass buffers go first (config 5 keeps 208 GB of rows resident; stream-ordered reuse)
+      keys = Buffer();
+      xstate = Buffer();
+      dbuf = Buffer();
+      const size_t sbytes = kern::kmeans_bin_scratch_bytes(x.rows, g.k);
+      Buffer bins = ctx.alloc(sbytes);
+      bool done = false;
+      if (req.stats_persist && req.prev_labels && req.sums_too && req.sums) {
+        // delta: moved rows only (+x new, -x old); above a quarter of the rows moved the
+        // scratch is too small and the statistics are recounted
+        int64_t entries = 0;
+        done = kern::kmeans_accumulate_moved(
+            x.data.data(), x.dtype == DType::BF16, x.rows, static_cast<int>(x.ld), x.cols,
+            req.prev_labels, labels, g.k, req.scale, req.sums, req.counts, bins.data(), sbytes,
+            &entries, s);
+        if (req.moved_rows) *req.moved_rows += entries / 2;
+      }
+      if (!done) {
+        if (req.stats_persist)
+          OAP_HIP_CHECK(hipMemsetAsync(req.sums, 0, sizeof(u64) * size_t(g.k) * (x.cols + 1), s));
+        if (!kern::kmeans_accumulate_binned(x.data.data(), x.dtype == DType::BF16, x.rows,
+                                            static_cast<int>(x.ld), x.cols, labels, g.k,
+                                            req.scale, req.sums_too ? req.sums : nullptr,
+                                            req.counts, bins.data(), s))
+          kern::kmeans_accumulate(x.data.data(), x.dtype == DType::BF16, x.rows,
+                                  static_cast<int>(x.ld), x.cols, labels, g.k, req.scale,
+                                  req.sums_too ? req.sums : nullptr, req.counts, s);
+      }
     }
     return a.cost_slab ? 2 * grid : 0;
   }
@@ -1108,6 +1134,21 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
   // pruning: per-row bounds (+ labels) persist across iterations, finalize reports the drift
   const bool prune = p.prune && !p.precise && x.cols <= 128 && x.rows > 0 && !lean_chunked;
+  // chunked lean pass with delta accumulation: local statistics persist, the labels alternate
+  // between two buffers so the previous assignment is at hand (moved rows only)
+  const bool cdelta = lean_chunked && p.delta && x.rows > 0;
+  Buffer cloc_b, lab_prev_b;
+  int32_t* lab_prev = nullptr;
+  int64_t cmoved = 0;
+  if (cdelta) {
+    cloc_b = ctx.alloc(sizeof(u64) * (kd + k));
+    lab_prev_b = ctx.alloc(sizeof(int32_t) * x.rows);
+    lab_prev = lab_prev_b.as<int32_t>();
+    req.sums = cloc_b.as<u64>();
+    req.counts = cloc_b.as<u64>() + kd;
+    req.stats_persist = true;
+    req.moved_rows = &cmoved;
+  }
   Buffer bounds_b, drift_b, pruned_d, tiles_b;
   if (prune) {
     bounds_b = ctx.alloc(sizeof(float) * 2 * x.rows);
@@ -1252,10 +1293,19 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       last_scanned = scan_it_all;
       it_scanned[b] = scan_it_all;
       scan_iters += scan_it_all ? 1 : 0;
-      if (!delta_it)
+      if (!delta_it && !cdelta)  // (the chunked lean pass zeroes its own on a recount)
         OAP_HIP_CHECK(hipMemsetAsync(delta ? loc_b.data() : stats.data(), 0,
                                      sizeof(u64) * (kd + k), s));
       req.labels_valid = it > 0;
+      if (cdelta) {
+        if (req.fast1) {  // the chunked lean pass runs: it writes the other label buffer
+          std::swap(req.labels, lab_prev);
+          req.prev_labels = it > 0 ? lab_prev : nullptr;
+        } else {  // the general chunked path (adaptive tier off) accumulates from zero
+          req.prev_labels = nullptr;
+          OAP_HIP_CHECK(hipMemsetAsync(cloc_b.data(), 0, sizeof(u64) * (kd + k), s));
+        }
+      }
       if (scan_all && prune) {
         const bool next_may_scan = b < nb_it - 1
                                        ? delta_on && !probing
@@ -1291,6 +1341,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         req.tile_count = nullptr;
       }
       int nb = gpu_assign(ctx, x, g, req, s);
+      if (cdelta)
+        OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), cloc_b.data(), sizeof(u64) * (kd + k),
+                                     hipMemcpyDeviceToDevice, s));
       if (req.xnorm && !req.tile_list) xnorm_ready = true;
       if (delta) {
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
@@ -1456,7 +1509,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     u64 dr[2] = {0, 0};
     ctx.copy_to_host(dr, ldstat_b.data(), 2 * sizeof(u64), s);
     res.deferred_rows = static_cast<int64_t>(dr[0]);
-    res.moved_rows = static_cast<int64_t>(dr[1]);
+    res.moved_rows = static_cast<int64_t>(dr[1]) + cmoved;
   }
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);

@@ -213,6 +213,15 @@ void kmeans_accumulate(const void* x, bool xbf16, int64_t n, int ld, int d,
 // of its range).  scratch: kmeans_bin_scratch_bytes(n, k).  Returns false (nothing launched)
 // when the layout does not apply; the caller then uses kmeans_accumulate.
 size_t kmeans_bin_scratch_bytes(int64_t n, int k);
+// Delta accumulation of the rows whose label changed (old -> new): +x into the new cluster, -x
+// into the old one (fixed point: exactly the full recount's change).  *entries = entries it
+// needed (2 per moved row); returns false (nothing accumulated, the caller recounts) when they
+// exceed the scratch's capacity.  Synchronizes `s` once (reads that count).
+bool kmeans_accumulate_moved(const void* x, bool xbf16, int64_t n, int ld, int d,
+                             const int32_t* old_labels, const int32_t* new_labels, int k,
+                             const float* scale, unsigned long long* sums,
+                             unsigned long long* counts, void* scratch, size_t scratch_bytes,
+                             int64_t* entries, hipStream_t s);
 bool kmeans_accumulate_binned(const void* x, bool xbf16, int64_t n, int ld, int d,
                               const int32_t* labels, int k, const float* scale,
                               unsigned long long* sums, unsigned long long* counts, void* scratch,
