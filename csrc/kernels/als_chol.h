@@ -18,13 +18,21 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // CU.  Occupancy beats bank conflicts here: 20-float (conflict-free) rows fit only 4 rows per CU
 // and ran 15% slower (0.200 vs 0.173 s/iter, 50M ratings, rank 100).
 constexpr int kBS = 16, kBlkF = 16 * kBS + 4;
+// RS: float stride of a block row.  16 packs tightest (the direct r x r solve is LDS-bound: 5
+// rows per CU); 20 makes the lane-per-row float4 accesses conflict-free (rows 80 B apart land on
+// distinct 4-bank groups) where occupancy is bound by registers anyway (the low-rank solve).
+template <int RS>
+constexpr int blk_floats() {
+  return 16 * RS + 4;
+}
+template <int RS = kBS>
 __device__ inline int mi(int i, int j) {
   const int bi = i >> 4, bj = j >> 4;
-  return (bi * (bi + 1) / 2 + bj) * kBlkF + (i & 15) * kBS + (j & 15);
+  return (bi * (bi + 1) / 2 + bj) * blk_floats<RS>() + (i & 15) * RS + (j & 15);
 }
-template <int NB>
+template <int NB, int RS = kBS>
 constexpr int packed_floats() {
-  return NB * (NB + 1) / 2 * kBlkF;
+  return NB * (NB + 1) / 2 * blk_floats<RS>();
 }
 
 // Right-looking blocked Cholesky, 16-wide panels: the diagonal block in registers (lane-per-row,
@@ -41,7 +49,7 @@ __device__ inline int fresh_lane() {
   return lane;
 }
 
-template <int NB>
+template <int NB, int RS = kBS>
 __device__ inline bool chol_factor(float* M, int first = 0) {
   constexpr int RP = 16 * NB;
   const int lane = fresh_lane();
@@ -53,7 +61,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
       const int rl = lane & 15;
 #pragma unroll
       for (int m = 0; m < 16; m += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + rl, o + m)]);
+        const float4 v = *reinterpret_cast<const float4*>(&M[mi<RS>(o + rl, o + m)]);
         t[m] = v.x;
         t[m + 1] = v.y;
         t[m + 2] = v.z;
@@ -78,7 +86,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
     if (lane < 16) {
 #pragma unroll
       for (int m = 0; m < 16; m += 4)
-        *reinterpret_cast<float4*>(&M[mi(o + lane, o + m)]) =
+        *reinterpret_cast<float4*>(&M[mi<RS>(o + lane, o + m)]) =
             make_float4(t[m], t[m + 1], t[m + 2], t[m + 3]);
     }
     __syncthreads();
@@ -88,7 +96,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
       float x[16];
 #pragma unroll
       for (int m = 0; m < 16; m += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
+        const float4 v = *reinterpret_cast<const float4*>(&M[mi<RS>(i, o + m)]);
         x[m] = v.x;
         x[m + 1] = v.y;
         x[m + 2] = v.z;
@@ -99,7 +107,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
         float lrow[16];
 #pragma unroll
         for (int m = 0; m < 16; m += 4) {
-          const float4 v = *reinterpret_cast<const float4*>(&M[mi(o + cc, o + m)]);
+          const float4 v = *reinterpret_cast<const float4*>(&M[mi<RS>(o + cc, o + m)]);
           lrow[m] = v.x;
           lrow[m + 1] = v.y;
           lrow[m + 2] = v.z;
@@ -112,7 +120,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
       }
 #pragma unroll
       for (int m = 0; m < 16; m += 4)
-        *reinterpret_cast<float4*>(&M[mi(i, o + m)]) =
+        *reinterpret_cast<float4*>(&M[mi<RS>(i, o + m)]) =
             make_float4(x[m], x[m + 1], x[m + 2], x[m + 3]);
     }
     __syncthreads();
@@ -122,18 +130,18 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
       for (int ib = jb + 1; ib < NB; ++ib) {
         float pa[4];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[mi(16 * ib + c, o + 4 * s4 + kk)];
+        for (int s4 = 0; s4 < 4; ++s4) pa[s4] = -M[mi<RS>(16 * ib + c, o + 4 * s4 + kk)];
         for (int kb = jb + 1; kb <= ib; ++kb) {
           f4 cacc;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) cacc[e] = M[mi(16 * ib + 4 * kk + e, 16 * kb + c)];
+          for (int e = 0; e < 4; ++e) cacc[e] = M[mi<RS>(16 * ib + 4 * kk + e, 16 * kb + c)];
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4) {
-            const float pb = M[mi(16 * kb + c, o + 4 * s4 + kk)];
+            const float pb = M[mi<RS>(16 * kb + c, o + 4 * s4 + kk)];
             cacc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[s4], pb, cacc, 0, 0, 0);
           }
 #pragma unroll
-          for (int e = 0; e < 4; ++e) M[mi(16 * ib + 4 * kk + e, 16 * kb + c)] = cacc[e];
+          for (int e = 0; e < 4; ++e) M[mi<RS>(16 * ib + 4 * kk + e, 16 * kb + c)] = cacc[e];
         }
       }
     }
@@ -147,7 +155,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
 // registers (16 sequential steps, readlane broadcasts) and the off-diagonal part is one
 // lane-parallel update — instead of r sequential LDS round trips per direction.  `bv`: RP floats
 // of LDS scratch.  `nsolve` < NB skips blocks (timing ablation).
-template <int NB>
+template <int NB, int RS = kBS>
 __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v1,
                                   int nsolve = NB) {
   constexpr int RP = 16 * NB;
@@ -161,7 +169,7 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
     float t[16];
 #pragma unroll
     for (int m = 0; m < 16; m += 4) {
-      const float4 q = *reinterpret_cast<const float4*>(&M[mi(o + rr, o + m)]);
+      const float4 q = *reinterpret_cast<const float4*>(&M[mi<RS>(o + rr, o + m)]);
       t[m] = q.x;
       t[m + 1] = q.y;
       t[m + 2] = q.z;
@@ -188,7 +196,7 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
           float acc2 = 0.f;
 #pragma unroll
           for (int m = 0; m < 16; m += 4) {
-            const float4 q = *reinterpret_cast<const float4*>(&M[mi(i, o + m)]);
+            const float4 q = *reinterpret_cast<const float4*>(&M[mi<RS>(i, o + m)]);
             acc2 = fmaf(q.x, z[m], acc2);
             acc2 = fmaf(q.y, z[m + 1], acc2);
             acc2 = fmaf(q.z, z[m + 2], acc2);
@@ -213,7 +221,7 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
       __syncthreads();
       const int m = lane & 15, g = lane >> 4;
       float part = 0.f;
-      for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[mi(i, o + m)], bv[i], part);
+      for (int i = o + 16 + g; i < RP; i += 4) part = fmaf(M[mi<RS>(i, o + m)], bv[i], part);
       part += __shfl_xor(part, 16, 64);
       part += __shfl_xor(part, 32, 64);
       const float sub = __shfl(part, (lane - base) & 15, 64);
@@ -224,7 +232,7 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
     float c[16];
     const int cp = mine ? rl : 0;
 #pragma unroll
-    for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi(o + mm, o + cp)];
+    for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi<RS>(o + mm, o + cp)];
 #pragma unroll
     for (int j = 15; j >= 0; --j) {
       const float xl = vd * __builtin_amdgcn_rcpf(c[j]);  // meaningful at lane base + j

@@ -36,6 +36,7 @@ namespace kern {
 namespace {
 
 using als::f4;
+constexpr int kRS = 20;  // conflict-free block rows (als_chol.h): occupancy is register-bound here
 
 struct LowRankArgs {
   const int64_t* rowptr;
@@ -72,7 +73,7 @@ template <int NBR, int NBN, bool KEEPW>
 __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* M = lds;                                 // n x n, packed lower blocks
-  float* bv = lds + als::packed_floats<NBN>();    // 64 floats (the backward solve stages 64 lanes)
+  float* bv = lds + als::packed_floats<NBN, kRS>();  // 64 floats (the backward solve: 64 lanes)
   float* gs = bv + 64;                            // 16 NBR floats: g while W is not resident
   float* dhs = gs + 16 * NBR;                     // 16 NBR floats: D^{-1/2}
   const int ld = a.ld;
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int ii = 16 * bi + 4 * kk + e, jj = 16 * bj + c;
-          M[als::mi(ii, jj)] = si[e] * sj * acc[e] + (ii == jj ? 1.f : 0.f);
+          M[als::mi<kRS>(ii, jj)] = si[e] * sj * acc[e] + (ii == jj ? 1.f : 0.f);
         }
       }
     }
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
     }
     __syncthreads();
 
-    const bool spd = als::chol_factor<NBN>(M);
+    const bool spd = als::chol_factor<NBN, kRS>(M);
     float* out = a.out + q * ld;
     if (!spd || fail_d) {
       if (lane == 0) atomicAdd(a.fail, 1ull);
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
       continue;
     }
     float v1 = 0.f;
-    als::chol_solve<NBN>(M, bv, h, v1);
+    als::chol_solve<NBN, kRS>(M, bv, h, v1);
     const float ss = h * sc;  // S s, lane l = element l
 
     // x_q = D^{-1/2} (g - W^T S s) = D^{-1/2} (g - D^{-1/2} Yq_u^T S s): the factor rows again
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
 template <int NBR, int NBN>
 void launch_lowrank(const LowRankArgs& a, int num_cus, hipStream_t s) {
   constexpr bool kKeepW = NBN * NBR <= 21;  // above: spills at 2 waves per SIMD (reload instead)
-  constexpr size_t lds = (als::packed_floats<NBN>() + 64 + 32 * NBR) * sizeof(float);
+  constexpr size_t lds = (als::packed_floats<NBN, kRS>() + 64 + 32 * NBR) * sizeof(float);
   const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 512))));
   const int grid = int(std::min<int64_t>(a.nrows, int64_t(num_cus) * per_cu));
   hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN, kKeepW>), dim3(grid), dim3(64), lds, s, a);
