@@ -264,7 +264,9 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
 
 template <int NBR, int NBN>
 void launch_lowrank(const LowRankArgs& a, int num_cus, hipStream_t s) {
-  constexpr bool kKeepW = NBN * NBR <= 21;  // above: spills at 2 waves per SIMD (reload instead)
+  // reloading W (L2-resident rows) beats holding it: 0.670 vs 0.686 s/iter at 1B ratings (the
+  // held registers cost occupancy / spills where the reload costs little bandwidth)
+  constexpr bool kKeepW = false;
   constexpr size_t lds = (als::packed_floats<NBN, kRS>() + 64 + 32 * NBR) * sizeof(float);
   const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 512))));
   const int grid = int(std::min<int64_t>(a.nrows, int64_t(num_cus) * per_cu));
