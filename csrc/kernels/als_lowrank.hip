@@ -67,10 +67,8 @@ __device__ inline float xor_sum16(float v) {
   return v;
 }
 
-// KEEPW: W stays in registers through the Cholesky (no second gather of the factor rows) when
-// the register budget allows it; otherwise the rows are re-read for W^T S s.
-template <int NBR, int NBN, bool KEEPW>
-__global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
+template <int NBR, int NBN>
+__global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRankArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* M = lds;                                 // n x n, packed lower blocks
   float* bv = lds + als::packed_floats<NBN, kRS>();  // 64 floats (the backward solve: 64 lanes)
@@ -124,59 +122,93 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
     const bool fail_d = __ballot(!okd) != 0;
     __syncthreads();
     auto dh4 = [&](int qb) { return *reinterpret_cast<const float4*>(dhs + 16 * qb + 4 * kk); };
-    float W[NBN][NBR][4];
-    float g[NBR][4];
-    // W fragments (rotated factors scaled by D^{-1/2}) and g = W^T w
+    // W fragments (rotated factors scaled by D^{-1/2}), g = W^T w (to LDS), the M tiles and
+    // S W g, accumulated over two halves of the fragment columns: half of W in registers at a
+    // time keeps the kernel at 3 waves per SIMD
+    constexpr int NT = NBN * (NBN + 1) / 2;
+    constexpr int QH = (NBR + 1) / 2;
+    f4 macc[NT];
 #pragma unroll
-    for (int qb = 0; qb < NBR; ++qb)
+    for (int t = 0; t < NT; ++t) macc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    float hp[NBN];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) g[qb][e] = 0.f;
+    for (int bi = 0; bi < NBN; ++bi) hp[bi] = 0.f;
+    auto half = [&](auto q0c) {
+      constexpr int q0 = decltype(q0c)::value;
+      constexpr int QN = q0 == 0 ? QH : NBR - QH;
+      float W[NBN][QH][4];
+      float g[QH][4];
 #pragma unroll
-    for (int bi = 0; bi < NBN; ++bi) {
-      const int i = 16 * bi + c;
-      const int item = __shfl(it, i, 64);
-      const float w_i = __shfl(wb, i, 64);
-      const float* yrow = a.src + static_cast<int64_t>(item) * ld + 4 * kk;
-      float4 y[NBR];
+      for (int qb = 0; qb < QN; ++qb)
 #pragma unroll
-      for (int qb = 0; qb < NBR; ++qb) y[qb] = *reinterpret_cast<const float4*>(yrow + 16 * qb);
+        for (int e = 0; e < 4; ++e) g[qb][e] = 0.f;
 #pragma unroll
-      for (int qb = 0; qb < NBR; ++qb) {
-        const float yv[4] = {y[qb].x, y[qb].y, y[qb].z, y[qb].w};
-        const float4 d = dh4(qb);
-        const float dv[4] = {d.x, d.y, d.z, d.w};
+      for (int bi = 0; bi < NBN; ++bi) {
+        const int i = 16 * bi + c;
+        const int item = __shfl(it, i, 64);
+        const float w_i = __shfl(wb, i, 64);
+        const float* yrow = a.src + static_cast<int64_t>(item) * ld + 4 * kk + 16 * q0;
+        float4 y[QH];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          W[bi][qb][e] = yv[e] * dv[e];
-          g[qb][e] = fmaf(w_i, W[bi][qb][e], g[qb][e]);
+        for (int qb = 0; qb < QN; ++qb) y[qb] = *reinterpret_cast<const float4*>(yrow + 16 * qb);
+#pragma unroll
+        for (int qb = 0; qb < QN; ++qb) {
+          const float yv[4] = {y[qb].x, y[qb].y, y[qb].z, y[qb].w};
+          const float4 d = dh4(q0 + qb);
+          const float dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            W[bi][qb][e] = yv[e] * dv[e];
+            g[qb][e] = fmaf(w_i, W[bi][qb][e], g[qb][e]);
+          }
         }
       }
-    }
 #pragma unroll
-    for (int qb = 0; qb < NBR; ++qb)
+      for (int qb = 0; qb < QN; ++qb) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) g[qb][e] = xor_sum16(g[qb][e]);
+        for (int e = 0; e < 4; ++e) g[qb][e] = xor_sum16(g[qb][e]);
+        if (c == 0)  // g leaves the registers (read back at the end)
+          *reinterpret_cast<float4*>(gs + 16 * (q0 + qb) + 4 * kk) =
+              make_float4(g[qb][0], g[qb][1], g[qb][2], g[qb][3]);
+      }
+      int t = 0;
+#pragma unroll
+      for (int bi = 0; bi < NBN; ++bi)
+#pragma unroll
+        for (int bj = 0; bj <= bi; ++bj, ++t)
+#pragma unroll
+          for (int qb = 0; qb < QN; ++qb)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              macc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(W[bi][qb][e], W[bj][qb][e], macc[t],
+                                                             0, 0, 0);
+#pragma unroll
+      for (int bi = 0; bi < NBN; ++bi)
+#pragma unroll
+        for (int qb = 0; qb < QN; ++qb)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hp[bi] = fmaf(W[bi][qb][e], g[qb][e], hp[bi]);
+    };
+    half(std::integral_constant<int, 0>{});
+    if constexpr (NBR > QH) half(std::integral_constant<int, QH>{});
 
     // M = I + S W W^T S into LDS (tile (bi, bj): lane holds rows 16 bi + 4 kk + e, column
     // 16 bj + c)
+    {
+      int t = 0;
 #pragma unroll
-    for (int bi = 0; bi < NBN; ++bi) {
-      float si[4];
+      for (int bi = 0; bi < NBN; ++bi) {
+        float si[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) si[e] = __shfl(sc, 16 * bi + 4 * kk + e, 64);
+        for (int e = 0; e < 4; ++e) si[e] = __shfl(sc, 16 * bi + 4 * kk + e, 64);
 #pragma unroll
-      for (int bj = 0; bj <= bi; ++bj) {
-        f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+        for (int bj = 0; bj <= bi; ++bj, ++t) {
+          const float sj = __shfl(sc, 16 * bj + c, 64);
 #pragma unroll
-        for (int qb = 0; qb < NBR; ++qb)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(W[bi][qb][e], W[bj][qb][e], acc, 0, 0, 0);
-        const float sj = __shfl(sc, 16 * bj + c, 64);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int ii = 16 * bi + 4 * kk + e, jj = 16 * bj + c;
-          M[als::mi<kRS>(ii, jj)] = si[e] * sj * acc[e] + (ii == jj ? 1.f : 0.f);
+          for (int e = 0; e < 4; ++e) {
+            const int ii = 16 * bi + 4 * kk + e, jj = 16 * bj + c;
+            M[als::mi<kRS>(ii, jj)] = si[e] * sj * macc[t][e] + (ii == jj ? 1.f : 0.f);
+          }
         }
       }
     }
@@ -184,23 +216,12 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
     float h = 0.f;
 #pragma unroll
     for (int bi = 0; bi < NBN; ++bi) {
-      float part = 0.f;
-#pragma unroll
-      for (int qb = 0; qb < NBR; ++qb)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) part = fmaf(W[bi][qb][e], g[qb][e], part);
+      float part = hp[bi];
       part += __shfl_xor(part, 16, 64);
       part += __shfl_xor(part, 32, 64);
       if (bi == kk) h = part;
     }
     h *= sc;  // lane l: s_l
-    // W and g leave the registers for the Cholesky (W is re-read from L2 afterwards)
-    if (c == 0) {
-#pragma unroll
-      for (int qb = 0; qb < NBR; ++qb)
-        *reinterpret_cast<float4*>(gs + 16 * qb + 4 * kk) =
-            make_float4(g[qb][0], g[qb][1], g[qb][2], g[qb][3]);
-    }
     __syncthreads();
 
     const bool spd = als::chol_factor<NBN, kRS>(M);
@@ -226,22 +247,15 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
     for (int bi = 0; bi < NBN; ++bi) {
       const int i = 16 * bi + c;
       const float s_i = __shfl(ss, i, 64);
-      if constexpr (KEEPW) {
+      const int item = __shfl(it, i, 64);
+      const float* yrow = a.src + static_cast<int64_t>(item) * ld + 4 * kk;
 #pragma unroll
-        for (int qb = 0; qb < NBR; ++qb)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) t[qb][e] = fmaf(W[bi][qb][e], s_i, t[qb][e]);
-      } else {
-        const int item = __shfl(it, i, 64);
-        const float* yrow = a.src + static_cast<int64_t>(item) * ld + 4 * kk;
-#pragma unroll
-        for (int qb = 0; qb < NBR; ++qb) {
-          const float4 y = *reinterpret_cast<const float4*>(yrow + 16 * qb);
-          t[qb][0] = fmaf(y.x, s_i, t[qb][0]);
-          t[qb][1] = fmaf(y.y, s_i, t[qb][1]);
-          t[qb][2] = fmaf(y.z, s_i, t[qb][2]);
-          t[qb][3] = fmaf(y.w, s_i, t[qb][3]);
-        }
+      for (int qb = 0; qb < NBR; ++qb) {
+        const float4 y = *reinterpret_cast<const float4*>(yrow + 16 * qb);
+        t[qb][0] = fmaf(y.x, s_i, t[qb][0]);
+        t[qb][1] = fmaf(y.y, s_i, t[qb][1]);
+        t[qb][2] = fmaf(y.z, s_i, t[qb][2]);
+        t[qb][3] = fmaf(y.w, s_i, t[qb][3]);
       }
     }
 #pragma unroll
@@ -252,8 +266,7 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
       const float4 gq = *reinterpret_cast<const float4*>(gs + 16 * qb + 4 * kk);
       const float gv[4] = {gq.x, gq.y, gq.z, gq.w};
 #pragma unroll
-      for (int e = 0; e < 4; ++e)  // KEEPW: t already carries D^{-1/2} (W = Yq_u D^{-1/2})
-        xv[e] = dv[e] * (gv[e] - (KEEPW ? 1.f : dv[e]) * xor_sum16(t[qb][e]));
+      for (int e = 0; e < 4; ++e) xv[e] = dv[e] * (gv[e] - dv[e] * xor_sum16(t[qb][e]));
       if (c == 0)
         *reinterpret_cast<float4*>(out + 16 * qb + 4 * kk) =
             make_float4(xv[0], xv[1], xv[2], xv[3]);
@@ -264,13 +277,10 @@ __global__ __launch_bounds__(64, 2) void oap_als_lowrank(LowRankArgs a) {
 
 template <int NBR, int NBN>
 void launch_lowrank(const LowRankArgs& a, int num_cus, hipStream_t s) {
-  // reloading W (L2-resident rows) beats holding it: 0.670 vs 0.686 s/iter at 1B ratings (the
-  // held registers cost occupancy / spills where the reload costs little bandwidth)
-  constexpr bool kKeepW = false;
   constexpr size_t lds = (als::packed_floats<NBN, kRS>() + 64 + 32 * NBR) * sizeof(float);
   const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 512))));
   const int grid = int(std::min<int64_t>(a.nrows, int64_t(num_cus) * per_cu));
-  hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN, kKeepW>), dim3(grid), dim3(64), lds, s, a);
+  hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN>), dim3(grid), dim3(64), lds, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
