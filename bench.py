@@ -89,8 +89,12 @@ def bench_kmeans(args, w):
     ingest_s = time.time() - t_ing
     # initial centers: k-means|| (identical for any world size), untimed
     t0 = time.time()
+    w.ctx.reset_metrics()
     init = N.kmeans_init(w.ctx, w.comm, table, k, "k-means||", 2, 7)
     init_s = time.time() - t0
+    init_phases = {name.split("/")[-1]: round(v["total_us"] / 1e3, 2)
+                   for name, v in w.ctx.metrics()["phases"].items()
+                   if name.startswith("kmeans/init/")}
     # warmup iterations (same fit from the same init; results discarded)
     if args.warmup > 0:
         N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, -1.0, precise=args.precise,
@@ -133,7 +137,8 @@ def bench_kmeans(args, w):
                 "rigorous error bound; rows inside it re-decided by the exact fp32 MFMA argmin "
                 "(assignments identical to exact fp32); delta accumulation of moved rows")
     extra = {"fit_wall_s_end_to_end": fit_s, "fit_iters": fit_iters,
-             "init_kmeans_parallel_s": init_s, "ingest_synth_s": ingest_s,
+             "init_kmeans_parallel_s": init_s, "init_phases_ms": init_phases,
+             "ingest_synth_s": ingest_s,
              "data_sigma": args.sigma, "data_box": args.box,
              # centers still move at the last timed step (Lloyd not converged)
              "max_center_shift_last": r["shift_history"][-1],
