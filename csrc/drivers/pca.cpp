@@ -72,7 +72,8 @@ void cpu_stats(Context& ctx, const DenseTable& x, const std::vector<double>& shi
 
 }  // namespace
 
-PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p) {
+PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p,
+                             bool device_cov) {
   TraceRange tr(&ctx.metrics(), "pca/covariance");
   const int d = x.cols;
   OAP_CHECK(d > 0, "PCA needs at least one feature");
@@ -109,7 +110,14 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
     comm_allreduce(ctx, comm, out.data(), cnt, DType::F64, ReduceOp::Sum, s);
     if (comm.on_device()) comm.wait(s);
     e2.record(s);
-    ctx.copy_to_host(stats.data(), out.data(), cnt * sizeof(double));
+    if (device_cov) {  // the covariance stays on the device; only c comes back (the mean)
+      res.dev_cov = ctx.alloc(sizeof(double) * size_t(d) * d);
+      kern::pca_cov(out.as<double>(), d, res.n, res.dev_cov.as<double>(), s);
+      ctx.copy_to_host(stats.data() + size_t(d) * d, out.as<double>() + size_t(d) * d,
+                       size_t(d) * sizeof(double));
+    } else {
+      ctx.copy_to_host(stats.data(), out.data(), cnt * sizeof(double));
+    }
     res.stats_ms = Event::elapsed_ms(e0, e1);
     res.allreduce_ms = Event::elapsed_ms(e1, e2);
     ctx.metrics().add("pca/syrk_kernel", res.stats_ms * 1e3,
@@ -128,13 +136,13 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
   const double n = double(res.n);
   const double* S = stats.data();
   const double* c = stats.data() + size_t(d) * d;
-  res.cov.resize(size_t(d) * d);
   res.mean.resize(d);
-  for (int i = 0; i < d; ++i) {
-    res.mean[i] = shift[i] + c[i] / n;
+  for (int i = 0; i < d; ++i) res.mean[i] = shift[i] + c[i] / n;
+  if (res.dev_cov.data()) return res;
+  res.cov.resize(size_t(d) * d);
+  for (int i = 0; i < d; ++i)
     for (int j = 0; j < d; ++j)
       res.cov[size_t(i) * d + j] = (S[size_t(i) * d + j] - c[i] * c[j] / n) / (n - 1.0);
-  }
   return res;
 }
 
@@ -142,7 +150,8 @@ PcaResult pca_fit(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p) {
   auto t0 = std::chrono::steady_clock::now();
   const int d = x.cols;
   OAP_CHECK(p.k >= 1 && p.k <= d, "PCA k must be in [1, numFeatures=" << d << "], got " << p.k);
-  PcaCovariance cv = pca_covariance(ctx, comm, x, p);
+  const bool gpu_eig = ctx.is_gpu() && p.gpu_eig && sym_eig_gpu_supported(ctx, d, p.k);
+  PcaCovariance cv = pca_covariance(ctx, comm, x, p, gpu_eig);
   PcaResult r;
   r.d = d;
   r.k = p.k;
@@ -154,12 +163,10 @@ PcaResult pca_fit(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p) {
   SymEig eg;
   {
     TraceRange tr(&ctx.metrics(), "pca/eigensolver");
-    if (p.gpu_eig && sym_eig_gpu_supported(ctx, d, p.k)) {
+    if (gpu_eig) {
       hipStream_t s = ctx.compute();
-      Buffer dcov = ctx.alloc(sizeof(double) * size_t(d) * d);
-      ctx.copy_to_backend(dcov.data(), cv.cov.data(), sizeof(double) * cv.cov.size(), s);
       GpuEigTiming t;
-      eg = sym_eig_topk_gpu(ctx, dcov.as<double>(), d, p.k, s, &t);
+      eg = sym_eig_topk_gpu(ctx, cv.dev_cov.as<double>(), d, p.k, s, &t);
       r.eig_on_gpu = true;
       r.eig_tridiag_ms = t.tridiag_ms;
       r.eig_host_ms = t.host_ms;

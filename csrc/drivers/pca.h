@@ -33,6 +33,9 @@ struct PcaCovariance {
   std::vector<double> mean;  // d
   double stats_ms = 0.0;     // local SYRK + reduce (device time on GPU)
   double allreduce_ms = 0.0;
+  // GPU engine with device_cov requested: `cov` stays empty and the covariance is here instead
+  // ([d][d] doubles on the device; the GPU eigensolver reads it without a host round trip)
+  Buffer dev_cov;
 };
 
 struct PcaResult {
@@ -47,7 +50,8 @@ struct PcaResult {
   double eig_tridiag_ms = 0.0, eig_host_ms = 0.0, eig_backtransform_ms = 0.0;
 };
 
-PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p);
+PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p,
+                             bool device_cov = false);
 PcaResult pca_fit(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p);
 
 }  // namespace oap

@@ -317,6 +317,8 @@ void als_init_factors(const int32_t* ids, int64_t n, int r, int ld, uint64_t see
                       hipStream_t s);
 void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
 
+// cov = (S - c c^T / n) / (n - 1) from pca_reduce's [S | c] output, on the device
+void pca_cov(const double* stats, int d, int64_t n, double* cov, hipStream_t s);
 // out: d x d symmetric (both triangles written), colsum: [d]
 void pca_reduce(const PcaPlan& p, const double* part, const double* cpart, int d, double* out,
                 double* colsum, hipStream_t s);

@@ -408,6 +408,20 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   }
 }
 
+// cov = (S - c c^T / n) / (n - 1) on the device (the host formula, operation for operation)
+__global__ void oap_pca_cov(const double* __restrict__ stats, int d, double n,
+                            double* __restrict__ cov) {
+  const double* S = stats;
+  const double* c = stats + size_t(d) * d;
+  const int64_t total = int64_t(d) * d;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    const int i = static_cast<int>(idx / d), j = static_cast<int>(idx - int64_t(i) * d);
+    const double q = c[i] * c[j];
+    cov[idx] = (S[idx] - q / n) / (n - 1.0);
+  }
+}
+
 __global__ void oap_pca_reduce(const double* __restrict__ part, const double* __restrict__ cpart,
                                int splits, int tiles, int nb, int d, int tw,
                                double* __restrict__ out, double* __restrict__ colsum) {
@@ -491,6 +505,13 @@ void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, 
   } else {
     hipLaunchKernelGGL(oap_pca_syrk<false>, dim3(p.grid), dim3(kSyrkThreads), 0, s, a);
   }
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void pca_cov(const double* stats, int d, int64_t n, double* cov, hipStream_t s) {
+  const int64_t total = int64_t(d) * d;
+  const int grid = static_cast<int>(std::min<int64_t>((total + 255) / 256, 4096));
+  hipLaunchKernelGGL(oap_pca_cov, dim3(grid), dim3(256), 0, s, stats, d, double(n), cov);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
