@@ -238,12 +238,13 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
 // 256 x 256 output tile per workgroup (d > 128): 8 waves in a 2 x 4 grid, each 128 x 64
 // (4 x 2 MFMA blocks, 128 accumulator registers).  Per staged row the tile does twice the MFMA
 // work of the 128-wide kernel, so the per-row staging VALU, the LDS writes, the barriers and the
-// L2 / HBM traffic per flop all halve.  16-row chunks, two LDS stages (96 KB): chunk c+1 is
+// L2 / HBM traffic per flop all halve.  32-row chunks, two LDS stages (160 KB): chunk c+1 is
 // converted into the other stage while chunk c feeds the MFMAs (one barrier per chunk), and the
 // rows of chunk c+2 are in flight in registers.
 constexpr int kTile2 = 256;
-constexpr int kChunk2 = 16;
-constexpr int kPS2 = kChunk2 + 8;        // 48 B per feature row: odd 16-byte slots
+constexpr int kChunk2 = 32;
+constexpr int kPS2 = kChunk2 + 8;        // 80 B per feature row: conflict-free b128 reads
+constexpr int kRpt2 = kChunk2 / 8;      // rows per loader thread
 constexpr int kPlane2 = kTile2 * kPS2;
 constexpr int kSyrk2Threads = 512;
 
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int wi = wave >> 2, wj = wave & 3;
-  // loader: rows 2*lg, 2*lg+1 of the chunk, features 4*lq .. 4*lq+3 of each side
+  // loader: rows kRpt2*lg .. kRpt2*lg+kRpt2-1 of the chunk, features 4*lq .. 4*lq+3 of each side
   const int lg = tid & 7, lq = tid >> 3;
   const int fi = ti * kTile2 + 4 * lq, fj = tj * kTile2 + 4 * lq;
   const bool okI = fi < a.ld, okJ = fj < a.ld;
@@ -272,26 +273,26 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   const float4 shI = *reinterpret_cast<const float4*>(a.shift + fi);
   const float4 shJ = *reinterpret_cast<const float4*>(a.shift + fj);
 
-  float4 vI[2], vJ[2];
+  float4 vI[kRpt2], vJ[kRpt2];
   double cs[4] = {0.0, 0.0, 0.0, 0.0};
   auto load = [&](int64_t r0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int64_t row = min(r0 + 2 * lg + i, r_end - 1);
+    for (int i = 0; i < kRpt2; ++i) {
+      const int64_t row = min(r0 + kRpt2 * lg + i, r_end - 1);
       const float* p = a.x + row * a.ld;
       vI[i] = *reinterpret_cast<const float4*>(p + fiL);
       if (!diag) vJ[i] = *reinterpret_cast<const float4*>(p + fjL);
     }
   };
-  auto stage = [&](__bf16* buf, int64_t r0, int side, const float4 (&v)[2], const float4 sh,
+  auto stage = [&](__bf16* buf, int64_t r0, int side, const float4 (&v)[kRpt2], const float4 sh,
                    bool sums) {
     __bf16* hi = buf + (2 * side) * kPlane2;
     __bf16* lo = hi + kPlane2;
     const bool okF = side == 0 ? okI : okJ;
-    float c[4][2];
+    float c[4][kRpt2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool ok = okF && r0 + 2 * lg + i < r_end;
+    for (int i = 0; i < kRpt2; ++i) {
+      const bool ok = okF && r0 + kRpt2 * lg + i < r_end;
       c[0][i] = ok ? v[i].x - sh.x : 0.f;
       c[1][i] = ok ? v[i].y - sh.y : 0.f;
       c[2][i] = ok ? v[i].z - sh.z : 0.f;
@@ -299,22 +300,27 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
     }
     if (sums) {
 #pragma unroll
-      for (int f = 0; f < 4; ++f) cs[f] += static_cast<double>(c[f][0] + c[f][1]);
+      for (int f = 0; f < 4; ++f) {
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < kRpt2; ++i) t += c[f][i];
+        cs[f] += static_cast<double>(t);
+      }
     }
 #pragma unroll
     for (int f = 0; f < 4; ++f) {
-      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-      bf16x2 ph, pl;
+      typedef __bf16 bf16xr __attribute__((ext_vector_type(kRpt2)));
+      bf16xr ph, pl;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < kRpt2; ++i) {
         __bf16 a_, b_;
         bf16_split(c[f][i], a_, b_);
         ph[i] = a_;
         pl[i] = b_;
       }
-      const int off = (4 * lq + f) * kPS2 + 2 * lg;
-      *reinterpret_cast<bf16x2*>(hi + off) = ph;
-      *reinterpret_cast<bf16x2*>(lo + off) = pl;
+      const int off = (4 * lq + f) * kPS2 + kRpt2 * lg;
+      *reinterpret_cast<bf16xr*>(hi + off) = ph;
+      *reinterpret_cast<bf16xr*>(lo + off) = pl;
     }
   };
 
@@ -361,27 +367,31 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   }
   for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk2) {
     const __bf16* buf = lds + cur * (4 * kPlane2);
-    bf16x8 ah[4], al[4], bh[2], bl[2];
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      ah[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + 32 * x * kPS2);
-      al[x] = *reinterpret_cast<const bf16x8*>(buf + kPlane2 + aoff + 32 * x * kPS2);
-    }
+    for (int ks = 0; ks < kChunk2 / 16; ++ks) {
+      bf16x8 ah[4], al[4], bh[2], bl[2];
 #pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      bh[y] = *reinterpret_cast<const bf16x8*>(buf + boff + 32 * y * kPS2);
-      bl[y] = *reinterpret_cast<const bf16x8*>(buf + kPlane2 + boff + 32 * y * kPS2);
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x)
+      for (int x = 0; x < 4; ++x) {
+        ah[x] = *reinterpret_cast<const bf16x8*>(buf + aoff + 32 * x * kPS2 + 16 * ks);
+        al[x] = *reinterpret_cast<const bf16x8*>(buf + kPlane2 + aoff + 32 * x * kPS2 + 16 * ks);
+      }
 #pragma unroll
       for (int y = 0; y < 2; ++y) {
-        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
-        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bl[y], acc[x][y], 0, 0, 0);
-        acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bh[y], acc[x][y], 0, 0, 0);
-        if (FOUR)
-          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
+        bh[y] = *reinterpret_cast<const bf16x8*>(buf + boff + 32 * y * kPS2 + 16 * ks);
+        bl[y] = *reinterpret_cast<const bf16x8*>(buf + kPlane2 + boff + 32 * y * kPS2 + 16 * ks);
       }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bh[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[x], bl[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bh[y], acc[x][y], 0, 0, 0);
+          if (FOUR)
+            acc[x][y] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[x], bl[y], acc[x][y], 0, 0, 0);
+        }
+    }
     if (r0 + kChunk2 < r_end) {  // the other stage was last read before the previous barrier
       __bf16* nb = lds + (cur ^ 1) * (4 * kPlane2);
       stage(nb, r0 + kChunk2, 0, vI, shI, diag);
