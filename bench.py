@@ -221,6 +221,9 @@ def main(argv=None):
                     help="skip the well-separated (sigma=1) reference run")
     ap.add_argument("--precise", action="store_true",
                     help="exact-fp32 MFMA distances only (no bf16-split fast path)")
+    ap.add_argument("--force-rccl", action="store_true",
+                    help="N=1: form a real 1-rank RCCL communicator (the multi-GPU device "
+                    "collective path) instead of the no-op local comm")
     args = ap.parse_args(argv)
     preset = {"kmeans": (100_000_000, 50, 200, "f32"),
               "kmeans_bf16": (1_000_000_000, 100, 1000, "bf16")}[args.config]
@@ -246,7 +249,7 @@ def main(argv=None):
     import oap_mllib_amd as O
 
     dev = os.environ.get("OAP_BENCH_DEVICE", "gpu")  # "cpu": CPU-engine rehearsal (tests)
-    w = O.init_world(O.get_config().replace(device=dev))
+    w = O.init_world(O.get_config().replace(device=dev, force_device_comm=args.force_rccl))
     out = bench_kmeans(args, w)
     if w.rank == 0:
         print(json.dumps(out), flush=True)

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--alpha", type=float, default=40.0)
     ap.add_argument("--reg", type=float, default=0.01)
+    ap.add_argument("--force-rccl", action="store_true",
+                    help="1 GPU: a real 1-rank RCCL communicator (device shuffle, comm-stream "
+                    "Gramian allreduce, chunked factor broadcasts) instead of the local comm")
     a = ap.parse_args()
     import numpy as np
 
@@ -30,7 +33,7 @@ def main():
     from oap_mllib_amd import _loader
 
     N = _loader.load()
-    w = O.init_world(O.get_config().replace(device="gpu"))
+    w = O.init_world(O.get_config().replace(device="gpu", force_device_comm=a.force_rccl))
     n_loc = a.ratings // w.size + (1 if w.rank < a.ratings % w.size else 0)
     t0 = time.time()
     rng = np.random.default_rng(1000 + w.rank)
@@ -58,7 +61,13 @@ def main():
             "extra": {"iter_ms": it_ms, "setup_s": out["setup_ms"] / 1e3,
                       "fit_wall_s": wall, "gram_ms_total": out["gram_ms"],
                       "solve_ms_total": out["solve_ms"], "comm_ms_total": out["comm_ms"],
-                      "failed_rows": out["failed_rows"], "datagen_s": gen_s}}))
+                      "failed_rows": out["failed_rows"], "datagen_s": gen_s,
+                      "comm": w.comm.name, "world_size": w.size,
+                      # factor exchange (chunked owner broadcasts on the comm stream)
+                      "factor_bcast_ms_total": out["bcast_ms"],
+                      "factor_bcast_recv_bytes": out["bcast_recv_bytes"],
+                      "factor_bcast_gbps": (out["bcast_recv_bytes"] / out["bcast_ms"] / 1e6
+                                            if out["bcast_ms"] > 0 else None)}}))
     O.shutdown_world()
 
 

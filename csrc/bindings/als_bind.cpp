@@ -75,6 +75,8 @@ void register_als(py::module_& m) {
         out["gram_ms"] = r.gram_ms;
         out["solve_ms"] = r.solve_ms;
         out["comm_ms"] = r.comm_ms;
+        out["bcast_ms"] = r.bcast_ms;
+        out["bcast_recv_bytes"] = r.bcast_recv_bytes;
         out["failed_rows"] = r.failed_rows;
         return out;
       },

@@ -255,7 +255,63 @@ PYBIND11_MODULE(_native, m) {
               c.wait(s);
             }
           },
-          py::arg("ctx"), py::arg("array"), py::arg("op") = "sum");
+          py::arg("ctx"), py::arg("array"), py::arg("op") = "sum")
+      .def_property_readonly("trivial", &Comm::trivial)
+      // ---- collectives on backend buffers (device memory for a GPU context), numpy in / out:
+      // they drive the same comm_* helpers the drivers use, so a 1-rank RCCL communicator runs
+      // its real device code (send/recv to self, grouped launches, watchdog waits) in tests
+      .def(
+          "exchange_f64",
+          [](Comm& c, std::shared_ptr<Context> ctx, const std::string& op,
+             py::array_t<double, py::array::c_style | py::array::forcecast> a,
+             std::vector<size_t> send_counts, std::vector<size_t> recv_counts, int root,
+             bool grouped) {
+            const size_t n = size_t(a.size());
+            const int P = c.size();
+            size_t out_n = n;
+            if (op == "allgather") out_n = n * P;
+            if (op == "alltoallv") {
+              OAP_CHECK(int(send_counts.size()) == P && int(recv_counts.size()) == P,
+                        "exchange_f64: counts need one entry per rank");
+              out_n = 0;
+              for (size_t v : recv_counts) out_n += v;
+            }
+            std::vector<double> hin(a.data(), a.data() + n), hout(std::max<size_t>(out_n, 1));
+            {
+              py::gil_scoped_release r;
+              ctx->activate();
+              hipStream_t s = ctx->is_gpu() ? ctx->compute() : nullptr;
+              Buffer din = ctx->alloc(std::max<size_t>(n, 1) * 8);
+              Buffer dout = ctx->alloc(std::max<size_t>(out_n, 1) * 8);
+              ctx->copy_to_backend(din.data(), hin.data(), n * 8, s);
+              RcclComm* rc = dynamic_cast<RcclComm*>(&c);
+              if (grouped && rc) rc->group_start();
+              if (op == "allreduce") {
+                comm_allreduce(*ctx, c, din.data(), n, DType::F64, ReduceOp::Sum, s);
+              } else if (op == "allreduce_max") {
+                comm_allreduce(*ctx, c, din.data(), n, DType::F64, ReduceOp::Max, s);
+              } else if (op == "allgather") {
+                comm_allgather(*ctx, c, din.data(), dout.data(), n, DType::F64, s);
+              } else if (op == "bcast") {
+                comm_bcast(*ctx, c, din.data(), n, DType::F64, root, s);
+              } else if (op == "alltoallv") {
+                comm_alltoallv(*ctx, c, din.data(), send_counts, dout.data(), recv_counts,
+                               DType::F64, s);
+              } else {
+                OAP_THROW(ConfigError, "exchange_f64: unknown op " << op);
+              }
+              if (grouped && rc) rc->group_end();
+              if (ctx->is_gpu()) c.wait(s);  // watchdog wait (RcclComm) / stream sync
+              const bool in_place = op == "allreduce" || op == "allreduce_max" || op == "bcast";
+              ctx->copy_to_host(hout.data(), (in_place ? din : dout).data(), out_n * 8, s);
+            }
+            hout.resize(out_n);
+            return py::array_t<double>(py::ssize_t(out_n), hout.data());
+          },
+          py::arg("ctx"), py::arg("op"), py::arg("array"),
+          py::arg("send_counts") = std::vector<size_t>{},
+          py::arg("recv_counts") = std::vector<size_t>{}, py::arg("root") = 0,
+          py::arg("grouped") = false);
   py::class_<LocalComm, Comm, std::shared_ptr<LocalComm>>(m, "LocalComm")
       .def(py::init<bool>(), py::arg("device") = false);
   py::class_<RcclComm, Comm, std::shared_ptr<RcclComm>>(m, "RcclComm")

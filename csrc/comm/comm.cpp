@@ -206,7 +206,7 @@ bool need_stage(Context& ctx, Comm& comm) { return ctx.is_gpu() && !comm.on_devi
 
 void comm_allreduce(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, ReduceOp op,
                     hipStream_t s) {
-  if (comm.size() == 1 || count == 0) return;
+  if (comm.trivial() || count == 0) return;
   if (!need_stage(ctx, comm)) {
     comm.allreduce(buf, count, dt, op, s);
     return;
@@ -256,7 +256,7 @@ void comm_alltoallv(Context& ctx, Comm& comm, const void* send,
 
 void comm_bcast(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, int root,
                 hipStream_t s) {
-  if (comm.size() == 1 || count == 0) return;
+  if (comm.trivial() || count == 0) return;
   if (!need_stage(ctx, comm)) {
     comm.bcast(buf, count, dt, root, s);
     return;
@@ -272,7 +272,7 @@ void comm_bcast(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, int
 
 void comm_allreduce_host(Context& ctx, Comm& comm, void* host, size_t count, DType dt,
                          ReduceOp op) {
-  if (comm.size() == 1 || count == 0) return;
+  if (comm.trivial() || count == 0) return;
   if (!comm.on_device()) {
     comm.allreduce(host, count, dt, op, nullptr);
     return;
@@ -293,7 +293,7 @@ void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
   size_t sn = 0, rn = 0;
   for (auto c : send_counts) sn += c;
   for (auto c : recv_counts) rn += c;
-  if (comm.size() == 1) {
+  if (comm.trivial()) {
     OAP_CHECK(sn == rn, "alltoallv: world of one with mismatched counts");
     if (sn) std::memmove(recv, send, sn * es);
     return;
@@ -312,7 +312,7 @@ void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
 }
 
 double comm_allreduce_scalar(Context& ctx, Comm& comm, double v, ReduceOp op) {
-  if (comm.size() == 1) return v;
+  if (comm.trivial()) return v;
   if (comm.on_device()) {
     Buffer d = ctx.alloc(sizeof(double));
     hipStream_t s = ctx.comm_stream();
@@ -328,7 +328,7 @@ double comm_allreduce_scalar(Context& ctx, Comm& comm, double v, ReduceOp op) {
 
 std::vector<int64_t> comm_allgather_i64(Context& ctx, Comm& comm, int64_t v) {
   std::vector<int64_t> out(comm.size(), v);
-  if (comm.size() == 1) return out;
+  if (comm.trivial()) return out;
   if (comm.on_device()) {
     Buffer d = ctx.alloc(sizeof(int64_t) * (comm.size() + 1));
     hipStream_t s = ctx.comm_stream();

@@ -30,6 +30,11 @@ class Comm {
   virtual int size() const = 0;
   virtual bool on_device() const = 0;  // true => buffers must be device pointers
   virtual const char* name() const = 0;
+  // True when every collective is a no-op (a world of one without a real communicator): the
+  // drivers then skip their exchange steps.  An RCCL communicator of one rank is NOT trivial —
+  // it runs every collective (send/recv to self, 1-rank allreduce / broadcast), which is how a
+  // 1-GPU box exercises the device-collective code paths of the multi-GPU drivers.
+  virtual bool trivial() const { return size() == 1; }
 
   // In-place allreduce.
   virtual void allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t s) = 0;
@@ -77,6 +82,7 @@ class RcclComm final : public Comm {
   int size() const override { return world_; }
   bool on_device() const override { return true; }
   const char* name() const override { return "rccl"; }
+  bool trivial() const override { return false; }
   void allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t s) override;
   void allgather(const void* send, void* recv, size_t count, DType dt, hipStream_t s) override;
   void alltoallv(const void* send, const std::vector<size_t>& send_counts, void* recv,

@@ -35,7 +35,7 @@ int owner_of(int32_t id, int P) { return int(((int64_t(id) % P) + P) % P); }
 std::vector<int64_t> allgather_i64(Context& ctx, Comm& comm, const std::vector<int64_t>& mine) {
   const int P = comm.size();
   std::vector<int64_t> all(mine.size() * P);
-  if (P == 1) {
+  if (comm.trivial()) {
     std::copy(mine.begin(), mine.end(), all.begin());
     return all;
   }
@@ -57,7 +57,7 @@ std::vector<int64_t> allgather_i64(Context& ctx, Comm& comm, const std::vector<i
 // rank order.
 std::vector<Rec> exchange(Context& ctx, Comm& comm, std::vector<std::vector<Rec>>& out) {
   const int P = comm.size(), me = comm.rank();
-  if (P == 1) return std::move(out[0]);
+  if (comm.trivial()) return std::move(out[0]);
   std::vector<int64_t> mine(P);
   for (int p = 0; p < P; ++p) mine[p] = int64_t(out[p].size());
   const std::vector<int64_t> all = allgather_i64(ctx, comm, mine);
@@ -96,7 +96,7 @@ std::vector<Rec> exchange(Context& ctx, Comm& comm, std::vector<std::vector<Rec>
 std::vector<int32_t> allgatherv_i32(Context& ctx, Comm& comm, const std::vector<int32_t>& mine,
                                     const std::vector<int64_t>& counts) {
   const int P = comm.size();
-  if (P == 1) return mine;
+  if (comm.trivial()) return mine;
   int64_t mx = 1;
   for (int64_t c : counts) mx = std::max(mx, c);
   std::vector<int64_t> pad(mx, 0);
@@ -305,41 +305,68 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   OAP_CHECK(p.rank >= 1, "ALS rank must be >= 1");
   OAP_CHECK(p.max_iter >= 0, "ALS maxIter must be >= 0");
   const int P = comm.size(), me = comm.rank();
+  // a trivial comm (world of one, no communicator) skips every exchange; any other comm — a
+  // 1-rank RCCL communicator included — runs the multi-rank code path end to end
+  const bool local = comm.trivial();
   const int r = p.rank, ld = int(round_up(size_t(r), 16));
   AlsResult res;
   res.rank = r;
   auto t_setup = std::chrono::steady_clock::now();
 
   Side U, I;
-  // ---- single rank on a GPU: re-indexing and both CSRs on the device (kernels/als_setup.hip)
+  // ---- on a GPU: re-indexing, the ratings shuffle and both CSRs on the device
+  // (kernels/als_setup.hip); OAP_ALS_HOST_SETUP=1 forces the host setup below
   kern::AlsDeviceSetup dev_setup;
+  kern::AlsDistSetup dist_setup;
   bool on_device = false;
-  if (P == 1 && ctx.is_gpu() && !std::getenv("OAP_ALS_HOST_SETUP")) {
+  kern::AlsDeviceCsr *dev_ucsr = nullptr, *dev_icsr = nullptr;
+  if (ctx.is_gpu() && !std::getenv("OAP_ALS_HOST_SETUP")) {
     ctx.activate();
-    on_device = kern::als_device_setup(ctx, users, items, ratings, n, ctx.compute(), &dev_setup);
+    if (local)
+      on_device = kern::als_device_setup(ctx, users, items, ratings, n, ctx.compute(), &dev_setup);
+    else
+      on_device = kern::als_device_setup_dist(ctx, comm, users, items, ratings, n, ctx.compute(),
+                                              &dist_setup);
   }
   if (on_device) {
-    auto fill = [](Side& S, std::vector<int32_t>& ids, kern::AlsDeviceCsr& c) {
-      S.n = c.nrows;
-      S.cnt = {c.nrows};
-      S.off = {0, c.nrows};
+    auto fill = [](Side& S, std::vector<int32_t>& ids, kern::AlsDeviceCsr& c,
+                   std::vector<int64_t> cnt, std::vector<int64_t> off) {
+      S.n = off.back();
+      S.cnt = std::move(cnt);
+      S.off = std::move(off);
       S.ids = std::move(ids);
       S.csr.ptr = c.ptr_h;  // (cols / values stay on the device)
     };
-    fill(U, dev_setup.user_ids, dev_setup.users);
-    fill(I, dev_setup.item_ids, dev_setup.items);
-    res.nnz = n;
+    if (local) {
+      const int64_t nu = dev_setup.users.nrows, ni = dev_setup.items.nrows;
+      fill(U, dev_setup.user_ids, dev_setup.users, {nu}, {0, nu});
+      fill(I, dev_setup.item_ids, dev_setup.items, {ni}, {0, ni});
+      dev_ucsr = &dev_setup.users;
+      dev_icsr = &dev_setup.items;
+      res.nnz = n;
+    } else {
+      fill(U, dist_setup.user_ids, dist_setup.users, dist_setup.ucnt, dist_setup.uoff);
+      fill(I, dist_setup.item_ids, dist_setup.items, dist_setup.icnt, dist_setup.ioff);
+      dev_ucsr = &dist_setup.users;
+      dev_icsr = &dist_setup.items;
+      res.nnz = dist_setup.nnz;
+    }
     res.setup_ms = ms_since(t_setup);
     ctx.metrics().add("als/setup", res.setup_ms * 1e3, n * int64_t(sizeof(Rec)) * 3);
-    if (Logger::instance().level() <= LogLevel::Info)
-      Logger::instance().log(LogLevel::Info, "als/device_setup",
-                             "\"upload_ms\":" + std::to_string(dev_setup.upload_ms) +
-                                 ",\"index_ms\":" + std::to_string(dev_setup.index_ms) +
-                                 ",\"sort_ms\":" + std::to_string(dev_setup.sort_ms));
+    if (Logger::instance().level() <= LogLevel::Info) {
+      const std::string det =
+          local ? "\"upload_ms\":" + std::to_string(dev_setup.upload_ms) +
+                      ",\"index_ms\":" + std::to_string(dev_setup.index_ms) +
+                      ",\"sort_ms\":" + std::to_string(dev_setup.sort_ms)
+                : "\"upload_ms\":" + std::to_string(dist_setup.upload_ms) +
+                      ",\"shuffle_ms\":" + std::to_string(dist_setup.shuffle_ms) +
+                      ",\"index_ms\":" + std::to_string(dist_setup.index_ms);
+      Logger::instance().log(LogLevel::Info, "als/device_setup", det);
+    }
   } else {
     // ---- 1. ratings -> item owners; dense item indices --------------------------------------
     std::vector<Rec> recv1;
-    if (P == 1) {
+    if (local) {
       recv1.resize(n);
       ctx.pool().parallel_for(n, [&](int, int64_t b, int64_t e) {
         for (int64_t k = b; k < e; ++k) recv1[k] = {users[k], items[k], ratings[k]};
@@ -359,7 +386,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     I.n = I.off[P];
     // ---- 2. -> user owners; dense user indices, user CSR (cols = global item index) ---------
     std::vector<Rec> recv2;
-    if (P == 1) {
+    if (local) {
       ctx.pool().parallel_for(int64_t(recv1.size()), [&](int, int64_t b, int64_t e) {
         for (int64_t k = b; k < e; ++k) recv1[k].b = int32_t(item_idx.rank(recv1[k].b));
       });
@@ -383,7 +410,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     });
     // ---- 3. (global user, global item) -> item owners: item CSR (cols = global user index) --
     std::vector<Rec> recv3;
-    if (P == 1) {
+    if (local) {
       recv3.resize(recv2.size());
       ctx.pool().parallel_for(int64_t(recv2.size()), [&](int, int64_t b, int64_t e) {
         for (int64_t k = b; k < e; ++k) recv3[k] = {recv2[k].b, recv2[k].a, recv2[k].r};
@@ -422,7 +449,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     // Multi-rank: each half solves its owned rows in C row-range chunks; chunk c of every rank
     // is broadcast (root = owner, straight into the replicated factor slab) on the comm stream
     // while chunk c+1 solves on the compute stream.
-    const int C = P > 1 ? 4 : 1;
+    const int C = local ? 1 : 4;
     // implicit rows with <= 64 ratings: low-rank (Woodbury) solve in the eigenbasis of Y^T Y
     // (kernels/als_lowrank.hip); OAP_ALS_LOWRANK=0 sends every row to the direct r x r solve
     const bool lowrank = [] {
@@ -543,8 +570,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       if (max_lr > 0) D.lr_scratch = ctx.alloc(size_t(max_lr) * ld * 4);
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
-    upload_side(U, dU, on_device ? &dev_setup.users : nullptr);
-    upload_side(I, dI, on_device ? &dev_setup.items : nullptr);
+    upload_side(U, dU, dev_ucsr);
+    upload_side(I, dI, dev_icsr);
     {  // initial user factors from their ids (world-size independent), or the caller's
       Buffer ids = ctx.alloc(std::max<size_t>(U.ids.size() * 4, 16));
       if (!U.ids.empty()) ctx.copy_to_backend(ids.data(), U.ids.data(), U.ids.size() * 4, s);
@@ -569,10 +596,11 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     Buffer zshift = ctx.alloc(size_t(ld + 128) * 4);
     ctx.memset(zshift.data(), 0, size_t(ld + 128) * 4);
     hipStream_t cs = ctx.comm_stream() ? ctx.comm_stream() : s;
-    const bool dev_comm = P > 1 && comm.on_device();
+    const bool dev_comm = !local && comm.on_device();
     struct HalfEvents {
       Event e0, e1, e2, e3;
       std::vector<Event> solved;  // per chunk (compute stream -> comm stream)
+      std::vector<Event> bc0, bc1;  // per chunk: its broadcasts on the comm stream
       Event gram_in, gram_out, gathered;
     };
     std::vector<HalfEvents> hev(2);
@@ -642,7 +670,11 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       a.dst = dD.f.as<float>() + Dst.off[me] * ld;  // owned rows, in place in the slab
       a.queue = ctr.as<unsigned long long>();
       a.fail = ctr.as<unsigned long long>() + 2;
-      if (int(E.solved.size()) != C) E.solved = std::vector<Event>(C);
+      if (int(E.solved.size()) != C) {
+        E.solved = std::vector<Event>(C);
+        E.bc0 = std::vector<Event>(C);
+        E.bc1 = std::vector<Event>(C);
+      }
       for (int c = 0; c < C; ++c) {
         a.short_rows = dD.short_rows.as<int32_t>() + dD.sr_off[c];
         a.n_short = dD.sr_off[c + 1] - dD.sr_off[c];
@@ -660,7 +692,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
           a.lr_scratch = dD.lr_scratch.as<float>();
         }
         kern::als_solve(a, cus, s);
-        if (P == 1) continue;
+        if (local) continue;
         // chunk c of every rank's rows -> every rank (root = owner; in place in the slab)
         auto bcast_chunk = [&](hipStream_t st) {
           if (comm.name() == std::string("rccl")) static_cast<RcclComm&>(comm).group_start();
@@ -675,7 +707,9 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         if (dev_comm) {
           E.solved[c].record(s);
           E.solved[c].wait_on(cs);
+          E.bc0[c].record(cs);
           bcast_chunk(cs);
+          E.bc1[c].record(cs);
         } else {
           bcast_chunk(s);
         }
@@ -701,11 +735,15 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       if (dev_comm) comm.wait(s);
       hev[1].e3.sync();
       for (HalfEvents& E : hev) {
+        if (dev_comm)
+          for (int c = 0; c < C; ++c) res.bcast_ms += Event::elapsed_ms(E.bc0[c], E.bc1[c]);
         res.gram_ms += Event::elapsed_ms(E.e0, E.e1);
         res.solve_ms += Event::elapsed_ms(E.e1, E.e2);
         res.comm_ms += Event::elapsed_ms(E.e2, E.e3);  // exposed (not overlapped) gather time
       }
       res.iter_ms.push_back(ms_since(t0));
+      if (!local)  // every rank's rows but its own, both halves
+        res.bcast_recv_bytes += (U.n - U.cnt[me] + I.n - I.cnt[me]) * int64_t(ld) * 4;
       maybe_inject_fault(me, "als_iter", it);
     }
     unsigned long long fails = 0;
@@ -791,7 +829,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       for (int64_t f : fail_part) fails += f;
       auto t2 = std::chrono::steady_clock::now();
       res.solve_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
-      if (P == 1) {
+      if (local) {
         std::copy(mine.begin(), mine.begin() + size_t(nloc) * ld, Fd.begin());
       } else {
         int64_t mx = 1;

@@ -45,6 +45,10 @@ struct AlsResult {
   double setup_ms = 0.0, train_ms = 0.0;
   std::vector<double> iter_ms;                    // per iteration (both halves)
   double solve_ms = 0.0, gram_ms = 0.0, comm_ms = 0.0;  // summed device/host phase times
+  // device comms: comm-stream time of the factor-chunk broadcasts (start -> end of each chunk's
+  // grouped broadcast, summed) and the bytes every rank received through them
+  double bcast_ms = 0.0;
+  int64_t bcast_recv_bytes = 0;
   int64_t failed_rows = 0;                        // rows whose system was not SPD
 };
 

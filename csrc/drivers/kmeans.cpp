@@ -42,7 +42,7 @@ void host_allreduce(Context& ctx, Comm& comm, void* host, size_t count, DType dt
 std::vector<double> host_allgatherv_rows(Context& ctx, Comm& comm, const std::vector<double>& mine,
                                          int cols) {
   int64_t my_rows = cols ? int64_t(mine.size()) / cols : 0;
-  if (comm.size() == 1) return mine;
+  if (comm.trivial()) return mine;
   auto counts = comm_allgather_i64(ctx, comm, my_rows);
   int64_t mx = 0;
   for (auto c : counts) mx = std::max(mx, c);
@@ -1364,7 +1364,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       else
         OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
       ev[b].e1.record(s);
-      if (comm.size() > 1) {
+      if (!comm.trivial()) {
         if (comm.on_device()) {
           if (rccl) rccl->group_start();
           comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
@@ -1434,7 +1434,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                     (0.25 * double(x.rows) * nb_it));
       tier2_seen = t2;
       if (ldstat_b.data()) deferred_seen = ldstat_h.as<u64>()[0];
-      if (comm.size() > 1) share = comm_allreduce_scalar(ctx, comm, share, ReduceOp::Max);
+      if (!comm.trivial()) share = comm_allreduce_scalar(ctx, comm, share, ReduceOp::Max);
       if (share > 1.0) {
         req.fast1 = false;
         Logger::instance().log(LogLevel::Info, "kmeans/tier1_off",
@@ -1492,7 +1492,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
       kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
     }
-    if (comm.size() > 1) {
+    if (!comm.trivial()) {
       comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
       if (comm.on_device()) comm.wait(s);  // the watchdog covers this collective too
     }
@@ -1701,7 +1701,7 @@ KMeansResult kmeans_fit_streamed(Context& ctx, Comm& comm, const float* host, in
       kern::sum_f64(costs.as<double>(), int(nchunks), cost_d.as<double>(), s);
     else
       OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
-    if (comm.size() > 1) {
+    if (!comm.trivial()) {
       comm_allreduce(ctx, comm, stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
       comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
       if (comm.on_device()) comm.wait(s);

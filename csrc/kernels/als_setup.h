@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <vector>
 
+#include "comm/comm.h"
 #include "runtime/context.h"
 
 namespace oap {
@@ -34,6 +35,22 @@ struct AlsDeviceSetup {
 // index (range > max(8 n, 2^26)): the caller falls back to the host setup.
 bool als_device_setup(Context& ctx, const int32_t* users, const int32_t* items,
                       const float* ratings, int64_t n, hipStream_t s, AlsDeviceSetup* out);
+
+// Multi-rank setup (any non-trivial comm; device buffers throughout).  Items are owned by
+// id mod P, users likewise; each side's dense global index is rank-major (rank q's owned ids,
+// ascending, at [off[q], off[q + 1])), exactly as the host setup in drivers/als.cpp orders them.
+struct AlsDistSetup {
+  std::vector<int64_t> ucnt, uoff, icnt, ioff;  // per-rank owned counts / global offsets
+  std::vector<int32_t> user_ids, item_ids;      // global index -> id (all ranks)
+  AlsDeviceCsr users, items;  // owned rows; cols = the other side's global index
+  int64_t nnz = 0;            // global rating count
+  double upload_ms = 0.0, shuffle_ms = 0.0, index_ms = 0.0;
+};
+
+// Collective: every rank of `comm` must call it.  Returns false on every rank (nothing built)
+// when a global id range is too sparse for the dense index (the caller uses the host setup).
+bool als_device_setup_dist(Context& ctx, Comm& comm, const int32_t* users, const int32_t* items,
+                           const float* ratings, int64_t n, hipStream_t s, AlsDistSetup* out);
 
 }  // namespace kern
 }  // namespace oap

@@ -188,7 +188,7 @@ std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t
       for (int c = 0; c < t.cols; ++c) mx[c] = std::max(mx[c], p[c]);
   }
   t.local_absmax = mx;
-  if (comm.size() > 1) {
+  if (!comm.trivial()) {
     if (comm.on_device() && ctx.is_gpu()) {
       Buffer d = ctx.alloc(sizeof(double) * t.cols);
       ctx.copy_to_backend(d.data(), mx.data(), sizeof(double) * t.cols, ctx.comm_stream());

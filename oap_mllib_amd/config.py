@@ -39,6 +39,10 @@ class Config:
     comm_timeout_s: float = 600.0
     #: use RCCL for GPU ranks (else host/gloo collectives staged through pinned memory)
     use_rccl: bool = True
+    #: a world of ONE GPU rank forms a real 1-rank RCCL communicator instead of the no-op local
+    #: comm, so every device-collective branch of the multi-GPU drivers (grouped allreduces,
+    #: comm-stream overlap, send/recv shuffles, chunked broadcasts) runs on a single GPU
+    force_device_comm: bool = False
     rendezvous_host: str = "127.0.0.1"
     rendezvous_port: int = 0
     #: PCA dispatch cap (the reference hard-codes numFeatures < 65535, PCA.scala:103)

@@ -143,8 +143,12 @@ def init_world(config: Config | None = None, rank: int | None = None,
         N = _loader.load()
         N.configure_logging(rank, device, cfg.log_level, cfg.log_file)
         w.ctx = N.Context(device, cfg.hbm_fraction, cfg.cpu_threads)
-        if size == 1:
+        if size == 1 and not (backend == "gpu" and cfg.force_device_comm):
             w.comm = N.LocalComm(backend == "gpu")
+        elif size == 1:  # forced 1-rank RCCL world (the device-collective paths on one GPU)
+            if not (cfg.use_rccl and N.rccl_available()):
+                raise RuntimeError("force_device_comm needs RCCL (use_rccl and librccl)")
+            w.comm = N.RcclComm(N.rccl_unique_id(), 1, 0, device, cfg.comm_timeout_s)
         elif backend == "gpu" and cfg.use_rccl and N.rccl_available():
             import torch.distributed as dist
 

@@ -74,3 +74,17 @@ def gpu_world():
                      local_rank=0)
     yield w
     O.shutdown_world()
+
+
+@pytest.fixture
+def rccl1_world():
+    """A world of one GPU rank with a REAL 1-rank RCCL communicator (force_device_comm): the
+    multi-GPU drivers' device-collective branches run on the single GPU of the box."""
+    import oap_mllib_amd as O
+
+    O.shutdown_world()
+    w = O.init_world(O.get_config().replace(device="gpu", device_id=0, force_device_comm=True),
+                     rank=0, size=1, local_rank=0)
+    assert w.comm.name == "rccl" and w.comm.size == 1 and not w.comm.trivial
+    yield w
+    O.shutdown_world()
