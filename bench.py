@@ -74,6 +74,34 @@ def _shard(args, w):
     return local, row0
 
 
+def _estimator_fit(args, w, N):
+    """The user-facing estimator end to end: ``KMeans(k, maxIter=20).fit(X)`` on this rank's
+    rows as a HOST numpy array (the same synthetic blobs, made on the device and copied down
+    untimed) — H2D ingestion, k-means|| init, Lloyd, and the summary pass (labels + clusterSizes)
+    are all inside the timed call.  The native fit of the same rows (already resident) is timed
+    alongside, so the estimator's overhead is visible."""
+    import oap_mllib_amd as O
+
+    rows_total, d, k = args.rows, args.dim, args.k
+    local, row0 = _shard(args, w)
+    t = N.synth_blobs(w.ctx, local, d, d, row0, k, args.box, args.sigma, 20240917, "f32")
+    X = t.download_f32(w.ctx) if w.is_gpu else t.to_numpy(w.ctx).astype(np.float32)
+    del t
+    _barrier_sync(w)
+    t0 = time.perf_counter()
+    m = O.KMeans(k=k, maxIter=20, seed=7).fit(X)
+    sizes = m.summary.clusterSizes
+    _barrier_sync(w)
+    est_s = float(w.allreduce_np(np.array([time.perf_counter() - t0]), "max")[0])
+    assert sum(sizes) == rows_total and m.fit_info["engine"] == w.backend, m.fit_info
+    fi = m.fit_info
+    return {"estimator_fit_wall_s": est_s, "fit_iters": m.summary.numIter,
+            "upload_s": fi.get("upload_seconds"), "init_s": fi.get("init_seconds"),
+            "lloyd_s": fi.get("iter_seconds"), "summary_pass_s": fi.get("summary_seconds"),
+            "host_rows_per_rank": int(local), "host_dtype": "float32",
+            "call": f"oap_mllib_amd.KMeans(k={k}, maxIter=20).fit(ndarray[{local}, {d}])"}
+
+
 def bench_kmeans(args, w):
     from oap_mllib_amd import _loader
 
@@ -181,6 +209,8 @@ def bench_kmeans(args, w):
             "ms_per_step": el2 / args.steps * 1e3, "pruned_frac": p2 / (tiles * args.steps),
             "max_center_shift_last": r2["shift_history"][-1]}
         del t2
+    if args.estimator:
+        extra["estimator"] = _estimator_fit(args, w, N)
     out = {
         "metric": "kmeans_samples_per_sec", "value": samples, "unit": "samples/s",
         "n_gpus": w.size, "steps": args.steps, "warmup": args.warmup,
@@ -221,6 +251,8 @@ def main(argv=None):
                     help="skip the well-separated (sigma=1) reference run")
     ap.add_argument("--precise", action="store_true",
                     help="exact-fp32 MFMA distances only (no bf16-split fast path)")
+    ap.add_argument("--no-estimator", dest="estimator", action="store_false",
+                    help="skip the user-facing KMeans(...).fit(host ndarray) timing")
     ap.add_argument("--force-rccl", action="store_true",
                     help="N=1: form a real 1-rank RCCL communicator (the multi-GPU device "
                     "collective path) instead of the no-op local comm")

@@ -349,6 +349,28 @@ PYBIND11_MODULE(_native, m) {
              return out;
            },
            py::arg("ctx"), py::arg("start") = 0, py::arg("count") = -1)
+      .def("download_f32",
+           [](DenseTable& t, std::shared_ptr<Context> ctx) {
+             // an f32 table's rows as a dense (rows, cols) float32 array (one pitched copy)
+             OAP_CHECK(t.dtype == DType::F32, "download_f32 needs an f32 table");
+             py::array_t<float> out({t.rows, int64_t(t.cols)});
+             float* dst = out.mutable_data();
+             {
+               py::gil_scoped_release r;
+               if (t.rows > 0 && ctx->is_gpu()) {
+                 ctx->activate();
+                 OAP_HIP_CHECK(hipMemcpy2D(dst, size_t(t.cols) * 4, t.data.data(), size_t(t.ld) * 4,
+                                           size_t(t.cols) * 4, size_t(t.rows),
+                                           hipMemcpyDeviceToHost));
+               } else {
+                 for (int64_t i = 0; i < t.rows; ++i)
+                   std::memcpy(dst + size_t(i) * t.cols, t.data.as<float>() + size_t(i) * t.ld,
+                               size_t(t.cols) * 4);
+               }
+             }
+             return out;
+           },
+           py::arg("ctx"))
       .def("set_global", [](DenseTable& t, int64_t off, int64_t tot) {
         t.global_offset = off;
         t.global_rows = tot;
@@ -579,6 +601,39 @@ PYBIND11_MODULE(_native, m) {
         }
         return py::make_tuple(labels, dist);
       });
+  // The estimator's summary pass (KMeans.scala:359-368, model.transform + clusterSizes): labels
+  // of the rows of an already-resident table (no re-upload, no per-row distances copied back)
+  // and the per-cluster counts, counted on the host pool.
+  m.def(
+      "kmeans_labels",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> centers) {
+        auto c = py::array_t<double, py::array::c_style | py::array::forcecast>(centers);
+        if (c.ndim() != 2 || c.shape(1) != t->cols)
+          throw ConfigError("centers must be k x d with d == table cols");
+        const int k = static_cast<int>(c.shape(0));
+        std::vector<double> cv(c.data(), c.data() + c.size());
+        py::array_t<int32_t> labels(t->rows);
+        py::array_t<int64_t> counts(k);
+        int32_t* lp = labels.mutable_data();
+        int64_t* cp = counts.mutable_data();
+        {
+          py::gil_scoped_release rel;
+          kmeans_predict(*ctx, *t, cv, k, lp, nullptr);
+          const int nt = ctx->pool().size();
+          std::vector<std::vector<int64_t>> part(nt);
+          ctx->pool().parallel_for(t->rows, [&](int ci, int64_t b, int64_t e) {
+            std::vector<int64_t>& h = part[ci];
+            h.assign(size_t(k), 0);
+            for (int64_t i = b; i < e; ++i)
+              if (lp[i] >= 0 && lp[i] < k) ++h[size_t(lp[i])];
+          });
+          std::fill(cp, cp + k, int64_t(0));
+          for (const auto& h : part)
+            for (size_t j = 0; j < h.size(); ++j) cp[j] += h[j];
+        }
+        return py::make_tuple(labels, counts);
+      },
+      py::arg("ctx"), py::arg("table"), py::arg("centers"));
   m.def("kmeans_set_lean_variant", &kmeans_set_lean_variant);
   m.def("kmeans_last_timing_deferred", []() { return last_timing_deferred(); });
   m.def(

@@ -56,25 +56,53 @@ class _KMeansParams:
 
 
 class KMeansSummary:
-    """Training summary (``ml.clustering.KMeansSummary``)."""
+    """Training summary (``ml.clustering.KMeansSummary``).
+
+    Spark builds it from ``model.transform(dataset)`` (KMeans.scala:359-368).  Here the fit hands
+    over the labels of the final model straight from the device pass over the still-resident
+    rows, and the counts it made (``clusterSizes``, global over the ranks); the ``predictions``
+    frame is only assembled when it is read, so a fit on 100M rows creates no per-row objects.
+    """
 
     def __init__(self, predictions, predictionCol: str, featuresCol: str, k: int,  # noqa: N803
-                 numIter: int, trainingCost: float):  # noqa: N803
-        self.predictions = predictions
+                 numIter: int, trainingCost: float, labels: np.ndarray | None = None,  # noqa: N803
+                 clusterSizes: list[int] | None = None):  # noqa: N803
+        self._predictions = predictions  # a frame, or a zero-argument builder of one
         self.predictionCol = predictionCol
         self.featuresCol = featuresCol
         self.k = k
         self.numIter = numIter
         self.trainingCost = trainingCost
+        self._labels = labels
+        self._sizes = clusterSizes
+
+    @property
+    def predictions(self):
+        if callable(self._predictions):
+            self._predictions = self._predictions()
+        return self._predictions
 
     @property
     def cluster(self):
+        if self._labels is not None:
+            import pandas as pd
+
+            return pd.DataFrame({self.predictionCol: self._labels})
         return self.predictions[[self.predictionCol]]
 
     @property
     def clusterSizes(self) -> list[int]:  # noqa: N802
-        lab = np.asarray(self.predictions[self.predictionCol].to_numpy(), dtype=np.int64)
+        if self._sizes is not None:
+            return list(self._sizes)
+        lab = (self._labels if self._labels is not None else
+               np.asarray(self.predictions[self.predictionCol].to_numpy(), dtype=np.int64))
         return np.bincount(lab, minlength=self.k)[: max(self.k, 0)].tolist()
+
+
+def _with_predictions(dataset, features_col: str, prediction_col: str, labels: np.ndarray):
+    df = as_frame(dataset, features_col)
+    df[prediction_col] = np.asarray(labels, dtype=np.int32)
+    return df
 
 
 class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
@@ -106,6 +134,7 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
             self.getOrDefault("tol")
         seed = self.getOrDefault("seed") & 0xFFFFFFFFFFFFFFFF
         t0 = time.time()
+        streamed = streamed_decision(w, X, engine)
         if engine == "vanilla":
             weights = None
             if self.isSet("weightCol") and self.getOrDefault("weightCol"):
@@ -119,13 +148,15 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
                             self.getOrDefault("distanceMeasure"), weights, None, allreduce)
             centers, cost, n_iter = r.centers, r.cost, r.num_iter
             extra = {"engine": "vanilla"}
-        elif engine == "gpu" and _streamed(w, X):
+        elif streamed:
             r, centers, cost, n_iter = self._fit_streamed(w, X, k, max_iter, tol, seed)
             extra = {"engine": engine, "streamed": True, "init_seconds": r["init_seconds"],
                      "iter_seconds": r["iter_seconds"], "global_rows": r["global_rows"]}
         else:
             N = _loader.load()
+            t_up = time.time()
             table = upload_table(w, X)
+            upload_s = time.time() - t_up
             ck = checkpoint.for_fit(w, self, X.shape)
             if ck is None:
                 r = N.kmeans_fit(w.ctx, w.comm, table, None, k, max_iter, tol,
@@ -135,17 +166,30 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
             else:
                 r, centers, cost, n_iter = self._fit_segmented(N, w, table, ck, k, max_iter, tol,
                                                                 seed)
+            # the summary pass (model.transform in KMeans.scala:359-368) over the SAME resident
+            # table: labels under the final centers + per-cluster counts, one device pass
+            t_lab = time.time()
+            labels, sizes = N.kmeans_labels(w.ctx, table, np.asarray(centers))
+            del table
             extra = {"engine": engine, "init_seconds": r["init_seconds"],
-                     "iter_seconds": r["iter_seconds"], "global_rows": r["global_rows"]}
+                     "iter_seconds": r["iter_seconds"], "global_rows": r["global_rows"],
+                     "upload_seconds": upload_s, "summary_seconds": time.time() - t_lab}
         model = KMeansModel(uid=self.uid, centers=np.asarray(centers), trainingCost=float(cost),
                             numIter=int(n_iter), distanceMeasure=self.getOrDefault(
                                 "distanceMeasure"))
         self._copyValues(model)
         model.setParent(self)
+        if "summary_seconds" not in extra:  # vanilla / streamed: predict in row chunks
+            labels, _ = model.predict_matrix(X)
+            labels = np.asarray(labels, dtype=np.int32)
+            sizes = np.bincount(labels, minlength=k)[:k]
+        if w.distributed:  # the summary covers the whole (distributed) dataset
+            sizes = w.allreduce_np(np.asarray(sizes, dtype=np.int64))
         model.fit_info = {"fit_seconds": time.time() - t0, **extra}
-        summary = KMeansSummary(model.transform(dataset), model.getOrDefault("predictionCol"),
-                                model.getOrDefault("featuresCol"), k, model.numIter,
-                                model.trainingCost)
+        fcol, pcol = model.getOrDefault("featuresCol"), model.getOrDefault("predictionCol")
+        summary = KMeansSummary(lambda: _with_predictions(dataset, fcol, pcol, labels), pcol, fcol,
+                                k, model.numIter, model.trainingCost, labels=labels,
+                                clusterSizes=[int(v) for v in np.asarray(sizes)[:k]])
         model.setSummary(summary)
         instr.logNamedValue("clusterSizes", summary.clusterSizes)
         instr.logNamedValue("engine", extra["engine"])
@@ -201,6 +245,18 @@ class KMeans(_KMeansParams, Estimator, DefaultParamsPersistence):
                 break
             k = centers.shape[0]
         return r, centers, cost, done
+
+
+def streamed_decision(w, X: np.ndarray, engine: str) -> bool:
+    """Whether this fit streams its rows from host memory — the same answer on every rank: the
+    streamed and resident fits issue different collective sequences, so one rank over its HBM
+    budget (uneven Spark partitions) makes every rank stream."""
+    if engine != "gpu":
+        return False
+    streamed = _streamed(w, X)
+    if w.distributed:
+        streamed = bool(w.allreduce_np(np.array([float(streamed)]), "max")[0] > 0)
+    return streamed
 
 
 def _streamed(w, X: np.ndarray) -> bool:

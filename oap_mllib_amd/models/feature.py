@@ -20,7 +20,7 @@ from typing import Any
 import numpy as np
 
 from .. import _loader
-from ..data import as_frame, to_matrix
+from ..data import as_frame, to_matrix, vector_column
 from ..fallback import pca_vanilla as vanilla
 from ..linalg import DenseMatrix, DenseVector
 from ..params import Param, gt, to_int, to_str
@@ -76,7 +76,7 @@ class PCA(_PCAParams, Estimator, DefaultParamsPersistence):
             from .clustering import upload_table
 
             N = _loader.load()
-            table = upload_table(w, X)
+            table = upload_table(w, X, layout="pca")  # f32 rows whatever storage_dtype says
             r = N.pca_fit(w.ctx, w.comm, table, k, False)
             pc, ev = np.asarray(r["pc"]), np.asarray(r["explained_variance"])
             extra.update({k_: r[k_] for k_ in ("stats_ms", "allreduce_ms", "eig_ms", "total_ms")})
@@ -108,10 +108,16 @@ class PCAModel(_PCAParams, Model, MLWritable, MLReadable):
         return np.asarray(X, dtype=np.float64) @ self.pc.toArray()
 
     def _transform(self, dataset):
+        import pandas as pd
+
         df = as_frame(dataset, self.getOrDefault("inputCol"))
         X = to_matrix(dataset, self.getOrDefault("inputCol"))
         Y = self.project(X) if len(X) else np.zeros((0, self.pc.numCols))
-        df[self.getOrDefault("outputCol")] = [DenseVector(r) for r in Y]
+        if isinstance(df[self.getOrDefault("inputCol")].dtype, pd.ArrowDtype):
+            # matrix / Arrow input: the projections stay one Arrow buffer (no per-row objects)
+            df[self.getOrDefault("outputCol")] = vector_column(Y)
+        else:
+            df[self.getOrDefault("outputCol")] = [DenseVector(r) for r in Y]
         return df
 
     def copy(self, extra: dict | None = None) -> "PCAModel":

@@ -172,8 +172,7 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
             iid, itf = np.asarray(out["item_ids"]), np.asarray(out["item_factors"])
             extra.update({k: out[k] for k in ("nnz", "setup_ms", "train_ms", "iter_ms", "gram_ms",
                                               "solve_ms", "comm_ms", "failed_rows")})
-        model = ALSModel(uid=self.uid, rank=rank, userFactors=_factor_frame(uid, uf),
-                         itemFactors=_factor_frame(iid, itf))
+        model = ALSModel(uid=self.uid, rank=rank, user_arrays=(uid, uf), item_arrays=(iid, itf))
         self._copyValues(model)
         model.setParent(self)
         model.fit_info = {"fit_seconds": time.time() - t0, **extra}
@@ -210,35 +209,83 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
 
 
 def _factor_frame(ids: np.ndarray, factors: np.ndarray):
+    """(id, features) frame of a factor matrix, sorted by id; the features column is one Arrow
+    fixed_size_list<float> buffer (no per-row Python objects)."""
     import pandas as pd
 
-    order = np.argsort(ids, kind="stable")
-    f = np.asarray(factors, dtype=np.float32)[order]
-    return pd.DataFrame({"id": np.asarray(ids, dtype=np.int32)[order],
-                         "features": [row for row in f]})
+    from ..data import vector_column
+
+    ids, F = _sorted_factors(ids, factors)
+    return pd.DataFrame({"id": ids.astype(np.int32), "features": vector_column(F)})
+
+
+def _sorted_factors(ids, factors, rank: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+    ids = np.asarray(ids)
+    F = np.asarray(factors, dtype=np.float32)
+    if F.ndim != 2:
+        F = F.reshape(len(ids), -1 if rank is None else rank)
+    if len(ids) > 1 and np.any(ids[1:] < ids[:-1]):
+        order = np.argsort(ids, kind="stable")
+        ids, F = ids[order], F[order]
+    return ids.astype(np.int64), np.ascontiguousarray(F)
+
+
+def _frame_factors(df, rank: int) -> tuple[np.ndarray, np.ndarray]:
+    from ..data import to_matrix
+
+    if len(df) == 0:
+        return np.zeros(0, np.int64), np.zeros((0, rank), np.float32)
+    return _sorted_factors(df["id"].to_numpy(), to_matrix(df, "features", np.float32), rank)
 
 
 class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
+    """Factors live as two contiguous (sorted ids, [n][rank] float32) pairs; the Spark-shaped
+    ``userFactors`` / ``itemFactors`` frames are views built on first access."""
+
     _uid_prefix = "als"
     _spark_class = "org.apache.spark.ml.recommendation.ALSModel"
 
     def __init__(self, uid: str | None = None, rank: int = 0, userFactors=None,
-                 itemFactors=None):  # noqa: N803
+                 itemFactors=None, user_arrays=None, item_arrays=None):  # noqa: N803
         super().__init__(uid)
         self.rank = int(rank)
-        self.userFactors = userFactors if userFactors is not None else _factor_frame(
-            np.zeros(0, np.int32), np.zeros((0, rank), np.float32))
-        self.itemFactors = itemFactors if itemFactors is not None else _factor_frame(
-            np.zeros(0, np.int32), np.zeros((0, rank), np.float32))
+        empty = (np.zeros(0, np.int64), np.zeros((0, self.rank), np.float32))
+        self._fac = {"user": empty, "item": empty}
+        self._frames: dict = {}
+        for which, frame, arrays in (("user", userFactors, user_arrays),
+                                     ("item", itemFactors, item_arrays)):
+            if arrays is not None:
+                self._fac[which] = _sorted_factors(arrays[0], arrays[1], self.rank)
+            elif frame is not None:
+                self._fac[which] = _frame_factors(frame, self.rank)
         self.fit_info: dict = {}
+
+    def _frame(self, which: str):
+        if which not in self._frames:
+            self._frames[which] = _factor_frame(*self._fac[which])
+        return self._frames[which]
+
+    @property
+    def userFactors(self):  # noqa: N802
+        return self._frame("user")
+
+    @userFactors.setter
+    def userFactors(self, df):  # noqa: N802
+        self._fac["user"] = _frame_factors(df, self.rank)
+        self._frames.pop("user", None)
+
+    @property
+    def itemFactors(self):  # noqa: N802
+        return self._frame("item")
+
+    @itemFactors.setter
+    def itemFactors(self, df):  # noqa: N802
+        self._fac["item"] = _frame_factors(df, self.rank)
+        self._frames.pop("item", None)
 
     # ---- factor access -----------------------------------------------------------------
     def _mat(self, which: str) -> tuple[np.ndarray, np.ndarray]:
-        df = self.userFactors if which == "user" else self.itemFactors
-        ids = df["id"].to_numpy().astype(np.int64)
-        F = (np.stack(df["features"].to_list()).astype(np.float32) if len(df)
-             else np.zeros((0, self.rank), np.float32))
-        return ids, F
+        return self._fac[which]
 
     def _lookup(self, which: str, keys: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
         ids, F = self._mat(which)
@@ -274,12 +321,20 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
     def _topk(self, src_ids, S, dst_ids, D, num: int, dst_col: str, src_col: str):
         import pandas as pd
 
+        import pyarrow as pa
+
         num = max(0, min(int(num), len(dst_ids)))
         recs_idx, recs_val = _blocked_topk(S, D, num)
-        recs = [[{dst_col: int(dst_ids[j]), "rating": float(v)} for j, v in zip(ri, rv)]
-                for ri, rv in zip(recs_idx, recs_val)]
+        # array<struct<dst: int, rating: float>> per source row, as ONE Arrow list array
+        dst = np.asarray(dst_ids, dtype=np.int32)[recs_idx.reshape(-1)] if recs_idx.size else \
+            np.zeros(0, np.int32)
+        st = pa.StructArray.from_arrays(
+            [pa.array(dst, pa.int32()), pa.array(recs_val.reshape(-1), pa.float32())],
+            names=[dst_col, "rating"])
+        offsets = pa.array(np.arange(len(recs_idx) + 1, dtype=np.int32) * num, pa.int32())
+        recs = pa.ListArray.from_arrays(offsets, st)
         return pd.DataFrame({src_col: np.asarray(src_ids, dtype=np.int32),
-                             "recommendations": recs})
+                             "recommendations": pd.arrays.ArrowExtensionArray(recs)})
 
     def recommendForAllUsers(self, numItems: int):  # noqa: N802,N803
         uids, U = self._mat("user")
@@ -311,8 +366,8 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
 
     def copy(self, extra: dict | None = None) -> "ALSModel":
         m = super().copy(extra)
-        m.userFactors = self.userFactors.copy()
-        m.itemFactors = self.itemFactors.copy()
+        m._fac = {w: (ids.copy(), F.copy()) for w, (ids, F) in self._fac.items()}
+        m._frames = {}
         return m
 
     # ---- persistence -------------------------------------------------------------------
@@ -331,8 +386,11 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
                                                "containsNull": False}, True)])
         for name, which in (("userFactors", "user"), ("itemFactors", "item")):
             ids, F = self._mat(which)
-            t = pa.Table.from_pydict({"id": ids.astype(np.int32),
-                                      "features": [row.tolist() for row in F]}, schema=schema)
+            offsets = pa.array(np.arange(len(ids) + 1, dtype=np.int32) * self.rank, pa.int32())
+            feats = pa.ListArray.from_arrays(offsets, pa.array(F.reshape(-1), pa.float32()),
+                                             type=schema.field("features").type)
+            t = pa.Table.from_arrays([pa.array(ids.astype(np.int32), pa.int32()), feats],
+                                     schema=schema)
             sf.write_parquet(os.path.join(path, name), t, spark)
 
     @classmethod
@@ -340,14 +398,19 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
         import os
 
         meta = sf.read_metadata(path, cls._spark_class)
-        frames = []
+        from ..data import _arrow_matrix
+
+        rank = int(meta["rank"])
+        arrays = []
         for name in ("userFactors", "itemFactors"):
-            t = sf.read_parquet_dir(os.path.join(path, name)).to_pydict()
-            frames.append(_factor_frame(np.asarray(t["id"], dtype=np.int32),
-                                        np.asarray(t["features"], dtype=np.float32).reshape(
-                                            len(t["id"]), int(meta["rank"]))))
-        m = cls(uid=meta["uid"], rank=int(meta["rank"]), userFactors=frames[0],
-                itemFactors=frames[1])
+            t = sf.read_parquet_dir(os.path.join(path, name))
+            ids = t.column("id").to_numpy()
+            F = (_arrow_matrix(t.column("features"), np.float32) if len(ids)
+                 else np.zeros((0, rank), np.float32))
+            if F is None:  # (null / ragged entries: the per-row reader)
+                F = np.asarray(t.column("features").to_pylist(), dtype=np.float32)
+            arrays.append((ids, F.reshape(len(ids), rank)))
+        m = cls(uid=meta["uid"], rank=rank, user_arrays=arrays[0], item_arrays=arrays[1])
         for k, v in meta.get("paramMap", {}).items():
             if m.hasParam(k):
                 m._set(**{k: v})

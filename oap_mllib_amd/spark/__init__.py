@@ -94,7 +94,7 @@ def import_model(payload: dict[str, bytes]):
     from ..linalg import DenseMatrix, DenseVector
     from ..models.clustering import KMeansModel
     from ..models.feature import PCAModel
-    from ..models.recommendation import ALSModel, _factor_frame
+    from ..models.recommendation import ALSModel
 
     meta = json.loads(payload["__meta__"].decode())
     arr = {k: np.load(io.BytesIO(v), allow_pickle=False) for k, v in payload.items()
@@ -108,8 +108,8 @@ def import_model(payload: dict[str, bytes]):
                      explainedVariance=DenseVector(arr["explainedVariance"]))
     else:
         m = ALSModel(uid=meta["uid"], rank=meta["rank"],
-                     userFactors=_factor_frame(arr["user_ids"], arr["user_factors"]),
-                     itemFactors=_factor_frame(arr["item_ids"], arr["item_factors"]))
+                     user_arrays=(arr["user_ids"], arr["user_factors"]),
+                     item_arrays=(arr["item_ids"], arr["item_factors"]))
     for k, v in meta["params"].items():
         if m.hasParam(k):
             m._set(**{k: v})
