@@ -3,7 +3,8 @@
 Rows are generated on the device (synthetic Gaussian blobs, row-sharded over ranks); reported:
 fit wall clock (covariance SYRK + allreduce + eigensolver), SYRK device time and its TFLOP/s
 (useful flops n*d*(d+1) of the symmetric product), allreduce and eigensolver times.
-Run: python benchmarks/bench_pca.py [--rows N] [--dim D] [--k K] [--reps R] [--precise]
+Run: python benchmarks/bench_pca.py [--rows N] [--dim D] [--k K] [--reps R]
+     [--precision exact|fast|fast4|both]
 """
 import argparse
 import json
@@ -20,7 +21,9 @@ def main():
     ap.add_argument("--dim", type=int, default=1000)
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--precise", action="store_true")
+    ap.add_argument("--precision", default="both", choices=["exact", "fast", "fast4", "both"],
+                    help="exact: fp64 products + sums (fp64 MFMA, the reference's precision); "
+                    "fast: bf16x3 split products; fast4: bf16x4; both: exact (headline) + fast")
     a = ap.parse_args()
     import numpy as np
 
@@ -36,28 +39,46 @@ def main():
     t = N.synth_blobs(w.ctx, n_loc, a.dim, N.kmeans_ld(a.dim), row0, 64, 10.0, 1.0, 1234)
     t.set_global(row0, a.rows)
     ingest = time.time() - t0
-    runs = []
-    for _ in range(a.reps + 1):
-        w.barrier()
-        t0 = time.time()
-        r = N.pca_fit(w.ctx, w.comm, t, a.k, a.precise)
-        w.barrier()
-        runs.append((time.time() - t0, r))
-    wall = [x[0] for x in runs[1:]]
-    best = min(range(len(wall)), key=lambda i: wall[i]) + 1
-    r = runs[best][1]
     flops = float(a.rows) * a.dim * (a.dim + 1)
+
+    def run(mode):
+        runs = []
+        for _ in range(a.reps + 1):
+            w.barrier()
+            t0 = time.time()
+            r = N.pca_fit(w.ctx, w.comm, t, a.k, mode == "fast4", exact=mode == "exact")
+            w.barrier()
+            runs.append((time.time() - t0, r))
+        wall = [x[0] for x in runs[1:]]
+        best = min(range(len(wall)), key=lambda i: wall[i]) + 1
+        r = runs[best][1]
+        return {"fit_wall_s": min(wall), "syrk_ms": r["stats_ms"],
+                "allreduce_ms": r["allreduce_ms"], "eig_ms": r["eig_ms"],
+                "native_total_ms": r["total_ms"],
+                "syrk_tflops": flops / (r["stats_ms"] * 1e-3) / 1e12, "all_wall_s": wall,
+                "explained_variance_head": list(r["explained_variance"][:5])}, r
+
+    modes = ["exact", "fast"] if a.precision == "both" else [a.precision]
+    res = {m: run(m) for m in modes}
+    head = modes[0]
+    dtype = {"exact": "fp32 in, fp64 products + fp64 accumulate (v_mfma_f64_16x16x4_f64)",
+             "fast": "fp32 in, bf16x3 MFMA, fp64 accumulate",
+             "fast4": "fp32 in, bf16x4 MFMA, fp64 accumulate"}[head]
     if w.rank == 0:
+        extra = dict(res[head][0])
+        extra["ingest_synth_s"] = ingest
+        extra["precision"] = head
+        for m in modes[1:]:
+            extra[m + "_mode"] = res[m][0]
+            ev_a = np.asarray(res[head][1]["explained_variance"])
+            ev_b = np.asarray(res[m][1]["explained_variance"])
+            extra[m + "_mode"]["max_abs_ev_diff_vs_" + head] = float(np.max(np.abs(ev_a - ev_b)))
         print(json.dumps({
-            "metric": "pca_fit_wall_s", "value": min(wall), "unit": "s", "n_gpus": w.size,
-            "higher_is_better": False, "dtype": "fp32 in, bf16x%d MFMA, fp64 accumulate"
-            % (4 if a.precise else 3), "data": "synthetic (gaussian blobs, on-device)",
+            "metric": "pca_fit_wall_s", "value": res[head][0]["fit_wall_s"], "unit": "s",
+            "n_gpus": w.size, "higher_is_better": False, "dtype": dtype,
+            "data": "synthetic (gaussian blobs, on-device)",
             "config": {"model": "pca top-%d" % a.k, "rows": a.rows, "dim": a.dim},
-            "extra": {"syrk_ms": r["stats_ms"], "allreduce_ms": r["allreduce_ms"],
-                      "eig_ms": r["eig_ms"], "native_total_ms": r["total_ms"],
-                      "syrk_tflops": flops / (r["stats_ms"] * 1e-3) / 1e12,
-                      "ingest_synth_s": ingest, "all_wall_s": wall,
-                      "explained_variance_head": list(r["explained_variance"][:5])}}))
+            "extra": extra}))
     O.shutdown_world()
 
 

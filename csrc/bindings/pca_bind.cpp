@@ -29,11 +29,12 @@ void register_pca(py::module_& m) {
   m.def(
       "pca_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
-         int k, bool precise, bool gpu_eig) {
+         int k, bool precise, bool gpu_eig, bool exact) {
         PcaParams p;
         p.k = k;
         p.precise = precise;
         p.gpu_eig = gpu_eig;
+        p.exact = exact;
         PcaResult r;
         {
           py::gil_scoped_release rel;
@@ -56,13 +57,14 @@ void register_pca(py::module_& m) {
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("k"),
-      py::arg("precise") = false, py::arg("gpu_eig") = true);
+      py::arg("precise") = false, py::arg("gpu_eig") = true, py::arg("exact") = false);
   m.def(
       "pca_covariance",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
-         bool precise) {
+         bool precise, bool exact) {
         PcaParams p;
         p.precise = precise;
+        p.exact = exact;
         PcaCovariance c;
         {
           py::gil_scoped_release rel;
@@ -76,7 +78,8 @@ void register_pca(py::module_& m) {
         out["allreduce_ms"] = c.allreduce_ms;
         return out;
       },
-      py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("precise") = false);
+      py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("precise") = false,
+      py::arg("exact") = false);
   m.def(
       "sym_eig",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> a, int k, int threads) {

@@ -1,6 +1,7 @@
 // C ABI over the native drivers (see oap_capi.h).  Exceptions never cross the boundary: every
 // entry point catches, stores the message in a thread-local buffer and returns a negative code.
 #include "capi/oap_capi.h"
+#include "comm/tcp_comm.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -127,6 +128,30 @@ int oap_ctx_join(oap_ctx* c, const unsigned char id[OAP_UNIQUE_ID_BYTES], int wo
     }
     std::string uid(reinterpret_cast<const char*>(id), OAP_UNIQUE_ID_BYTES);
     c->comm = std::make_shared<oap::RcclComm>(uid, world, rank, c->ctx->device(), timeout_s);
+  });
+}
+
+int oap_ctx_join_kvs(oap_ctx* c, const char* ip_port, int world, int rank, double timeout_s) {
+  return guarded([&] {
+    OAP_CHECK(c && c->ctx, "null context");
+    OAP_CHECK(world >= 1 && rank >= 0 && rank < world, "bad world/rank " << world << "/" << rank);
+    std::string ip;
+    int port = 0;
+    OAP_CHECK(ip_port && oap::parse_kvs_address(ip_port, &ip, &port),
+              "expected an \"ip_port\" rendezvous address, got '" << (ip_port ? ip_port : "")
+                                                                     << "'");
+    if (world == 1) {
+      c->comm = std::make_shared<oap::LocalComm>(c->ctx->is_gpu());
+      return;
+    }
+    auto store = std::make_shared<oap::TcpStore>(ip, port, world, rank, timeout_s);
+    if (c->ctx->is_gpu()) {
+      std::string uid = rank == 0 ? oap::rccl_unique_id() : std::string(OAP_UNIQUE_ID_BYTES, '\0');
+      store->broadcast(uid.data(), uid.size());
+      c->comm = std::make_shared<oap::RcclComm>(uid, world, rank, c->ctx->device(), timeout_s);
+    } else {
+      c->comm = std::make_shared<oap::TcpComm>(store);
+    }
   });
 }
 

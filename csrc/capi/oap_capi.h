@@ -46,6 +46,13 @@ OAP_API void oap_ctx_destroy(oap_ctx* ctx);
 OAP_API int oap_rccl_unique_id(unsigned char out[OAP_UNIQUE_ID_BYTES]);
 OAP_API int oap_ctx_join(oap_ctx* ctx, const unsigned char id[OAP_UNIQUE_ID_BYTES], int world,
                          int rank, double timeout_s);
+/* The reference's KVS contract: OneCCL.init(size, rank, "ip_port") (OneCCL.cpp:47-86).  Rank 0
+ * listens on ip:port (a port from c_getAvailPort's bind scan), the others connect to it.  GPU
+ * contexts: rank 0's RCCL unique id travels over that store, then every rank joins RCCL.  CPU
+ * contexts: the store's sockets carry the host collectives (TcpComm, star through rank 0).
+ * Accepts "ip_port" or "ip:port". */
+OAP_API int oap_ctx_join_kvs(oap_ctx* ctx, const char* ip_port, int world, int rank,
+                             double timeout_s);
 OAP_API int oap_ctx_world_size(const oap_ctx* ctx);
 OAP_API int oap_ctx_rank(const oap_ctx* ctx);
 

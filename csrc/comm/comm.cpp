@@ -131,21 +131,31 @@ void RcclComm::alltoallv(const void* send, const std::vector<size_t>& send_count
   OAP_CHECK(static_cast<int>(send_counts.size()) == world_ &&
                 static_cast<int>(recv_counts.size()) == world_,
             "alltoallv: counts must have one entry per rank");
-  size_t es = dtype_size(dt);
+  const size_t es = dtype_size(dt);
   auto c = static_cast<ncclComm_t>(comm_);
-  OAP_NCCL_CHECK(ncclGroupStart());
-  size_t soff = 0, roff = 0;
-  for (int p = 0; p < world_; ++p) {
-    if (send_counts[p])
-      OAP_NCCL_CHECK(ncclSend(static_cast<const char*>(send) + soff * es, send_counts[p],
-                              to_nccl(dt), p, c, s));
-    if (recv_counts[p])
-      OAP_NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + roff * es, recv_counts[p], to_nccl(dt),
-                              p, c, s));
-    soff += send_counts[p];
-    roff += recv_counts[p];
+  // Segments move in rounds of at most kChunk bytes per peer (a 1B-rating shuffle sends GBs
+  // per peer): bounded transfers per send/recv pair and per group.  Both sides of a pair agree
+  // on the counts, hence on the number of rounds; p2p ops match in order per pair, so ranks may
+  // run different numbers of rounds.
+  constexpr size_t kChunk = size_t(1) << 28;  // 256 MiB
+  const size_t chunk = std::max<size_t>(1, kChunk / es);
+  size_t most = 0;
+  for (int p = 0; p < world_; ++p) most = std::max({most, send_counts[p], recv_counts[p]});
+  for (size_t done = 0; done < most; done += chunk) {
+    OAP_NCCL_CHECK(ncclGroupStart());
+    size_t soff = 0, roff = 0;
+    for (int p = 0; p < world_; ++p) {
+      if (send_counts[p] > done)
+        OAP_NCCL_CHECK(ncclSend(static_cast<const char*>(send) + (soff + done) * es,
+                                std::min(chunk, send_counts[p] - done), to_nccl(dt), p, c, s));
+      if (recv_counts[p] > done)
+        OAP_NCCL_CHECK(ncclRecv(static_cast<char*>(recv) + (roff + done) * es,
+                                std::min(chunk, recv_counts[p] - done), to_nccl(dt), p, c, s));
+      soff += send_counts[p];
+      roff += recv_counts[p];
+    }
+    OAP_NCCL_CHECK(ncclGroupEnd());
   }
-  OAP_NCCL_CHECK(ncclGroupEnd());
 }
 
 void RcclComm::bcast(void* buf, size_t count, DType dt, int root, hipStream_t s) {

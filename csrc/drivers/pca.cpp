@@ -86,23 +86,35 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
   const size_t cnt = size_t(d) * d + d;
   std::vector<double> stats(cnt, 0.0);
   if (ctx.is_gpu()) {
-    OAP_CHECK(x.dtype == DType::F32, "GPU PCA expects an f32 table");
+    OAP_CHECK(x.dtype == DType::F32 || (p.exact && x.dtype == DType::F64),
+              "GPU PCA expects an f32 table (f32 or f64 in exact mode)");
     ctx.activate();
     hipStream_t s = ctx.compute();
-    const kern::PcaPlan plan = kern::pca_syrk_plan(x.rows, d, ctx.info().cu_count);
+    const kern::PcaPlan plan = p.exact ? kern::pca_syrk_plan_f64(x.rows, d, ctx.info().cu_count)
+                                       : kern::pca_syrk_plan(x.rows, d, ctx.info().cu_count);
     Buffer part = ctx.alloc(plan.part_elems * sizeof(double));
     Buffer cpart = ctx.alloc(plan.cpart_elems * sizeof(double));
-    Buffer shf = ctx.alloc(plan.shift_elems * sizeof(float));
+    Buffer shf = ctx.alloc(plan.shift_elems * sizeof(double));
     Buffer out = ctx.alloc(cnt * sizeof(double));
-    std::vector<float> hs(plan.shift_elems, 0.f);
-    for (int c = 0; c < d; ++c) hs[c] = float(shift[c]);
-    ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(float), s);
+    if (p.exact) {  // the fp64 shift itself (no fp32 rounding: exact mode subtracts in fp64)
+      std::vector<double> hs(plan.shift_elems, 0.0);
+      for (int c = 0; c < d; ++c) hs[c] = shift[c];
+      ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(double), s);
+    } else {
+      std::vector<float> hs(plan.shift_elems, 0.f);
+      for (int c = 0; c < d; ++c) hs[c] = float(shift[c]);
+      ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(float), s);
+    }
     Event e0, e1, e2;
     e0.record(s);
     {
       TraceRange k(&ctx.metrics(), "pca/syrk_launch");
-      kern::pca_syrk(x.data.as<float>(), x.rows, x.ld, d, shf.as<float>(), plan, part.as<double>(),
-                     cpart.as<double>(), p.precise, p.flush_rows, s);
+      if (p.exact)
+        kern::pca_syrk_f64(x.data.data(), x.dtype == DType::F64, x.rows, x.ld, d,
+                           shf.as<double>(), plan, part.as<double>(), cpart.as<double>(), s);
+      else
+        kern::pca_syrk(x.data.as<float>(), x.rows, x.ld, d, shf.as<float>(), plan,
+                       part.as<double>(), cpart.as<double>(), p.precise, p.flush_rows, s);
       kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), d, out.as<double>(),
                        out.as<double>() + size_t(d) * d, s);
     }

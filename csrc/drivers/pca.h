@@ -22,6 +22,9 @@ namespace oap {
 struct PcaParams {
   int k = 1;
   bool precise = false;  // 4-term bf16 split products (adds lo*lo); default 3-term
+  // reference precision (oneDAL fp64, PCADALImpl.cpp:31): fp64 products and sums of f32 or f64
+  // rows on the fp64 MFMA; the fast path (bf16 split products) otherwise
+  bool exact = false;
   int flush_rows = 4096; // rows accumulated in fp32 before the fp64 flush (GPU)
   bool gpu_eig = true;   // device eigensolver (linalg/eigen_gpu.h) when the context is a GPU
 };

@@ -6,9 +6,11 @@
 //
 // Mapping (reference -> here):
 //  * OneCCL$: c_init(size, rank, "ip_port" | hex unique id, CCLParam{long commSize, rankId}).
-//    With size > 1 the string must carry the hex RCCL unique id that rank 0 made with
-//    c_uniqueId() and the launcher distributed (Spark BarrierTaskContext.allGather): no KVS
-//    server, no port scan (OneCCL.cpp:47-247).  One persistent context per executor process.
+//    With size > 1 the string is either the reference's KVS address "ip_port" (rank 0 serves
+//    a TCP rendezvous there: the RCCL unique id for GPU contexts, the host collectives
+//    themselves for CPU contexts — comm/tcp_comm.h), or the hex RCCL unique id that rank 0 made
+//    with c_uniqueId() and the launcher distributed (Spark BarrierTaskContext.allGather).  One
+//    persistent context per executor process.
 //    setEnv / c_getAvailPort keep the reference's behaviour (OneCCL.cpp:127-247).
 //  * OneDAL$: native row tables (f64, row-major) — setNumericTableValue (one value,
 //    OneDAL.cpp:35-43), cSetDoubleBatch (row batch, :50-60), cAddNumericTable (append, :67-76),
@@ -152,20 +154,20 @@ JNIEXPORT jint JNICALL Java_org_apache_spark_ml_util_OneCCL_00024_c_1init(JNIEnv
   if (!ensure_ctx(env)) return -1;
   if (size > 1) {
     const char* s = env->GetStringUTFChars(uid_hex, nullptr);
-    const size_t n = s ? std::strlen(s) : 0;
+    const std::string str = s ? s : "";
+    if (s) env->ReleaseStringUTFChars(uid_hex, s);
     unsigned char id[OAP_UNIQUE_ID_BYTES] = {0};
-    bool ok = n == 2 * OAP_UNIQUE_ID_BYTES;
-    for (size_t i = 0; ok && i < n; i += 2) {
-      const int hi = hexval(s[i]), lo = hexval(s[i + 1]);
-      ok = hi >= 0 && lo >= 0;
+    bool hex = str.size() == 2 * OAP_UNIQUE_ID_BYTES;
+    for (size_t i = 0; hex && i < str.size(); i += 2) {
+      const int hi = hexval(str[i]), lo = hexval(str[i + 1]);
+      hex = hi >= 0 && lo >= 0;
       id[i / 2] = static_cast<unsigned char>(hi * 16 + lo);
     }
-    if (s) env->ReleaseStringUTFChars(uid_hex, s);
-    if (!ok) {
-      throw_java(env, "c_init: expected the hex RCCL unique id from c_uniqueId() (no KVS)");
-      return -1;
-    }
-    if (!check(env, oap_ctx_join(g_ctx, id, size, rank, 600.0))) return -1;
+    // the hex RCCL unique id from c_uniqueId(), or the reference's KVS string "ip_port"
+    // (KMeansDALImpl.scala:39-50): rank 0 serves the rendezvous at that address
+    const int rc = hex ? oap_ctx_join(g_ctx, id, size, rank, 600.0)
+                       : oap_ctx_join_kvs(g_ctx, str.c_str(), size, rank, 600.0);
+    if (!check(env, rc)) return -1;
   }
   // CCLParam.commSize / rankId are Java longs (CCLParam.java:20-21)
   if (!set_long(env, param, "commSize", oap_ctx_world_size(g_ctx))) return -1;
@@ -296,23 +298,35 @@ JNIEXPORT jlong JNICALL Java_org_apache_spark_ml_util_OneDAL_00024_cNewCSRNumeri
     JNIEnv* env, jobject, jfloatArray data, jlongArray col_indices, jlongArray row_offsets,
     jlong n_features, jlong n_vectors) {
   const jsize nnz = env->GetArrayLength(data);
+  const jsize n_off = env->GetArrayLength(row_offsets);
+  // The reference's bufferToCSRNumericTable (ALSDALImpl.scala:184-230) starts from offsets [1]
+  // at row 0, so a partition whose lowest key has no ratings (or no ratings at all) carries a
+  // leading empty row: [1, 1, ...] with csrRowNum + 2 entries.  That leading row is dropped —
+  // CSR row i stays the i-th distinct key, as cShuffleData's key table maps it.
   if (env->GetArrayLength(col_indices) != nnz || n_vectors < 0 ||
-      env->GetArrayLength(row_offsets) != n_vectors + 1) {
+      (n_off != n_vectors + 1 && n_off != n_vectors + 2)) {
     throw_java(env, "cNewCSRNumericTable: inconsistent CSR array lengths");
     return 0;
+  }
+  std::vector<int64_t> offs(static_cast<size_t>(n_off));
+  if (n_off) env->GetLongArrayRegion(row_offsets, 0, n_off, reinterpret_cast<jlong*>(offs.data()));
+  if (n_off == n_vectors + 2) {
+    if (offs[0] != 1 || offs[1] != 1) {
+      throw_java(env, "cNewCSRNumericTable: inconsistent CSR array lengths");
+      return 0;
+    }
+    offs.erase(offs.begin());
   }
   auto* t = new CsrTable;
   t->rows = n_vectors;
   t->cols = n_features;
   t->vals.resize(size_t(nnz));
   t->colidx.resize(size_t(nnz));
-  t->rowptr.resize(size_t(n_vectors) + 1);
+  t->rowptr = std::move(offs);
   if (nnz) {
     env->GetFloatArrayRegion(data, 0, nnz, t->vals.data());
     env->GetLongArrayRegion(col_indices, 0, nnz, reinterpret_cast<jlong*>(t->colidx.data()));
   }
-  env->GetLongArrayRegion(row_offsets, 0, jsize(n_vectors + 1),
-                          reinterpret_cast<jlong*>(t->rowptr.data()));
   bool ok = t->rowptr[0] == 1 && t->rowptr[size_t(n_vectors)] == int64_t(nnz) + 1;
   for (int64_t i = 0; ok && i < n_vectors; ++i) ok = t->rowptr[i] <= t->rowptr[i + 1];
   for (auto& v : t->rowptr) --v;

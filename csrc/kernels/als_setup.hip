@@ -167,6 +167,29 @@ __global__ void oap_als_csr_keys(const int32_t* __restrict__ rowid, const int32_
   }
 }
 
+// order-independent checksums of the three columns: sum of the 32-bit patterns (wrap-free for
+// up to 2^31 ratings); the shuffle verifies that every rating arrived exactly once
+__global__ void oap_als_checksum(const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                                 const float* __restrict__ r, int64_t n,
+                                 unsigned long long* __restrict__ out) {
+  unsigned long long sa = 0, sb = 0, sr = 0;
+  OAP_GRID_LOOP(k, n) {
+    sa += uint32_t(a[k]);
+    sb += uint32_t(b[k]);
+    sr += __float_as_uint(r[k]);
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    sa += __shfl_xor(sa, m, 64);
+    sb += __shfl_xor(sb, m, 64);
+    sr += __shfl_xor(sr, m, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&out[0], sa);
+    atomicAdd(&out[1], sb);
+    atomicAdd(&out[2], sr);
+  }
+}
+
 __global__ void oap_als_copy_i32(const int32_t* __restrict__ src, int64_t n,
                                  int32_t* __restrict__ dst) {
   OAP_GRID_LOOP(k, n) dst[k] = src[k];
@@ -384,7 +407,22 @@ Soa shuffle(Context& ctx, Comm& comm, Soa& in, bool by_a, const std::vector<int6
   comm_alltoallv(ctx, comm, send.a.data(), sc, recv.a.data(), rc, DType::I32, s);
   comm_alltoallv(ctx, comm, send.b.data(), sc, recv.b.data(), rc, DType::I32, s);
   comm_alltoallv(ctx, comm, send.r.data(), sc, recv.r.data(), rc, DType::F32, s);
+  // integrity: the world's sent and received column checksums must agree
+  Buffer ck = ctx.alloc(64);
+  OAP_HIP_CHECK(hipMemsetAsync(ck.data(), 0, 64, s));
+  const int cg = std::min(grid_of(std::max(n, m)), 1024);
+  hipLaunchKernelGGL(oap_als_checksum, dim3(cg), dim3(kThreads), 0, s, send.a.as<int32_t>(),
+                     send.b.as<int32_t>(), send.r.as<float>(), n, ck.as<unsigned long long>());
+  hipLaunchKernelGGL(oap_als_checksum, dim3(cg), dim3(kThreads), 0, s, recv.a.as<int32_t>(),
+                     recv.b.as<int32_t>(), recv.r.as<float>(), m, ck.as<unsigned long long>() + 3);
+  OAP_HIP_CHECK(hipGetLastError());
   comm.wait(s);  // (the watchdog covers the exchange; send buffers are freed below)
+  int64_t sums[6];
+  ctx.copy_to_host(sums, ck.data(), sizeof(sums), s);
+  comm_allreduce_host(ctx, comm, sums, 6, DType::I64, ReduceOp::Sum);
+  if (!(sums[0] == sums[3] && sums[1] == sums[4] && sums[2] == sums[5]))
+    OAP_THROW(CommError,
+              "ALS device shuffle: checksum mismatch (ratings lost or corrupted in the exchange)");
   return recv;
 }
 

@@ -271,6 +271,12 @@ PcaPlan pca_syrk_plan(int64_t n, int d, int num_cus);
 // part/cpart: fp64 slabs of p.part_elems / p.cpart_elems; shift: [p.shift_elems] zero padded.
 void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, const PcaPlan& p,
               double* part, double* cpart, bool four, int flush_rows, hipStream_t s);
+// Exact (reference-precision) statistics: fp64 products and sums on v_mfma_f64_16x16x4_f64 of
+// f32 or f64 rows (x_f64), 128-wide tiles; shift: fp64 [p.shift_elems] zero padded.  The slabs
+// reduce with pca_reduce like the fast path's.
+PcaPlan pca_syrk_plan_f64(int64_t n, int d, int num_cus);
+void pca_syrk_f64(const void* x, bool x_f64, int64_t n, int64_t ld, int d, const double* shift,
+                  const PcaPlan& p, double* part, double* cpart, hipStream_t s);
 // ---- ALS (kernels/als.hip) -------------------------------------------------------------------
 struct AlsSolveArgs {
   const int64_t* rowptr = nullptr;  // [nrows+1] CSR of the destination rows

@@ -418,6 +418,177 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
   }
 }
 
+// ---- exact mode: fp64 products, fp64 accumulation (v_mfma_f64_16x16x4_f64) -------------------
+// The reference's precision (oneDAL fp64 step1Local, PCADALImpl.cpp:31,63-69): every product
+// (x_i - s_i)(x_j - s_j) is formed and summed in fp64 — fp32 rows are widened exactly, fp64 rows
+// are used as they are.  128 x 128 output tile per 256-thread workgroup; each wave owns a 64 x 64
+// quarter = 4 x 4 blocks of 16 x 16 (16 independent accumulators of 4 doubles).  Rows are staged
+// 16 at a time through LDS as fp64 [feature][row] planes (double buffered, one barrier per
+// chunk); an A or B fragment is ONE ds_read_b64 per lane.  The accumulators are fp64 for the
+// whole split: no intermediate flush, the slab is written once.
+constexpr int kXTile = 128;
+constexpr int kXRows = 16;              // rows per LDS stage (4 k-steps of the 16x16x4 MFMA)
+constexpr int kXS = kXRows + 2;         // plane stride in doubles (36 dwords: 2-way at most)
+constexpr int kXPlane = kXTile * kXS;   // doubles per side plane
+constexpr int kXThreads = 256;
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+struct SyrkF64Args {
+  const void* x;
+  int64_t n, ld;
+  int d;
+  const double* shift;  // [nb*128], zero padded
+  int nb, tiles, splits;
+  int64_t rows_per_split;
+  double* part;         // [splits][tiles][128*128]
+  double* cpart;        // [splits][nb][128]
+};
+
+// 8 features f0 .. f0+7 of one row.  VEC: 16-byte aligned rows and ld % 8 == 0, so a group is
+// either wholly inside the row or wholly past it.
+template <typename T, bool VEC>
+__device__ inline void load8(const T* __restrict__ p, int f0, int ld, double (&v)[8]) {
+  if constexpr (VEC) {
+    if (f0 < ld) {
+      if constexpr (sizeof(T) == 4) {
+        const float4 a = *reinterpret_cast<const float4*>(p + f0);
+        const float4 b = *reinterpret_cast<const float4*>(p + f0 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double2 a = *reinterpret_cast<const double2*>(p + f0 + 2 * q);
+          v[2 * q] = a.x;
+          v[2 * q + 1] = a.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = 0.0;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = f0 + q < ld ? double(p[f0 + q]) : 0.0;
+  }
+}
+
+template <typename T, bool VEC>
+__global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) {
+  __shared__ double lds[2 * 2 * kXPlane];  // [stage][side][feature][row]
+  const int G = a.splits * a.tiles;
+  const int per = gridDim.x / 8;  // XCD-aware: the tiles of one split share an XCD (its L2)
+  const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (L >= G) return;
+  const int split = L / a.tiles, tile = L - split * a.tiles;
+  int ti, tj;
+  tile_coords(tile, a.nb, ti, tj);
+  const bool diag = ti == tj;
+  const int64_t r_begin = int64_t(split) * a.rows_per_split;
+  const int64_t r_end = min(a.n, r_begin + a.rows_per_split);
+  const T* __restrict__ X = static_cast<const T*>(a.x);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave >> 1, wj = wave & 1;
+  // loader: row lr of the stage, features 8*lq .. 8*lq+7 of each side
+  const int lr = tid >> 4, lq = tid & 15;
+  const int fI = ti * kXTile + 8 * lq, fJ = tj * kXTile + 8 * lq;
+  double shI[8], shJ[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    shI[q] = a.shift[fI + q];
+    shJ[q] = a.shift[fJ + q];
+  }
+  double vI[8] = {0, 0, 0, 0, 0, 0, 0, 0}, vJ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int ld = int(a.ld);  // (< 2^31: checked on the host)
+  // unconditional loads (row clamped to the split's last row): stage() masks what lies outside
+  auto load = [&](int64_t r0) {
+    const T* p = X + min(r0 + lr, r_end - 1) * a.ld;
+    load8<T, VEC>(p, fI, ld, vI);
+    if (!diag) load8<T, VEC>(p, fJ, ld, vJ);
+  };
+  // centre (fp64, exact for fp32 rows) and transpose into the planes; rows past r_end and
+  // features past d contribute exact zeros
+  auto stage = [&](double* buf, int64_t r0) {
+    const bool okr = r0 + lr < r_end;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double c = (okr && fI + q < a.d) ? vI[q] - shI[q] : 0.0;
+      if (diag) cs[q] += c;
+      buf[(8 * lq + q) * kXS + lr] = c;
+    }
+    if (!diag) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const double c = (okr && fJ + q < a.d) ? vJ[q] - shJ[q] : 0.0;
+        buf[kXPlane + (8 * lq + q) * kXS + lr] = c;
+      }
+    }
+  };
+
+  f64x4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // fragments: lane l holds A[i = l & 15][k = l >> 4] = plane[feature][row k]
+  const int fa = 64 * wi + (lane & 15), fb = 64 * wj + (lane & 15), kr = lane >> 4;
+  const int boff = diag ? 0 : kXPlane;
+  int cur = 0;
+  if (r_begin < r_end) {
+    load(r_begin);
+    stage(lds, r_begin);
+    if (r_begin + kXRows < r_end) load(r_begin + kXRows);
+    __syncthreads();
+  }
+  for (int64_t r0 = r_begin; r0 < r_end; r0 += kXRows) {
+    const double* buf = lds + cur * (2 * kXPlane);
+#pragma unroll
+    for (int ks = 0; ks < kXRows / 4; ++ks) {
+      double av[4], bv[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) av[x] = buf[(fa + 16 * x) * kXS + 4 * ks + kr];
+#pragma unroll
+      for (int y = 0; y < 4; ++y) bv[y] = buf[boff + (fb + 16 * y) * kXS + 4 * ks + kr];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+    }
+    if (r0 + kXRows < r_end) {  // the other stage was last read before the previous barrier
+      stage(lds + (cur ^ 1) * (2 * kXPlane), r0 + kXRows);
+      if (r0 + 2 * kXRows < r_end) load(r0 + 2 * kXRows);
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // the split's fp64 sums, written once: C/D map col = lane & 15, row = (lane >> 4) + 4 reg
+  double* slab = a.part + (size_t(split) * a.tiles + tile) * (kXTile * kXTile);
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = 64 * wi + 16 * x + (lane >> 4) + 4 * e;
+        const int col = 64 * wj + 16 * y + (lane & 15);
+        slab[row * kXTile + col] = acc[x][y][e];
+      }
+  if (diag) {  // column sums over the 16 loader rows: through LDS (the stages are free now)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) lds[lr * kXTile + 8 * lq + q] = cs[q];
+    __syncthreads();
+    if (tid < kXTile) {
+      double v = 0.0;
+      for (int q = 0; q < kXRows; ++q) v += lds[q * kXTile + tid];
+      a.cpart[(size_t(split) * a.nb + ti) * kXTile + tid] = v;
+    }
+  }
+}
+
 // cov = (S - c c^T / n) / (n - 1) on the device (the host formula, operation for operation)
 __global__ void oap_pca_cov(const double* __restrict__ stats, int d, double n,
                             double* __restrict__ cov) {
@@ -515,6 +686,58 @@ void pca_syrk(const float* x, int64_t n, int64_t ld, int d, const float* shift, 
   } else {
     hipLaunchKernelGGL(oap_pca_syrk<false>, dim3(p.grid), dim3(kSyrkThreads), 0, s, a);
   }
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+PcaPlan pca_syrk_plan_f64(int64_t n, int d, int num_cus) {
+  PcaPlan p;
+  p.tw = kXTile;
+  p.nb = (d + p.tw - 1) / p.tw;
+  p.tiles = p.nb * (p.nb + 1) / 2;
+  const int64_t want = int64_t(std::max(num_cus, 64)) * 4;  // 2 resident per CU x 2 waves
+  int64_t s = (want + p.tiles - 1) / p.tiles;
+  const int64_t max_s = std::max<int64_t>(1, (n + 8 * kXRows - 1) / (8 * kXRows));
+  s = std::max<int64_t>(1, std::min(s, max_s));
+  const int64_t slab_tile = int64_t(p.tw) * p.tw * 8;
+  while (s > 1 && s * p.tiles * slab_tile > (int64_t(1) << 30)) --s;
+  p.splits = static_cast<int>(s);
+  p.rows_per_split = round_up((n + s - 1) / s, kXRows);
+  if (p.rows_per_split == 0) p.rows_per_split = kXRows;
+  p.part_elems = size_t(p.splits) * p.tiles * p.tw * p.tw;
+  p.cpart_elems = size_t(p.splits) * p.nb * p.tw;
+  p.shift_elems = size_t(p.nb) * p.tw;
+  p.grid = static_cast<int>(round_up(int64_t(p.splits) * p.tiles, 8));
+  return p;
+}
+
+void pca_syrk_f64(const void* x, bool x_f64, int64_t n, int64_t ld, int d, const double* shift,
+                  const PcaPlan& p, double* part, double* cpart, hipStream_t s) {
+  OAP_CHECK(p.tw == kXTile, "pca_syrk_f64 needs a pca_syrk_plan_f64 plan");
+  OAP_CHECK(ld >= d && ld < INT32_MAX, "pca_syrk_f64: bad ld");
+  SyrkF64Args a;
+  a.x = x;
+  a.n = n;
+  a.ld = ld;
+  a.d = d;
+  a.shift = shift;
+  a.nb = p.nb;
+  a.tiles = p.tiles;
+  a.splits = p.splits;
+  a.rows_per_split = p.rows_per_split;
+  const size_t es = x_f64 ? 8 : 4;
+  const bool vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && ld % 8 == 0 &&
+                   (size_t(ld) * es) % 16 == 0;
+  a.part = part;
+  a.cpart = cpart;
+  const dim3 g(p.grid), b(kXThreads);
+  if (x_f64 && vec)
+    hipLaunchKernelGGL((oap_pca_syrk_f64<double, true>), g, b, 0, s, a);
+  else if (x_f64)
+    hipLaunchKernelGGL((oap_pca_syrk_f64<double, false>), g, b, 0, s, a);
+  else if (vec)
+    hipLaunchKernelGGL((oap_pca_syrk_f64<float, true>), g, b, 0, s, a);
+  else
+    hipLaunchKernelGGL((oap_pca_syrk_f64<float, false>), g, b, 0, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 

@@ -63,8 +63,10 @@ DenseTable upload_dense(Context& ctx, const void* host, DType src_t, int64_t row
     });
     return t;
   }
-  OAP_CHECK(storage == DType::F32 || storage == DType::BF16,
-            "GPU tables are f32 or bf16, got " << dtype_name(storage));
+  // f64 device tables serve the exact (reference-precision) PCA statistics only; K-Means reads
+  // f32 / bf16 rows (check_gpu_table)
+  OAP_CHECK(storage == DType::F32 || storage == DType::BF16 || storage == DType::F64,
+            "GPU tables are f32, bf16 or f64, got " << dtype_name(storage));
   ctx.activate();
   t.data = ctx.alloc(t.bytes() == 0 ? 256 : t.bytes());
   if (rows == 0) return t;

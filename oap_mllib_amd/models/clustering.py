@@ -272,13 +272,16 @@ def _streamed(w, X: np.ndarray) -> bool:
 
 
 def upload_table(w, X: np.ndarray, layout: str = "kmeans"):
-    """Rank-local matrix -> native DenseTable on the world's backend."""
+    """Rank-local matrix -> native DenseTable on the world's backend.  layout "pca": f32 rows
+    ("pca_exact": f64 input rows stay f64, the exact-mode kernel reads them as they are)."""
     N = _loader.load()
     d = X.shape[1]
     if w.is_gpu:
         st = w.config.storage_dtype
         if layout == "kmeans":
             ld = N.kmeans_ld(d, st)
+        elif layout == "pca_exact" and X.dtype == np.float64:
+            st, ld = "f64", d
         else:
             st, ld = "f32", d  # PCA reads f32 rows
         src = X if X.dtype in (np.float32, np.float64) else X.astype(np.float64)

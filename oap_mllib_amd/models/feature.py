@@ -76,8 +76,11 @@ class PCA(_PCAParams, Estimator, DefaultParamsPersistence):
             from .clustering import upload_table
 
             N = _loader.load()
-            table = upload_table(w, X, layout="pca")  # f32 rows whatever storage_dtype says
-            r = N.pca_fit(w.ctx, w.comm, table, k, False)
+            exact = w.config.pca_precision != "fast"
+            # f32 rows whatever storage_dtype says; exact mode keeps f64 input rows f64
+            table = upload_table(w, X, layout="pca_exact" if exact else "pca")
+            r = N.pca_fit(w.ctx, w.comm, table, k, False, exact=exact)
+            extra["precision"] = "exact" if exact else "fast"
             pc, ev = np.asarray(r["pc"]), np.asarray(r["explained_variance"])
             extra.update({k_: r[k_] for k_ in ("stats_ms", "allreduce_ms", "eig_ms", "total_ms")})
         model = PCAModel(uid=self.uid, pc=DenseMatrix.from_array(pc),

@@ -91,3 +91,69 @@ def test_gpu_close_to_cpu_engine(native, gpu_world):
     np.testing.assert_allclose(r_gpu["explained_variance"], r_cpu["explained_variance"],
                                atol=2e-6)
     np.testing.assert_allclose(np.abs(r_gpu["pc"]), np.abs(r_cpu["pc"]), atol=1e-4)
+
+
+# ---------------------------------------------------------------- exact (reference fp64) mode
+def _cov_exact(native, w, X, layout="pca_exact"):
+    from oap_mllib_amd.models.clustering import upload_table
+
+    t = upload_table(w, X, layout=layout)
+    r = native.pca_covariance(w.ctx, w.comm, t, False, exact=True)
+    return np.asarray(r["cov"]), np.asarray(r["mean"])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("n,d", [(5, 3), (37, 7), (1000, 50), (4099, 127), (3000, 128),
+                                 (2500, 129), (2000, 301), (20000, 1000)])
+def test_exact_mode_matches_np_cov(native, gpu_world, dtype, n, d):
+    """fp64 products and sums on v_mfma_f64_16x16x4_f64: np.cov (fp64) of the same rows to
+    1e-12, scale-normalised — the reference's oneDAL fp64 precision (PCADALImpl.cpp:31)."""
+    rng = np.random.default_rng(n * 3 + d)
+    X = (rng.normal(size=(n, d)) @ (rng.normal(size=(d, d)) / np.sqrt(d))
+         + rng.normal(size=d) * 5).astype(dtype)
+    C, mu = _cov_exact(native, gpu_world, X)
+    X64 = X.astype(np.float64)
+    Cr = np.cov(X64.T, ddof=1)
+    assert np.max(np.abs(C - Cr)) / np.max(np.abs(Cr)) < 1e-12
+    np.testing.assert_allclose(mu, X64.mean(axis=0), rtol=0, atol=1e-12 * (1 + np.abs(X64).max()))
+
+
+def test_exact_mode_f64_rows_not_rounded(native, gpu_world):
+    """f64 rows whose low bits fp32 would drop: the exact path keeps them."""
+    rng = np.random.default_rng(8)
+    base = rng.normal(size=(6000, 24))
+    X = 1.0 + base * 1e-9  # fp32 rounding would erase the whole signal
+    C, _ = _cov_exact(native, gpu_world, X)
+    Cr = np.cov(X.T, ddof=1)
+    assert np.max(np.abs(C - Cr)) / np.max(np.abs(Cr)) < 1e-9
+
+
+def test_exact_is_default_and_fast_selectable(gpu_world):
+    rng = np.random.default_rng(12)
+    X = rng.normal(size=(20000, 64)) * np.geomspace(5, 0.2, 64) + 3.0
+    m = O.PCA(k=4, inputCol="features").fit(X)
+    assert m.fit_info["engine"] == "gpu" and m.fit_info["precision"] == "exact"
+    wr = np.sort(np.linalg.eigvalsh(np.cov(X.T, ddof=1)))[::-1]
+    np.testing.assert_allclose(m.explainedVariance.toArray(), wr[:4] / wr.sum(), rtol=1e-10)
+    O.set_config(O.get_config().replace(pca_precision="fast"))
+    try:
+        O.shutdown_world()
+        O.init_world(O.get_config().replace(device="gpu", device_id=0))
+        f = O.PCA(k=4, inputCol="features").fit(X)
+        assert f.fit_info["precision"] == "fast"
+        np.testing.assert_allclose(f.explainedVariance.toArray(), wr[:4] / wr.sum(), atol=1e-5)
+    finally:
+        O.set_config(O.get_config().replace(pca_precision="exact"))
+
+
+def test_exact_with_bf16_storage_config(gpu_world):
+    """PCA uploads with its own layout: a bf16 K-Means storage config does not reach it."""
+    O.set_config(O.get_config().replace(storage_dtype="bf16"))
+    try:
+        O.shutdown_world()
+        O.init_world(O.get_config().replace(device="gpu", device_id=0))
+        X = np.random.default_rng(1).normal(size=(3000, 20))
+        m = O.PCA(k=3, inputCol="features").fit(X)
+        assert m.fit_info["engine"] == "gpu"
+    finally:
+        O.set_config(O.get_config().replace(storage_dtype="f32"))
