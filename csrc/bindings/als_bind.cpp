@@ -16,6 +16,33 @@ namespace py = pybind11;
 using namespace oap;
 
 void register_als(py::module_& m) {
+  // the device Jacobi of kernels/als_eig.hip on a given symmetric matrix (tests)
+  m.def(
+      "als_gram_eig",
+      [](std::shared_ptr<Context> ctx,
+         py::array_t<double, py::array::c_style | py::array::forcecast> g, int ld) {
+        if (g.ndim() != 2 || g.shape(0) != g.shape(1)) throw ConfigError("square matrix needed");
+        if (!ctx->is_gpu()) throw ConfigError("als_gram_eig needs a GPU context");
+        const int r = int(g.shape(0));
+        if (ld <= 0) ld = int(round_up(size_t(r), 16));
+        py::array_t<float> q({ld, ld}), qt({ld, ld}), e(ld);
+        {
+          py::gil_scoped_release rel;
+          ctx->activate();
+          hipStream_t s = ctx->compute();
+          Buffer dg = ctx->alloc(size_t(r) * r * 8), dq = ctx->alloc(size_t(ld) * ld * 4),
+                 dqt = ctx->alloc(size_t(ld) * ld * 4), de = ctx->alloc(size_t(ld) * 4),
+                 sc = ctx->alloc(kern::als_gram_eig_scratch_bytes(r));
+          ctx->copy_to_backend(dg.data(), g.data(), size_t(r) * r * 8, s);
+          kern::als_gram_eig(dg.as<double>(), r, ld, sc.as<double>(), dq.as<float>(),
+                             dqt.as<float>(), de.as<float>(), s);
+          ctx->copy_to_host(q.mutable_data(), dq.data(), size_t(ld) * ld * 4, s);
+          ctx->copy_to_host(qt.mutable_data(), dqt.data(), size_t(ld) * ld * 4, s);
+          ctx->copy_to_host(e.mutable_data(), de.data(), size_t(ld) * 4, s);
+        }
+        return py::make_tuple(q, qt, e);
+      },
+      py::arg("ctx"), py::arg("gram"), py::arg("ld") = 0);
   m.def(
       "als_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,

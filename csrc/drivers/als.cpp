@@ -587,11 +587,11 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     }
     Buffer ctr = ctx.alloc(64);
     ctx.memset(ctr.data(), 0, 64);
-    // low-rank path state: eigenbasis of the source Gramian (host, then device)
+    // low-rank path state: eigenbasis of the source Gramian, computed on the device
+    // (kernels/als_eig.hip) straight from the allreduced fp64 Gramian — no host round trip
     Buffer lrQ = ctx.alloc(size_t(ld) * ld * 4), lrQT = ctx.alloc(size_t(ld) * ld * 4),
            lrEig = ctx.alloc(size_t(ld) * 4);
-    std::vector<float> hQ(size_t(ld) * ld), hQT(size_t(ld) * ld), hEig(ld);
-    std::vector<double> hG(size_t(r) * r);
+    Buffer eig_scratch = ctx.alloc(kern::als_gram_eig_scratch_bytes(r));
     Buffer gram64 = ctx.alloc((size_t(r) * r + r) * 8), gram32 = ctx.alloc(size_t(r) * r * 4);
     Buffer zshift = ctx.alloc(size_t(ld + 128) * 4);
     ctx.memset(zshift.data(), 0, size_t(ld + 128) * 4);
@@ -628,28 +628,14 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         }
         kern::f64_to_f32(gram64.as<double>(), gram32.as<float>(), int64_t(r) * r, s);
       }
-      // low-rank path: Y^T Y = Q Lambda Q^T on the host (fp64, identical on every rank), the
-      // source factors rotated once into that basis
+      // low-rank path: Y^T Y = Q Lambda Q^T on the device (fp64 Jacobi, identical on every
+      // rank: the same allreduced Gramian in, the same deterministic sweeps), the source
+      // factors rotated once into that basis — all stream-ordered behind the allreduce
       bool lr_on = false;
       for (const auto& o : dD.lro) lr_on = lr_on || o[4] > o[0];
       if (lr_on) {
-        if (dev_comm) comm.wait(s);  // the Gramian allreduce, under the collective watchdog
-        ctx.copy_to_host(hG.data(), gram64.data(), hG.size() * 8, s);
-        const SymEig eg = sym_eig(hG, r, &ctx.pool());
-        std::fill(hQ.begin(), hQ.end(), 0.f);
-        std::fill(hQT.begin(), hQT.end(), 0.f);
-        for (int k = 0; k < ld; ++k) {
-          hEig[k] = k < r ? float(std::max(eg.values[k], 0.0)) : 1.f;
-          for (int j = 0; j < ld; ++j) {
-            const float v = (k < r && j < r) ? float(eg.vectors[size_t(k) * r + j])
-                                             : (k == j ? 1.f : 0.f);
-            hQ[size_t(k) * ld + j] = v;
-            hQT[size_t(j) * ld + k] = v;
-          }
-        }
-        ctx.copy_to_backend(lrQ.data(), hQ.data(), hQ.size() * 4, s);
-        ctx.copy_to_backend(lrQT.data(), hQT.data(), hQT.size() * 4, s);
-        ctx.copy_to_backend(lrEig.data(), hEig.data(), hEig.size() * 4, s);
+        kern::als_gram_eig(gram64.as<double>(), r, ld, eig_scratch.as<double>(), lrQ.as<float>(),
+                           lrQT.as<float>(), lrEig.as<float>(), s);
         if (!dS.rot.data()) dS.rot = ctx.alloc(std::max<size_t>(size_t(Src.n) * ld * 4, 256));
         kern::als_rotate(dS.f.as<float>(), nullptr, dS.rot.as<float>(), nullptr, Src.n,
                          lrQ.as<float>(), ld, cus, s);
@@ -731,7 +717,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         TraceRange tr(&ctx.metrics(), "als/half_users");
         half(hev[1], U, dU, I, dI);
       }
-      // one host wait per iteration (both halves queued back to back)
+      // one host wait per iteration (both halves queued back to back, nothing in between)
       if (dev_comm) comm.wait(s);
       hev[1].e3.sync();
       for (HalfEvents& E : hev) {

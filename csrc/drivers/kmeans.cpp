@@ -1614,10 +1614,21 @@ KMeansResult kmeans_fit_streamed(Context& ctx, Comm& comm, const float* host, in
   const int64_t cr = std::min<int64_t>(chunk_rows, std::max<int64_t>(rows, 1));
   Buffer dev[2] = {ctx.alloc(size_t(cr) * ld * 4), ctx.alloc(size_t(cr) * ld * 4)};
   for (auto& b : dev) OAP_HIP_CHECK(hipMemsetAsync(b.data(), 0, size_t(cr) * ld * 4, s));
-  bool registered = false;
-  if (rows > 0)
-    registered = hipHostRegister(const_cast<float*>(host), size_t(rows) * d * 4,
-                                 hipHostRegisterDefault) == hipSuccess;
+  // the caller's rows stay page-locked for the fit only: the guard unregisters them on every
+  // exit path (a CommError or an injected fault from the loop included)
+  struct HostRegistration {
+    void* p = nullptr;
+    hipStream_t s0 = nullptr, s1 = nullptr;  // drained first: no DMA may still read the rows
+    ~HostRegistration() {
+      if (!p) return;
+      (void)hipStreamSynchronize(s0);
+      (void)hipStreamSynchronize(s1);
+      (void)hipHostUnregister(p);
+    }
+  } registration{nullptr, s, hs};
+  if (rows > 0 && hipHostRegister(const_cast<float*>(host), size_t(rows) * d * 4,
+                                  hipHostRegisterDefault) == hipSuccess)
+    registration.p = const_cast<float*>(host);
   (void)hipGetLastError();  // (a refused registration leaves pageable DMA)
   Event loaded[2], used[2];
   used[0].record(s);
@@ -1718,7 +1729,6 @@ KMeansResult kmeans_fit_streamed(Context& ctx, Comm& comm, const float* host, in
     }
   }
   OAP_HIP_CHECK(hipStreamSynchronize(s));
-  if (registered) (void)hipHostUnregister(const_cast<float*>(host));
   res.centers.resize(kd);
   ctx.copy_to_host(res.centers.data(), c64.data(), sizeof(double) * kd, s);
   std::vector<u64> cnt(k);

@@ -322,6 +322,13 @@ void als_rotate(const float* in, const int32_t* in_rows, float* out, const int32
 void als_init_factors(const int32_t* ids, int64_t n, int r, int ld, uint64_t seed, float* out,
                       hipStream_t s);
 void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
+// ---- ALS Gramian eigenbasis on the device (kernels/als_eig.hip) ----------------------------
+// gram: fp64 r x r symmetric (device).  Q / QT: float [ld][ld] (eigenvectors as columns of Q,
+// identity padding), eig: float [ld] (max(lambda, 0), padding 1).  scratch: device bytes of
+// als_gram_eig_scratch_bytes(r) (fp64 V when it does not fit in LDS next to A).
+size_t als_gram_eig_scratch_bytes(int r);
+void als_gram_eig(const double* gram, int r, int ld, double* scratch, float* Q, float* QT,
+                  float* eig, hipStream_t s, int max_sweeps = 30, double tol = 1e-14);
 
 // cov = (S - c c^T / n) / (n - 1) from pca_reduce's [S | c] output, on the device
 void pca_cov(const double* stats, int d, int64_t n, double* cov, hipStream_t s);

@@ -426,11 +426,14 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
 // 16 at a time through LDS as fp64 [feature][row] planes (double buffered, one barrier per
 // chunk); an A or B fragment is ONE ds_read_b64 per lane.  The accumulators are fp64 for the
 // whole split: no intermediate flush, the slab is written once.
+// 8 waves (2 x 4) of 64 x 32 each: 8 accumulators (64 VGPRs) per wave — with 16 per wave the
+// f64 MFMA chain ran at under half its rate (measured: tools/mfma_f64_probe.hip, 71-78 TFLOP/s
+// with 8 independent accumulators per wave, 30-37 with 16).
 constexpr int kXTile = 128;
 constexpr int kXRows = 16;              // rows per LDS stage (4 k-steps of the 16x16x4 MFMA)
 constexpr int kXS = kXRows + 2;         // plane stride in doubles (36 dwords: 2-way at most)
 constexpr int kXPlane = kXTile * kXS;   // doubles per side plane
-constexpr int kXThreads = 256;
+constexpr int kXThreads = 512;
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
@@ -445,32 +448,27 @@ struct SyrkF64Args {
   double* cpart;        // [splits][nb][128]
 };
 
-// 8 features f0 .. f0+7 of one row.  VEC: 16-byte aligned rows and ld % 8 == 0, so a group is
+// 4 features f0 .. f0+3 of one row.  VEC: 16-byte aligned rows and ld % 4 == 0, so a group is
 // either wholly inside the row or wholly past it.
 template <typename T, bool VEC>
-__device__ inline void load8(const T* __restrict__ p, int f0, int ld, double (&v)[8]) {
+__device__ inline void load4(const T* __restrict__ p, int f0, int ld, double (&v)[4]) {
   if constexpr (VEC) {
     if (f0 < ld) {
       if constexpr (sizeof(T) == 4) {
         const float4 a = *reinterpret_cast<const float4*>(p + f0);
-        const float4 b = *reinterpret_cast<const float4*>(p + f0 + 4);
         v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
       } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double2 a = *reinterpret_cast<const double2*>(p + f0 + 2 * q);
-          v[2 * q] = a.x;
-          v[2 * q + 1] = a.y;
-        }
+        const double2 a = *reinterpret_cast<const double2*>(p + f0);
+        const double2 b = *reinterpret_cast<const double2*>(p + f0 + 2);
+        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = 0.0;
+      for (int q = 0; q < 4; ++q) v[q] = 0.0;
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = f0 + q < ld ? double(p[f0 + q]) : 0.0;
+    for (int q = 0; q < 4; ++q) v[q] = f0 + q < ld ? double(p[f0 + q]) : 0.0;
   }
 }
 
@@ -490,51 +488,51 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
   const T* __restrict__ X = static_cast<const T*>(a.x);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
-  // loader: row lr of the stage, features 8*lq .. 8*lq+7 of each side
-  const int lr = tid >> 4, lq = tid & 15;
-  const int fI = ti * kXTile + 8 * lq, fJ = tj * kXTile + 8 * lq;
-  double shI[8], shJ[8];
+  const int wi = wave >> 2, wj = wave & 3;  // 2 x 4 waves, 64 x 32 each
+  // loader: row lr of the stage, features 4*lq .. 4*lq+3 of each side
+  const int lr = tid >> 5, lq = tid & 31;
+  const int fI = ti * kXTile + 4 * lq, fJ = tj * kXTile + 4 * lq;
+  double shI[4], shJ[4];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < 4; ++q) {
     shI[q] = a.shift[fI + q];
     shJ[q] = a.shift[fJ + q];
   }
-  double vI[8] = {0, 0, 0, 0, 0, 0, 0, 0}, vJ[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  double cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double vI[4] = {0, 0, 0, 0}, vJ[4] = {0, 0, 0, 0};
+  double cs[4] = {0, 0, 0, 0};
   const int ld = int(a.ld);  // (< 2^31: checked on the host)
   // unconditional loads (row clamped to the split's last row): stage() masks what lies outside
   auto load = [&](int64_t r0) {
     const T* p = X + min(r0 + lr, r_end - 1) * a.ld;
-    load8<T, VEC>(p, fI, ld, vI);
-    if (!diag) load8<T, VEC>(p, fJ, ld, vJ);
+    load4<T, VEC>(p, fI, ld, vI);
+    if (!diag) load4<T, VEC>(p, fJ, ld, vJ);
   };
   // centre (fp64, exact for fp32 rows) and transpose into the planes; rows past r_end and
   // features past d contribute exact zeros
   auto stage = [&](double* buf, int64_t r0) {
     const bool okr = r0 + lr < r_end;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
+    for (int q = 0; q < 4; ++q) {
       const double c = (okr && fI + q < a.d) ? vI[q] - shI[q] : 0.0;
       if (diag) cs[q] += c;
-      buf[(8 * lq + q) * kXS + lr] = c;
+      buf[(4 * lq + q) * kXS + lr] = c;
     }
     if (!diag) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < 4; ++q) {
         const double c = (okr && fJ + q < a.d) ? vJ[q] - shJ[q] : 0.0;
-        buf[kXPlane + (8 * lq + q) * kXS + lr] = c;
+        buf[kXPlane + (4 * lq + q) * kXS + lr] = c;
       }
     }
   };
 
-  f64x4 acc[4][4];
+  f64x4 acc[4][2];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int y = 0; y < 2; ++y) acc[x][y] = f64x4{0.0, 0.0, 0.0, 0.0};
   // fragments: lane l holds A[i = l & 15][k = l >> 4] = plane[feature][row k]
-  const int fa = 64 * wi + (lane & 15), fb = 64 * wj + (lane & 15), kr = lane >> 4;
+  const int fa = 64 * wi + (lane & 15), fb = 32 * wj + (lane & 15), kr = lane >> 4;
   const int boff = diag ? 0 : kXPlane;
   int cur = 0;
   if (r_begin < r_end) {
@@ -547,15 +545,15 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     const double* buf = lds + cur * (2 * kXPlane);
 #pragma unroll
     for (int ks = 0; ks < kXRows / 4; ++ks) {
-      double av[4], bv[4];
+      double av[4], bv[2];
 #pragma unroll
       for (int x = 0; x < 4; ++x) av[x] = buf[(fa + 16 * x) * kXS + 4 * ks + kr];
 #pragma unroll
-      for (int y = 0; y < 4; ++y) bv[y] = buf[boff + (fb + 16 * y) * kXS + 4 * ks + kr];
+      for (int y = 0; y < 2; ++y) bv[y] = buf[boff + (fb + 16 * y) * kXS + 4 * ks + kr];
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
-        for (int y = 0; y < 4; ++y)
+        for (int y = 0; y < 2; ++y)
           acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
     }
     if (r0 + kXRows < r_end) {  // the other stage was last read before the previous barrier
@@ -570,16 +568,16 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y)
+    for (int y = 0; y < 2; ++y)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = 64 * wi + 16 * x + (lane >> 4) + 4 * e;
-        const int col = 64 * wj + 16 * y + (lane & 15);
+        const int col = 32 * wj + 16 * y + (lane & 15);
         slab[row * kXTile + col] = acc[x][y][e];
       }
   if (diag) {  // column sums over the 16 loader rows: through LDS (the stages are free now)
 #pragma unroll
-    for (int q = 0; q < 8; ++q) lds[lr * kXTile + 8 * lq + q] = cs[q];
+    for (int q = 0; q < 4; ++q) lds[lr * kXTile + 4 * lq + q] = cs[q];
     __syncthreads();
     if (tid < kXTile) {
       double v = 0.0;
@@ -694,9 +692,22 @@ PcaPlan pca_syrk_plan_f64(int64_t n, int d, int num_cus) {
   p.tw = kXTile;
   p.nb = (d + p.tw - 1) / p.tw;
   p.tiles = p.nb * (p.nb + 1) / 2;
-  const int64_t want = int64_t(std::max(num_cus, 64)) * 4;  // 2 resident per CU x 2 waves
-  int64_t s = (want + p.tiles - 1) / p.tiles;
+  // one 512-thread workgroup per CU: pick the split count whose (splits x tiles) workgroups
+  // fill whole rounds of the CUs (t = 36 tiles at d = 1000 -> 64 splits = 9 full rounds of 256),
+  // at least two rounds when the rows allow it
+  const int64_t R = std::max(num_cus, 64);
   const int64_t max_s = std::max<int64_t>(1, (n + 8 * kXRows - 1) / (8 * kXRows));
+  const int64_t s_lo = std::max<int64_t>(1, (2 * R + p.tiles - 1) / p.tiles);
+  int64_t s = s_lo;
+  double best = 1e30;
+  for (int64_t c = s_lo; c <= 4 * s_lo; ++c) {
+    const int64_t g = c * p.tiles;
+    const double waste = double((g + R - 1) / R * R) / double(g);
+    if (waste < best - 1e-9) {
+      best = waste;
+      s = c;
+    }
+  }
   s = std::max<int64_t>(1, std::min(s, max_s));
   const int64_t slab_tile = int64_t(p.tw) * p.tw * 8;
   while (s > 1 && s * p.tiles * slab_tile > (int64_t(1) << 30)) --s;
@@ -725,7 +736,7 @@ void pca_syrk_f64(const void* x, bool x_f64, int64_t n, int64_t ld, int d, const
   a.splits = p.splits;
   a.rows_per_split = p.rows_per_split;
   const size_t es = x_f64 ? 8 : 4;
-  const bool vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && ld % 8 == 0 &&
+  const bool vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && ld % 4 == 0 &&
                    (size_t(ld) * es) % 16 == 0;
   a.part = part;
   a.cpart = cpart;

@@ -188,6 +188,32 @@ def table_to_input(estimator, table):
     return vectors_from_arrow(table.column(cols[0]))
 
 
+def batches_to_input(estimator, batches) -> Any:
+    """This partition's Arrow record batches (mapInArrow) -> what estimator.fit accepts.  An
+    empty partition (no batches at all, e.g. after repartition(num_ranks) of a small frame)
+    yields an empty input instead of failing in Table.from_batches."""
+    import pyarrow as pa
+
+    batches = list(batches)
+    if not batches:
+        return _partition_to_input(estimator, [])
+    return table_to_input(estimator, pa.Table.from_batches(batches))
+
+
+def _agree_on_width(ctx, estimator, data):
+    """Vector estimators: a rank with no rows learns the feature count from its peers (barrier
+    allGather), so every rank enters the fit with the same d."""
+    from ..models.recommendation import ALS
+
+    if isinstance(estimator, ALS):
+        return data
+    d_local = int(data.shape[1]) if getattr(data, "ndim", 0) == 2 and len(data) else 0
+    d = max(int(v) for v in ctx.allGather(str(d_local)))
+    if len(data) == 0:
+        return np.zeros((0, d))
+    return data
+
+
 def _partition_to_input(estimator, rows: list):
     """Spark Rows of this partition (the pre-3.5 RDD barrier path) -> what estimator.fit
     accepts, column-wise through numpy (one pass over the rows per column)."""
@@ -249,7 +275,7 @@ def fit(estimator, df, num_ranks: int, spark_conf: dict | None = None):
         O.init_world(resolve(spark_conf=conf))
         est = est_cls(uid=est_uid)
         est._set(**est_params)
-        model = est.fit(make_input(est))
+        model = est.fit(_agree_on_width(ctx, est, make_input(est)))
         payload = export_model(model) if rank == 0 else None
         O.shutdown_world()
         ctx.barrier()
@@ -264,8 +290,8 @@ def fit(estimator, df, num_ranks: int, spark_conf: dict | None = None):
     def arrow_task(batches):  # Arrow barrier path: record batches
         import pyarrow as pa
 
-        table = pa.Table.from_batches(list(batches))
-        payload = run_rank(lambda est: table_to_input(est, table))
+        batches = list(batches)
+        payload = run_rank(lambda est: batches_to_input(est, batches))
         if payload is not None:
             keys = list(payload)
             yield pa.RecordBatch.from_arrays(

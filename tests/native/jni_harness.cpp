@@ -15,6 +15,9 @@
 #include <string>
 #include <vector>
 
+#include <sys/wait.h>
+#include <unistd.h>
+
 // ---------------------------------------------------------------- fake VM objects
 struct _jfieldID {
   std::string name, sig;
@@ -195,7 +198,94 @@ static std::vector<double> table_values(JNIEnv* env, jlong h) {
       ->v;
 }
 
-int main() {
+// ---- a 2-process world through the reference's KVS string: c_init(2, r, "127.0.0.1_<port>")
+// (OneCCL.scala:32-46 -> OneCCL.cpp:47-86), then K-Means on each rank's half of a 3-blob
+// dataset from the same initial centers; both ranks must return the single-process centers.
+static std::vector<double> blobs3(int n) {
+  std::vector<double> X;
+  for (int i = 0; i < n; ++i) {
+    const int c = i % 3;
+    for (int j = 0; j < 3; ++j)
+      X.push_back(10.0 * c + j + 0.01 * double((i * 37 + j * 11) % 17) - 0.08);
+  }
+  return X;
+}
+
+static std::vector<double> kmeans_rank(JNIEnv* env, int world, int rank, const std::string& kvs,
+                                       double* cost) {
+  FakeObject* param = make_obj("CCLParam");
+  auto* ipport = new FakeString;
+  ipport->s = kvs;
+  REQUIRE(Java_org_apache_spark_ml_util_OneCCL_00024_c_1init(env, nullptr, world, rank, ipport,
+                                                             param) == 0);
+  REQUIRE(g_errors.empty());
+  REQUIRE(param->vals.at("commSize") == world && param->vals.at("rankId") == rank);
+  const int n = 300;
+  const std::vector<double> X = blobs3(n);
+  std::vector<double> mine;
+  for (int i = rank; i < n; i += world)  // a strided (non-range) partition
+    mine.insert(mine.end(), X.begin() + 3 * i, X.begin() + 3 * i + 3);
+  const jlong xt = table_from(env, mine, 3);
+  const jlong ct = table_from(env, std::vector<double>(X.begin(), X.begin() + 9), 3);
+  FakeObject* kres = make_obj("KMeansResult");
+  const jlong centers =
+      Java_org_apache_spark_ml_clustering_KMeansDALImpl_cKMeansDALComputeWithInitCenters(
+          env, nullptr, xt, ct, 3, 1e-6, 20, world, 1, kres);
+  REQUIRE(g_errors.empty() && centers != 0);
+  *cost = kres->vals.at("totalCost");
+  std::vector<double> cv = table_values(env, centers);
+  for (jlong h : {xt, ct, centers})
+    Java_org_apache_spark_ml_util_OneDAL_00024_cFreeDataMemory(env, nullptr, h);
+  Java_org_apache_spark_ml_util_OneCCL_00024_c_1cleanup(env, nullptr);
+  return cv;
+}
+
+static int world2(const char* port) {
+  const std::string kvs = std::string("127.0.0.1_") + port;
+  int fds[2][2];
+  pid_t pid[2];
+  for (int r = 0; r < 2; ++r) {  // fork before anything initialises a runtime
+    REQUIRE(pipe(fds[r]) == 0);
+    pid[r] = fork();
+    REQUIRE(pid[r] >= 0);
+    if (pid[r] == 0) {
+      close(fds[r][0]);
+      JNIEnv e;
+      double cost = 0.0;
+      std::vector<double> cv = kmeans_rank(&e, 2, r, kvs, &cost);
+      cv.push_back(cost);
+      const ssize_t w = write(fds[r][1], cv.data(), cv.size() * sizeof(double));
+      _exit(w == ssize_t(cv.size() * sizeof(double)) ? 0 : 3);
+    }
+    close(fds[r][1]);
+  }
+  std::vector<double> got[2];
+  for (int r = 0; r < 2; ++r) {
+    got[r].resize(10);
+    size_t off = 0;
+    while (off < 10 * sizeof(double)) {
+      const ssize_t n = read(fds[r][0], reinterpret_cast<char*>(got[r].data()) + off,
+                             10 * sizeof(double) - off);
+      if (n <= 0) break;
+      off += size_t(n);
+    }
+    int st = 0;
+    waitpid(pid[r], &st, 0);
+    REQUIRE(WIFEXITED(st) && WEXITSTATUS(st) == 0 && off == 10 * sizeof(double));
+  }
+  JNIEnv e;
+  double cost1 = 0.0;
+  std::vector<double> one = kmeans_rank(&e, 1, 0, kvs, &cost1);
+  for (int r = 0; r < 2; ++r) {
+    for (int j = 0; j < 9; ++j) REQUIRE(std::fabs(got[r][j] - one[j]) < 1e-12);
+    REQUIRE(std::fabs(got[r][9] - cost1) < 1e-9 * (1.0 + cost1));
+  }
+  std::printf("JNI_WORLD2_OK\n");
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc == 3 && std::string(argv[1]) == "world2") return world2(argv[2]);
   JNIEnv env_obj;
   JNIEnv* env = &env_obj;
 
@@ -331,6 +421,34 @@ int main() {
       }
     }
   REQUIRE(fit_pos / npos > fit_neg / nneg);  // implicit preference: observed pairs score higher
+
+  // ---- bufferToCSRNumericTable's leading empty row (ALSDALImpl.scala:198-222): a partition
+  // whose lowest key is unrated emits offsets [1, 1, ...] (csrRowNum + 2 entries); an empty
+  // partition emits [1, 1] with csrRowNum = 0
+  {
+    auto* v2 = new FakeFloats;
+    auto *c2 = new FakeLongs, *o2 = new FakeLongs;
+    v2->v = {1.f, 2.f, 3.f};
+    c2->v = {1, 3, 2};
+    o2->v = {1, 1, 3, 4};  // leading empty row, then rows {1,3} and {2}
+    const jlong h2 = Java_org_apache_spark_ml_util_OneDAL_00024_cNewCSRNumericTable(
+        env, nullptr, v2, c2, o2, 3, 2);
+    REQUIRE(g_errors.empty() && h2 != 0);
+    Java_org_apache_spark_ml_util_OneDAL_00024_cFreeCSRTable(env, nullptr, h2);
+    auto* v3 = new FakeFloats;
+    auto *c3 = new FakeLongs, *o3 = new FakeLongs;
+    o3->v = {1, 1};
+    const jlong h3 = Java_org_apache_spark_ml_util_OneDAL_00024_cNewCSRNumericTable(
+        env, nullptr, v3, c3, o3, 3, 0);
+    REQUIRE(g_errors.empty() && h3 != 0);
+    Java_org_apache_spark_ml_util_OneDAL_00024_cFreeCSRTable(env, nullptr, h3);
+    auto* o4 = new FakeLongs;
+    o4->v = {1, 2, 3, 4};  // rows + 2 entries without the leading empty row: rejected
+    Java_org_apache_spark_ml_util_OneDAL_00024_cNewCSRNumericTable(env, nullptr, v2, c2, o4, 3,
+                                                                  2);
+    REQUIRE(!g_errors.empty());
+    g_errors.clear();
+  }
 
   // ---- a wrong field type is caught like a real VM would (NoSuchFieldError, nothing written)
   FakeObject* wrong = make_obj("KMeansResult");

@@ -131,3 +131,22 @@ def test_lowrank_path_matches_direct_and_oracle(native, gpu_world, monkeypatch, 
         scale = np.abs(rk).max()
         np.testing.assert_allclose(lr[key], direct[key], atol=1e-3 * scale)
         np.testing.assert_allclose(lr[key], rk, atol=2e-3 * scale)
+
+
+@pytest.mark.parametrize("r", [1, 2, 7, 33, 64, 100, 101, 128])
+def test_device_gram_eig_matches_numpy(native, gpu_world, r):
+    """kernels/als_eig.hip: the fp64 parallel Jacobi that feeds the low-rank solve (no host
+    round trip) against numpy.linalg.eigh, including the V-in-global variant (r > 100)."""
+    rng = np.random.default_rng(r)
+    Y = rng.normal(size=(4 * r + 5, r)) * np.geomspace(10, 0.01, r)
+    G = Y.T @ Y
+    Q, QT, e = native.als_gram_eig(gpu_world.ctx, G)
+    ld = Q.shape[0]
+    Qr = Q[:r, :r].astype(np.float64)
+    np.testing.assert_array_equal(Q, QT.T)
+    np.testing.assert_allclose(Qr.T @ Qr, np.eye(r), atol=2e-6)
+    recon = (Qr * e[:r].astype(np.float64)) @ Qr.T
+    assert np.max(np.abs(recon - G)) < 2e-6 * np.max(np.abs(G))
+    np.testing.assert_allclose(np.sort(e[:r]), np.sort(np.linalg.eigvalsh(G)),
+                               rtol=0, atol=1e-6 * np.max(np.abs(G)))
+    assert np.all(e[r:] == 1.0) and np.all(Q[r:, r:] == np.eye(ld - r))

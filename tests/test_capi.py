@@ -197,3 +197,34 @@ def test_jni_shim_runs_against_recording_vm(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
                        env={**__import__("os").environ, "HIP_VISIBLE_DEVICES": ""})
     assert r.returncode == 0 and "JNI_HARNESS_OK" in r.stdout, r.stdout + r.stderr
+
+
+def test_jni_c_init_kvs_two_process_world(tmp_path):
+    """The reference's rendezvous contract end to end: two executor processes call
+    c_init(2, rank, "127.0.0.1_<port>") (OneCCL.scala:32-46, OneCCL.cpp:47-86); rank 0 serves the
+    store at that address, the host collectives run over it (CPU engine), and
+    cKMeansDALComputeWithInitCenters returns the single-process centers on both ranks."""
+    import shutil
+    import socket
+    import subprocess
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    lib = root / "oap_mllib_amd" / "liboap_mllib.so"
+    if cxx is None or not lib.exists():
+        pytest.skip("needs a host C++ compiler and the built liboap_mllib.so")
+    exe = tmp_path / "jni_harness"
+    r = subprocess.run([cxx, "-std=c++17", "-O1", "-Wall", "-Werror",
+                        f"-I{root / 'tests/native/jni_stub'}", f"-I{root / 'csrc'}",
+                        str(root / "tests/native/jni_harness.cpp"),
+                        str(root / "csrc/jni/oap_jni.cpp"), f"-L{lib.parent}", "-loap_mllib",
+                        f"-Wl,-rpath,{lib.parent}", "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    with socket.socket() as s:  # a free port for rank 0's store
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([str(exe), "world2", str(port)], capture_output=True, text=True,
+                       timeout=120, env={**__import__("os").environ, "HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode == 0 and "JNI_WORLD2_OK" in r.stdout, r.stdout + r.stderr

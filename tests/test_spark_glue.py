@@ -73,6 +73,27 @@ def test_arrow_vector_column_to_matrix():
     assert S._input_columns(O.PCA(inputCol="v")) == ["v"]
 
 
+def test_empty_arrow_partition():
+    """mapInArrow hands an empty partition no record batches at all: the rank
+    still gets a (0-row) input, and vector estimators learn d from their peers."""
+    import pyarrow as pa
+
+    X = S.batches_to_input(O.KMeans(), [])
+    assert X.shape[0] == 0
+    r = S.batches_to_input(O.ALS(), iter([]))
+    assert len(r["user"]) == len(r["item"]) == len(r["rating"]) == 0
+    b = pa.RecordBatch.from_pydict({"user": [1], "item": [2], "rating": [3.0]})
+    assert S.batches_to_input(O.ALS(), [b])["item"].tolist() == [2]
+
+    class Ctx:  # BarrierTaskContext.allGather of the peers' widths
+        def allGather(self, v):
+            return [v, "6"]
+
+    assert S._agree_on_width(Ctx(), O.KMeans(), X).shape == (0, 6)
+    full = np.ones((3, 6))
+    assert S._agree_on_width(Ctx(), O.PCA(), full) is full
+
+
 @pytest.mark.skipif(not S.spark_available(), reason="pyspark not installed")
 def test_barrier_fit_local_spark():  # pragma: no cover - needs pyspark
     from pyspark.ml.linalg import Vectors as SV
