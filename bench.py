@@ -153,17 +153,29 @@ def bench_kmeans(args, w):
     samples = rows_total * args.steps / el_max
     flops = 2.0 * rows_total * k * d
     comm_name = getattr(w.comm, "name", "none") if w.comm is not None else "none"
-    kpad = -(-k // 32) * 32
-    if args.precise:
-        path = "fp32-exact MFMA"
-    elif d <= 128 and kpad > N.kmeans_lds_kmax(d, False):
-        path = ("chunked large-k passes: tiered bf16 MFMA distances per centroid chunk (merge "
-                "mode, exact-fp32 re-decision of near ties; assignments identical to exact fp32), "
-                "label-driven binned accumulation")
-    else:
-        path = ("lean pass: one fp16 MFMA product per k-step (v_mfma_f32_32x32x16_f16) with a "
-                "rigorous error bound; rows inside it re-decided by the exact fp32 MFMA argmin "
-                "(assignments identical to exact fp32); delta accumulation of moved rows")
+    # the label names the kernel path the timed fit's last iteration actually took
+    # (kmeans_fit's assign_path), described for the record
+    described = {
+        "lean_fp16": "lean pass: one fp16 MFMA product per k-step (v_mfma_f32_32x32x16_f16) with "
+                     "a rigorous error bound; rows inside it re-decided by the exact fp32 MFMA "
+                     "argmin (assignments identical to exact fp32)",
+        "lean_fp16_delta": "lean fp16 MFMA pass + exact fp32 re-decision; delta accumulation "
+                           "of moved rows",
+        "lean_fp16_delta_scan": "bound scan + lean fp16 MFMA pass over the listed tiles + exact "
+                                "fp32 re-decision; delta accumulation of moved rows",
+        "lean_fp16_centroid_chunked": "centroid-chunked lean fp16 MFMA pass (running top-2 keys "
+                                      "across centroid chunks) + chunked exact fp32 re-decision; "
+                                      "label-driven binned accumulation",
+        "lean_fp16_centroid_chunked_delta": "centroid-chunked lean fp16 MFMA pass + chunked "
+                                            "exact fp32 re-decision; binned accumulation of the "
+                                            "moved rows only",
+        "tiered_bf16_mfma": "tiered bf16 MFMA distances (exact-fp32 re-decision of near ties)",
+        "tiered_bf16_mfma_chunked": "centroid-chunked tiered bf16 MFMA distances",
+        "exact_fp32_mfma": "fp32-exact MFMA (v_mfma_f32_32x32x2_f32)",
+        "wide_mfma": "wide-row MFMA tier-1 + exact re-decision (d > 128)",
+    }
+    path = r.get("assign_path", "unknown")
+    path_desc = described.get(path, path)
     extra = {"fit_wall_s_end_to_end": fit_s, "fit_iters": fit_iters,
              "init_kmeans_parallel_s": init_s, "init_phases_ms": init_phases,
              "ingest_synth_s": ingest_s,
@@ -193,6 +205,7 @@ def bench_kmeans(args, w):
              "rccl_ranks": w.size if comm_name == "rccl" else 0,
              "world_size": w.size,
              "distance_path": path,
+             "distance_path_desc": path_desc,
              "cost": r["cost"]}
     del table
     if args.separable_extra and args.sigma != 1.0:

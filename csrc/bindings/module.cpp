@@ -515,6 +515,7 @@ PYBIND11_MODULE(_native, m) {
         out["refine_tiles"] = r.refine_tiles;
         out["tier3_tiles"] = r.tier3_tiles;
         out["pruned_tiles"] = r.pruned_tiles;
+        out["assign_path"] = r.assign_path;
         out["deferred_rows"] = r.deferred_rows;
         out["moved_rows"] = r.moved_rows;
         return out;

@@ -290,6 +290,10 @@ size_t lean_defer_bytes(int64_t rows, int d, int num_cus, int* grid, int64_t* ca
   return sizeof(int32_t) * size_t(*grid) * size_t(*cap) + sizeof(unsigned) * 16 * size_t(*grid);
 }
 
+// The distance path the last gpu_assign of this thread took (reported with the fit result, so
+// a benchmark names the kernel that actually ran).
+thread_local const char* t_assign_path = "none";
+
 // Returns the number of cost partials written to req.cost_slab.
 int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const AssignReq& req,
                hipStream_t s) {
@@ -353,6 +357,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
         a.tile_count = req.tile_count;
       }
     }
+    t_assign_path = req.delta ? (req.tile_list ? "lean_fp16_delta_scan" : "lean_fp16_delta")
+                              : "lean_fp16";
     kern::kmeans_lloyd(a, grid, lean_variant(x.cols), s);
     kern::KMeansAssignArgs b = a;
     b.defer_rows = nullptr;
@@ -380,6 +386,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
       labels = lab.as<int32_t>();
     }
     a.labels = labels;
+    t_assign_path = "wide_mfma";
     dbuf = ctx.alloc(sizeof(int32_t) * size_t(x.rows) + 64);
     unsigned* dcount = reinterpret_cast<unsigned*>(dbuf.as<int32_t>() + x.rows);
     kern::kmeans_wide_assign(a, ctx.info().cu_count, dbuf.as<int32_t>(), dcount, s);
@@ -407,6 +414,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
       a.tile_list = req.tile_list;
       a.tile_count = req.tile_count;
     }
+    t_assign_path = req.precise ? "exact_fp32_mfma" : "tiered_bf16_mfma";
     return kern::kmeans_assign(a, ctx.info().cu_count, s);
   }
   OAP_CHECK(!req.delta, "kmeans delta accumulation is single-launch only");
@@ -417,6 +425,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     // fp32 centers carrying (best, index); labels drive the binned accumulation.
     const int lk = kern::kmeans_lloyd_chunk_kmax(x.cols);
     const int ek = kern::kmeans_exact_chunk_kmax(x.cols);
+    t_assign_path = req.stats_persist && req.prev_labels ? "lean_fp16_centroid_chunked_delta"
+                                                         : "lean_fp16_centroid_chunked";
     auto split = [&](int cap, int* n) {
       *n = (g.k + cap - 1) / cap;
       return static_cast<int>(round_up((g.k + *n - 1) / *n, 32));
@@ -511,6 +521,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     return a.cost_slab ? 2 * grid : 0;
   }
   // ---- chunked path (more centroids than one LDS plan holds)
+  t_assign_path = "tiered_bf16_mfma_chunked";
   Buffer lab, dist;
   int32_t* labels = req.labels;
   float* mind = req.mindist;
@@ -1523,6 +1534,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   M.set_value("kmeans/refine_tiles", double(res.refine_tiles));
   M.set_value("kmeans/samples_per_sec",
               res.iter_seconds > 0 ? double(x.global_rows) * res.num_iter / res.iter_seconds : 0);
+  res.assign_path = t_assign_path;
   return res;
 }
 

@@ -16,6 +16,13 @@ __host__ __device__ inline size_t round16(size_t v) { return (v + 15) / 16 * 16;
 __host__ __device__ inline int stride_bf16(int dp) { return dp + 8; }  // (dp+8)/8 odd slots
 __host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)/4 odd slots
 
+// v_med3_i32 as a pure operation (schedulable: no volatile)
+__device__ inline int med3_i32_pure(int a, int b, int c) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ inline int med3_i32(int a, int b, int c) {
   int r;
   asm volatile("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));

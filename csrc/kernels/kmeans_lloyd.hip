@@ -394,31 +394,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         k1 = min(k1, (__float_as_int(acc[0]) & ~0x3ff) | (c0 + 4 * h));
         return;
       }
-      int t1[4], t2[4];
       // padded centers carry the largest finite bias: they never win, so no chunk needs a
-      // branch for them
+      // branch for them.  Keys (one v_and_or each) fold into the chunk's top-2 two at a time:
+      // with t1 <= t2, the smallest of {t1, t2, a, b} is min3(t1, a, b) and the second smallest
+      // min(t2, med3(t1, a, b)) — 3 VALU per 2 keys (the old 4-lane tree took 4 per 2 keys
+      // plus 12 to merge its lanes)
+      int key[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int off = 8 * (e >> 2) + (e & 3);
-        const int key = (__float_as_int(acc[e]) & ~0x3ff) | off;
-        const int q = e & 3;
-        if (e < 4) {
-          t1[q] = key;
-          t2[q] = 0x7fffffff;
-        } else {
-          t2[q] = med3_i32(t1[q], t2[q], key);  // 2nd smallest of {t1, t2, key}, t1 <= t2
-          t1[q] = min(t1[q], key);
-        }
+      for (int e = 0; e < 16; ++e)
+        key[e] = (__float_as_int(acc[e]) & ~0x3ff) | (8 * (e >> 2) + (e & 3));
+      int t1 = min(key[0], key[1]), t2 = max(key[0], key[1]);
+#pragma unroll
+      for (int e = 2; e < 16; e += 2) {
+        t2 = min(t2, med3_i32_pure(t1, key[e], key[e + 1]));
+        t1 = min(min(t1, key[e]), key[e + 1]);
       }
-      auto merge2 = [](int& x1, int& x2, int y1, int y2) {
-        x2 = min(max(x1, y1), min(x2, y2));
-        x1 = min(x1, y1);
-      };
-      merge2(t1[0], t2[0], t1[1], t2[1]);
-      merge2(t1[2], t2[2], t1[3], t2[3]);
-      merge2(t1[0], t2[0], t1[2], t2[2]);
       const int base = c0 + 4 * h + kbase;  // disjoint from every in-chunk offset's bits
-      const int i1 = t1[0] | base, i2 = t2[0] | base;
+      const int i1 = t1 | base, i2 = t2 | base;
       k2 = min(max(k1, i1), min(k2, i2));
       k1 = min(k1, i1);
     };

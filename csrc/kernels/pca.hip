@@ -430,8 +430,8 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
 // f64 MFMA chain ran at under half its rate (measured: tools/mfma_f64_probe.hip, 71-78 TFLOP/s
 // with 8 independent accumulators per wave, 30-37 with 16).
 constexpr int kXTile = 128;
-constexpr int kXRows = 16;              // rows per LDS stage (4 k-steps of the 16x16x4 MFMA)
-constexpr int kXS = kXRows + 2;         // plane stride in doubles (36 dwords: 2-way at most)
+constexpr int kXRows = 32;              // rows per LDS stage (8 k-steps of the 16x16x4 MFMA)
+constexpr int kXS = kXRows + 2;         // plane stride in doubles (68 dwords: conflict-free)
 constexpr int kXPlane = kXTile * kXS;   // doubles per side plane
 constexpr int kXThreads = 512;
 
@@ -489,7 +489,8 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wi = wave >> 2, wj = wave & 3;  // 2 x 4 waves, 64 x 32 each
-  // loader: row lr of the stage, features 4*lq .. 4*lq+3 of each side
+  // loader: rows lr + 16 j (j < kXRows / 16) of the stage, features 4*lq .. 4*lq+3 of each side
+  constexpr int kRpt = kXRows / 16;
   const int lr = tid >> 5, lq = tid & 31;
   const int fI = ti * kXTile + 4 * lq, fJ = tj * kXTile + 4 * lq;
   double shI[4], shJ[4];
@@ -498,30 +499,40 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     shI[q] = a.shift[fI + q];
     shJ[q] = a.shift[fJ + q];
   }
-  double vI[4] = {0, 0, 0, 0}, vJ[4] = {0, 0, 0, 0};
+  double vI[kRpt][4], vJ[kRpt][4];
+#pragma unroll
+  for (int j = 0; j < kRpt; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) vI[j][q] = vJ[j][q] = 0.0;
   double cs[4] = {0, 0, 0, 0};
   const int ld = int(a.ld);  // (< 2^31: checked on the host)
   // unconditional loads (row clamped to the split's last row): stage() masks what lies outside
   auto load = [&](int64_t r0) {
-    const T* p = X + min(r0 + lr, r_end - 1) * a.ld;
-    load4<T, VEC>(p, fI, ld, vI);
-    if (!diag) load4<T, VEC>(p, fJ, ld, vJ);
+#pragma unroll
+    for (int j = 0; j < kRpt; ++j) {
+      const T* p = X + min(r0 + lr + 16 * j, r_end - 1) * a.ld;
+      load4<T, VEC>(p, fI, ld, vI[j]);
+      if (!diag) load4<T, VEC>(p, fJ, ld, vJ[j]);
+    }
   };
   // centre (fp64, exact for fp32 rows) and transpose into the planes; rows past r_end and
   // features past d contribute exact zeros
   auto stage = [&](double* buf, int64_t r0) {
-    const bool okr = r0 + lr < r_end;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const double c = (okr && fI + q < a.d) ? vI[q] - shI[q] : 0.0;
-      if (diag) cs[q] += c;
-      buf[(4 * lq + q) * kXS + lr] = c;
-    }
-    if (!diag) {
+    for (int j = 0; j < kRpt; ++j) {
+      const bool okr = r0 + lr + 16 * j < r_end;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double c = (okr && fJ + q < a.d) ? vJ[q] - shJ[q] : 0.0;
-        buf[kXPlane + (4 * lq + q) * kXS + lr] = c;
+        const double c = (okr && fI + q < a.d) ? vI[j][q] - shI[q] : 0.0;
+        if (diag) cs[q] += c;
+        buf[(4 * lq + q) * kXS + lr + 16 * j] = c;
+      }
+      if (!diag) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double c = (okr && fJ + q < a.d) ? vJ[j][q] - shJ[q] : 0.0;
+          buf[kXPlane + (4 * lq + q) * kXS + lr + 16 * j] = c;
+        }
       }
     }
   };
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     __syncthreads();
     if (tid < kXTile) {
       double v = 0.0;
-      for (int q = 0; q < kXRows; ++q) v += lds[q * kXTile + tid];
+      for (int q = 0; q < 16; ++q) v += lds[q * kXTile + tid];
       a.cpart[(size_t(split) * a.nb + ti) * kXTile + tid] = v;
     }
   }
