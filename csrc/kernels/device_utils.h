@@ -10,6 +10,14 @@
 namespace oap {
 namespace kern {
 
+// Workgroup barrier that waits for this wave's LDS operations only.  __syncthreads() adds a
+// workgroup-scope release fence, which on gfx9-family waitcnt semantics (vmcnt counts loads AND
+// stores) drains every outstanding global load — it defeats register prefetch of the next
+// chunk's rows across the barrier.  Use this where the barrier only orders LDS traffic.
+__device__ inline void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

@@ -21,9 +21,10 @@
 //   so centers and typical rows sit in fp16's normal range; a row too large for it
 //   (alpha^2 |x|^2 >= 2^20) is simply deferred.
 // * Bias features carry both norms through the MFMA as hi/lo pairs scaled by 2^-4:
-//   x' = [alpha x, 16, 16, hi, lo (alpha^2 |x|^2 / 16)], c' = [-2 alpha c, hi, lo
-//   (alpha^2 |c|^2 / 16), 16, 16], so the accumulator ends at alpha^2 |x - c|^2 with no seeding
-//   VALU and only the cross term carrying fp16 error.
+//   x' = [alpha x, 0.., 16, 16, hi, lo (alpha^2 |x|^2 / 16)], c' = [-2 alpha c, 0.., hi, lo
+//   (alpha^2 |c|^2 / 16), 16, 16] (the four bias slots are the last four of the k-steps), so the
+//   accumulator ends at alpha^2 |x - c|^2 with no seeding VALU and only the cross term carrying
+//   fp16 error.
 // * Only the fp16 plane lives in LDS: the fixed-point fp64 accumulator fits beside it and the
 //   workgroup has 16 waves (4 per SIMD), so one wave's VALU epilogue, another's MFMAs and a
 //   third's HBM loads overlap.
@@ -160,19 +161,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const float alpha = lean_alpha(cmax);
   const float a2 = alpha * alpha;
 
-  // ---- stage c' = [-2 alpha c, hi, lo (alpha^2 |c|^2 / 16), 16, 16] (fp16) once per workgroup
+  // ---- stage c' = [-2 alpha c, 0 .., hi, lo (alpha^2 |c|^2 / 16), 16, 16] (fp16) once per
+  // workgroup; the four bias features sit in the LAST four slots (DP - 4 .. DP - 1, d <= DP - 4
+  // by the choice of KS), i.e. in the h = 1 lanes' j = 4..7 of the last k-step for every d: the
+  // per-tile operand build then patches two fixed dwords instead of testing every slot against
+  // a lane-dependent position (24 hoisted lane masks -> SGPR spills -> v_readlane per use)
   for (int idx = tid; idx < kpad * DP; idx += NT) {
     const int c = idx / DP, f = idx - c * DP;
     _Float16 v;
     if (f < d) {
       v = static_cast<_Float16>(-2.f * alpha * a.centers[idx]);
-    } else if (f == d || f == d + 1) {
+    } else if (f == DP - 4 || f == DP - 3) {
       _Float16 hi, lo;
       // padded centers: the largest finite bias (their distance never wins)
       split_f16((c < k) ? a2 * a.cnorm[c] * (1.f / kBiasUnit) : 60000.f, hi, lo);
-      v = (f == d) ? hi : lo;
+      v = (f == DP - 4) ? hi : lo;
     } else {
-      v = static_cast<_Float16>((f == d + 2 || f == d + 3) ? kBiasUnit : 0.f);
+      v = static_cast<_Float16>(f >= DP - 2 ? kBiasUnit : 0.f);
     }
     ph[c * sb + f] = v;
   }
@@ -212,7 +217,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   int32_t* dseg = a.defer_rows + blockIdx.x * a.seg_cap + wave * sub_cap;
   unsigned n_def = 0;  // wave-uniform
   double my_cost = 0.0;
-  const int jb = d - 16 * (KS - 1) - 8 * h;  // lane-local slot of bias feature d (may be < 0)
 
   auto tile_of = [&](int64_t q) -> int64_t {
     if (npos == 0) return 0;  // (prefetch of an empty range: any real tile)
@@ -353,13 +357,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           v[j] = q[0];
           v[j + 1] = q[1];
         }
-        if (s == KS - 1) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            v[j] = (j == jb || j == jb + 1) ? unit : v[j];
-            v[j] = (j == jb + 2) ? nh : v[j];
-            v[j] = (j == jb + 3) ? nl : v[j];
-          }
+        if (s == KS - 1) {  // h = 1 lanes: slots 4..7 = [16, 16, hi, lo] (x is 0 there)
+          v[4] = h ? unit : v[4];
+          v[5] = h ? unit : v[5];
+          v[6] = h ? nh : v[6];
+          v[7] = h ? nl : v[7];
         }
         xh[s] = v;
       }

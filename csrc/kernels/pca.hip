@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
     stage(lds, r_begin, 0, vIa, shI, diag);
     if (!diag) stage(lds, r_begin, 1, vJa, shJ, false);
     if (r_begin + kChunk < r_end) load(r_begin + kChunk, vIb, vJb);
-    __syncthreads();
+    lds_barrier();
   }
   // one chunk: MFMAs on LDS buffer `cur`; rows of chunk r0 + 2 kChunk -> (nI, nJ) (the set that
   // held chunk r0, already staged); chunk r0 + kChunk from (sI, sJ) -> the other LDS buffer
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kSyrkThreads, 2) void oap_pca_syrk(SyrkArgs a) {
       stage(nb, r0 + kChunk, 0, sI, shI, diag);
       if (!diag) stage(nb, r0 + kChunk, 1, sJ, shJ, false);
     }
-    __syncthreads();
+    lds_barrier();
     cur ^= 1;
     if (++since == a.flush_chunks) {
       flush();
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
     stage(lds, r_begin, 0, vI, shI, diag);
     if (!diag) stage(lds, r_begin, 1, vJ, shJ, false);
     if (r_begin + kChunk2 < r_end) load(r_begin + kChunk2);
-    __syncthreads();
+    lds_barrier();
   }
   for (int64_t r0 = r_begin; r0 < r_end; r0 += kChunk2) {
     const __bf16* buf = lds + cur * (4 * kPlane2);
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(kSyrk2Threads) void oap_pca_syrk_w256(SyrkArgs a) {
       if (!diag) stage(nb, r0 + kChunk2, 1, vJ, shJ, false);
       if (r0 + 2 * kChunk2 < r_end) load(r0 + 2 * kChunk2);
     }
-    __syncthreads();
+    lds_barrier();
     cur ^= 1;
     if (++since == flush_every) {
       flush();
@@ -448,27 +448,25 @@ struct SyrkF64Args {
   double* cpart;        // [splits][nb][128]
 };
 
-// 4 features f0 .. f0+3 of one row.  VEC: 16-byte aligned rows and ld % 4 == 0, so a group is
-// either wholly inside the row or wholly past it.
+// 4 features f0 .. f0+3 of one row, loaded unconditionally (a group past the row end reads the
+// row's first group instead; stage() zeroes every feature >= d): a conditional load ends in a
+// divergent region whose join waits for it (s_waitcnt vmcnt(0) right behind each load), which
+// serialised the row prefetch.  VEC: 16-byte aligned rows and ld % 4 == 0.
 template <typename T, bool VEC>
-__device__ inline void load4(const T* __restrict__ p, int f0, int ld, double (&v)[4]) {
+__device__ inline void load4(const T* __restrict__ p, int f0, int ld, T (&v)[4]) {
   if constexpr (VEC) {
-    if (f0 < ld) {
-      if constexpr (sizeof(T) == 4) {
-        const float4 a = *reinterpret_cast<const float4*>(p + f0);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-      } else {
-        const double2 a = *reinterpret_cast<const double2*>(p + f0);
-        const double2 b = *reinterpret_cast<const double2*>(p + f0 + 2);
-        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
-      }
+    const int fl = f0 < ld ? f0 : 0;
+    if constexpr (sizeof(T) == 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p + fl);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
     } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = 0.0;
+      const double2 a = *reinterpret_cast<const double2*>(p + fl);
+      const double2 b = *reinterpret_cast<const double2*>(p + fl + 2);
+      v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = f0 + q < ld ? double(p[f0 + q]) : 0.0;
+    for (int q = 0; q < 4; ++q) v[q] = p[min(f0 + q, ld - 1)];
   }
 }
 
@@ -499,11 +497,13 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     shI[q] = a.shift[fI + q];
     shJ[q] = a.shift[fJ + q];
   }
-  double vI[kRpt][4], vJ[kRpt][4];
+  // the rows stay in their storage type until stage() widens them: a conversion right behind
+  // the load would wait for it (the prefetch must stay in flight under a chunk of MFMAs)
+  T vI[kRpt][4], vJ[kRpt][4];
 #pragma unroll
   for (int j = 0; j < kRpt; ++j)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) vI[j][q] = vJ[j][q] = 0.0;
+    for (int q = 0; q < 4; ++q) vI[j][q] = vJ[j][q] = T(0);
   double cs[4] = {0, 0, 0, 0};
   const int ld = int(a.ld);  // (< 2^31: checked on the host)
   // unconditional loads (row clamped to the split's last row): stage() masks what lies outside
@@ -512,27 +512,33 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     for (int j = 0; j < kRpt; ++j) {
       const T* p = X + min(r0 + lr + 16 * j, r_end - 1) * a.ld;
       load4<T, VEC>(p, fI, ld, vI[j]);
-      if (!diag) load4<T, VEC>(p, fJ, ld, vJ[j]);
+      load4<T, VEC>(p, fJ, ld, vJ[j]);  // (diagonal tiles re-read their own block: no branch)
     }
   };
   // centre (fp64, exact for fp32 rows) and transpose into the planes; rows past r_end and
-  // features past d contribute exact zeros
+  // features past d contribute exact zeros — through 0/1 factors, not branches (the loaded
+  // values are finite data either way: rows clamped, groups clamped)
+  double mI[4], mJ[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    mI[q] = fI + q < a.d ? 1.0 : 0.0;
+    mJ[q] = fJ + q < a.d ? 1.0 : 0.0;
+  }
   auto stage = [&](double* buf, int64_t r0) {
 #pragma unroll
     for (int j = 0; j < kRpt; ++j) {
-      const bool okr = r0 + lr + 16 * j < r_end;
+      const double mr = r0 + lr + 16 * j < r_end ? 1.0 : 0.0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double c = (okr && fI + q < a.d) ? vI[j][q] - shI[q] : 0.0;
-        if (diag) cs[q] += c;
+        const double c = (double(vI[j][q]) - shI[q]) * (mr * mI[q]);
+        cs[q] += c;  // (only the diagonal tiles store their column sums)
         buf[(4 * lq + q) * kXS + lr + 16 * j] = c;
       }
       if (!diag) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const double c = (okr && fJ + q < a.d) ? vJ[j][q] - shJ[q] : 0.0;
-          buf[kXPlane + (4 * lq + q) * kXS + lr + 16 * j] = c;
-        }
+        for (int q = 0; q < 4; ++q)
+          buf[kXPlane + (4 * lq + q) * kXS + lr + 16 * j] =
+              (double(vJ[j][q]) - shJ[q]) * (mr * mJ[q]);
       }
     }
   };
@@ -550,7 +556,7 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     load(r_begin);
     stage(lds, r_begin);
     if (r_begin + kXRows < r_end) load(r_begin + kXRows);
-    __syncthreads();
+    lds_barrier();
   }
   for (int64_t r0 = r_begin; r0 < r_end; r0 += kXRows) {
     const double* buf = lds + cur * (2 * kXPlane);
@@ -571,7 +577,7 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
       stage(lds + (cur ^ 1) * (2 * kXPlane), r0 + kXRows);
       if (r0 + 2 * kXRows < r_end) load(r0 + 2 * kXRows);
     }
-    __syncthreads();
+    lds_barrier();
     cur ^= 1;
   }
   // the split's fp64 sums, written once: C/D map col = lane & 15, row = (lane >> 4) + 4 reg
