@@ -25,7 +25,10 @@ namespace {
 
 constexpr int kEigThreads = 1024;
 
-__device__ inline int rr_pos(int m, int t, int n) { return m == 0 ? 0 : ((m - 1 + t) % (n - 1)) + 1; }
+// round-robin tournament seat of player m in round t (player 0 fixed, the others rotate)
+__device__ inline int rr_pos(int m, int t, int n) {
+  return m == 0 ? 0 : ((m - 1 + t) % (n - 1)) + 1;
+}
 
 template <bool VLDS>
 __global__ __launch_bounds__(kEigThreads) void oap_als_jacobi_eig(const double* __restrict__ G,
