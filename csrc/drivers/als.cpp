@@ -456,6 +456,12 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       const char* e = std::getenv("OAP_ALS_LOWRANK");
       return !e || std::atoi(e) != 0;
     }();
+    // long-row chunks: split-fp16 Gramian (kernels/als.hip); OAP_ALS_GRAM=fp32 keeps the
+    // exact-fp32 MFMA products
+    const bool x3_gram = [] {
+      const char* e = std::getenv("OAP_ALS_GRAM");
+      return !e || std::string(e) != "fp32";
+    }();
     struct Dev {
       Buffer f, ptr, col, val;
       Buffer short_rows, long_rows, long_chunk_ptr, chunk_begin, chunk_end, partials;
@@ -463,6 +469,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       // rot: this side's factors in the eigenbasis of their Gramian (when it is a source)
       std::vector<std::array<int64_t, 5>> lro;
       Buffer rot, lr_scratch;
+      // split-fp16 long-row Gramian scale inputs: [max |rating| (fixed), max |source factor|]
+      Buffer absmax;
       // per row-range chunk c: [sr_off[c], sr_off[c+1]) of short_rows, [lr_off[c], ...) of
       // long_rows (long_chunk_ptr segment at lr_off[c] + c), [cb_off[c], ...) of chunk_begin/end
       std::vector<int64_t> sr_off, lr_off, cb_off;
@@ -568,6 +576,12 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       int64_t max_lr = 0;
       for (const auto& o : D.lro) max_lr = std::max(max_lr, o[4] - o[0]);
       if (max_lr > 0) D.lr_scratch = ctx.alloc(size_t(max_lr) * ld * 4);
+      if (!lr.empty() && x3_gram) {
+        D.absmax = ctx.alloc(16);
+        ctx.memset(D.absmax.data(), 0, 16);
+        kern::als_absmax(D.val.as<float>(), S.csr.ptr.empty() ? 0 : S.csr.ptr.back(),
+                         D.absmax.as<unsigned>(), s);
+      }
       OAP_HIP_CHECK(hipStreamSynchronize(s));
     };
     upload_side(U, dU, dev_ucsr);
@@ -640,12 +654,17 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         kern::als_rotate(dS.f.as<float>(), nullptr, dS.rot.as<float>(), nullptr, Src.n,
                          lrQ.as<float>(), ld, cus, s);
       }
+      if (dD.absmax.data()) {  // this half's source factors bound the split-fp16 scale
+        OAP_HIP_CHECK(hipMemsetAsync(dD.absmax.as<unsigned>() + 1, 0, 4, s));
+        kern::als_absmax(dS.f.as<float>(), Src.n * ld, dD.absmax.as<unsigned>() + 1, s);
+      }
       E.e1.record(s);
       kern::AlsSolveArgs a;
       a.rowptr = dD.ptr.as<int64_t>();
       a.cols = dD.col.as<int32_t>();
       a.vals = dD.val.as<float>();
       a.partials = dD.partials.as<float>();
+      a.absmax = dD.absmax.data() ? dD.absmax.as<unsigned>() : nullptr;
       a.src = dS.f.as<float>();
       a.ld = ld;
       a.r = r;

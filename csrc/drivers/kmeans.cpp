@@ -1250,9 +1250,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // adaptive delta: when the scan prunes few tiles (overlapping clusters), its pass and the
   // delta bookkeeping cost more than they save — run full passes (which refresh labels and
   // bounds) and probe the scan again every few iterations
+  // (a scan that prunes nothing backs off exponentially: probes every probe_gap batches, the
+  // gap doubling after each failed probe, so an overlapping-cluster fit pays for at most a few
+  // scans and otherwise runs exactly the unpruned delta path)
   bool delta_on = true;
   bool probing = false;  // delta_on was set by a probe: scan one iteration, then decide
   int delta_probe = 0;
+  const int probe_gap0 = p.tol < 0 ? 1 : 4;  // (batches of kBatch iterations vs single ones)
+  int probe_gap = probe_gap0;
   u64 pruned_seen = 0;
 
   kern::KMeansFinalizeArgs fa;
@@ -1305,8 +1310,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (req.fast1: the lean kernel runs; only it does delta accumulation)
       const bool delta_it = delta && it > 0 && req.fast1;
       // (a probe batch scans its first iteration only: the next batch decides from it)
-      const bool scan_it_all =
-          scan_all && it > 0 && req.fast1 && delta_on && (!probing || b == 0);  // rank-uniform
+      // (the first batch scans its third iteration only: one right after the init's large
+      // move rarely prunes)
+      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on &&
+                               (!probing || b == 0);  // rank-uniform
       const bool scan_it = scan_it_all && scan;
       last_scanned = scan_it_all;
       it_scanned[b] = scan_it_all;
@@ -1325,9 +1332,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         }
       }
       if (scan_all && prune) {
-        const bool next_may_scan = b < nb_it - 1
-                                       ? delta_on && !probing
-                                       : delta_on || delta_probe + 1 >= (B == 1 ? 4 : 1);
+        const bool next_may_scan =
+            it >= 1 && (b < nb_it - 1 ? delta_on && !probing
+                                      : delta_on || delta_probe + 1 >= probe_gap);
         req.bounds = (scan_it || next_may_scan) ? bounds_full : nullptr;
         req.xnorm = xnorm_ready ? nullptr : xnorm_full;
       }
@@ -1470,7 +1477,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           (frac < 0.02 || ((scan_iters > 1 || was_probe) && frac < 0.2))) {
         delta_on = false;
         delta_probe = 0;
-      } else if (!delta_on && ++delta_probe >= (B == 1 ? 4 : 1)) {
+        // nothing pruned: wait 4x the base gap before probing again; each failed probe doubles
+        if (frac < 0.02) probe_gap = std::min(std::max(probe_gap * 2, 4 * probe_gap0), 64);
+        else if (was_probe) probe_gap = std::min(probe_gap * 2, 16 * probe_gap0);
+      } else if (delta_on && scan_iters > 0) {
+        probe_gap = probe_gap0;
+      } else if (!delta_on && ++delta_probe >= probe_gap) {
         delta_on = true;  // probe: the centers may have settled
         probing = B > 1;
       }

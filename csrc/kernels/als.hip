@@ -14,6 +14,14 @@
 //    into chunks whose partial (tiles, b, n_u) go to a scratch slab (oap_als_partial) and are
 //    summed in chunk order by the solve kernel — power-law rows neither serialise on one wave
 //    nor lose determinism.
+//  * Long-row chunks (the bulk of a power-law item side) take a split-fp16 Gramian instead:
+//    z = sqrt(c1) y S (S a power of two from max |rating| and max |factor|) is carried as
+//    z_hi + z_lo, two fp16 values holding 22 significant bits, and z z^T as
+//    hi hi^T + hi lo^T + lo hi^T on v_mfma_f32_16x16x32_f16 with fp32 accumulation: three MFMAs
+//    of 16x the fp32 rate per 32 ratings instead of eight fp32 16x16x4 ones (5.3x the
+//    throughput); the dropped lo lo^T and the lo rounding leave ~3 2^-22 relative per product,
+//    below the fp32 accumulation error of a >4096-term sum (OAP_ALS_GRAM=fp32 restores the
+//    exact-fp32 products).
 //  * Solve: the assembled matrix goes to LDS (row stride RP+4: conflict-free MFMA fragment
 //    reads) and is factored by a right-looking blocked Cholesky with 16-wide panels: the
 //    diagonal block in registers (lane-per-row, cross-lane broadcasts), the panel TRSM
@@ -68,7 +76,12 @@ struct PartialArgs {
   float alpha;
   int implicit;
   float* partials;
+  const unsigned* absmax;  // split-fp16 path: [max |rating|, max |source factor|] (float bits)
 };
+
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int NB>
 constexpr int partial_floats() {
@@ -229,14 +242,133 @@ __device__ inline void accumulate_pipe(const int32_t* __restrict__ cols,
   }
 }
 
+// Split-fp16 Gramian + b + n_u of ratings [p0, p1) (long-row chunks), in the C layout of the
+// 16x16 MFMAs (the same tiles accumulate() produces).  32 ratings per step on
+// v_mfma_f32_16x16x32_f16: lane (g, c) = (lane >> 4, lane & 15) holds features 16 f + c of
+// ratings 8 g .. 8 g + 7, which is both the A fragment (row i = c, k = 8 g + e) and the B fragment
+// (k = 8 g + e, column j = c) of z^T, so one register set per feature block serves every tile.
+// The next step's factor values load into the registers the current step has just converted
+// (its fp16 fragments are separate): one step of MFMA work covers the gather latency; the
+// (item, rating) pairs are fetched two steps ahead.  b and n_u stay fp32 on the VALU.
+template <int NB>
+__device__ inline void accumulate_x3(const int32_t* __restrict__ cols,
+                                     const float* __restrict__ vals, int64_t p0, int64_t p1,
+                                     const float* __restrict__ src, int ld, float alpha,
+                                     bool implicit, float scale, f4 (&acc)[NB * (NB + 1) / 2],
+                                     float (&bacc)[NB], int& nexp) {
+  constexpr int kStep = 32;
+  const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+  auto fetch = [&](int64_t p, int& it, float& rv) {
+    const int64_t q = p + (lane & 31);
+    const bool ok = q < p1;
+    it = ok ? cols[q] : -1;
+    rv = ok ? vals[q] : 0.f;
+  };
+  auto load = [&](int it_l, float rv_l, float (&y)[8][NB], float (&rvs)[8], bool (&oks)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int item = __shfl(it_l, 8 * g + e, 64);
+      rvs[e] = __shfl(rv_l, 8 * g + e, 64);
+      oks[e] = item >= 0;
+      const float* yrow = src + static_cast<int64_t>(oks[e] ? item : 0) * ld + c;
+#pragma unroll
+      for (int f = 0; f < NB; ++f) y[e][f] = yrow[16 * f];
+    }
+  };
+  if (p0 >= p1) return;
+  int it_b = -1;
+  float rv_b = 0.f;
+  fetch(p0, it_b, rv_b);
+  float y[8][NB], rvs[8];
+  bool oks[8];
+  load(it_b, rv_b, y, rvs, oks);
+  if (p0 + kStep < p1) fetch(p0 + kStep, it_b, rv_b);
+  for (int64_t p = p0; p < p1; p += kStep) {
+    // weights (absent ratings: 0)
+    float sq[8], wb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float rv = rvs[e];
+      const bool ok = oks[e];
+      float wa;
+      if (implicit) {
+        const float c1 = alpha * fabsf(rv);
+        wa = ok ? c1 : 0.f;
+        wb[e] = (ok && rv > 0.f) ? 1.f + c1 : 0.f;
+        nexp += (ok && rv > 0.f && c == 0) ? 1 : 0;
+      } else {
+        wa = ok ? 1.f : 0.f;
+        wb[e] = ok ? rv : 0.f;
+        nexp += (ok && c == 0) ? 1 : 0;
+      }
+      sq[e] = sqrtf(wa) * scale;
+    }
+    // b on the VALU; z = sqrt(w) y S split into fp16 hi + lo fragments
+    h16x8 zh[NB], zl[NB];
+#pragma unroll
+    for (int f = 0; f < NB; ++f) {
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        bacc[f] = fmaf(wb[e], y[e][f], bacc[f]);
+        bacc[f] = fmaf(wb[e + 1], y[e + 1][f], bacc[f]);
+        const f32x2 z = f32x2{y[e][f], y[e + 1][f]} * f32x2{sq[e], sq[e + 1]};
+        const h16x2 hi = __builtin_convertvector(z, h16x2);
+        const h16x2 lo = __builtin_convertvector(z - __builtin_convertvector(hi, f32x2), h16x2);
+        zh[f][e] = hi[0];
+        zh[f][e + 1] = hi[1];
+        zl[f][e] = lo[0];
+        zl[f][e + 1] = lo[1];
+      }
+    }
+    // the next step's pairs and factor values are in flight under this step's MFMAs
+    const bool more = p + kStep < p1;  // wave-uniform
+    if (more) load(it_b, rv_b, y, rvs, oks);
+    if (p + 2 * kStep < p1) fetch(p + 2 * kStep, it_b, rv_b);
+    // hi hi^T, then hi lo^T, then lo hi^T: consecutive MFMAs never chain on one accumulator
+    int t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = 0; bj <= bi; ++bj, ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zh[bi], zh[bj], acc[t], 0, 0, 0);
+    t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = 0; bj <= bi; ++bj, ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zh[bi], zl[bj], acc[t], 0, 0, 0);
+    t = 0;
+#pragma unroll
+    for (int bi = 0; bi < NB; ++bi)
+#pragma unroll
+      for (int bj = 0; bj <= bi; ++bj, ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(zl[bi], zh[bj], acc[t], 0, 0, 0);
+  }
+}
+
+// power-of-two S with max |sqrt(w) y| S <= 2^14 (fp16 hi parts stay finite, lo parts normal for
+// values within 2^-17 of the largest), and 1 / S^2 — exact, so the Gramian is S-independent
+__device__ inline void x3_scale(const unsigned* absmax, float alpha, bool implicit, float& s,
+                                float& inv_s2) {
+  const float rmax = __uint_as_float(absmax[0]), ymax = __uint_as_float(absmax[1]);
+  const float bound = sqrtf(implicit ? alpha * rmax : 1.f) * ymax;
+  int e = 0;
+  if (bound > 0.f && bound < 3e38f) frexpf(bound, &e);  // bound < 2^e
+  e = e < -40 ? -40 : (e > 40 ? 40 : e);
+  s = ldexpf(1.f, 14 - e);
+  inv_s2 = ldexpf(1.f, 2 * (e - 14));
+}
+
 // Partial Gramian of one long-row chunk, pipelined accumulation at one wave per SIMD (all 512
 // registers: the 28 accumulator tiles plus two blocks of factor rows in flight; 2 waves/SIMD with
 // 256 registers each measured slower, 170 -> 199 ms/iter; 1 wave/SIMD without the pipeline 170;
 // this form 140 at 1B ratings).
-template <int NB>
-__global__ __launch_bounds__(kAlsThreads) void oap_als_partial(PartialArgs a) {
+template <int NB, bool X3>
+__global__ __launch_bounds__(kAlsThreads, 1) void oap_als_partial(PartialArgs a) {
   constexpr int NT = NB * (NB + 1) / 2;
   const int lane = threadIdx.x;
+  float s = 1.f, inv_s2 = 1.f;
+  if constexpr (X3) x3_scale(a.absmax, a.alpha, a.implicit != 0, s, inv_s2);
   for (int64_t q = blockIdx.x; q < a.nchunks; q += gridDim.x) {
     f4 acc[NT];
 #pragma unroll
@@ -245,13 +377,17 @@ __global__ __launch_bounds__(kAlsThreads) void oap_als_partial(PartialArgs a) {
 #pragma unroll
     for (int f = 0; f < NB; ++f) bacc[f] = 0.f;
     int nexp = 0;
-    accumulate_pipe<NB, 4>(a.cols, a.vals, a.chunk_begin[q], a.chunk_end[q], a.src, a.ld, a.alpha,
-                           a.implicit != 0, acc, bacc, nexp);
+    if constexpr (X3)
+      accumulate_x3<NB>(a.cols, a.vals, a.chunk_begin[q], a.chunk_end[q], a.src, a.ld, a.alpha,
+                        a.implicit != 0, s, acc, bacc, nexp);
+    else
+      accumulate_pipe<NB, 4>(a.cols, a.vals, a.chunk_begin[q], a.chunk_end[q], a.src, a.ld,
+                             a.alpha, a.implicit != 0, acc, bacc, nexp);
     float* out = a.partials + q * partial_floats<NB>();
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) out[t * 256 + e * 64 + lane] = acc[t][e];
+      for (int e = 0; e < 4; ++e) out[t * 256 + e * 64 + lane] = acc[t][e] * inv_s2;
 #pragma unroll
     for (int f = 0; f < NB; ++f) out[NT * 256 + f * 64 + lane] = bacc[f];
     out[NT * 256 + NB * 64 + lane] = static_cast<float>(nexp);
@@ -420,9 +556,12 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     pa.alpha = s.alpha;
     pa.implicit = s.implicit ? 1 : 0;
     pa.partials = s.partials;
-    hipLaunchKernelGGL(oap_als_partial<NB>,
-                       dim3(int(std::min<int64_t>(s.n_chunks, int64_t(num_cus) * 4))),
-                       dim3(kAlsThreads), 0, st, pa);
+    pa.absmax = s.absmax;
+    const dim3 pgrid(int(std::min<int64_t>(s.n_chunks, int64_t(num_cus) * 8)));
+    if (s.absmax)
+      hipLaunchKernelGGL((oap_als_partial<NB, true>), pgrid, dim3(kAlsThreads), 0, st, pa);
+    else
+      hipLaunchKernelGGL((oap_als_partial<NB, false>), pgrid, dim3(kAlsThreads), 0, st, pa);
     OAP_HIP_CHECK(hipGetLastError());
     OAP_HIP_CHECK(hipMemsetAsync(s.queue + 1, 0, sizeof(unsigned long long), st));
     a.rows = s.long_rows;
@@ -431,6 +570,28 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     a.partials = s.partials;
     a.queue = s.queue + 1;
     launch_solve<NB, true>(a, int(std::min<int64_t>(s.n_long, int64_t(num_cus) * per_cu)), st);
+  }
+}
+
+// max |x| as float bits (non-negative floats order as unsigned integers): one atomic per block
+__global__ __launch_bounds__(256) void oap_als_absmax(const float* __restrict__ x, int64_t n,
+                                                      unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  float m = 0.f;
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0 ? n / 4 : 0;
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n4; i += int64_t(gridDim.x) * 256) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  for (int64_t i = 4 * n4 + blockIdx.x * int64_t(256) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * 256)
+    m = fmaxf(m, fabsf(x[i]));
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomicMax(out, __float_as_uint(m));  // (NaN compares false: ignored)
   }
 }
 
@@ -486,6 +647,13 @@ void als_solve(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     case 7: run<7>(s, num_cus, st); break;
     default: run<8>(s, num_cus, st); break;
   }
+}
+
+void als_absmax(const float* x, int64_t n, unsigned* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(oap_als_absmax, dim3(grid_for((n + 3) / 4, 256, 2048)), dim3(256), 0, s, x,
+                     n, out);
+  OAP_HIP_CHECK(hipGetLastError());
 }
 
 void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s) {

@@ -25,6 +25,8 @@
 //    the packed-lower LDS image (kernels/als_chol.h), padding rows (s = 0) are identity;
 //  * the blocked Cholesky and both triangular solves of kernels/als_chol.h at NB = NBN;
 //  * g, S W g and W^T S s are fragment-local FMAs plus cross-lane (DPP) reductions.
+#include <cstdlib>
+
 #include "kernels/als_chol.h"
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
@@ -51,6 +53,8 @@ struct LowRankArgs {
   float* out;  // [nrows][ld] rotated solutions, by position in `rows`
   unsigned long long* queue;
   unsigned long long* fail;
+  int ablate;  // timing ablations (OAP_ALS_ABLATE): 16 no M MFMAs, 32 no Cholesky / solves,
+               // 64 no second factor read
 };
 
 template <int CTRL>
@@ -172,6 +176,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
               make_float4(g[qb][0], g[qb][1], g[qb][2], g[qb][3]);
       }
       int t = 0;
+      if (!(a.ablate & 16))
 #pragma unroll
       for (int bi = 0; bi < NBN; ++bi)
 #pragma unroll
@@ -224,7 +229,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
     h *= sc;  // lane l: s_l
     __syncthreads();
 
-    const bool spd = als::chol_factor<NBN, kRS>(M);
+    const bool spd = (a.ablate & 32) ? true : als::chol_factor<NBN, kRS>(M);
     float* out = a.out + q * ld;
     if (!spd || fail_d) {
       if (lane == 0) atomicAdd(a.fail, 1ull);
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
       continue;
     }
     float v1 = 0.f;
-    als::chol_solve<NBN, kRS>(M, bv, h, v1);
+    if (!(a.ablate & 32)) als::chol_solve<NBN, kRS>(M, bv, h, v1);
     const float ss = h * sc;  // S s, lane l = element l
 
     // x_q = D^{-1/2} (g - W^T S s) = D^{-1/2} (g - D^{-1/2} Yq_u^T S s): the factor rows again
@@ -244,7 +249,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
 #pragma unroll
       for (int e = 0; e < 4; ++e) t[qb][e] = 0.f;
 #pragma unroll
-    for (int bi = 0; bi < NBN; ++bi) {
+    for (int bi = 0; bi < ((a.ablate & 64) ? 0 : NBN); ++bi) {
       const int i = 16 * bi + c;
       const float s_i = __shfl(ss, i, 64);
       const int item = __shfl(it, i, 64);
@@ -296,6 +301,11 @@ void lowrank_classes(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
   a.alpha = s.alpha;
   a.lambda = s.lambda;
   a.fail = s.fail;
+  static const int ablate = [] {
+    const char* e = std::getenv("OAP_ALS_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.ablate = ablate;
   // class j: rows [lr_off[j], lr_off[j+1]) of short_rows hold 16 (4 - j) - 15 .. 16 (4 - j) ratings
   for (int j = 0; j < 4; ++j) {
     const int64_t b = s.lr_off[j], e = s.lr_off[j + 1];

@@ -293,6 +293,9 @@ struct AlsSolveArgs {
   const int64_t* chunk_end = nullptr;
   int64_t n_chunks = 0;
   float* partials = nullptr;                // [n_chunks][als_partial_floats(r)]
+  // long-row chunks: split-fp16 Gramian scaled from [max |rating|, max |source factor|]
+  // (device, float bits, als_absmax); null: exact-fp32 MFMA products
+  const unsigned* absmax = nullptr;
   const float* src = nullptr;       // source factors [n_src][ld]
   int ld = 0, r = 0;
   const float* yty = nullptr;       // [r][r] Gramian of ALL source factors (implicit)
@@ -322,6 +325,8 @@ void als_rotate(const float* in, const int32_t* in_rows, float* out, const int32
 void als_init_factors(const int32_t* ids, int64_t n, int r, int ld, uint64_t seed, float* out,
                       hipStream_t s);
 void f64_to_f32(const double* in, float* out, int64_t n, hipStream_t s);
+// *out = max(*out, max |x_i|) as float bits (caller zeroes *out first)
+void als_absmax(const float* x, int64_t n, unsigned* out, hipStream_t s);
 // ---- ALS Gramian eigenbasis on the device (kernels/als_eig.hip) ----------------------------
 // gram: fp64 r x r symmetric (device).  Q / QT: float [ld][ld] (eigenvectors as columns of Q,
 // identity padding), eig: float [ld] (max(lambda, 0), padding 1).  scratch: device bytes of

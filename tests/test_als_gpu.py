@@ -53,6 +53,36 @@ def test_gpu_long_rows_and_determinism(native, gpu_world):
                                atol=3e-3 * np.abs(ref.item_factors).max())
 
 
+@pytest.mark.parametrize("rank,implicit,rmax", [(100, True, 5.0), (33, True, 3e4),
+                                                (20, False, 5.0), (128, True, 1.0)])
+def test_long_row_split_fp16_gramian(native, gpu_world, monkeypatch, rank, implicit, rmax):
+    """Rows with > 4096 ratings take the split-fp16 (hi + lo, three MFMAs) chunk Gramian: it
+    stays within fp32-path noise of the exact-fp32 MFMA products (OAP_ALS_GRAM=fp32) and of the
+    fp64 oracle, over a large rating range (the power-of-two operand scale)."""
+    rng = np.random.default_rng(rank)
+    n = 60000
+    i = (rng.zipf(1.3, n) % 300).astype(np.int32)
+    u = rng.integers(0, 4000, n).astype(np.int32)
+    r = (rng.uniform(0.5, 1.0, n) * rmax).astype(np.float32)
+    assert np.bincount(i).max() > 2 * 4096  # several chunks of one long row
+    def fit():
+        return native.als_fit(gpu_world.ctx, gpu_world.comm, u, i, r, rank, 2, 0.05, 1.0,
+                              implicit, 3)
+    x3 = fit()
+    monkeypatch.setenv("OAP_ALS_GRAM", "fp32")
+    f32 = fit()
+    assert x3["failed_rows"] == 0 and f32["failed_rows"] == 0
+    ref = als_vanilla.fit(u, i, r, rank, 2, 0.05, implicit, 1.0, False, 3)
+    for key, rk in (("item_factors", ref.item_factors), ("user_factors", ref.user_factors)):
+        scale = np.abs(rk).max()
+        d32 = np.abs(x3[key] - f32[key]).max() / scale
+        d64 = np.abs(x3[key] - rk).max() / scale
+        e64 = np.abs(f32[key] - rk).max() / scale
+        print(f"{key}: x3-fp32 {d32:.2e}  x3-fp64 {d64:.2e}  fp32-fp64 {e64:.2e}")
+        assert d64 <= max(3e-3, 2 * e64)
+        assert d32 <= max(1e-3, 2 * e64)
+
+
 def test_api_gpu_engine(gpu_world):
     rng = np.random.default_rng(2)
     U = rng.uniform(-1, 1, (30, 3))

@@ -8,7 +8,7 @@ fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2"; exit $1;; esac; 
 for st in "$@"; do
   case $st in
     test)
-      timeout -k 10 800 python -u -m pytest ${PYTEST_TARGET:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu_$T.log 2>&1
+      timeout -k 10 800 python -u -m pytest ${PYTEST_TARGET:-tests} -m gpu -x -v ${PYTEST_EXTRA:-} --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu_$T.log 2>&1
       rc=$?; echo pytest_rc=$rc; grep -E "FAILED|passed|failed" gpurun_out/pytest_gpu_$T.log | tail -5; fatal $rc pytest;;
     bench)
       timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench_$T.json 2> gpurun_out/bench_$T.err
