@@ -163,6 +163,12 @@ def bench_kmeans(args, w):
                            "of moved rows",
         "lean_fp16_delta_scan": "bound scan + lean fp16 MFMA pass over the listed tiles + exact "
                                 "fp32 re-decision; delta accumulation of moved rows",
+        "lean_fp16_image_delta": "lean fp16 MFMA pass streaming the resident fp16 operand image "
+                                 "(written by the fit's first pass) + exact fp32 re-decision "
+                                 "from the f32 rows; delta accumulation of moved rows",
+        "lean_fp16_image_delta_scan": "bound scan + lean fp16 MFMA pass over the listed tiles' "
+                                      "resident fp16 operand image + exact fp32 re-decision; "
+                                      "delta accumulation of moved rows",
         "lean_fp16_centroid_chunked": "centroid-chunked lean fp16 MFMA pass (running top-2 keys "
                                       "across centroid chunks) + chunked exact fp32 re-decision; "
                                       "label-driven binned accumulation",
@@ -197,6 +203,8 @@ def bench_kmeans(args, w):
              # rows the tier-1 pass left to the exact fp32 MFMA re-decision (near ties)
              "deferred_rows_per_iter": r.get("deferred_rows", 0) / max(args.steps, 1),
              "moved_rows_per_iter": r.get("moved_rows", 0) / max(args.steps, 1),
+             # Lloyd passes that streamed the fp16 operand image instead of the f32 rows
+             "image_passes": r.get("image_passes", 0),
              "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),
              "tiles_per_pass": tiles,
              "ms_per_step_unpruned": ms_unpruned,

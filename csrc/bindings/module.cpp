@@ -518,6 +518,7 @@ PYBIND11_MODULE(_native, m) {
         out["assign_path"] = r.assign_path;
         out["deferred_rows"] = r.deferred_rows;
         out["moved_rows"] = r.moved_rows;
+        out["image_passes"] = r.image_passes;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

@@ -250,6 +250,10 @@ struct AssignReq {
   bool stats_persist = false;
   const int32_t* prev_labels = nullptr;
   int64_t* moved_rows = nullptr;  // host counter of the rows the delta accumulated
+  // lean kernel's resident fp16 operand image (KMeansAssignArgs::ximg / img_beta / img_mode)
+  void* ximg = nullptr;
+  float* img_beta = nullptr;
+  int img_mode = 0;
 };
 
 int& lean_variant_ref() {  // -1: by width (below)
@@ -347,6 +351,9 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.deferred_rows = req.deferred_rows;
     a.tile_list = nullptr;
     a.tile_count = nullptr;
+    a.ximg = req.ximg;
+    a.img_beta = req.img_beta;
+    a.img_mode = req.img_mode;
     if (req.delta) {  // delta accumulation; over the scan's tile list when there is one
       OAP_CHECK(req.labels && req.labels_valid,
                 "kmeans delta accumulation needs the previous iteration's labels");
@@ -357,10 +364,14 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
         a.tile_count = req.tile_count;
       }
     }
-    t_assign_path = req.delta ? (req.tile_list ? "lean_fp16_delta_scan" : "lean_fp16_delta")
-                              : "lean_fp16";
+    t_assign_path = req.img_mode == 2
+                        ? (req.tile_list ? "lean_fp16_image_delta_scan" : "lean_fp16_image_delta")
+                    : req.delta ? (req.tile_list ? "lean_fp16_delta_scan" : "lean_fp16_delta")
+                                : "lean_fp16";
     kern::kmeans_lloyd(a, grid, lean_variant(x.cols), s);
     kern::KMeansAssignArgs b = a;
+    b.ximg = nullptr;
+    b.img_mode = 0;
     b.defer_rows = nullptr;
     b.defer_row_count = nullptr;
     b.deferred_rows = nullptr;
@@ -1242,6 +1253,23 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     req.deferred_rows = ldstat_b.as<u64>();
   }
   u64 deferred_seen = 0;
+  // Resident fp16 operand image (f32 rows, delta path): the first full lean pass writes each
+  // tile's MFMA B operand (fp16 of beta x + bias slots, 2 B per padded feature instead of 4) and
+  // the delta passes after it stream that instead of the f32 rows — 128 instead of 208 B per
+  // row at d = 50 — reading f32 rows only for moved rows and the exact re-decisions.  Taken
+  // when the image fits beside the arena's other buffers with a quarter of its budget to spare.
+  Buffer img_b, img_beta_b;
+  bool img_ready = false;
+  {
+    const char* e = std::getenv("OAP_KMEANS_IMAGE");
+    const size_t ib = kern::kmeans_lloyd_image_bytes(x.rows, x.cols);
+    DeviceArena* ar = ctx.backend() == Backend::GPU ? ctx.arena() : nullptr;
+    if (delta && req.defer_rows && x.dtype == DType::F32 && ib > 0 && !(e && *e == '0') && ar &&
+        ar->used() + ib + ar->budget() / 4 <= ar->budget()) {
+      img_b = ctx.alloc(ib);
+      img_beta_b = ctx.alloc(sizeof(float) * 4);
+    }
+  }
   // with the adaptive scan off, full passes write the per-row bounds (8 B/row) only where a
   // following iteration may scan, and the per-tile max |x|^2 (constant) once
   float* const bounds_full = req.bounds;
@@ -1365,7 +1393,19 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         req.tile_list = nullptr;
         req.tile_count = nullptr;
       }
+      // operand image: written by the first full lean pass, read by costless delta passes
+      req.ximg = img_b.data();
+      req.img_beta = img_beta_b.as<float>();
+      req.img_mode = 0;
+      if (img_b.data() && lean_applies(x, k, g.kpad, req)) {
+        if (!img_ready && !req.tile_list && req.cost_slab)
+          req.img_mode = 1;
+        else if (img_ready && delta_it && !req.cost_slab && !req.mindist && !req.xnorm)
+          req.img_mode = 2;
+      }
       int nb = gpu_assign(ctx, x, g, req, s);
+      if (req.img_mode == 1) img_ready = true;
+      if (req.img_mode == 2) ++res.image_passes;
       if (cdelta)
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), cloc_b.data(), sizeof(u64) * (kd + k),
                                      hipMemcpyDeviceToDevice, s));

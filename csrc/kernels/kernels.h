@@ -136,6 +136,13 @@ struct KMeansAssignArgs {
   int kglob = 0;
   int32_t* lean_keys = nullptr;
   float* xstate = nullptr;
+  // Resident fp16 operand image of f32 rows (lean kernel, single launch): [ceil(n/32)][KS][64]
+  // fragments of 8 halves (kmeans_lloyd_image_bytes), the MFMA B operand of each 32-row tile
+  // with its bias slots, at the scale *img_beta.  img_mode 1: this full pass writes image and
+  // scale; 2: this pass takes its operands from the image (f32 rows only for accumulation).
+  void* ximg = nullptr;
+  float* img_beta = nullptr;
+  int img_mode = 0;
   const float* centers_all = nullptr;
 };
 // Lean tier-1 Lloyd kernel (kmeans_lloyd.hip): applicable when the centroid hi plane + the
@@ -151,6 +158,8 @@ int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves);
 // selects the workgroup shape (0: 16 waves; tuning: 1-3).  Writes `grid`
 // cost partials.
 int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s);
+// Bytes of the lean kernel's fp16 operand image of n f32 rows of width d (0: not applicable).
+size_t kmeans_lloyd_image_bytes(int64_t n, int d);
 // Largest centroid chunks (multiples of 32) of the chunked lean pass at dimension d: the lean
 // kernel's fp16 plane and the exact kernel's fp32 centers (0: d not supported).
 int kmeans_lloyd_chunk_kmax(int d);

@@ -36,6 +36,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "kernels/kmeans_frag.h"
 #include "kernels/kmeans_internal.h"
@@ -46,6 +47,10 @@ namespace kern {
 namespace {
 
 using namespace kmdev;
+
+// the kernel's helper lambdas share its argument block by reference: one of them left out of
+// line (several call sites) would force a private copy of LeanArgs into scratch
+#define OAP_AI __attribute__((always_inline))
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -82,6 +87,11 @@ struct LeanArgs {
   int2* keys;
   const float* centers_all;
   int kbase, kglob, chunk_mode;
+  // resident fp16 operand image (f32 rows, KMeansAssignArgs::ximg): 1 = this full pass writes
+  // it (and its scale), 2 = this pass reads it instead of the f32 rows
+  _Float16* ximg;
+  float* img_beta;
+  int img_mode;
 };
 
 struct LeanSmem {
@@ -158,8 +168,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   double* wcost = reinterpret_cast<double*>(smem + L.wcost);
   const int tid = threadIdx.x;
   const float cmax = a.cstat[0];
-  const float alpha = lean_alpha(cmax);
+  float alpha = lean_alpha(cmax);
+  // The operand image holds fp16(beta x) for a scale beta fixed when it was written (a quarter
+  // of that pass's alpha: 4x headroom for the rows and 16x for later centers).  A pass reads it
+  // only while the plane at that scale stays representable (beta max|c| <= 2^9: -2 beta c and
+  // beta^2 |c|^2 / 16 inside fp16); otherwise it reads the f32 rows as usual.
+  bool use_img = false;
+  if constexpr (!XB && PF == 2 && !COST) {
+    if (a.img_mode == 2) {
+      const float bt = a.img_beta[0];
+      use_img = bt * cmax <= 512.f;
+      if (use_img) alpha = bt;
+    }
+  }
   const float a2 = alpha * alpha;
+  const float beta_w = 0.25f * alpha;  // the scale a writing pass gives the image
+  if (a.img_mode == 1 && blockIdx.x == 0 && tid == 0) a.img_beta[0] = beta_w;
 
   // ---- stage c' = [-2 alpha c, 0 .., hi, lo (alpha^2 |c|^2 / 16), 16, 16] (fp16) once per
   // workgroup; the four bias features sit in the LAST four slots (DP - 4 .. DP - 1, d <= DP - 4
@@ -218,14 +242,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   unsigned n_def = 0;  // wave-uniform
   double my_cost = 0.0;
 
-  auto tile_of = [&](int64_t q) -> int64_t {
+  auto tile_of = [&](int64_t q) OAP_AI -> int64_t {
     if (npos == 0) return 0;  // (prefetch of an empty range: any real tile)
     q = q < npos ? q : npos - 1;
     if (!listed) return t0 + q;
     const int64_t tl = int64_t(seg[q]);
     return tl < 0 ? 0 : (tl < ntiles_all ? tl : ntiles_all - 1);
   };
-  auto load_row = [&](int64_t row, F& dst) {
+  auto load_row = [&](int64_t row, F& dst) OAP_AI {
     if (a.ablate & 16) {  // timing ablation: no row loads (synthetic values)
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -266,13 +290,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         }
     }
   };
-  auto load_tile = [&](int64_t tile, F& dst) {
+  auto load_tile = [&](int64_t tile, F& dst) OAP_AI {
     const int64_t row = tile * 32 + r;
     load_row(row < a.n ? row : a.n - 1, dst);
   };
+  // image layout: [tile][k-step][lane][8 halves] — every load is one contiguous 1 KB per wave
+  auto img_frag = [&](int64_t tile, int s) OAP_AI -> f16x8* {
+    return reinterpret_cast<f16x8*>(a.ximg) + (tile * KS + s) * 64 + lane;
+  };
+  auto load_img = [&](int64_t tile, f16x8 (&dst)[KS]) OAP_AI {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) dst[s] = *img_frag(tile, s);
+  };
 
   // fixed-point accumulation of one row into cluster b (neg: subtract it)
-  auto add_row = [&](const F& xv, int b, bool neg) {
+  auto add_row = [&](const F& xv, int b, bool neg) OAP_AI {
     if (h == 0) atomicAdd(&cnt_l[b], neg ? 0xffffffffu : 1u);
     if (!a.sums_too) return;
     const float sgn = neg ? -1.f : 1.f;
@@ -302,7 +334,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   // with every lane busy (rows re-read from L2: their tile was just streamed)
   unsigned n_mv = 0;  // wave-uniform
   u64 moved_total = 0;
-  auto flush_moved = [&](unsigned cnt) {  // accumulate staged entries [0, min(cnt, 32))
+  auto flush_moved = [&](unsigned cnt) OAP_AI {  // accumulate staged entries [0, min(cnt, 32))
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const bool on = unsigned(r) < cnt;
@@ -322,60 +354,104 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     moved_total += cnt < 32 ? cnt : 32;
   };
 
-  auto process = [&](const int64_t pos, const int64_t tile, F& x, F& xn, const int64_t pf) {
+  // fp16 operand of s * x with the bias slots [16, 16, hi, lo (s^2 |x|^2 / 16)] (nx2 = |x|^2)
+  auto build_operand = [&](const F& x, float s_, float nx2, f16x8 (&out)[KS]) OAP_AI {
+    _Float16 nh, nl;
+    split_f16(s_ * s_ * nx2 * (1.f / kBiasUnit), nh, nl);
+    const _Float16 unit = static_cast<_Float16>(kBiasUnit);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      f16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {  // v_pk_mul_f32 + v_cvt_pk_f16_f32 (RNE): 1 op / value
+        const f32x2 p = f32x2{x.at(s, j), x.at(s, j + 1)} * s_;
+        const f16x2 q = __builtin_convertvector(p, f16x2);
+        v[j] = q[0];
+        v[j + 1] = q[1];
+      }
+      if (s == KS - 1) {  // h = 1 lanes: slots 4..7 = [16, 16, hi, lo] (x is 0 there)
+        v[4] = h ? unit : v[4];
+        v[5] = h ? unit : v[5];
+        v[6] = h ? nh : v[6];
+        v[7] = h ? nl : v[7];
+      }
+      out[s] = v;
+    }
+  };
+
+  // img_t: std::true_type — the operands come from the resident image (xi: this tile's, xin:
+  // where the next tile's are loaded once xi is copied), the f32 rows are read only by the
+  // accumulation
+  auto process = [&](auto img_t, const int64_t pos, const int64_t tile, F& x, F& xn,
+                     const int64_t pf, f16x8 (&xi)[KS], f16x8 (&xin)[KS]) OAP_AI {
+    constexpr bool IMG = decltype(img_t)::value;
     const int64_t row = tile * 32 + r;
     const bool valid = pos < npos && row < a.n;
-    if constexpr (PF == 1) load_tile(tile_of(pf), xn);  // next tile: in flight under this one
+    if constexpr (!IMG && PF == 1) load_tile(tile_of(pf), xn);  // next tile: in flight
+    // running pair of a chunked pass (one half takes it: no duplicate), merged after the chunk
+    // loop — loaded here, ahead of the next tile's prefetch, so no wait in the loop covers the
+    // prefetch (s_waitcnt vmcnt counts in issue order)
+    int2 kin = make_int2(0x7fffffff, 0x7fffffff);
+    if (keys_in && h == 0 && valid) kin = a.keys[row];
     int old = -1;
     if (a.delta && valid) old = a.labels[row];
-    float nx2 = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
-    nx2 += __shfl_xor(nx2, 32, 64);
-    if (a.xnorm && pos < npos) {  // per-tile max |x|^2 (the delta scan's pruning margin)
-      float tmax = nx2;
-#pragma unroll
-      for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));
-      if (lane == 0) a.xnorm[tile] = tmax;
-    }
-    const float nx2_s = a2 * nx2;
     // MFMA B operand: fp16 of alpha x with the bias slots [16, 16, hi, lo (alpha^2 |x|^2 / 16)]
     f16x8 xh[KS];
-    {
-      _Float16 nh, nl;
-      split_f16(nx2_s * (1.f / kBiasUnit), nh, nl);
-      const _Float16 unit = static_cast<_Float16>(kBiasUnit);
+    float nx2_s;
+    if constexpr (IMG) {
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        f16x8 v;
+      for (int s = 0; s < KS; ++s) xh[s] = xi[s];
+      load_img(tile_of(pf), xin);  // the next tile's operands (xin may be xi): in flight
+      // alpha^2 |x|^2 from the bias pair (h = 1 lanes' slots 6, 7 of the last k-step)
+      const float mine = kBiasUnit * (static_cast<float>(xh[KS - 1][6]) +
+                                      static_cast<float>(xh[KS - 1][7]));
+      const float other = __shfl_xor(mine, 32, 64);
+      nx2_s = h ? mine : other;
+    } else {
+      float nx2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {  // v_pk_mul_f32 + v_cvt_pk_f16_f32 (RNE): 1 op / value
-          const f32x2 p = f32x2{x.at(s, j), x.at(s, j + 1)} * alpha;
-          const f16x2 q = __builtin_convertvector(p, f16x2);
-          v[j] = q[0];
-          v[j + 1] = q[1];
+      for (int s = 0; s < KS; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
+      nx2 += __shfl_xor(nx2, 32, 64);
+      if (a.xnorm && pos < npos) {  // per-tile max |x|^2 (the delta scan's pruning margin)
+        float tmax = nx2;
+#pragma unroll
+        for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));
+        if (lane == 0) a.xnorm[tile] = tmax;
+      }
+      nx2_s = a2 * nx2;
+      build_operand(x, alpha, nx2, xh);
+      if constexpr (!XB && COST) {  // (full passes compute the cost)
+        if (a.img_mode == 1 && pos < npos) {  // write the image (every lane of a real tile)
+          _Float16 nh, nl;
+          split_f16(beta_w * beta_w * nx2 * (1.f / kBiasUnit), nh, nl);
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {  // one k-step at a time (few extra live registers)
+            f16x8 v;
+#pragma unroll
+            for (int j = 0; j < 8; j += 2) {
+              const f16x2 q = __builtin_convertvector(f32x2{x.at(s, j), x.at(s, j + 1)} * beta_w,
+                                                      f16x2);
+              v[j] = q[0];
+              v[j + 1] = q[1];
+            }
+            if (s == KS - 1) {
+              v[4] = h ? static_cast<_Float16>(kBiasUnit) : v[4];
+              v[5] = h ? static_cast<_Float16>(kBiasUnit) : v[5];
+              v[6] = h ? nh : v[6];
+              v[7] = h ? nl : v[7];
+            }
+            *img_frag(tile, s) = v;
+          }
         }
-        if (s == KS - 1) {  // h = 1 lanes: slots 4..7 = [16, 16, hi, lo] (x is 0 there)
-          v[4] = h ? unit : v[4];
-          v[5] = h ? unit : v[5];
-          v[6] = h ? nh : v[6];
-          v[7] = h ? nl : v[7];
-        }
-        xh[s] = v;
       }
     }
-    if constexpr (PF == 2) load_tile(tile_of(pf), x);  // x's registers now carry the next tile
+    if constexpr (!IMG && PF == 2) load_tile(tile_of(pf), x);  // x now carries the next tile
     // ---- tier 1: one fp16 product per k-step; top-2 on integer keys (the distance's bits with
     // the low 10 mantissa bits replaced by the in-chunk offset; value order, lowest index first)
     int k1 = 0x7fffffff, k2 = 0x7fffffff;
-    if (keys_in && h == 0 && valid) {  // one half starts from the running pair (no duplicate)
-      const int2 kv = a.keys[row];
-      k1 = kv.x;
-      k2 = kv.y;
-    }
-    auto mfma_chunk = [&](int c0, f32x16& acc) {
+    auto mfma_chunk = [&](int c0, f32x16& acc) OAP_AI {
       const _Float16* ap = ph + size_t(c0 + r) * sb + 8 * h;
       f16x8 av[KS];
 #pragma unroll
@@ -391,7 +467,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
       }
     };
-    auto epilogue = [&](int c0, const f32x16& acc) {
+    auto epilogue = [&](int c0, const f32x16& acc) OAP_AI {
       if (a.ablate & 32) {  // timing ablation: consume the accumulators with one op per chunk
         k1 = min(k1, (__float_as_int(acc[0]) & ~0x3ff) | (c0 + 4 * h));
         return;
@@ -469,6 +545,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         mfma_chunk(c0, acc);
         epilogue(c0, acc);
       }
+      k2 = min(max(k1, kin.x), min(k2, kin.y));  // (top-2 of the union: order-free)
+      k1 = min(k1, kin.x);
       const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
       k2 = min(max(k1, o1), min(k2, o2));
       k1 = min(k1, o1);
@@ -566,18 +644,32 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
   };
 
-  if constexpr (PF == 1) {
+  const std::false_type rows_t{};
+  f16x8 no_img[KS];  // (unused by the f32-row passes)
+  if (use_img) {
+    // image passes: the tile's operand fragments are copied out of the load registers (KS x 4
+    // moves) and the next tile's loads go straight into them, in flight under this tile (one
+    // call site: a ping-pong of two register sets needs two inlined copies of the pass body)
+    if constexpr (!XB && PF == 2 && !COST) {
+      F unused;
+      f16x8 ia[KS];
+      load_img(tile_of(t), ia);
+      for (; t < npos; t += stride)  // t is wave-uniform: every branch stays uniform
+        process(std::true_type{}, t, tile_of(t), unused, unused, t + stride, ia, ia);
+    }
+  } else if constexpr (PF == 1) {
     F xa, xb;
     load_tile(tile_of(t), xa);
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      process(t, tile_of(t), xa, xb, t + stride);
+      process(rows_t, t, tile_of(t), xa, xb, t + stride, no_img, no_img);
       if (t + stride >= npos) break;
-      process(t + stride, tile_of(t + stride), xb, xa, t + 2 * stride);
+      process(rows_t, t + stride, tile_of(t + stride), xb, xa, t + 2 * stride, no_img, no_img);
     }
   } else if constexpr (PF == 2) {
     F xa;
     load_tile(tile_of(t), xa);
-    for (; t < npos; t += stride) process(t, tile_of(t), xa, xa, t + stride);
+    for (; t < npos; t += stride)
+      process(rows_t, t, tile_of(t), xa, xa, t + stride, no_img, no_img);
   } else {
     F xa;
     int64_t tl = tile_of(t);
@@ -585,7 +677,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       const int64_t tcur = tl;
       load_tile(tcur, xa);
       tl = tile_of(t + stride);  // listed passes: the next tile index lands under this tile
-      process(t, tcur, xa, xa, 0);
+      process(rows_t, t, tcur, xa, xa, 0, no_img, no_img);
     }
   }
 
@@ -1112,6 +1204,12 @@ int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
   return int64_t(waves) * ((per_block + waves - 1) / waves) * 32;
 }
 
+size_t kmeans_lloyd_image_bytes(int64_t n, int d) {
+  if (n <= 0 || d <= 0 || d + 4 > 128) return 0;
+  const int ks = (d + 4 + 15) / 16;
+  return size_t((n + 31) / 32) * size_t(ks) * 64 * 16;
+}
+
 int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s) {
   // the chunked driver (centers_all set) pairs this pass with a chunked exact pass, so only the
   // lean plane has to fit (a single lean chunk runs as chunk_mode 0)
@@ -1127,6 +1225,13 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
             "kmeans_lloyd: unsupported arguments");
   OAP_CHECK(!a.delta || a.labels, "kmeans_lloyd: delta mode needs the previous labels");
   OAP_CHECK(!a.tile_list || (a.delta && a.tile_count), "kmeans_lloyd: tile list without delta");
+  // the operand image: f32 rows, one launch; written by a full pass, read without the per-tile
+  // |x|^2 output (that comes from the f32 rows)
+  OAP_CHECK(!a.ximg || a.img_mode == 0 ||
+                (!a.xbf16 && !a.centers_all && a.img_beta &&
+                 (a.img_mode == 1 ? !a.tile_list && (a.cost_slab || a.mindist)
+                                  : (a.img_mode == 2 && !a.xnorm))),
+            "kmeans_lloyd: bad operand-image arguments");
   if (a.n == 0) return 0;
   LeanArgs l;
   l.x = a.x;
@@ -1162,6 +1267,9 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.kbase = a.base;
   l.kglob = a.kglob;
   l.chunk_mode = a.chunk_mode;
+  l.ximg = static_cast<_Float16*>(a.ximg);
+  l.img_beta = a.img_beta;
+  l.img_mode = a.ximg ? a.img_mode : 0;
   // the exact per-row cost is computed when a cost or mindist is asked for
   const bool cost = a.cost_slab != nullptr || a.mindist != nullptr;
   if (a.xbf16)

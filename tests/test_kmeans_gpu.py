@@ -324,6 +324,43 @@ def test_lean_pass_bitwise_equals_precise_on_overlapping_data(native, d, k, sigm
     assert rf2["cost"] == rf["cost"] and rf2["deferred_rows"] == rf["deferred_rows"]
 
 
+@pytest.mark.parametrize("d,k,sigma,tol", [(50, 200, 8.0, -1.0), (20, 64, 6.0, -1.0),
+                                           (12, 7, 4.0, 0.0), (124, 30, 5.0, -1.0)])
+def test_operand_image_bitwise(native, monkeypatch, d, k, sigma, tol):
+    """Delta passes that stream the resident fp16 operand image (instead of the f32 rows) give
+    the f32-row fit and the exact-fp32 fit bitwise (batched and per-iteration loops)."""
+    n = 150000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, sigma, 91)
+    init = t.to_numpy(g, 0, k) + 0.25
+    comm = native.LocalComm(True)
+    ri = native.kmeans_fit(g, comm, t, init, k, 8, tol)
+    monkeypatch.setenv("OAP_KMEANS_IMAGE", "0")
+    rr = native.kmeans_fit(g, comm, t, init, k, 8, tol)
+    rp = native.kmeans_fit(g, comm, t, init, k, 8, tol, precise=True)
+    assert ri["image_passes"] > 0 and rr["image_passes"] == 0
+    assert ri["num_iter"] == rr["num_iter"] == rp["num_iter"]
+    for r in (ri, rr):
+        assert r["last_counts"] == rp["last_counts"]
+        assert np.array_equal(r["centers"], rp["centers"])
+        assert abs(r["cost"] - rp["cost"]) <= 1e-12 * rp["cost"]
+
+
+def test_operand_image_scale_fallback(native):
+    """Initial centers far smaller than the data fix a large image scale; once the centers grow
+    past its range (beta max|c| > 2^9) the passes read the f32 rows — still the exact fit."""
+    n, d, k = 100000, 30, 40
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 50.0, 2.0, 5)
+    init = (t.to_numpy(g, 0, k) * 1e-3).astype(np.float32).astype(np.float64)
+    comm = native.LocalComm(True)
+    ri = native.kmeans_fit(g, comm, t, init, k, 6, -1.0)
+    rp = native.kmeans_fit(g, comm, t, init, k, 6, -1.0, precise=True)
+    assert ri["image_passes"] > 0
+    assert ri["last_counts"] == rp["last_counts"]
+    assert np.array_equal(ri["centers"], rp["centers"])
+
+
 @pytest.mark.parametrize("variant", [0, 3, 5, 7])
 def test_lean_variants_agree(native, variant):
     """Every workgroup shape of the lean kernel gives the same fit."""
