@@ -519,6 +519,7 @@ PYBIND11_MODULE(_native, m) {
         out["deferred_rows"] = r.deferred_rows;
         out["moved_rows"] = r.moved_rows;
         out["image_passes"] = r.image_passes;
+        out["image_bytes"] = r.image_bytes;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

@@ -265,10 +265,20 @@ int& lean_variant_ref() {  // -1: by width (below)
 }
 // Workgroup shape of the lean kernel: 16 waves (4 per SIMD, 128 registers) unless the rows are
 // 7-8 k-steps wide, where 128 registers spill (config 5, d = 100: 232 B/lane of scratch) and 12
-// waves (168 registers) measured 3.5% faster (396 -> 382 ms/iter at 1B rows).
-int lean_variant(int d) {
+// waves (168 registers) measured 3.5% faster (396 -> 382 ms/iter at 1B rows).  Rows of <= 4
+// k-steps whose plane fits 7-8 chunks of 32 centroids (k <= 224 at d <= 60) can take the
+// register-resident plane (variant 11, 8 waves, no LDS reads in the distance loop) with
+// OAP_KMEANS_REG_PLANE=1.
+int lean_variant(int d, int kpad) {
   const int v = lean_variant_ref();
-  return v >= 0 ? v : (d + 4 > 96 ? 3 : 0);
+  const int rch = kern::kmeans_lloyd_rch(d);
+  const bool reg_ok = rch > 0 && kpad <= 32 * rch;
+  if (v >= 0) return (v == 11 && !reg_ok) ? 0 : v;
+  const char* e = std::getenv("OAP_KMEANS_REG_PLANE");
+  if (reg_ok && e && *e == '1') return 11;
+  // (variant 6 — fragment reads grouped ahead of each MFMA chain — measured ~1% ahead of 0 on
+  // the headline shape in two runs; the register plane 6% behind: profiles/r3/lean_variants_*)
+  return d + 4 > 96 ? 3 : 6;
 }
 
 // Whether gpu_assign takes the lean path for this request.
@@ -288,9 +298,9 @@ bool lean_chunked_applies(const DenseTable& x, const GpuCenters& g, const Assign
          kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
 }
 
-size_t lean_defer_bytes(int64_t rows, int d, int num_cus, int* grid, int64_t* cap) {
+size_t lean_defer_bytes(int64_t rows, int d, int kpad, int num_cus, int* grid, int64_t* cap) {
   *grid = kern::kmeans_lloyd_grid(rows, num_cus);
-  *cap = kern::kmeans_lloyd_seg_cap(rows, *grid, kern::kmeans_lloyd_waves(lean_variant(d)));
+  *cap = kern::kmeans_lloyd_seg_cap(rows, *grid, kern::kmeans_lloyd_waves(lean_variant(d, kpad)));
   return sizeof(int32_t) * size_t(*grid) * size_t(*cap) + sizeof(unsigned) * 16 * size_t(*grid);
 }
 
@@ -336,7 +346,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     // ---- lean tier-1 pass, then the general kernel re-decides the deferred rows exactly
     int grid = 0;
     int64_t cap = 0;
-    const size_t dbytes = lean_defer_bytes(x.rows, x.cols, ctx.info().cu_count, &grid, &cap);
+    const size_t dbytes =
+        lean_defer_bytes(x.rows, x.cols, g.kpad, ctx.info().cu_count, &grid, &cap);
     Buffer dbuf;
     int32_t* drows = req.defer_rows;
     unsigned* dcnt = req.defer_count;
@@ -368,7 +379,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
                         ? (req.tile_list ? "lean_fp16_image_delta_scan" : "lean_fp16_image_delta")
                     : req.delta ? (req.tile_list ? "lean_fp16_delta_scan" : "lean_fp16_delta")
                                 : "lean_fp16";
-    kern::kmeans_lloyd(a, grid, lean_variant(x.cols), s);
+    kern::kmeans_lloyd(a, grid, lean_variant(x.cols, a.kpad), s);
     kern::KMeansAssignArgs b = a;
     b.ximg = nullptr;
     b.img_mode = 0;
@@ -377,7 +388,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.deferred_rows = nullptr;
     b.row_list = drows;
     b.row_count = dcnt;
-    b.row_subs = kern::kmeans_lloyd_waves(lean_variant(x.cols));
+    b.row_subs = kern::kmeans_lloyd_waves(lean_variant(x.cols, a.kpad));
     b.tile_list = nullptr;
     b.tile_count = nullptr;
     b.xnorm = nullptr;
@@ -446,7 +457,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     const int lsz = split(lk, &nl), esz = split(ek, &ne);
     int grid = 0;
     int64_t cap = 0;
-    Buffer dbuf = ctx.alloc(lean_defer_bytes(x.rows, x.cols, ctx.info().cu_count, &grid, &cap));
+    Buffer dbuf =
+        ctx.alloc(lean_defer_bytes(x.rows, x.cols, g.kpad, ctx.info().cu_count, &grid, &cap));
     int32_t* drows = dbuf.as<int32_t>();
     unsigned* dcnt = reinterpret_cast<unsigned*>(drows + size_t(grid) * size_t(cap));
     Buffer keys = ctx.alloc(sizeof(int32_t) * 2 * size_t(x.rows));
@@ -485,7 +497,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
       kern::KMeansAssignArgs b = a;
       b.deferred_rows = req.deferred_rows;
       chunk(b, ci * lsz, lsz, ci, nl);
-      kern::kmeans_lloyd(b, grid, lean_variant(x.cols), s);
+      kern::kmeans_lloyd(b, grid, lean_variant(x.cols, g.kpad), s);
     }
     for (int ci = 0; ci < ne; ++ci) {
       kern::KMeansAssignArgs b = a;
@@ -494,7 +506,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
       b.deferred_rows = nullptr;
       b.row_list = drows;
       b.row_count = dcnt;
-      b.row_subs = kern::kmeans_lloyd_waves(lean_variant(x.cols));
+      b.row_subs = kern::kmeans_lloyd_waves(lean_variant(x.cols, g.kpad));
       b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
       chunk(b, ci * esz, esz, ci, ne);
       kern::kmeans_exact_rows(b, grid, s);
@@ -1242,7 +1254,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   if (x.rows > 0 && lean_applies(x, k, g.kpad, req)) {
     int lg = 0;
     int64_t lcap = 0;
-    ldefer_b = ctx.alloc(lean_defer_bytes(x.rows, x.cols, ctx.info().cu_count, &lg, &lcap));
+    ldefer_b =
+        ctx.alloc(lean_defer_bytes(x.rows, x.cols, g.kpad, ctx.info().cu_count, &lg, &lcap));
     req.defer_rows = ldefer_b.as<int32_t>();
     req.defer_count = reinterpret_cast<unsigned*>(req.defer_rows + size_t(lg) * size_t(lcap));
   }
@@ -1268,6 +1281,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         ar->used() + ib + ar->budget() / 4 <= ar->budget()) {
       img_b = ctx.alloc(ib);
       img_beta_b = ctx.alloc(sizeof(float) * 4);
+      res.image_bytes = static_cast<int64_t>(ib);
     }
   }
   // with the adaptive scan off, full passes write the per-row bounds (8 B/row) only where a

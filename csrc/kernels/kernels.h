@@ -152,6 +152,8 @@ int kmeans_lloyd_grid(int64_t n, int num_cus);
 // Waves per workgroup of a lean-kernel variant; per-workgroup capacity of its deferral list
 // (rows; `waves` sub-segments of seg_cap / waves each, counts [grid][16]).
 int kmeans_lloyd_waves(int variant);
+// Chunks of 32 centroids the register-resident-plane variant (11) holds at width d (0: none).
+int kmeans_lloyd_rch(int d);
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves);
 // One pass: rows whose tier-1 answer is sure are finished (labels / mindist / bounds / cost /
 // fixed-point statistics, delta mode over tile_list); the others go to a.defer_rows.  variant

@@ -16,6 +16,29 @@ __host__ __device__ inline size_t round16(size_t v) { return (v + 15) / 16 * 16;
 __host__ __device__ inline int stride_bf16(int dp) { return dp + 8; }  // (dp+8)/8 odd slots
 __host__ __device__ inline int stride_f32(int dp) { return dp + 4; }   // (dp+4)/4 odd slots
 
+// Raw buffer resource over [base, base + bytes) (gfx9 dword3 0x00020000).  Loads / stores
+// through it at an out-of-range offset read 0 / are dropped by the buffer unit, so a per-lane
+// predicate becomes an offset instead of a branch: the instruction is issued on every path,
+// the count of vector-memory operations per loop trip stays fixed, and the compiler's wait for
+// an older prefetch can stay partial (s_waitcnt vmcnt counts in issue order; a conditional
+// store makes it fall back to vmcnt(0) — a wait for this tile's own stores).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kBufOff = 0x80000000u;
+__device__ inline __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), static_cast<short>(0),
+                                           static_cast<int>(bytes), 0x00020000);
+}
+__device__ inline void buf_store_b32(__amdgpu_buffer_rsrc_t rs, uint32_t off, int v, bool on) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, rs, on ? off : kBufOff, 0, 0);
+}
+__device__ inline void buf_store_f2(__amdgpu_buffer_rsrc_t rs, uint32_t off, float2 v, bool on) {
+  const u32x2 w = {__float_as_uint(v.x), __float_as_uint(v.y)};
+  __builtin_amdgcn_raw_buffer_store_b64(w, rs, on ? off : kBufOff, 0, 0);
+}
+__device__ inline int buf_load_b32(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool on) {
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, on ? off : kBufOff, 0, 0);
+}
+
 // v_med3_i32 as a pure operation (schedulable: no volatile)
 __device__ inline int med3_i32_pure(int a, int b, int c) {
   int r;

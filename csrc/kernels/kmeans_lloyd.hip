@@ -142,10 +142,18 @@ __device__ inline void split_f16(float v, _Float16& hi, _Float16& lo) {
 // re-read theirs), so PF 2 can reuse their registers, and the bounds' upper half comes from the
 // tier-1 distance plus its error bound.
 // U: k chunks per step of the distance loop (1 or 2).
-template <int KS, bool XB, int WAVES, int PF, bool COST, int U, bool SG = false>
+// RCH > 0: register-resident plane — every wave copies the whole fp16 plane (kpad <= 32 RCH
+// centroids, RCH x KS fragments of 4 registers) out of LDS once, so the distance loop reads no
+// LDS at all (the LDS plane otherwise costs each tile 7 x 4 ds_read_b128 per wave, as many LDS
+// cycles as MFMA cycles at 4 waves/SIMD, and exposes their latency before every MFMA); chunk
+// c + 1's MFMA chain is issued before chunk c's epilogue (two accumulators), so one wave keeps
+// the matrix pipe busy under its own VALU.  Run at 2 waves/SIMD (8 per workgroup).
+template <int KS, bool XB, int WAVES, int PF, bool COST, int U, bool SG = false, int RCH = 0>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a) {
   constexpr int DP = 16 * KS;
   constexpr int NT = WAVES * 64;
+  // image passes: tiles of operands in flight per wave (3 waves/SIMD have the registers for 2)
+  constexpr int PD = WAVES == 12 ? 2 : 1;
   using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int kpad = a.kpad, k = a.k, d = a.d;
@@ -182,6 +190,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
   }
   const float a2 = alpha * alpha;
+  const float inv_a2 = 1.f / a2;  // (a power of two: multiplying is the division, bitwise)
   const float beta_w = 0.25f * alpha;  // the scale a writing pass gives the image
   if (a.img_mode == 1 && blockIdx.x == 0 && tid == 0) a.img_beta[0] = beta_w;
 
@@ -213,8 +222,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   }
   __syncthreads();
 
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform)
   const int r = lane & 31, h = lane >> 5;
+  // register-resident plane: this lane's A fragments of every chunk (zero past kpad)
+  f16x8 pr[RCH > 0 ? RCH : 1][KS];
+  if constexpr (RCH > 0) {
+#pragma unroll
+    for (int c = 0; c < RCH; ++c)
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        pr[c][s] = (32 * c < kpad) ? *reinterpret_cast<const f16x8*>(
+                                         ph + size_t(32 * c + r) * sb + 8 * h + 16 * s)
+                                   : f16x8{};
+  }
   // tier-1 bound on two candidates' distance error (alpha^2 units): the cross term
   // 2 x 2 x 2^-10 |alpha c||alpha x| (fp16 products), fp16 subnormals d 2^-14, the bias pairs
   // 2^-21 (|c|^2 + |x|^2), fp32 accumulation 4e-5 (cmax^2 + |x|^2), plus the key truncation
@@ -225,7 +245,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const float thr_c = (XB ? 0.0020f : 0.0040f) * cm_s;
   const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
   const float mrel = 4e-7f * float(d + 8);                // fp32 evaluation margin (bounds)
-  const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);  // direct-form |x - c|^2 rounding
+  // direct-form |x - c|^2 rounding; the bound square roots are v_sqrt_f32 (1 ulp: inside the
+  // 1e-6 relative widening of both bounds)
+  const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);
   const int64_t ntiles_all = (a.n + 31) / 32;
   const bool listed = a.tile_list != nullptr;
   const int64_t T = a.tiles_per_block;
@@ -240,13 +262,25 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const int64_t sub_cap = a.seg_cap / WAVES;
   int32_t* dseg = a.defer_rows + blockIdx.x * a.seg_cap + wave * sub_cap;
   unsigned n_def = 0;  // wave-uniform
+  // per-row outputs through buffer resources over this workgroup's rows (listed tiles are the
+  // workgroup's own too): predicated by offset, issued on every path (see buf_rsrc)
+  const int64_t row0 = t0 * 32;
+  const int64_t wrows = row0 < a.n ? (a.n - row0 < T * 32 ? a.n - row0 : T * 32) : 0;
+  const __amdgpu_buffer_rsrc_t rs_lab =
+      buf_rsrc(a.labels ? a.labels + row0 : nullptr, a.labels ? uint32_t(wrows * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t rs_bnd =
+      buf_rsrc(a.bounds ? a.bounds + row0 : nullptr, a.bounds ? uint32_t(wrows * 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rs_def = buf_rsrc(dseg, uint32_t(sub_cap * 4));
   double my_cost = 0.0;
 
   auto tile_of = [&](int64_t q) OAP_AI -> int64_t {
     if (npos == 0) return 0;  // (prefetch of an empty range: any real tile)
     q = q < npos ? q : npos - 1;
     if (!listed) return t0 + q;
-    const int64_t tl = int64_t(seg[q]);
+    // (scalar load: the index is wave-uniform, and a vector load here would be the youngest
+    // memory op, so the wait for it would also wait for the prefetch)
+    typedef const int32_t __attribute__((address_space(4)))* seg_cptr;
+    const int64_t tl = int64_t(((seg_cptr)(seg))[q]);
     return tl < 0 ? 0 : (tl < ntiles_all ? tl : ntiles_all - 1);
   };
   auto load_row = [&](int64_t row, F& dst) OAP_AI {
@@ -392,16 +426,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     // loop — loaded here, ahead of the next tile's prefetch, so no wait in the loop covers the
     // prefetch (s_waitcnt vmcnt counts in issue order)
     int2 kin = make_int2(0x7fffffff, 0x7fffffff);
-    if (keys_in && h == 0 && valid) kin = a.keys[row];
-    int old = -1;
-    if (a.delta && valid) old = a.labels[row];
+    if (!IMG && keys_in && h == 0 && valid) kin = a.keys[row];
+    const uint32_t roff = uint32_t(row - row0);  // (valid rows: this workgroup's)
+    int old = buf_load_b32(rs_lab, roff * 4, a.delta && valid);
+    old = (a.delta && valid) ? old : -1;
     // MFMA B operand: fp16 of alpha x with the bias slots [16, 16, hi, lo (alpha^2 |x|^2 / 16)]
     f16x8 xh[KS];
     float nx2_s;
     if constexpr (IMG) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) xh[s] = xi[s];
-      load_img(tile_of(pf), xin);  // the next tile's operands (xin may be xi): in flight
+      if constexpr (PD == 2) {  // xi takes the next tile's (landed or in flight), xin pf's
+#pragma unroll
+        for (int s = 0; s < KS; ++s) xi[s] = xin[s];
+      }
+      load_img(tile_of(pf), xin);  // operands PD tiles ahead (PD 1: xin is xi): in flight
       // alpha^2 |x|^2 from the bias pair (h = 1 lanes' slots 6, 7 of the last k-step)
       const float mine = kBiasUnit * (static_cast<float>(xh[KS - 1][6]) +
                                       static_cast<float>(xh[KS - 1][7]));
@@ -496,6 +535,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     float b1 = 0.f, b2 = 0.f, tt = 0.f;
     if (do_dist) {
       int c0 = 0;
+      if constexpr (RCH > 0) {
+        // software-pipelined over chunks: issue chunk c's MFMA chain, then fold chunk c - 1
+        f32x16 accA, accB;
+        auto chain = [&](int c, f32x16& acc) OAP_AI {
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr[c][0], xh[0], f32x16{}, 0, 0, 0);
+#pragma unroll
+          for (int s = 1; s < KS; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr[c][s], xh[s], acc, 0, 0, 0);
+        };
+        const int nch = kpad >> 5;  // <= RCH (kmeans_lloyd checks)
+#pragma unroll
+        for (int c = 0; c <= RCH; ++c) {
+          if (c < RCH && c < nch) chain(c, (c & 1) ? accB : accA);
+          if (c >= 1 && c - 1 < nch) epilogue(32 * (c - 1), ((c - 1) & 1) ? accB : accA);
+        }
+        c0 = kpad;
+      }
       if constexpr (U == 2) {
         // two chunks per step: all 2 KS fragment reads issue together, two independent MFMA
         // chains, then both epilogues (ILP the single-chunk loop lacks)
@@ -550,13 +606,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
       k2 = min(max(k1, o1), min(k2, o2));
       k1 = min(k1, o1);
-      if (keys_out) {  // not the last chunk: carry the pair to the next one
+      if (!IMG && keys_out) {  // not the last chunk: carry the pair to the next one
         if (h == 0 && valid) a.keys[row] = make_int2(k1, k2);
         return;
       }
       b1 = __int_as_float(k1 & ~0x3ff);
       b2 = __int_as_float(k2 & ~0x3ff);
-      tt = fmaf(thr_c, sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
+      tt = fmaf(thr_c, __builtin_amdgcn_sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s +
+           2.5e-4f * fabsf(b2);
       // rows beyond fp16's comfortable range (alpha |x| >= 2^10) are always re-decided
       unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
     } else {
@@ -566,11 +623,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     }
     // ---- defer unsure rows to the exact re-decision (wave-private sub-segment, in order)
     const unsigned long long um = __ballot(unsure && h == 0);
-    if (um) {
-      if (unsure && h == 0)
-        dseg[n_def + __popcll(um & ((1ull << lane) - 1ull))] = static_cast<int32_t>(row);
-      n_def += static_cast<unsigned>(__popcll(um));
-    }
+    buf_store_b32(rs_def, (n_def + __popcll(um & ((1ull << lane) - 1ull))) * 4u,
+                  static_cast<int32_t>(row), unsure && h == 0);
+    n_def += static_cast<unsigned>(__popcll(um));
     const bool done = valid && !unsure;
     int b = k1 & 0x3ff;
     b = (b < kglob) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
@@ -611,15 +666,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           part = fmaf(e, e, part);
         }
       const float rowcost = part + __shfl_xor(part, 32, 64);
-      if (done && h == 0) {
-        if (a.labels) a.labels[row] = b;
+      const bool out = done && h == 0;
+      buf_store_b32(rs_lab, roff * 4, b, out);
+      // every other candidate's alpha^2 distance is >= b2 - tt; back to data units
+      const float lo = (b2 - (tt + mrel * (nx2_s + cm_s * cm_s))) * inv_a2;
+      buf_store_f2(rs_bnd, roff * 8,
+                   make_float2(__builtin_amdgcn_sqrtf(rowcost) * ueps + 1e-30f,
+                               __builtin_amdgcn_sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f)),
+                   out);
+      if (out) {
         if (a.mindist) a.mindist[row] = rowcost;
-        if (a.bounds) {
-          // every other candidate's alpha^2 distance is >= b2 - tt; back to data units
-          const float lo = (b2 - (tt + mrel * (nx2_s + cm_s * cm_s))) / a2;
-          a.bounds[row] = make_float2(sqrtf(rowcost) * ueps + 1e-30f,
-                                      sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
-        }
         my_cost += double(rowcost);
       }
     } else {
@@ -631,16 +687,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           xr = x;
         add_row(xr, b, false);
       }
-      if (done && h == 0) {
-        if (a.labels) a.labels[row] = b;
-        if (a.bounds) {
-          // the pick's alpha^2 distance is <= b1 + tt, every other one >= b2 - tt
-          const float mg = mrel * (nx2_s + cm_s * cm_s);
-          const float up = (b1 + tt + mg) / a2, lo = (b2 - (tt + mg)) / a2;
-          a.bounds[row] = make_float2(sqrtf(fmaxf(up, 0.f)) * (1.f + 1e-6f) + 1e-30f,
-                                      sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
-        }
-      }
+      const bool out = done && h == 0;
+      buf_store_b32(rs_lab, roff * 4, b, out);
+      // the pick's alpha^2 distance is <= b1 + tt, every other one >= b2 - tt
+      const float mg = mrel * (nx2_s + cm_s * cm_s);
+      const float up = (b1 + tt + mg) * inv_a2, lo = (b2 - (tt + mg)) * inv_a2;
+      buf_store_f2(rs_bnd, roff * 8,
+                   make_float2(
+                       __builtin_amdgcn_sqrtf(fmaxf(up, 0.f)) * (1.f + 1e-6f) + 1e-30f,
+                       __builtin_amdgcn_sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f)),
+                   out);
     }
   };
 
@@ -652,10 +708,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     // call site: a ping-pong of two register sets needs two inlined copies of the pass body)
     if constexpr (!XB && PF == 2 && !COST) {
       F unused;
-      f16x8 ia[KS];
+      f16x8 ia[KS], ib[KS];
       load_img(tile_of(t), ia);
+      if constexpr (PD == 2) load_img(tile_of(t + stride), ib);
       for (; t < npos; t += stride)  // t is wave-uniform: every branch stays uniform
-        process(std::true_type{}, t, tile_of(t), unused, unused, t + stride, ia, ia);
+        process(std::true_type{}, t, tile_of(t), unused, unused, t + PD * stride, ia,
+                PD == 2 ? ib : ia);
     }
   } else if constexpr (PF == 1) {
     F xa, xb;
@@ -709,18 +767,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   }
 }
 
-template <int KS, bool XB, int WAVES, int PF, bool COST, int U = 1, bool SG = false>
+template <int KS, bool XB, int WAVES, int PF, bool COST, int U = 1, bool SG = false, int RCH = 0>
 void launch_lean(const LeanArgs& a, int grid, hipStream_t s) {
   const LeanSmem L =
       lean_plan(16 * KS, a.kpad, a.k, a.d, a.accumulate, a.sums_too, WAVES, a.delta != 0);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG>),
+        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG, RCH>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG>), dim3(grid),
+  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG, RCH>), dim3(grid),
                      dim3(WAVES * 64), L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
@@ -754,6 +812,13 @@ void launch_lean_v(const LeanArgs& a, int grid, int variant, bool cost, hipStrea
       if (cost) launch_lean<KS, XB, 16, 0, true, 3>(a, grid, s);
       else launch_lean<KS, XB, 16, 0, false, 3>(a, grid, s);
       break;
+    case 11:  // 2 waves/SIMD, register-resident plane (kpad <= 32 kmeans_lloyd_rch(d))
+      if constexpr (KS <= 4) {
+        constexpr int R = KS == 4 ? 7 : 8;
+        if (cost) launch_lean<KS, XB, 8, 0, true, 1, false, R>(a, grid, s);
+        else launch_lean<KS, XB, 8, 2, false, 1, false, R>(a, grid, s);
+      }
+      break;  // (other widths: rejected by kmeans_lloyd)
     case 7:  // 3 waves/SIMD, two chunks per step, prefetch without the cost
       if (cost) launch_lean<KS, XB, 12, 0, true, 2>(a, grid, s);
       else launch_lean<KS, XB, 12, 2, false, 2>(a, grid, s);
@@ -1196,7 +1261,13 @@ int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid) {
 }
 
 int kmeans_lloyd_waves(int variant) {
+  if (variant == 11) return 8;
   return (variant == 3 || variant == 5 || variant == 7 || variant == 8 || variant == 9) ? 12 : 16;
+}
+
+int kmeans_lloyd_rch(int d) {
+  const int ks = (d + 4 + 15) / 16;
+  return ks <= 3 ? 8 : (ks == 4 ? 7 : 0);
 }
 
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
@@ -1223,6 +1294,8 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, kmeans_lloyd_waves(variant)) &&
                 a.ld == kmeans_ld(a.d, a.xbf16),
             "kmeans_lloyd: unsupported arguments");
+  OAP_CHECK(variant != 11 || (kmeans_lloyd_rch(a.d) > 0 && a.kpad <= 32 * kmeans_lloyd_rch(a.d)),
+            "kmeans_lloyd: the register-plane variant needs kpad <= 32 kmeans_lloyd_rch(d)");
   OAP_CHECK(!a.delta || a.labels, "kmeans_lloyd: delta mode needs the previous labels");
   OAP_CHECK(!a.tile_list || (a.delta && a.tile_count), "kmeans_lloyd: tile list without delta");
   // the operand image: f32 rows, one launch; written by a full pass, read without the per-tile

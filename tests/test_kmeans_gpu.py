@@ -349,21 +349,25 @@ def test_operand_image_bitwise(native, monkeypatch, d, k, sigma, tol):
 def test_operand_image_scale_fallback(native):
     """Initial centers far smaller than the data fix a large image scale; once the centers grow
     past its range (beta max|c| > 2^9) the passes read the f32 rows — still the exact fit."""
-    n, d, k = 100000, 30, 40
+    n, d, k = 100000, 20, 40
     g = native.Context(0, 0.5, 0)
     t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 50.0, 2.0, 5)
     init = (t.to_numpy(g, 0, k) * 1e-3).astype(np.float32).astype(np.float64)
     comm = native.LocalComm(True)
     ri = native.kmeans_fit(g, comm, t, init, k, 6, -1.0)
     rp = native.kmeans_fit(g, comm, t, init, k, 6, -1.0, precise=True)
+    print({key: ri[key] for key in ("image_passes", "image_bytes", "deferred_rows", "moved_rows",
+                                    "assign_path", "num_iter")})
     assert ri["image_passes"] > 0
     assert ri["last_counts"] == rp["last_counts"]
     assert np.array_equal(ri["centers"], rp["centers"])
 
 
-@pytest.mark.parametrize("variant", [0, 3, 5, 7])
-def test_lean_variants_agree(native, variant):
-    """Every workgroup shape of the lean kernel gives the same fit."""
+@pytest.mark.parametrize("variant", [0, 3, 5, 7, 11])
+def test_lean_variants_agree(native, monkeypatch, variant):
+    """Every workgroup shape of the lean kernel gives the same fit (f32-row operands: the
+    operand image's scale moves a few rows across the tier-1 bound, not any label)."""
+    monkeypatch.setenv("OAP_KMEANS_IMAGE", "0")
     g = native.Context(0, 0.5, 0)
     t = native.synth_blobs(g, 200000, 50, native.kmeans_ld(50), 0, 100, 10.0, 8.0, 3)
     init = t.to_numpy(g, 0, 100)
