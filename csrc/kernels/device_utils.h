@@ -23,6 +23,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned long long u64;
 
+// The value of lane l ^ 32 (the other half of the wave), as __shfl_xor(v, 32): one
+// v_permlane32_swap (a VALU op) instead of an LDS ds_bpermute round trip
+// (checked on gfx950 by tools/probes/permlane32_probe.hip).
+__device__ inline int xor32_i(int v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (threadIdx.x & 32) ? p[0] : p[1];
+}
+__device__ inline float xor32_f(float v) { return __int_as_float(xor32_i(__float_as_int(v))); }
+
 __device__ inline double wave_sum_f64(double v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);

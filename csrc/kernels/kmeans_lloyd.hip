@@ -444,7 +444,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       // alpha^2 |x|^2 from the bias pair (h = 1 lanes' slots 6, 7 of the last k-step)
       const float mine = kBiasUnit * (static_cast<float>(xh[KS - 1][6]) +
                                       static_cast<float>(xh[KS - 1][7]));
-      const float other = __shfl_xor(mine, 32, 64);
+      const float other = xor32_f(mine);
       nx2_s = h ? mine : other;
     } else {
       float nx2 = 0.f;
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
-      nx2 += __shfl_xor(nx2, 32, 64);
+      nx2 += xor32_f(nx2);
       if (a.xnorm && pos < npos) {  // per-tile max |x|^2 (the delta scan's pruning margin)
         float tmax = nx2;
 #pragma unroll
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       }
       k2 = min(max(k1, kin.x), min(k2, kin.y));  // (top-2 of the union: order-free)
       k1 = min(k1, kin.x);
-      const int o1 = __shfl_xor(k1, 32, 64), o2 = __shfl_xor(k2, 32, 64);
+      const int o1 = xor32_i(k1), o2 = xor32_i(k2);
       k2 = min(max(k1, o1), min(k2, o2));
       k1 = min(k1, o1);
       if (!IMG && keys_out) {  // not the last chunk: carry the pair to the next one
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           const float e = xr.at(s, j) - cb[s][j];
           part = fmaf(e, e, part);
         }
-      const float rowcost = part + __shfl_xor(part, 32, 64);
+      const float rowcost = part + xor32_f(part);
       const bool out = done && h == 0;
       buf_store_b32(rs_lab, roff * 4, b, out);
       // every other candidate's alpha^2 distance is >= b2 - tt; back to data units
