@@ -25,10 +25,11 @@ def test_gpu_matches_oracle(native, gpu_world, rank, alpha, iters):
     ref = als_vanilla.fit(u, i, r, rank, iters, 0.1, True, alpha, False, 7)
     assert out["failed_rows"] == 0
     assert np.array_equal(out["user_ids"], ref.user_ids)
-    scale = np.abs(ref.user_factors).max()
-    np.testing.assert_allclose(out["user_factors"], ref.user_factors, atol=2e-3 * scale)
-    np.testing.assert_allclose(out["item_factors"], ref.item_factors,
-                               atol=2e-3 * np.abs(ref.item_factors).max())
+    eu = np.abs(out["user_factors"] - ref.user_factors).max() / np.abs(ref.user_factors).max()
+    ei = np.abs(out["item_factors"] - ref.item_factors).max() / np.abs(ref.item_factors).max()
+    print(f"rank {rank}: max |gpu - fp64| / max |fp64|: users {eu:.2e} items {ei:.2e}")
+    # measured on MI355X: <= 2.2e-5 (rank 33, alpha 10); fp32 Gramian + Cholesky vs fp64
+    assert eu < 1e-4 and ei < 1e-4
 
 
 def test_gpu_explicit_kernel_matches_oracle(native, gpu_world):

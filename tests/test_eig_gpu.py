@@ -57,7 +57,9 @@ def test_gpu_eig_speed_d1000(native, ctx):
     _, _, tm = native.sym_eig_gpu(ctx, a, 50)
     wall = (time.perf_counter() - t0) * 1e3
     print("eig d=1000 k=50:", tm, "wall_ms", wall)
-    assert tm["tridiag_ms"] < 50.0  # (regression guard; the target is <= 10 ms total)
+    # measured on MI355X: tridiag 6.6 + bisection 0.7 + host 0.6 + back-transform 0.8 ms
+    total = tm["tridiag_ms"] + tm["bisect_ms"] + tm["host_ms"] + tm["backtransform_ms"]
+    assert tm["tridiag_ms"] < 10.0 and total < 15.0
 
 
 def test_pca_uses_gpu_eig(native):
