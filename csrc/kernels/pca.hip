@@ -558,8 +558,26 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     if (r_begin + kXRows < r_end) load(r_begin + kXRows);
     lds_barrier();
   }
+  // one staged element of the next chunk (el = 8 j + 2 q + side): the staging is spread over
+  // the k-steps, between MFMA groups, instead of running as its own phase before the barrier
+  // (same elements, same order per column sum: bitwise the phase form)
+  auto stage_el = [&](double* nb, int64_t rn, int el) {
+    const int side = el & 1, q = (el >> 1) & 3, j = el >> 3;
+    const double mr = rn + lr + 16 * j < r_end ? 1.0 : 0.0;
+    if (side == 0) {
+      const double c = (double(vI[j][q]) - shI[q]) * (mr * mI[q]);
+      cs[q] += c;
+      nb[(4 * lq + q) * kXS + lr + 16 * j] = c;
+    } else if (!diag) {
+      nb[kXPlane + (4 * lq + q) * kXS + lr + 16 * j] = (double(vJ[j][q]) - shJ[q]) * (mr * mJ[q]);
+    }
+  };
+  constexpr int kEl = kRpt * 8, kPerStep = kEl / (kXRows / 4);
+  static_assert(kEl % (kXRows / 4) == 0, "staging elements per k-step");
   for (int64_t r0 = r_begin; r0 < r_end; r0 += kXRows) {
     const double* buf = lds + cur * (2 * kXPlane);
+    double* nbuf = lds + (cur ^ 1) * (2 * kXPlane);  // last read before the previous barrier
+    const bool more = r0 + kXRows < r_end;
 #pragma unroll
     for (int ks = 0; ks < kXRows / 4; ++ks) {
       double av[4], bv[2];
@@ -572,11 +590,12 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
 #pragma unroll
         for (int y = 0; y < 2; ++y)
           acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+      if (more) {
+#pragma unroll
+        for (int e = 0; e < kPerStep; ++e) stage_el(nbuf, r0 + kXRows, ks * kPerStep + e);
+      }
     }
-    if (r0 + kXRows < r_end) {  // the other stage was last read before the previous barrier
-      stage(lds + (cur ^ 1) * (2 * kXPlane), r0 + kXRows);
-      if (r0 + 2 * kXRows < r_end) load(r0 + 2 * kXRows);
-    }
+    if (more && r0 + 2 * kXRows < r_end) load(r0 + 2 * kXRows);
     lds_barrier();
     cur ^= 1;
   }
