@@ -386,6 +386,86 @@ __global__ __launch_bounds__(256) void oap_als_rotate(const float* __restrict__ 
   }
 }
 
+// The same product on the f32 matrix cores (v_mfma_f32_16x16x4_f32: exact f32 products, the
+// VALU form's rate per clock but without its per-FMA LDS broadcast reads): 256 threads, a
+// 64-row tile in LDS, wave w owns rows 16 w .. 16 w + 15 and all NB column blocks (NB
+// accumulators of 4), R stays in LDS for the whole launch.
+template <int NB>
+__global__ __launch_bounds__(256) void oap_als_rotate_mfma(const float* __restrict__ in,
+                                                           const int32_t* __restrict__ in_rows,
+                                                           float* __restrict__ out,
+                                                           const int32_t* __restrict__ out_rows,
+                                                           int64_t n, const float* __restrict__ R) {
+  constexpr int LD = 16 * NB, XS = LD + 1;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Rs = lds;            // LD x LD, row k = input feature
+  float* Xs = lds + LD * LD;  // 64 x XS
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  for (int i = t; i < LD * LD / 4; i += 256)
+    reinterpret_cast<float4*>(Rs)[i] = reinterpret_cast<const float4*>(R)[i];
+  for (int64_t r0 = int64_t(blockIdx.x) * 64; r0 < n; r0 += int64_t(gridDim.x) * 64) {
+    __syncthreads();
+    for (int i = t; i < 64 * (LD / 4); i += 256) {
+      const int rr = i / (LD / 4), c4 = i % (LD / 4);
+      const int64_t gi = r0 + rr;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gi < n) {
+        const int64_t src_row = in_rows ? in_rows[gi] : gi;
+        v = *reinterpret_cast<const float4*>(in + src_row * LD + 4 * c4);
+      }
+      float* xd = Xs + rr * XS + 4 * c4;
+      xd[0] = v.x;
+      xd[1] = v.y;
+      xd[2] = v.z;
+      xd[3] = v.w;
+    }
+    __syncthreads();
+    f4 acc[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[b] = f4{0.f, 0.f, 0.f, 0.f};
+    const float* xa = Xs + (16 * wave + i16) * XS + kq;  // A: row i16 of the wave, k = 4 ks + kq
+    const float* rb = Rs + kq * LD + i16;                // B: k = 4 ks + kq, column 16 b + i16
+#pragma unroll 4
+    for (int ks = 0; ks < LD / 4; ++ks) {
+      const float av = xa[4 * ks];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, rb[4 * ks * LD + 16 * b], acc[b], 0, 0,
+                                                      0);
+    }
+    // C/D layout: lane holds column 16 b + i16 of rows 4 kq + e of the wave's 16
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t gi = r0 + 16 * wave + 4 * kq + e;
+      if (gi < n) {
+        const int64_t dst_row = out_rows ? out_rows[gi] : gi;
+        float* o = out + dst_row * LD + i16;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) o[16 * b] = acc[b][e];
+      }
+    }
+  }
+}
+
+template <int NB>
+void launch_rotate_mfma(const float* in, const int32_t* in_rows, float* out,
+                        const int32_t* out_rows, int64_t n, const float* R, int num_cus,
+                        hipStream_t s) {
+  constexpr int LD = 16 * NB;
+  const size_t lds = size_t(LD * LD + 64 * (LD + 1)) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_als_rotate_mfma<NB>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int grid = int(std::min<int64_t>((n + 63) / 64, int64_t(num_cus) * 2));
+  hipLaunchKernelGGL(oap_als_rotate_mfma<NB>, dim3(grid), dim3(256), lds, s, in, in_rows, out,
+                     out_rows, n, R);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
 template <int CW>
 void launch_rotate(const float* in, const int32_t* in_rows, float* out, const int32_t* out_rows,
                    int64_t n, const float* R, int num_cus, hipStream_t s) {
@@ -432,6 +512,22 @@ void als_rotate(const float* in, const int32_t* in_rows, float* out, const int32
   if (n <= 0) return;
   OAP_CHECK(ld % 16 == 0 && ld >= 16 && ld <= 128,
             "als_rotate: ld must be 16..128, multiple of 16");
+  static const bool valu = [] {
+    const char* e = std::getenv("OAP_ALS_ROTATE_VALU");
+    return e && *e == '1';
+  }();
+  if (!valu) {
+    switch (ld / 16) {
+      case 1: launch_rotate_mfma<1>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      case 2: launch_rotate_mfma<2>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      case 3: launch_rotate_mfma<3>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      case 4: launch_rotate_mfma<4>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      case 5: launch_rotate_mfma<5>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      case 6: launch_rotate_mfma<6>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      case 7: launch_rotate_mfma<7>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+      default: launch_rotate_mfma<8>(in, in_rows, out, out_rows, n, R, num_cus, s); return;
+    }
+  }
   switch (ld / 16) {
     case 1: launch_rotate<4>(in, in_rows, out, out_rows, n, R, num_cus, s); break;
     case 2: launch_rotate<8>(in, in_rows, out, out_rows, n, R, num_cus, s); break;
