@@ -80,24 +80,38 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
   float* dhs = gs + 16 * NBR;                     // 16 NBR floats: D^{-1/2}
   const int ld = a.ld;
 
-  while (true) {
-    // lane masks recomputed per row (kernels/als_chol.h: fresh_lane)
-    const int lane = als::fresh_lane(), kk = lane >> 4, c = lane & 15;
+  // Row headers run one row ahead: the queue pop, the row id, its CSR bounds and its (item,
+  // rating) pairs are four dependent memory round trips.  Each level of the NEXT row is issued
+  // during one phase of the current row (D^{-1/2}, the two W halves, the Cholesky) and consumed
+  // in the next, so only the factor-row gathers stay exposed.  Loads are unconditional (indices
+  // clamped) so no branch makes the compiler drain the memory counter.
+  const int64_t last = a.nrows - 1;  // (launched with a.nrows >= 1)
+  int64_t q, hp1;
+  int hit;
+  float hrv;
+  int64_t hp0;
+  {
+    const int lane = als::fresh_lane();
     unsigned long long q_u = 0;
     if (lane == 0) q_u = atomicAdd(a.queue, 1ull);
-    const int64_t q = static_cast<int64_t>(__shfl(q_u, 0, 64));
-    if (q >= a.nrows) break;
-    const int64_t row = a.rows[q];
-    const int64_t p0 = a.rowptr[row];
-    const int n = static_cast<int>(a.rowptr[row + 1] - p0);  // <= 16 NBN (host-checked)
+    q = static_cast<int64_t>(__shfl(q_u, 0, 64));
+    const int64_t row = a.rows[q < a.nrows ? q : last];
+    hp0 = a.rowptr[row];
+    hp1 = a.rowptr[row + 1];
+    const int64_t ql = hp0 + (lane < int(hp1 - hp0) ? lane : 0);
+    hit = a.cols[ql];
+    hrv = a.vals[ql];
+  }
+  while (q < a.nrows) {
+    // lane masks recomputed per row (kernels/als_chol.h: fresh_lane)
+    const int lane = als::fresh_lane(), kk = lane >> 4, c = lane & 15;
+    const int n = static_cast<int>(hp1 - hp0);  // <= 16 NBN (host-checked)
+    unsigned long long qn_u = 0;
+    if (lane == 0) qn_u = atomicAdd(a.queue, 1ull);  // the next row's slot (in flight)
 
     // per-rating scalars, lane l = rating l (lanes >= n: weight 0)
-    int it = 0;
-    float rv = 0.f;
-    if (lane < n) {
-      it = a.cols[p0 + lane];
-      rv = a.vals[p0 + lane];
-    }
+    const int it = lane < n ? hit : 0;
+    const float rv = lane < n ? hrv : 0.f;
     const float cw = a.alpha * fabsf(rv);
     const float sc = sqrtf(cw);
     const bool pos = lane < n && rv > 0.f;
@@ -125,6 +139,8 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
     }
     const bool fail_d = __ballot(!okd) != 0;
     __syncthreads();
+    const int64_t qn = static_cast<int64_t>(__shfl(qn_u, 0, 64));
+    const int64_t rown = a.rows[qn < a.nrows ? qn : last];  // (in flight under the first half)
     auto dh4 = [&](int qb) { return *reinterpret_cast<const float4*>(dhs + 16 * qb + 4 * kk); };
     // W fragments (rotated factors scaled by D^{-1/2}), g = W^T w (to LDS), the M tiles and
     // S W g, accumulated over two halves of the fragment columns: half of W in registers at a
@@ -195,6 +211,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
           for (int e = 0; e < 4; ++e) hp[bi] = fmaf(W[bi][qb][e], g[qb][e], hp[bi]);
     };
     half(std::integral_constant<int, 0>{});
+    const int64_t p0n = a.rowptr[rown], p1n = a.rowptr[rown + 1];  // (under the second half)
     if constexpr (NBR > QH) half(std::integral_constant<int, QH>{});
 
     // M = I + S W W^T S into LDS (tile (bi, bj): lane holds rows 16 bi + 4 kk + e, column
@@ -228,6 +245,17 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
     }
     h *= sc;  // lane l: s_l
     __syncthreads();
+    // the next row's (item, rating) pairs, in flight under the Cholesky
+    const int64_t qln = p0n + (lane < int(p1n - p0n) ? lane : 0);
+    const int itn = a.cols[qln];
+    const float rvn = a.vals[qln];
+    auto advance = [&]() {
+      q = qn;
+      hp0 = p0n;
+      hp1 = p1n;
+      hit = itn;
+      hrv = rvn;
+    };
 
     const bool spd = (a.ablate & 32) ? true : als::chol_factor<NBN, kRS>(M);
     float* out = a.out + q * ld;
@@ -235,6 +263,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
       if (lane == 0) atomicAdd(a.fail, 1ull);
       for (int k = lane; k < ld; k += 64) out[k] = 0.f;
       __syncthreads();
+      advance();
       continue;
     }
     float v1 = 0.f;
@@ -277,6 +306,7 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
             make_float4(xv[0], xv[1], xv[2], xv[3]);
     }
     __syncthreads();
+    advance();
   }
 }
 
