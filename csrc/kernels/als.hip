@@ -402,13 +402,23 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
   float* M = lds;  // lower 16x16 blocks, packed (mi)
   float* bv = lds + NB * (NB + 1) / 2 * kBlkF;  // RP
   const int r = a.r, lane = threadIdx.x;
-
-  while (true) {
+  // the next row's queue slot, row id and CSR bounds are fetched one row ahead (three
+  // dependent round trips), each under one phase of the current row (see als_lowrank.hip)
+  const int64_t last = a.nrows - 1;  // (launched with a.nrows >= 1)
+  int64_t q, row, hp0 = 0, hp1 = 0;
+  {
     unsigned long long q_u = 0;
     if (lane == 0) q_u = atomicAdd(a.queue, 1ull);
-    const int64_t q = static_cast<int64_t>(__shfl(q_u, 0, 64));
-    if (q >= a.nrows) break;
-    const int64_t row = a.rows[q];
+    q = static_cast<int64_t>(__shfl(q_u, 0, 64));
+    row = a.rows[q < a.nrows ? q : last];
+    if constexpr (!LONG) {
+      hp0 = a.rowptr[row];
+      hp1 = a.rowptr[row + 1];
+    }
+  }
+  while (q < a.nrows) {
+    unsigned long long qn_u = 0;
+    if (lane == 0) qn_u = atomicAdd(a.queue, 1ull);  // (in flight under the Gramian)
 
     f4 acc[NT];
 #pragma unroll
@@ -430,9 +440,11 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         nexp += static_cast<int>(pp[NT * 256 + NB * 64 + lane]);
       }
     } else if (!(a.ablate & 1)) {
-      accumulate<NB>(a.cols, a.vals, a.rowptr[row], a.rowptr[row + 1], a.src, a.ld, a.alpha,
-                     a.implicit != 0, acc, bacc, nexp);
+      accumulate<NB>(a.cols, a.vals, hp0, hp1, a.src, a.ld, a.alpha, a.implicit != 0, acc, bacc,
+                     nexp);
     }
+    const int64_t qn = static_cast<int64_t>(__shfl(qn_u, 0, 64));
+    const int64_t rown = a.rows[qn < a.nrows ? qn : last];  // (in flight under the assembly)
 #pragma unroll
     for (int f = 0; f < NB; ++f) {
       bacc[f] += __shfl_xor(bacc[f], 16, 64);
@@ -470,6 +482,17 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       }
     }
     __syncthreads();
+    int64_t p0n = 0, p1n = 0;
+    if constexpr (!LONG) {  // (in flight under the Cholesky)
+      p0n = a.rowptr[rown];
+      p1n = a.rowptr[rown + 1];
+    }
+    auto advance = [&]() {
+      q = qn;
+      row = rown;
+      hp0 = p0n;
+      hp1 = p1n;
+    };
 
     // ---- blocked right-looking Cholesky, 16-wide panels (kernels/als_chol.h)
     const bool spd = als::chol_factor<NB>(M, (a.ablate & 2) ? NB : 0);
@@ -478,6 +501,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
       if (lane == 0) atomicAdd(a.fail, 1ull);
       for (int i = lane; i < a.ld; i += 64) out[i] = 0.f;
       __syncthreads();
+      advance();
       continue;
     }
     // ---- blocked triangular solves, right-hand side in registers: lane l holds rows l and
@@ -490,6 +514,7 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
     if (lane + 64 < a.ld) out[lane + 64] = lane + 64 < r ? v1 : 0.f;
     for (int i = lane + 128; i < a.ld; i += 64) out[i] = 0.f;
     __syncthreads();
+    advance();
   }
 }
 
