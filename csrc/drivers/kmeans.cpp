@@ -1342,7 +1342,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   bool last_costless = false;  // the last iteration computed no cost (rank-uniform)
   for (int it0 = 0, nb_it = 0; it0 < p.max_iter && !stop; it0 += nb_it) {
     // the first batch is short so the adaptive choices (tier, scan) are made early
-    nb_it = std::min(it0 == 0 && B > 3 ? 3 : B, p.max_iter - it0);
+    // (with the scan on, the first batch ends after the first delta iteration: its moved-row
+    // share gates the first scan probe)
+    nb_it = std::min(it0 == 0 && B > 3 ? (scan_all ? 2 : 3) : B, p.max_iter - it0);
     scan_iters = 0;
     for (int b = 0; b < nb_it; ++b) {
       const int it = it0 + b;
@@ -1459,7 +1461,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
     if (ldstat_b.data())
-      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), sizeof(u64),
+      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), 2 * sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     u64 pruned_now = 0;
     if (scan)
@@ -1527,6 +1529,20 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (one scan right after a large move says little: turn off on two, or on a hopeless one)
       const bool was_probe = probing;
       probing = false;
+      // first batch (iterations 0-1, no scan yet): with more than 3% of the rows moving in the
+      // first delta iteration at most (0.97)^32 of the 32-row tiles can be free of movers — the
+      // first scan would prune almost nothing (overlapping clusters) and costs a bound write,
+      // a scan and a listed pass: back off as after a hopeless probe
+      if (it0 == 0 && scan_iters == 0 && delta_on && nb_it >= 2) {  // (rank-uniform)
+        double mv = ldstat_b.data() && x.rows > 0
+                        ? double(ldstat_h.as<u64>()[1]) / double(x.rows) : 0.0;
+        if (!comm.trivial()) mv = comm_allreduce_scalar(ctx, comm, mv, ReduceOp::Max);
+        if (mv > 0.03) {
+          delta_on = false;
+          delta_probe = 0;
+          probe_gap = std::min(std::max(probe_gap * 2, 4 * probe_gap0), 64);
+        }
+      }
       if (delta_on && scan_iters > 0 &&
           (frac < 0.02 || ((scan_iters > 1 || was_probe) && frac < 0.2))) {
         delta_on = false;

@@ -271,6 +271,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const __amdgpu_buffer_rsrc_t rs_bnd =
       buf_rsrc(a.bounds ? a.bounds + row0 : nullptr, a.bounds ? uint32_t(wrows * 8) : 0u);
   const __amdgpu_buffer_rsrc_t rs_def = buf_rsrc(dseg, uint32_t(sub_cap * 4));
+  const __amdgpu_buffer_rsrc_t rs_md =
+      buf_rsrc(a.mindist ? a.mindist + row0 : nullptr, a.mindist ? uint32_t(wrows * 4) : 0u);
+  const __amdgpu_buffer_rsrc_t rs_xn =
+      buf_rsrc(a.xnorm ? a.xnorm + t0 : nullptr, a.xnorm ? uint32_t((wrows + 31) / 32 * 4) : 0u);
   double my_cost = 0.0;
 
   auto tile_of = [&](int64_t q) OAP_AI -> int64_t {
@@ -453,12 +457,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += xor32_f(nx2);
-      if (a.xnorm && pos < npos) {  // per-tile max |x|^2 (the delta scan's pruning margin)
-        float tmax = nx2;
+      // per-tile max |x|^2 (the delta scan's pruning margin): the reduction only where it is
+      // asked for, the store predicated by offset (issued on every path, see buf_rsrc)
+      float tmax = nx2;
+      if (a.xnorm) {
 #pragma unroll
         for (int m = 16; m >= 1; m >>= 1) tmax = fmaxf(tmax, __shfl_xor(tmax, m, 64));
-        if (lane == 0) a.xnorm[tile] = tmax;
       }
+      buf_store_b32(rs_xn, uint32_t(tile - t0) * 4u, __float_as_int(tmax),
+                    a.xnorm && lane == 0 && pos < npos);
       nx2_s = a2 * nx2;
       build_operand(x, alpha, nx2, xh);
       if constexpr (!XB && COST) {  // (full passes compute the cost)
@@ -674,10 +681,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
                    make_float2(__builtin_amdgcn_sqrtf(rowcost) * ueps + 1e-30f,
                                __builtin_amdgcn_sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f)),
                    out);
-      if (out) {
-        if (a.mindist) a.mindist[row] = rowcost;
-        my_cost += double(rowcost);
-      }
+      buf_store_b32(rs_md, roff * 4, __float_as_int(rowcost), out);
+      if (out) my_cost += double(rowcost);
     } else {
       if (acc_row && !a.delta) {  // only rows that add re-read (x may hold the next tile)
         F xr;
