@@ -342,30 +342,33 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   };
 
   // fixed-point accumulation of one row into cluster b (neg: subtract it)
-  auto add_row = [&](const F& xv, int b, bool neg) OAP_AI {
-    if (h == 0) atomicAdd(&cnt_l[b], neg ? 0xffffffffu : 1u);
+  // fixed-point accumulation of one row: +x into cluster b, and -x into cluster bo when bo >= 0
+  // (a moved row of a delta pass: the integers are formed once for both)
+  auto add_row2 = [&](const F& xv, int b, int bo) OAP_AI {
+    if (h == 0) {
+      atomicAdd(&cnt_l[b], 1u);
+      if (bo >= 0) atomicAdd(&cnt_l[bo], 0xffffffffu);
+    }
     if (!a.sums_too) return;
-    const float sgn = neg ? -1.f : 1.f;
     double* ap = acc_l + b * (d | 1) + 8 * h;
+    double* aq = acc_l + (bo >= 0 ? bo : 0) * (d | 1) + 8 * h;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int f0 = 16 * s + 8 * h;
       const float4 s0 = *reinterpret_cast<const float4*>(sc_l + f0);
       const float4 s1 = *reinterpret_cast<const float4*>(sc_l + f0 + 4);
       const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      if (s < KS - 1) {  // k-steps below KS-1 hold real features only (KS = ceil((d+4)/16))
+      // k-steps below KS-1 hold real features only (KS = ceil((d+4)/16)); the last one d - f0
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          atomicAdd(ap + 16 * s + j, sgn * static_cast<double>(rintf(xv.at(s, j) * scv[j])));
-      } else {
-        const int nv = d - f0;  // real features of this lane's half of the last k-step
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < nv)
-            atomicAdd(ap + 16 * s + j, sgn * static_cast<double>(rintf(xv.at(s, j) * scv[j])));
-      }
+      for (int j = 0; j < 8; ++j)
+        if (s < KS - 1 || j < d - f0) {
+          const double v = static_cast<double>(rintf(xv.at(s, j) * scv[j]));
+          atomicAdd(ap + 16 * s + j, v);
+          if (bo >= 0) atomicAdd(aq + 16 * s + j, -v);
+        }
     }
   };
+  auto add_row = [&](const F& xv, int b) OAP_AI { add_row2(xv, b, -1); };
 
   // delta passes: a tile's few moved rows would each cost the whole wave 2 KS x 8 predicated
   // LDS atomics; instead they are staged in the wave's LDS slots and accumulated 32 at a time
@@ -380,8 +383,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     if (on) {
       F xr;
       load_row(int64_t(e.x), xr);
-      add_row(xr, e.y & 0xffff, false);
-      add_row(xr, e.y >> 16, true);
+      add_row2(xr, e.y & 0xffff, e.y >> 16);
     }
     if (cnt > 32) {  // slide the rest down (read all before any write: in-order LDS)
       const int2 rest = mv_l[32 + r];
@@ -663,7 +665,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 #pragma unroll
           for (int j = 0; j < 8; ++j) cb[s][j] = 0.f;
       }
-      if (acc_row && !a.delta) add_row(xr, b, false);
+      if (acc_row && !a.delta) add_row(xr, b);
       float part = 0.f;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -690,7 +692,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           load_tile(tile, xr);
         else
           xr = x;
-        add_row(xr, b, false);
+        add_row(xr, b);
       }
       const bool out = done && h == 0;
       buf_store_b32(rs_lab, roff * 4, b, out);
