@@ -278,7 +278,7 @@ int lean_variant(int d, int kpad) {
   if (reg_ok && e && *e == '1') return 11;
   // (variant 6 — fragment reads grouped ahead of each MFMA chain — measured ~1% ahead of 0 on
   // the headline shape in two runs; the register plane 6% behind: profiles/r3/lean_variants_*)
-  return d + 4 > 96 ? 3 : 6;
+  return d + 4 > 96 ? 8 : 6;  // (wide rows: 12 waves, grouped fragment reads — config 5 -2%)
 }
 
 // Whether gpu_assign takes the lean path for this request.
