@@ -1265,7 +1265,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     ctx.memset(ldstat_b.data(), 0, 2 * sizeof(u64), s);
     req.deferred_rows = ldstat_b.as<u64>();
   }
-  u64 deferred_seen = 0;
+  u64 deferred_seen = 0, moved_seen = 0;
   // Resident fp16 operand image (f32 rows, delta path): the first full lean pass writes each
   // tile's MFMA B operand (fp16 of beta x + bias slots, 2 B per padded feature instead of 4) and
   // the delta passes after it stream that instead of the f32 rows — 128 instead of 208 B per
@@ -1507,7 +1507,17 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         share = std::max(share, double(ldstat_h.as<u64>()[0] - deferred_seen) /
                                     (0.25 * double(x.rows) * nb_it));
       tier2_seen = t2;
-      if (ldstat_b.data()) deferred_seen = ldstat_h.as<u64>()[0];
+      if (ldstat_b.data() && Logger::instance().level() <= LogLevel::Info) {
+        Logger::instance().log(
+            LogLevel::Info, "kmeans/batch_rows",
+            "\"iters\":[" + std::to_string(it0) + "," + std::to_string(it0 + nb_it - 1) +
+                "],\"deferred\":" + std::to_string(ldstat_h.as<u64>()[0] - deferred_seen) +
+                ",\"moved\":" + std::to_string(ldstat_h.as<u64>()[1] - moved_seen));
+      }
+      if (ldstat_b.data()) {
+        deferred_seen = ldstat_h.as<u64>()[0];
+        moved_seen = ldstat_h.as<u64>()[1];
+      }
       if (!comm.trivial()) share = comm_allreduce_scalar(ctx, comm, share, ReduceOp::Max);
       if (share > 1.0) {
         req.fast1 = false;
