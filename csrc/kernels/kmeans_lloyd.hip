@@ -434,8 +434,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     int2 kin = make_int2(0x7fffffff, 0x7fffffff);
     if (!IMG && keys_in && h == 0 && valid) kin = a.keys[row];
     const uint32_t roff = uint32_t(row - row0);  // (valid rows: this workgroup's)
-    int old = buf_load_b32(rs_lab, roff * 4, a.delta && valid);
-    old = (a.delta && valid) ? old : -1;
+    // image passes are always delta passes of a single-launch fit: no chunk keys, no timing
+    // ablations — compile-time constants there (fewer live uniform switches)
+    const bool dl = IMG || a.delta;
+    int old = buf_load_b32(rs_lab, roff * 4, dl && valid);
+    old = (dl && valid) ? old : -1;
     // MFMA B operand: fp16 of alpha x with the bias slots [16, 16, hi, lo (alpha^2 |x|^2 / 16)]
     f16x8 xh[KS];
     float nx2_s;
@@ -516,7 +519,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       }
     };
     auto epilogue = [&](int c0, const f32x16& acc) OAP_AI {
-      if (a.ablate & 32) {  // timing ablation: consume the accumulators with one op per chunk
+      if (!IMG && (a.ablate & 32)) {  // timing ablation: one op per chunk
         k1 = min(k1, (__float_as_int(acc[0]) & ~0x3ff) | (c0 + 4 * h));
         return;
       }
@@ -535,14 +538,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         t2 = min(t2, med3_i32_pure(t1, key[e], key[e + 1]));
         t1 = min(min(t1, key[e]), key[e + 1]);
       }
-      const int base = c0 + 4 * h + kbase;  // disjoint from every in-chunk offset's bits
+      const int base = c0 + 4 * h + (IMG ? 0 : kbase);  // disjoint from every in-chunk offset
       const int i1 = t1 | base, i2 = t2 | base;
       k2 = min(max(k1, i1), min(k2, i2));
       k1 = min(k1, i1);
     };
     bool unsure;
     float b1 = 0.f, b2 = 0.f, tt = 0.f;
-    if (do_dist) {
+    if (IMG || do_dist) {
       int c0 = 0;
       if constexpr (RCH > 0) {
         // software-pipelined over chunks: issue chunk c's MFMA chain, then fold chunk c - 1
@@ -637,9 +640,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     n_def += static_cast<unsigned>(__popcll(um));
     const bool done = valid && !unsure;
     int b = k1 & 0x3ff;
-    b = (b < kglob) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
-    const bool acc_row = done && do_acc && (!a.delta || (old >= 0 && old != b));
-    if (a.delta) {  // stage moved rows (wave-private slots, in row order)
+    b = (b < (IMG ? k : kglob)) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
+    const bool acc_row = done && (IMG ? accumulate : do_acc) && (!dl || (old >= 0 && old != b));
+    if (dl) {  // stage moved rows (wave-private slots, in row order)
       const unsigned long long mm = __ballot(acc_row && h == 0);
       if (mm) {
         if (acc_row && h == 0)
@@ -686,7 +689,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       buf_store_b32(rs_md, roff * 4, __float_as_int(rowcost), out);
       if (out) my_cost += double(rowcost);
     } else {
-      if (acc_row && !a.delta) {  // only rows that add re-read (x may hold the next tile)
+      if (acc_row && !dl) {  // only rows that add re-read (x may hold the next tile)
         F xr;
         if constexpr (PF == 2)
           load_tile(tile, xr);
