@@ -576,7 +576,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       int64_t max_lr = 0;
       for (const auto& o : D.lro) max_lr = std::max(max_lr, o[4] - o[0]);
       if (max_lr > 0) D.lr_scratch = ctx.alloc(size_t(max_lr) * ld * 4);
-      if (!lr.empty() && x3_gram) {
+      if ((!lr.empty() || !sr.empty()) && x3_gram) {
         D.absmax = ctx.alloc(16);
         ctx.memset(D.absmax.data(), 0, 16);
         kern::als_absmax(D.val.as<float>(), S.csr.ptr.empty() ? 0 : S.csr.ptr.back(),

@@ -21,7 +21,9 @@
 //    of 16x the fp32 rate per 32 ratings instead of eight fp32 16x16x4 ones (5.3x the
 //    throughput); the dropped lo lo^T and the lo rounding leave ~3 2^-22 relative per product,
 //    below the fp32 accumulation error of a >4096-term sum (OAP_ALS_GRAM=fp32 restores the
-//    exact-fp32 products).
+//    exact-fp32 products).  The direct solve of the mid-length rows (64 < n_u <= 4096) takes the
+//    same Gramian at one wave per SIMD (the pipelined x3 loop needs ~430 registers;
+//    OAP_ALS_DIRECT_X3=0 keeps its fp32 16x16x4 loop at two waves per SIMD).
 //  * Solve: the assembled matrix goes to LDS (row stride RP+4: conflict-free MFMA fragment
 //    reads) and is factored by a right-looking blocked Cholesky with 16-wide panels: the
 //    diagonal block in registers (lane-per-row, cross-lane broadcasts), the panel TRSM
@@ -63,6 +65,7 @@ struct SolveArgs {
   unsigned long long* fail;
   int ablate;  // timing ablations (OAP_ALS_ABLATE): 1 no Gramian, 2 no Cholesky, 4 no solves,
                // 8 no YtY loads
+  const unsigned* absmax;  // split-fp16 direct Gramian (X3): as PartialArgs::absmax
 };
 
 struct PartialArgs {
@@ -250,7 +253,7 @@ __device__ inline void accumulate_pipe(const int32_t* __restrict__ cols,
 // The next step's factor values load into the registers the current step has just converted
 // (its fp16 fragments are separate): one step of MFMA work covers the gather latency; the
 // (item, rating) pairs are fetched two steps ahead.  b and n_u stay fp32 on the VALU.
-template <int NB>
+template <int NB, bool PIPE = true>
 __device__ inline void accumulate_x3(const int32_t* __restrict__ cols,
                                      const float* __restrict__ vals, int64_t p0, int64_t p1,
                                      const float* __restrict__ src, int ld, float alpha,
@@ -284,6 +287,10 @@ __device__ inline void accumulate_x3(const int32_t* __restrict__ cols,
   load(it_b, rv_b, y, rvs, oks);
   if (p0 + kStep < p1) fetch(p0 + kStep, it_b, rv_b);
   for (int64_t p = p0; p < p1; p += kStep) {
+    // PIPE = false (the 2-wave/SIMD direct solve: 256 registers): this step's rows load at the
+    // top of the step, the y registers die into the fp16 fragments before the MFMAs
+    if (!PIPE && p != p0) load(it_b, rv_b, y, rvs, oks);
+    if (!PIPE && p + kStep < p1) fetch(p + kStep, it_b, rv_b);
     // weights (absent ratings: 0)
     float sq[8], wb[8];
 #pragma unroll
@@ -322,8 +329,8 @@ __device__ inline void accumulate_x3(const int32_t* __restrict__ cols,
     }
     // the next step's pairs and factor values are in flight under this step's MFMAs
     const bool more = p + kStep < p1;  // wave-uniform
-    if (more) load(it_b, rv_b, y, rvs, oks);
-    if (p + 2 * kStep < p1) fetch(p + 2 * kStep, it_b, rv_b);
+    if (PIPE && more) load(it_b, rv_b, y, rvs, oks);
+    if (PIPE && p + 2 * kStep < p1) fetch(p + 2 * kStep, it_b, rv_b);
     // hi hi^T, then hi lo^T, then lo hi^T: consecutive MFMAs never chain on one accumulator
     int t = 0;
 #pragma unroll
@@ -394,10 +401,13 @@ __global__ __launch_bounds__(kAlsThreads, 1) void oap_als_partial(PartialArgs a)
   }
 }
 
-template <int NB, bool LONG>
-__global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
+template <int NB, bool LONG, bool X3>
+__global__ __launch_bounds__(kAlsThreads, X3 ? 1 : 2) void oap_als_solve(SolveArgs a) {
+  static_assert(!(LONG && X3), "long rows sum precomputed partials");
   constexpr int NT = NB * (NB + 1) / 2;
   constexpr int RP = 16 * NB;
+  float xs = 1.f, inv_xs2 = 1.f;
+  if constexpr (X3) x3_scale(a.absmax, a.alpha, a.implicit != 0, xs, inv_xs2);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* M = lds;  // lower 16x16 blocks, packed (mi)
   float* bv = lds + NB * (NB + 1) / 2 * kBlkF;  // RP
@@ -440,8 +450,15 @@ __global__ __launch_bounds__(kAlsThreads, 2) void oap_als_solve(SolveArgs a) {
         nexp += static_cast<int>(pp[NT * 256 + NB * 64 + lane]);
       }
     } else if (!(a.ablate & 1)) {
-      accumulate<NB>(a.cols, a.vals, hp0, hp1, a.src, a.ld, a.alpha, a.implicit != 0, acc, bacc,
-                     nexp);
+      if constexpr (X3) {
+        accumulate_x3<NB>(a.cols, a.vals, hp0, hp1, a.src, a.ld, a.alpha,
+                          a.implicit != 0, xs, acc, bacc, nexp);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] *= inv_xs2;
+      } else {
+        accumulate<NB>(a.cols, a.vals, hp0, hp1, a.src, a.ld, a.alpha, a.implicit != 0, acc,
+                       bacc, nexp);
+      }
     }
     const int64_t qn = static_cast<int64_t>(__shfl(qn_u, 0, 64));
     const int64_t rown = a.rows[qn < a.nrows ? qn : last];  // (in flight under the assembly)
@@ -524,15 +541,15 @@ size_t solve_lds() {
   return (size_t(NB * (NB + 1) / 2) * kBlkF + std::max(16 * NB, 128)) * sizeof(float);
 }
 
-template <int NB, bool LONG>
+template <int NB, bool LONG, bool X3 = false>
 void launch_solve(const SolveArgs& a, int grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_als_solve<NB, LONG>),
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_als_solve<NB, LONG, X3>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL((oap_als_solve<NB, LONG>), dim3(grid), dim3(kAlsThreads), solve_lds<NB>(),
+  hipLaunchKernelGGL((oap_als_solve<NB, LONG, X3>), dim3(grid), dim3(kAlsThreads), solve_lds<NB>(),
                      s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
@@ -566,7 +583,18 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     a.rows = s.short_rows;
     a.nrows = n_direct;
     a.queue = s.queue;
-    launch_solve<NB, false>(a, int(std::min<int64_t>(n_direct, int64_t(num_cus) * per_cu)), st);
+    // split-fp16 Gramian for the direct rows too (OAP_ALS_DIRECT_X3=0: exact-fp32 products)
+    static const bool direct_x3 = [] {
+      const char* e = std::getenv("OAP_ALS_DIRECT_X3");
+      return !e || std::atoi(e) != 0;
+    }();
+    a.absmax = direct_x3 ? s.absmax : nullptr;
+    const int grid = int(std::min<int64_t>(n_direct, int64_t(num_cus) * per_cu));
+    if (a.absmax)
+      launch_solve<NB, false, true>(a, grid, st);
+    else
+      launch_solve<NB, false, false>(a, grid, st);
+    a.absmax = nullptr;
   }
   als_solve_lowrank(s, num_cus, st);
   if (s.n_long > 0) {
