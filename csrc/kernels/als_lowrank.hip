@@ -71,8 +71,8 @@ __device__ inline float xor_sum16(float v) {
   return v;
 }
 
-template <int NBR, int NBN>
-__global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRankArgs a) {
+template <int NBR, int NBN, int OCC>
+__global__ __launch_bounds__(64, OCC) void oap_als_lowrank(LowRankArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* M = lds;                                 // n x n, packed lower blocks
   float* bv = lds + als::packed_floats<NBN, kRS>();  // 64 floats (the backward solve: 64 lanes)
@@ -310,12 +310,12 @@ __global__ __launch_bounds__(64, (NBN >= 4 ? 2 : 3)) void oap_als_lowrank(LowRan
   }
 }
 
-template <int NBR, int NBN>
+template <int NBR, int NBN, int OCC = (NBN >= 4 ? 2 : 3)>
 void launch_lowrank(const LowRankArgs& a, int num_cus, hipStream_t s) {
   constexpr size_t lds = (als::packed_floats<NBN, kRS>() + 64 + 32 * NBR) * sizeof(float);
   const int per_cu = std::max<int>(1, std::min<int>(16, int((160 * 1024) / (lds + 512))));
   const int grid = int(std::min<int64_t>(a.nrows, int64_t(num_cus) * per_cu));
-  hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN>), dim3(grid), dim3(64), lds, s, a);
+  hipLaunchKernelGGL((oap_als_lowrank<NBR, NBN, OCC>), dim3(grid), dim3(64), lds, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
@@ -336,6 +336,10 @@ void lowrank_classes(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     return e ? std::atoi(e) : 0;
   }();
   a.ablate = ablate;
+  static const int lr3_occ = [] {  // waves/SIMD of the 33-48-rating class (timing experiments)
+    const char* e = std::getenv("OAP_ALS_LR3_OCC");
+    return e ? std::atoi(e) : 0;
+  }();
   // class j: rows [lr_off[j], lr_off[j+1]) of short_rows hold 16 (4 - j) - 15 .. 16 (4 - j) ratings
   for (int j = 0; j < 4; ++j) {
     const int64_t b = s.lr_off[j], e = s.lr_off[j + 1];
@@ -347,7 +351,14 @@ void lowrank_classes(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     OAP_HIP_CHECK(hipMemsetAsync(a.queue, 0, sizeof(unsigned long long), st));
     switch (j) {
       case 0: launch_lowrank<NBR, 4>(a, num_cus, st); break;
-      case 1: launch_lowrank<NBR, 3>(a, num_cus, st); break;
+      case 1:
+        if (lr3_occ == 2)
+          launch_lowrank<NBR, 3, 2>(a, num_cus, st);
+        else if (lr3_occ == 4)
+          launch_lowrank<NBR, 3, 4>(a, num_cus, st);
+        else
+          launch_lowrank<NBR, 3>(a, num_cus, st);
+        break;
       case 2: launch_lowrank<NBR, 2>(a, num_cus, st); break;
       default: launch_lowrank<NBR, 1>(a, num_cus, st); break;
     }
