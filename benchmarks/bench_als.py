@@ -54,7 +54,8 @@ def main():
         print(json.dumps({
             "metric": "als_iteration_s", "value": sum(steady) / len(steady) / 1e3, "unit": "s",
             "n_gpus": w.size, "higher_is_better": False,
-            "dtype": "fp32 factors; Gramian: fp32 MFMA (rows <= 64 ratings), split-fp16 hi+lo MFMA with fp32 accumulation (longer rows); fp32 Cholesky",
+            "dtype": ("fp32 factors; Gramian: fp32 MFMA (rows <= 64 ratings), split-fp16 "
+                      "hi+lo MFMA with fp32 accumulation (longer rows); fp32 Cholesky"),
             "data": "synthetic implicit counts (uniform users, power-law items)",
             "config": {"model": "als implicit rank %d" % a.rank, "ratings": int(out["nnz"]),
                        "users": len(out["user_ids"]), "items": len(out["item_ids"])},
