@@ -474,7 +474,14 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       // per row-range chunk c: [sr_off[c], sr_off[c+1]) of short_rows, [lr_off[c], ...) of
       // long_rows (long_chunk_ptr segment at lr_off[c] + c), [cb_off[c], ...) of chunk_begin/end
       std::vector<int64_t> sr_off, lr_off, cb_off;
+      // per chunk: leading short rows longer than x3_min (split-fp16 direct Gramian)
+      std::vector<int64_t> x3n;
     } dU, dI;
+    // direct rows at most this long keep the fp32 Gramian (OAP_ALS_X3_MIN_LEN)
+    const int64_t x3_min = [] {
+      const char* e = std::getenv("OAP_ALS_X3_MIN_LEN");
+      return e ? std::atoll(e) : int64_t(128);
+    }();
     // rows longer than kLong ratings are split into kLong-sized chunks (partial Gramians)
     constexpr int64_t kLong = 4096;
     auto upload_side = [&](Side& S, Dev& D, kern::AlsDeviceCsr* dc) {
@@ -543,6 +550,11 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
           lo5[4] = nsh;
         }
         D.lro.push_back(lo5);
+        {
+          int64_t nx = 0;
+          for (const auto& [len, i] : order) nx += (len <= kLong && len > x3_min) ? 1 : 0;
+          D.x3n.push_back(nx);
+        }
         for (const auto& [len, i] : order) {
           if (len > kLong) {
             lr.push_back(i);
@@ -690,6 +702,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         a.chunk_end = dD.chunk_end.as<int64_t>() + dD.cb_off[c];
         a.n_chunks = dD.cb_off[c + 1] - dD.cb_off[c];
         for (int j = 0; j < 5; ++j) a.lr_off[j] = dD.lro[c][j];
+        a.n_direct_x3 = dD.x3n[c];
         if (lr_on) {
           a.lr_src = dS.rot.as<float>();
           a.lr_eig = lrEig.as<float>();

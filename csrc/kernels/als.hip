@@ -21,9 +21,10 @@
 //    of 16x the fp32 rate per 32 ratings instead of eight fp32 16x16x4 ones (5.3x the
 //    throughput); the dropped lo lo^T and the lo rounding leave ~3 2^-22 relative per product,
 //    below the fp32 accumulation error of a >4096-term sum (OAP_ALS_GRAM=fp32 restores the
-//    exact-fp32 products).  The direct solve of the mid-length rows (64 < n_u <= 4096) takes the
-//    same Gramian at one wave per SIMD (the pipelined x3 loop needs ~430 registers;
-//    OAP_ALS_DIRECT_X3=0 keeps its fp32 16x16x4 loop at two waves per SIMD).
+//    exact-fp32 products).  The direct solve of the mid-length rows (128 < n_u <= 4096,
+//    OAP_ALS_X3_MIN_LEN) takes the same Gramian at one wave per SIMD (the pipelined x3 loop
+//    needs ~430 registers); shorter direct rows are Cholesky-bound and keep the fp32 16x16x4 loop
+//    at two waves per SIMD (OAP_ALS_DIRECT_X3=0: every direct row).
 //  * Solve: the assembled matrix goes to LDS (row stride RP+4: conflict-free MFMA fragment
 //    reads) and is factored by a right-looking blocked Cholesky with 16-wide panels: the
 //    diagonal block in registers (lane-per-row, cross-lane broadcasts), the panel TRSM
@@ -589,12 +590,24 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
       return !e || std::atoi(e) != 0;
     }();
     a.absmax = direct_x3 ? s.absmax : nullptr;
-    const int grid = int(std::min<int64_t>(n_direct, int64_t(num_cus) * per_cu));
-    if (a.absmax)
-      launch_solve<NB, false, true>(a, grid, st);
-    else
-      launch_solve<NB, false, false>(a, grid, st);
+    // the longest rows on the split-fp16 Gramian, the short tail on the fp32 one at two waves
+    // per SIMD (its rows are Cholesky-bound: 30 vs 38 ms per user half at 1B ratings)
+    const int64_t n_x3 =
+        a.absmax ? (s.n_direct_x3 < 0 ? n_direct : std::min(n_direct, s.n_direct_x3)) : 0;
+    if (n_x3 > 0) {
+      a.nrows = n_x3;
+      launch_solve<NB, false, true>(
+          a, int(std::min<int64_t>(n_x3, int64_t(num_cus) * per_cu)), st);
+    }
     a.absmax = nullptr;
+    if (n_direct > n_x3) {
+      OAP_HIP_CHECK(hipMemsetAsync(s.queue + 3, 0, sizeof(unsigned long long), st));
+      a.rows = s.short_rows + n_x3;
+      a.nrows = n_direct - n_x3;
+      a.queue = s.queue + 3;
+      launch_solve<NB, false, false>(
+          a, int(std::min<int64_t>(n_direct - n_x3, int64_t(num_cus) * per_cu)), st);
+    }
   }
   als_solve_lowrank(s, num_cus, st);
   if (s.n_long > 0) {

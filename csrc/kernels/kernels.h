@@ -307,13 +307,16 @@ struct AlsSolveArgs {
   // long-row chunks: split-fp16 Gramian scaled from [max |rating|, max |source factor|]
   // (device, float bits, als_absmax); null: exact-fp32 MFMA products
   const unsigned* absmax = nullptr;
+  // direct rows (short_rows by decreasing length): the first n_direct_x3 take the split-fp16
+  // Gramian, the rest the fp32 one (-1: all split-fp16 when absmax is set)
+  int64_t n_direct_x3 = -1;
   const float* src = nullptr;       // source factors [n_src][ld]
   int ld = 0, r = 0;
   const float* yty = nullptr;       // [r][r] Gramian of ALL source factors (implicit)
   float alpha = 1.f, lambda = 0.f;
   bool implicit = true;
   float* dst = nullptr;             // [nrows][ld], indexed by destination row
-  unsigned long long* queue = nullptr;  // device scratch: 8 counters (2 and 3 unused)
+  unsigned long long* queue = nullptr;  // device scratch: 8 counters ([2] is the driver's fail)
   unsigned long long* fail = nullptr;   // device counter of non-SPD rows
   // Low-rank (Woodbury) path for implicit rows with <= als_lowrank_max_len() ratings
   // (kernels/als_lowrank.hip): short_rows[lr_off[0], lr_off[4]) are those rows by decreasing
