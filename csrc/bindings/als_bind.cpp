@@ -85,10 +85,13 @@ void register_als(py::module_& m) {
           if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
           return a;
         };
-        auto fac = [&](const std::vector<float>& v, size_t rows) {
-          py::array_t<float> a({int64_t(rows), int64_t(r.rank)});
-          if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
-          return a;
+        auto fac = [&](const HostArray<float>& v, size_t rows) {
+          if (v.empty() || rows == 0) return py::array_t<float>({int64_t(rows), int64_t(r.rank)});
+          // zero-copy: the array keeps the native buffer alive
+          auto* keep = new std::shared_ptr<float>(v.owner());
+          py::capsule owner(keep, [](void* q) { delete static_cast<std::shared_ptr<float>*>(q); });
+          return py::array_t<float>({int64_t(rows), int64_t(r.rank)},
+                                    {int64_t(r.rank) * 4, int64_t(4)}, v.data(), owner);
         };
         py::dict out;
         out["user_ids"] = ids(r.user_ids);

@@ -640,6 +640,39 @@ PYBIND11_MODULE(_native, m) {
   m.def("kmeans_set_lean_variant", &kmeans_set_lean_variant);
   m.def("kmeans_last_timing_deferred", []() { return last_timing_deferred(); });
   m.def(
+      "kmeans_image_timing",
+      [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> ca,
+         py::array_t<double> cb, int reps, int kernel, int cfg, bool fallback) {
+        auto a = py::array_t<double, py::array::c_style | py::array::forcecast>(ca);
+        auto b = py::array_t<double, py::array::c_style | py::array::forcecast>(cb);
+        OAP_CHECK(a.ndim() == 2 && b.ndim() == 2 && a.shape(0) == b.shape(0) &&
+                      a.shape(1) == b.shape(1) && a.shape(1) == t->cols,
+                  "kmeans_image_timing: centers must both be [k][d]");
+        std::vector<double> av(a.data(), a.data() + a.size()), bv(b.data(), b.data() + b.size());
+        const int k = static_cast<int>(a.shape(0));
+        ImageTiming r;
+        {
+          py::gil_scoped_release rel;
+          r = kmeans_image_timing(*ctx, *t, av, bv, k, reps, kernel, cfg, fallback);
+        }
+        py::dict out;
+        out["lean_ms"] = r.lean_ms;
+        out["pass_ms"] = r.pass_ms;
+        out["deferred_rows"] = r.deferred_rows;
+        out["moved_rows"] = r.moved_rows;
+        out["image_passes"] = r.image_passes;
+        out["path"] = r.path;
+        py::array_t<int32_t> lab(static_cast<py::ssize_t>(r.labels.size()));
+        std::memcpy(lab.mutable_data(), r.labels.data(), r.labels.size() * 4);
+        py::array_t<uint64_t> st(static_cast<py::ssize_t>(r.stats.size()));
+        std::memcpy(st.mutable_data(), r.stats.data(), r.stats.size() * 8);
+        out["labels"] = lab;
+        out["stats"] = st;
+        return out;
+      },
+      py::arg("ctx"), py::arg("table"), py::arg("centers_a"), py::arg("centers_b"),
+      py::arg("reps") = 5, py::arg("kernel") = 1, py::arg("cfg") = -1, py::arg("fallback") = true);
+  m.def(
       "kmeans_assign_timing",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<DenseTable> t, py::array_t<double> centers,
          int reps, bool precise, int ablate) {

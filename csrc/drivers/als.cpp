@@ -767,10 +767,15 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     unsigned long long fails = 0;
     ctx.copy_to_host(&fails, ctr.as<unsigned long long>() + 2, 8);
     res.failed_rows = int64_t(comm_allreduce_scalar(ctx, comm, double(fails), ReduceOp::Sum));
-    Xh.resize(size_t(U.n) * ld);
-    Yh.resize(size_t(I.n) * ld);
-    if (U.n) ctx.copy_to_host(Xh.data(), dU.f.data(), Xh.size() * 4);
-    if (I.n) ctx.copy_to_host(Yh.data(), dI.f.data(), Yh.size() * 4);
+    // the result handoff (the reference copies each factor row into a Java array,
+    // ALSDALImpl.cpp:500-576): pitched 2D copies drop the ld padding on the GPU side into pinned
+    // staging, drained by the thread pool straight into the returned (uninitialised) arrays
+    res.user_factors = HostArray<float>::alloc(size_t(U.n) * r);
+    res.item_factors = HostArray<float>::alloc(size_t(I.n) * r);
+    ctx.download_rows(res.user_factors.data(), size_t(r) * 4, dU.f.data(), size_t(ld) * 4,
+                      size_t(r) * 4, U.n, s);
+    ctx.download_rows(res.item_factors.data(), size_t(r) * 4, dI.f.data(), size_t(ld) * 4,
+                      size_t(r) * 4, I.n, s);
   } else {
     Xh.assign(size_t(U.n) * ld, 0.f);
     Yh.assign(size_t(I.n) * ld, 0.f);
@@ -874,12 +879,14 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   res.train_ms = ms_since(t_train);
   res.user_ids = U.ids;
   res.item_ids = I.ids;
-  res.user_factors.resize(size_t(U.n) * r);
-  res.item_factors.resize(size_t(I.n) * r);
-  for (int64_t i = 0; i < U.n; ++i)
-    std::copy(&Xh[size_t(i) * ld], &Xh[size_t(i) * ld] + r, &res.user_factors[size_t(i) * r]);
-  for (int64_t i = 0; i < I.n; ++i)
-    std::copy(&Yh[size_t(i) * ld], &Yh[size_t(i) * ld] + r, &res.item_factors[size_t(i) * r]);
+  if (!Xh.empty() || !Yh.empty()) {  // (host engine: repack [n][ld] -> [n][r] on the pool)
+    res.user_factors = HostArray<float>::alloc(size_t(U.n) * r);
+    res.item_factors = HostArray<float>::alloc(size_t(I.n) * r);
+    ctx.download_rows(res.user_factors.data(), size_t(r) * 4, Xh.data(), size_t(ld) * 4,
+                      size_t(r) * 4, U.n);
+    ctx.download_rows(res.item_factors.data(), size_t(r) * 4, Yh.data(), size_t(ld) * 4,
+                      size_t(r) * 4, I.n);
+  }
   if (me == 0 && Logger::instance().level() <= LogLevel::Info)
     Logger::instance().log(LogLevel::Info, "als/fit",
                            "\"nnz\":" + std::to_string(res.nnz) + ",\"users\":" +

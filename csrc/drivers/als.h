@@ -40,7 +40,7 @@ struct AlsParams {
 struct AlsResult {
   int rank = 0;
   std::vector<int32_t> user_ids, item_ids;      // global index order
-  std::vector<float> user_factors, item_factors;  // [n][rank] row-major
+  HostArray<float> user_factors, item_factors;    // [n][rank] row-major
   int64_t nnz = 0;                                // global ratings
   double setup_ms = 0.0, train_ms = 0.0;
   std::vector<double> iter_ms;                    // per iteration (both halves)

@@ -254,7 +254,31 @@ struct AssignReq {
   void* ximg = nullptr;
   float* img_beta = nullptr;
   int img_mode = 0;
+  // img_mode 2: also launch the f32-row fallback (kmeans_lloyd img_mode 3) after the image
+  // kernel, for the case the image's scale cannot hold the current centers (the host clears it
+  // once the rows' norms prove that impossible)
+  bool img_fallback = true;
+  int img_kernel = -1;      // -1: OAP_KMEANS_IMG_KERNEL (default on), 0 kmeans_lloyd, 1 lean_img
+  int img_cfg = -1;         // oap_kmeans_lean_img configuration (-1: OAP_KMEANS_IMG_CFG / default)
+  bool skip_exact = false;  // timing probes: the lean pass only
 };
+
+// The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
+// OAP_KMEANS_IMG_KERNEL=0; OAP_KMEANS_IMG_CFG picks a configuration (timing probes).
+bool img_kernel_default() {
+  static const bool on = [] {
+    const char* e = std::getenv("OAP_KMEANS_IMG_KERNEL");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+int img_cfg_default() {
+  static const int c = [] {
+    const char* e = std::getenv("OAP_KMEANS_IMG_CFG");
+    return e ? std::atoi(e) : -1;
+  }();
+  return c;
+}
 
 int& lean_variant_ref() {  // -1: by width (below)
   static int v = [] {
@@ -379,7 +403,23 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
                         ? (req.tile_list ? "lean_fp16_image_delta_scan" : "lean_fp16_image_delta")
                     : req.delta ? (req.tile_list ? "lean_fp16_delta_scan" : "lean_fp16_delta")
                                 : "lean_fp16";
-    kern::kmeans_lloyd(a, grid, lean_variant(x.cols, a.kpad), s);
+    const int lv = lean_variant(x.cols, a.kpad);
+    const int lw = kern::kmeans_lloyd_waves(lv);
+    const bool img_k = req.img_kernel >= 0 ? req.img_kernel == 1 : img_kernel_default();
+    // (variants 3 / 10 have no image branch: their img_mode 3 would not be a fallback only)
+    if (req.img_mode == 2 && img_k && lv != 3 && lv != 10 &&
+        kern::kmeans_lean_img_supported(x.cols, g.k, lw)) {
+      kern::kmeans_lean_img(a, grid, lw, req.img_cfg >= 0 ? req.img_cfg : img_cfg_default(), s);
+      if (req.img_fallback) {
+        kern::KMeansAssignArgs f = a;
+        f.img_mode = 3;
+        kern::kmeans_lloyd(f, grid, lv, s);
+      }
+      t_assign_path = req.tile_list ? "lean_img_kernel_delta_scan" : "lean_img_kernel_delta";
+    } else {
+      kern::kmeans_lloyd(a, grid, lv, s);
+    }
+    if (req.skip_exact) return 0;
     kern::KMeansAssignArgs b = a;
     b.ximg = nullptr;
     b.img_mode = 0;
@@ -1260,9 +1300,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     req.defer_count = reinterpret_cast<unsigned*>(req.defer_rows + size_t(lg) * size_t(lcap));
   }
   if (x.rows > 0 && (req.defer_rows || lean_chunked)) {
-    ldstat_b = ctx.alloc(2 * sizeof(u64));  // [deferred rows, moved rows staged]
-    ldstat_h = ctx.alloc_pinned(2 * sizeof(u64));
-    ctx.memset(ldstat_b.data(), 0, 2 * sizeof(u64), s);
+    // [deferred rows, moved rows staged, passes that read the operand image]
+    ldstat_b = ctx.alloc(3 * sizeof(u64));
+    ldstat_h = ctx.alloc_pinned(3 * sizeof(u64));
+    ctx.memset(ldstat_b.data(), 0, 3 * sizeof(u64), s);
     req.deferred_rows = ldstat_b.as<u64>();
   }
   u64 deferred_seen = 0, moved_seen = 0;
@@ -1421,7 +1462,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
       int nb = gpu_assign(ctx, x, g, req, s);
       if (req.img_mode == 1) img_ready = true;
-      if (req.img_mode == 2) ++res.image_passes;
       if (cdelta)
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), cloc_b.data(), sizeof(u64) * (kd + k),
                                      hipMemcpyDeviceToDevice, s));
@@ -1461,7 +1501,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
     if (ldstat_b.data())
-      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), 2 * sizeof(u64),
+      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), 3 * sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     u64 pruned_now = 0;
     if (scan)
@@ -1616,10 +1656,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     res.pruned_tiles = static_cast<int64_t>(pt);
   }
   if (ldstat_b.data()) {
-    u64 dr[2] = {0, 0};
-    ctx.copy_to_host(dr, ldstat_b.data(), 2 * sizeof(u64), s);
+    u64 dr[3] = {0, 0, 0};
+    ctx.copy_to_host(dr, ldstat_b.data(), 3 * sizeof(u64), s);
     res.deferred_rows = static_cast<int64_t>(dr[0]);
     res.moved_rows = static_cast<int64_t>(dr[1]) + cmoved;
+    res.image_passes = static_cast<int>(dr[2]);  // counted by the passes that read the image
   }
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
@@ -1897,8 +1938,8 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
     req.counts = a.counts;
     req.cost_slab = (ablate & 4) ? nullptr : a.cost_slab;  // 4: the Lloyd pass without a cost
     req.fast1 = true;
-    Buffer dr = ctx.alloc(2 * sizeof(u64));
-    ctx.memset(dr.data(), 0, 2 * sizeof(u64), s);
+    Buffer dr = ctx.alloc(3 * sizeof(u64));
+    ctx.memset(dr.data(), 0, 3 * sizeof(u64), s);
     req.deferred_rows = dr.as<u64>();
     OAP_CHECK(lean_applies(x, k, g.kpad, req), "lean path not applicable");
     gpu_assign(ctx, x, g, req, s);  // warm
@@ -1919,6 +1960,98 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
   e1.record(s);
   e1.sync();
   return Event::elapsed_ms(e0, e1) / std::max(reps, 1);
+}
+
+
+// Steady-state image-pass timing (tools/kmeans_img_probe.py): a full lean pass at centers_a
+// writes the operand image and the labels, then each rep restores those labels and statistics
+// and times one delta image pass at centers_b (the moved rows of a Lloyd step): the lean pass
+// alone (kernel: 0 kmeans_lloyd, 1 kmeans_lean_img with configuration cfg) and, separately, the
+// pass plus the exact re-decision of its deferred rows.
+ImageTiming kmeans_image_timing(Context& ctx, const DenseTable& x,
+                                const std::vector<double>& centers_a,
+                                const std::vector<double>& centers_b, int k, int reps, int kernel,
+                                int cfg, bool fallback) {
+  OAP_CHECK(ctx.is_gpu() && x.dtype == DType::F32, "kmeans_image_timing needs f32 rows on a GPU");
+  check_gpu_table(x);
+  ctx.activate();
+  const int d = x.cols;
+  hipStream_t s = ctx.compute();
+  GpuCenters ga = upload_centers(ctx, centers_a, k, d);
+  GpuCenters gb = upload_centers(ctx, centers_b, k, d);
+  std::vector<double> absmax(d, 64.0);
+  FixedPoint fp = fixed_point_scales(absmax, x.rows, x.rows);
+  Buffer scale = ctx.alloc(sizeof(float) * (round_up(d, 4) + 4));
+  ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4));
+  ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d);
+  const size_t nst = size_t(k) * d + k;
+  Buffer stats = ctx.alloc(sizeof(u64) * nst), stats0 = ctx.alloc(sizeof(u64) * nst);
+  Buffer slab = ctx.alloc(sizeof(double) * kern::kmeans_cost_slab_size(ctx.info().cu_count));
+  Buffer lab = ctx.alloc(sizeof(int32_t) * size_t(x.rows));
+  Buffer lab0 = ctx.alloc(sizeof(int32_t) * size_t(x.rows));
+  const size_t ib = kern::kmeans_lloyd_image_bytes(x.rows, d);
+  OAP_CHECK(ib > 0, "kmeans_image_timing: no operand image at d=" << d);
+  Buffer img = ctx.alloc(ib), beta = ctx.alloc(sizeof(float) * 4);
+  Buffer dr = ctx.alloc(3 * sizeof(u64));
+  ctx.memset(stats.data(), 0, sizeof(u64) * nst, s);
+  ctx.memset(dr.data(), 0, 3 * sizeof(u64), s);
+  AssignReq req;
+  req.accumulate = true;
+  req.sums_too = true;
+  req.scale = scale.as<float>();
+  req.sums = stats.as<u64>();
+  req.counts = stats.as<u64>() + size_t(k) * d;
+  req.labels = lab.as<int32_t>();
+  req.cost_slab = slab.as<double>();
+  req.fast1 = true;
+  req.ximg = img.data();
+  req.img_beta = beta.as<float>();
+  req.img_mode = 1;
+  req.deferred_rows = dr.as<u64>();
+  OAP_CHECK(lean_applies(x, k, ga.kpad, req), "kmeans_image_timing: lean path not applicable");
+  gpu_assign(ctx, x, ga, req, s);  // writes the image and every label
+  OAP_HIP_CHECK(hipMemcpyAsync(lab0.data(), lab.data(), sizeof(int32_t) * size_t(x.rows),
+                               hipMemcpyDeviceToDevice, s));
+  OAP_HIP_CHECK(hipMemcpyAsync(stats0.data(), stats.data(), sizeof(u64) * nst,
+                               hipMemcpyDeviceToDevice, s));
+  req.cost_slab = nullptr;
+  req.img_mode = 2;
+  req.delta = true;
+  req.labels_valid = true;
+  req.img_kernel = kernel;
+  req.img_cfg = cfg;
+  req.img_fallback = fallback;
+  ImageTiming out;
+  Event e0, e1;
+  for (int pass = 0; pass < 2; ++pass) {
+    req.skip_exact = pass == 0;
+    double tot = 0.0;
+    for (int i = 0; i <= reps; ++i) {  // (rep 0 warms)
+      OAP_HIP_CHECK(hipMemcpyAsync(lab.data(), lab0.data(), sizeof(int32_t) * size_t(x.rows),
+                                   hipMemcpyDeviceToDevice, s));
+      OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), stats0.data(), sizeof(u64) * nst,
+                                   hipMemcpyDeviceToDevice, s));
+      ctx.memset(dr.data(), 0, 3 * sizeof(u64), s);
+      e0.record(s);
+      gpu_assign(ctx, x, gb, req, s);
+      e1.record(s);
+      e1.sync();
+      if (i > 0) tot += Event::elapsed_ms(e0, e1);
+    }
+    (pass == 0 ? out.lean_ms : out.pass_ms) = tot / std::max(reps, 1);
+  }
+  u64 h[3] = {0, 0, 0};
+  ctx.copy_to_host(h, dr.data(), 3 * sizeof(u64), s);
+  out.deferred_rows = static_cast<int64_t>(h[0]);
+  out.moved_rows = static_cast<int64_t>(h[1]);
+  out.image_passes = static_cast<int64_t>(h[2]);
+  // the last rep's result: labels and statistics (for A/B equality checks)
+  out.labels.resize(size_t(x.rows));
+  ctx.copy_to_host(out.labels.data(), lab.data(), sizeof(int32_t) * size_t(x.rows), s);
+  out.stats.resize(nst);
+  ctx.copy_to_host(out.stats.data(), stats.data(), sizeof(u64) * nst, s);
+  out.path = t_assign_path;
+  return out;
 }
 
 }  // namespace oap

@@ -95,6 +95,20 @@ void kmeans_predict_device(Context& ctx, const DenseTable& x, const std::vector<
 // ablations (kern::KMeansAssignArgs::ablate) — the per-phase cost breakdown used for tuning.
 double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector<double>& centers,
                             int k, int reps, bool precise, int ablate);
+// Steady-state image-pass probe (see kmeans.cpp): ms of one delta pass over the fp16 operand
+// image (lean kernel alone, and with the exact re-decision), its deferred / moved rows, and the
+// resulting labels and statistics.  kernel: 0 kmeans_lloyd, 1 kmeans_lean_img (cfg, -1 default).
+struct ImageTiming {
+  double lean_ms = 0.0, pass_ms = 0.0;
+  int64_t deferred_rows = 0, moved_rows = 0, image_passes = 0;
+  std::vector<int32_t> labels;
+  std::vector<uint64_t> stats;
+  std::string path;
+};
+ImageTiming kmeans_image_timing(Context& ctx, const DenseTable& x,
+                                const std::vector<double>& centers_a,
+                                const std::vector<double>& centers_b, int k, int reps, int kernel,
+                                int cfg, bool fallback);
 // Workgroup shape of the lean tier-1 kernel (tuning; default from OAP_KMEANS_LEAN_VARIANT).
 void kmeans_set_lean_variant(int v);
 // Deferred rows per pass of the last lean-path timing (ablate bit 64).

@@ -117,7 +117,8 @@ struct KMeansAssignArgs {
   // appended to this workgroup's segment ([grid][row_seg_cap], count defer_row_count[block]).
   int32_t* defer_rows = nullptr;
   unsigned* defer_row_count = nullptr;
-  // optional counters [deferred rows, moved rows staged by delta passes]
+  // optional counters [deferred rows, moved rows staged by delta passes, passes that read the
+  // operand image] (3 entries)
   unsigned long long* deferred_rows = nullptr;
   // Row-list (refine) mode: rows still unsure after the bf16x3 tier are appended to
   // exact_rows ([grid][8][exact_sub_cap], one sub-segment per wave, counts exact_count
@@ -162,6 +163,13 @@ int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves);
 int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s);
 // Bytes of the lean kernel's fp16 operand image of n f32 rows of width d (0: not applicable).
 size_t kmeans_lloyd_image_bytes(int64_t n, int d);
+// Steady-state image pass (kmeans_lean_img.hip): the delta Lloyd pass over the resident fp16
+// operand image as its own compile-time-specialised kernel (same outputs as kmeans_lloyd with
+// img_mode 2).  `waves` must be the lean variant's (kmeans_lloyd_waves: the deferral
+// sub-segments), cfg < 0 the default configuration.  When the image's scale cannot hold the
+// current centers the kernel does nothing; kmeans_lloyd with img_mode 3 then runs the pass.
+bool kmeans_lean_img_supported(int d, int k, int waves);
+void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s);
 // Largest centroid chunks (multiples of 32) of the chunked lean pass at dimension d: the lean
 // kernel's fp16 plane and the exact kernel's fp32 centers (0: d not supported).
 int kmeans_lloyd_chunk_kmax(int d);

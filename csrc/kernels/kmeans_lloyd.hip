@@ -183,16 +183,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   // beta^2 |c|^2 / 16 inside fp16); otherwise it reads the f32 rows as usual.
   bool use_img = false;
   if constexpr (!XB && PF == 2 && !COST) {
-    if (a.img_mode == 2) {
+    if (a.img_mode == 2 || a.img_mode == 3) {
       const float bt = a.img_beta[0];
       use_img = bt * cmax <= 512.f;
       if (use_img) alpha = bt;
+      // img_mode 3: the f32-row fallback of oap_kmeans_lean_img (kmeans_lean_img.hip), which
+      // ran this pass already whenever the image is usable
+      if (use_img && a.img_mode == 3) return;
     }
   }
   const float a2 = alpha * alpha;
   const float inv_a2 = 1.f / a2;  // (a power of two: multiplying is the division, bitwise)
   const float beta_w = 0.25f * alpha;  // the scale a writing pass gives the image
   if (a.img_mode == 1 && blockIdx.x == 0 && tid == 0) a.img_beta[0] = beta_w;
+  // (deferred_rows[2]: passes that actually read the image)
+  if (use_img && blockIdx.x == 0 && tid == 0 && a.deferred_rows)
+    atomicAdd(a.deferred_rows + 2, 1ull);
 
   // ---- stage c' = [-2 alpha c, 0 .., hi, lo (alpha^2 |c|^2 / 16), 16, 16] (fp16) once per
   // workgroup; the four bias features sit in the LAST four slots (DP - 4 .. DP - 1, d <= DP - 4
@@ -1313,7 +1319,8 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   OAP_CHECK(!a.ximg || a.img_mode == 0 ||
                 (!a.xbf16 && !a.centers_all && a.img_beta &&
                  (a.img_mode == 1 ? !a.tile_list && (a.cost_slab || a.mindist)
-                                  : (a.img_mode == 2 && !a.xnorm))),
+                                  : ((a.img_mode == 2 || a.img_mode == 3) && !a.xnorm &&
+                                     !a.cost_slab && !a.mindist))),
             "kmeans_lloyd: bad operand-image arguments");
   if (a.n == 0) return 0;
   LeanArgs l;

@@ -140,6 +140,58 @@ void Context::copy_to_host(void* dst, const void* src, size_t bytes, hipStream_t
   }
 }
 
+void Context::download_rows(void* dst, size_t dst_pitch, const void* src, size_t src_pitch,
+                            size_t width, int64_t rows, hipStream_t s) {
+  if (rows <= 0 || width == 0) return;
+  OAP_CHECK(width <= dst_pitch && width <= src_pitch, "download_rows: width exceeds a pitch");
+  if (backend_ != Backend::GPU) {
+    pool_->parallel_for(rows, [&](int, int64_t b, int64_t e) {
+      for (int64_t i = b; i < e; ++i)
+        std::memcpy(static_cast<char*>(dst) + size_t(i) * dst_pitch,
+                    static_cast<const char*>(src) + size_t(i) * src_pitch, width);
+    });
+    return;
+  }
+  hipStream_t st = s ? s : compute();
+  constexpr size_t kStage = size_t(64) << 20;
+  const int64_t per = std::max<int64_t>(1, int64_t(kStage / width));
+  if (stage_[0].empty()) {
+    stage_[0] = Buffer::pinned(std::max(kStage, width));
+    stage_[1] = Buffer::pinned(std::max(kStage, width));
+  }
+  const int64_t nch = (rows + per - 1) / per;
+  Event done[2];
+  auto issue = [&](int64_t c) {
+    const int64_t r0 = c * per, nr = std::min(per, rows - r0);
+    OAP_HIP_CHECK(hipMemcpy2DAsync(stage_[c & 1].data(), width,
+                                   static_cast<const char*>(src) + size_t(r0) * src_pitch,
+                                   src_pitch, width, size_t(nr), hipMemcpyDeviceToHost, st));
+    done[c & 1].record(st);
+  };
+  issue(0);
+  if (nch > 1) issue(1);
+  for (int64_t c = 0; c < nch; ++c) {
+    done[c & 1].sync();
+    const int64_t r0 = c * per, nr = std::min(per, rows - r0);
+    const char* from = stage_[c & 1].as<char>();
+    char* to = static_cast<char*>(dst) + size_t(r0) * dst_pitch;
+    if (dst_pitch == width) {
+      const size_t bytes = size_t(nr) * width;
+      const int64_t parts = std::min<int64_t>(int64_t(pool_->size()) * 4, int64_t(bytes >> 20) + 1);
+      pool_->parallel_for(parts, [&](int, int64_t b, int64_t e) {
+        const size_t lo = bytes * size_t(b) / size_t(parts), hi = bytes * size_t(e) / size_t(parts);
+        std::memcpy(to + lo, from + lo, hi - lo);
+      });
+    } else {
+      pool_->parallel_for(nr, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i)
+          std::memcpy(to + size_t(i) * dst_pitch, from + size_t(i) * width, width);
+      });
+    }
+    if (c + 2 < nch) issue(c + 2);  // (this stage is drained)
+  }
+}
+
 void Context::memset(void* dst, int value, size_t bytes, hipStream_t s) {
   if (bytes == 0) return;
   if (backend_ == Backend::GPU) {

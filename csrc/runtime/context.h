@@ -91,6 +91,12 @@ class Context {
   void copy_to_backend(void* dst, const void* host_src, size_t bytes, hipStream_t s = nullptr);
   void copy_to_host(void* host_dst, const void* src, size_t bytes, hipStream_t s = nullptr);
   void memset(void* dst, int value, size_t bytes, hipStream_t s = nullptr);
+  // Row-pitched download of `rows` rows of `width` bytes (device pitch src_pitch, host pitch
+  // dst_pitch) into pageable host memory: 2D copies into two pinned staging buffers on stream s,
+  // each drained by the thread pool while the next one transfers (padding dropped on the GPU
+  // side; no pageable DMA, no single-threaded copy).  Blocks until done.
+  void download_rows(void* dst, size_t dst_pitch, const void* src, size_t src_pitch, size_t width,
+                     int64_t rows, hipStream_t s = nullptr);
 
  private:
   Backend backend_;
@@ -100,6 +106,7 @@ class Context {
   std::unique_ptr<Stream> compute_, comm_, h2d_;
   std::unique_ptr<ThreadPool> pool_;
   Metrics metrics_;
+  Buffer stage_[2];  // download_rows staging (allocated on first use)
 };
 
 // Number of visible HIP devices (0 when no GPU / no driver).

@@ -3,6 +3,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <sys/mman.h>
+
 #include "runtime/log.h"
 
 namespace oap {
@@ -139,6 +141,17 @@ size_t DeviceArena::reserved() const {
 }
 
 // ------------------------------------------------------------------------------------ Buffer
+void* host_alloc_large(size_t bytes) {
+  constexpr size_t kHuge = size_t(2) << 20;
+  const size_t sz = round_up(bytes == 0 ? 64 : bytes, bytes >= kHuge ? kHuge : 64);
+  void* p = std::aligned_alloc(bytes >= kHuge ? kHuge : 64, sz);
+  if (!p) OAP_THROW(OutOfMemoryError, "host allocation of " << bytes << " B failed");
+  if (bytes >= kHuge) madvise(p, sz, MADV_HUGEPAGE);  // (advice only)
+  return p;
+}
+
+void host_free_large(void* p) { std::free(p); }
+
 Buffer Buffer::host(size_t bytes) {
   Buffer b;
   size_t sz = round_up(bytes == 0 ? 64 : bytes, 64);

@@ -102,4 +102,32 @@ class Buffer {
   std::shared_ptr<DeviceArena> arena_;
 };
 
+// Large host result array (model factors, labels): uninitialised (no zero pass over GBs),
+// 2 MiB-aligned with transparent huge pages requested (few first-touch faults when the download
+// threads fill it), and shared so a binding can hand it to numpy without a copy.
+void* host_alloc_large(size_t bytes);
+void host_free_large(void* p);
+
+template <typename T>
+class HostArray {
+ public:
+  HostArray() = default;
+  static HostArray alloc(size_t n) {
+    HostArray a;
+    a.n_ = n;
+    a.p_ = std::shared_ptr<T>(static_cast<T*>(host_alloc_large(n * sizeof(T))),
+                              [](T* q) { host_free_large(q); });
+    return a;
+  }
+  T* data() const { return p_.get(); }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T& operator[](size_t i) const { return p_.get()[i]; }
+  const std::shared_ptr<T>& owner() const { return p_; }
+
+ private:
+  std::shared_ptr<T> p_;
+  size_t n_ = 0;
+};
+
 }  // namespace oap

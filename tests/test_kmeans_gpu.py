@@ -358,7 +358,9 @@ def test_operand_image_scale_fallback(native):
     rp = native.kmeans_fit(g, comm, t, init, k, 6, -1.0, precise=True)
     print({key: ri[key] for key in ("image_passes", "image_bytes", "deferred_rows", "moved_rows",
                                     "assign_path", "num_iter")})
-    assert ri["image_passes"] > 0
+    # (image_passes counts the passes that actually read the image: the grown centers force
+    # the f32 rows on at least one delta pass)
+    assert ri["image_bytes"] > 0 and ri["image_passes"] < ri["num_iter"] - 1
     assert ri["last_counts"] == rp["last_counts"]
     assert np.array_equal(ri["centers"], rp["centers"])
 
@@ -469,4 +471,50 @@ def test_lean_chunked_large_k_bitwise(native, monkeypatch, d, k, sigma, dtype):
     lab, dist = native.kmeans_predict(g, t, rl["centers"])
     ref_lab, ref_d = vanilla.find_closest(X, rl["centers"])
     assert (lab == ref_lab).mean() > 0.9999
+
+
+
+@pytest.mark.parametrize("d,k,sigma", [(50, 200, 8.0), (20, 37, 4.0), (12, 7, 4.0), (60, 100, 6.0),
+                                       (100, 50, 5.0), (40, 230, 4.0), (26, 160, 3.0)])
+def test_image_kernel_matches_lloyd_image_branch(native, d, k, sigma):
+    """The dedicated steady-state image kernel (kmeans_lean_img.hip) gives the general lean
+    kernel's image branch bitwise: labels, fixed-point statistics, deferred and moved rows (one
+    delta pass at the next Lloyd step's centers; partial last chunks, one chunk, 12-wave rows),
+    in each of its configurations, with and without the f32-row fallback launch."""
+    n = 120000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, sigma, 17)
+    comm = native.LocalComm(True)
+    init = t.to_numpy(g, 0, k) + 0.125
+    ca = np.asarray(native.kmeans_fit(g, comm, t, init, k, 3, -1.0)["centers"]).reshape(k, d)
+    cb = np.asarray(native.kmeans_fit(g, comm, t, ca, k, 1, -1.0)["centers"]).reshape(k, d)
+    ref = native.kmeans_image_timing(g, t, ca, cb, 1, 0, -1, True)
+    assert ref["image_passes"] > 0 and ref["moved_rows"] > 0
+    for cfg, fb in ((-1, True), (-1, False), (0, True), (2, True), (3, False)):
+        r = native.kmeans_image_timing(g, t, ca, cb, 1, 1, cfg, fb)
+        assert r["path"].startswith("lean_img_kernel"), r["path"]
+        assert r["image_passes"] == ref["image_passes"]
+        assert r["deferred_rows"] == ref["deferred_rows"]
+        assert r["moved_rows"] == ref["moved_rows"]
+        assert np.array_equal(r["labels"], ref["labels"])
+        assert np.array_equal(r["stats"], ref["stats"])
+
+
+def test_image_kernel_scale_fallback(native):
+    """An image written at a scale the next centers outgrow (beta max|c| > 2^9): the dedicated
+    image kernel does nothing and its f32-row fallback launch takes the pass — labels and
+    statistics equal the general kernel's (which falls back inside), and no pass reads the
+    image."""
+    n, d, k = 100000, 20, 40
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 50.0, 2.0, 5)
+    comm = native.LocalComm(True)
+    cb = np.asarray(native.kmeans_fit(g, comm, t, t.to_numpy(g, 0, k), k, 2, -1.0)["centers"])
+    cb = cb.reshape(k, d)
+    ca = (cb * 1e-3).astype(np.float32).astype(np.float64)
+    ref = native.kmeans_image_timing(g, t, ca, cb, 1, 0, -1, True)
+    r = native.kmeans_image_timing(g, t, ca, cb, 1, 1, -1, True)
+    assert ref["image_passes"] == 0 and r["image_passes"] == 0
+    assert np.array_equal(r["labels"], ref["labels"]) and np.array_equal(r["stats"], ref["stats"])
+    assert r["moved_rows"] == ref["moved_rows"] > 0
 
