@@ -175,6 +175,13 @@ def bench_kmeans(args, w):
         "lean_fp16_centroid_chunked_delta": "centroid-chunked lean fp16 MFMA pass + chunked "
                                             "exact fp32 re-decision; binned accumulation of the "
                                             "moved rows only",
+        "lean_img_kernel_delta": "dedicated steady-state image kernel (oap_kmeans_lean_img): "
+                                 "lean fp16 MFMA pass over the resident operand image + exact "
+                                 "fp32 re-decision; delta accumulation of moved rows",
+        "lean_img_kernel_delta_rowscan": "row-level Hamerly scan + the image kernel over the rows "
+                                         "it could not prune (gathered from the row-major "
+                                         "operand image) + exact fp32 re-decision; delta "
+                                         "accumulation of moved rows",
         "tiered_bf16_mfma": "tiered bf16 MFMA distances (exact-fp32 re-decision of near ties)",
         "tiered_bf16_mfma_chunked": "centroid-chunked tiered bf16 MFMA distances",
         "exact_fp32_mfma": "fp32-exact MFMA (v_mfma_f32_32x32x2_f32)",
@@ -191,6 +198,9 @@ def bench_kmeans(args, w):
              "center_shift_history": [round(v, 4) for v in r["shift_history"]],
              # share of (tile, iteration) pairs whose distance work the exact bounds skipped
              "pruned_frac": pruned_g / (tiles * args.steps),
+             # share of (row, iteration) pairs the row-level scan proved unchanged
+             "pruned_rows_frac": float(w.allreduce_np(np.array(
+                 [float(r.get("pruned_rows", 0))]), "sum")[0]) / (rows_total * args.steps),
              "assign_kernel_ms": ak["total_us"] / max(ak["count"], 1) / 1e3,
              "allreduce_us": ar["total_us"] / max(ar["count"], 1),
              # device time of one whole iteration minus assign and allreduce: finalize,
@@ -215,6 +225,23 @@ def bench_kmeans(args, w):
              "distance_path": path,
              "distance_path_desc": path_desc,
              "cost": r["cost"]}
+    # CPU comparison (BASELINE.md protocol: no Spark on the GPU host -> a labelled fp64 CPU
+    # proxy of the same Lloyd step on this host's cores, on a row subsample of the same data
+    # and the same initial centers; the rate scales linearly with rows)
+    cpu = None
+    if args.cpu_rows > 0 and w.is_gpu:
+        if w.rank == 0:
+            sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                            "benchmarks"))
+            from cpu_baseline import kmeans_proxy
+
+            Xs = table.to_numpy(w.ctx, 0, min(args.cpu_rows, local))
+            cpu = kmeans_proxy(Xs, np.asarray(init, dtype=np.float64).reshape(k, d),
+                               iters=args.cpu_iters)
+            del Xs
+        w.barrier()
+    if cpu is not None:
+        extra["cpu_baseline"] = cpu
     del table
     if args.separable_extra and args.sigma != 1.0:
         # round-1 regime (well-separated blobs): converges in ~2 iterations, later iterations
@@ -236,7 +263,9 @@ def bench_kmeans(args, w):
         "metric": "kmeans_samples_per_sec", "value": samples, "unit": "samples/s",
         "n_gpus": w.size, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el_max / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
-        "vs_baseline": None, "dtype": "fp32" if st == "f32" else "bf16",
+        # whole-job GPU samples/s over the CPU proxy's samples/s on this host (extra.cpu_baseline)
+        "vs_baseline": samples / cpu["samples_per_sec"] if cpu else None,
+        "dtype": "fp32" if st == "f32" else "bf16",
         "data": f"synthetic (overlapping gaussian blobs sigma={args.sigma}, box={args.box}, "
                 "generated on-device; random k-means|| init)",
         "config": {"model": f"kmeans k={k} d={d} (Lloyd, euclidean)", "global_batch": rows_total,
@@ -274,6 +303,10 @@ def main(argv=None):
                     help="exact-fp32 MFMA distances only (no bf16-split fast path)")
     ap.add_argument("--no-estimator", dest="estimator", action="store_false",
                     help="skip the user-facing KMeans(...).fit(host ndarray) timing")
+    ap.add_argument("--cpu-rows", type=int, default=2_000_000,
+                    help="rows of the CPU-proxy baseline (scikit-learn fp64 Lloyd on this "
+                    "host's cores; 0 skips it and vs_baseline is null)")
+    ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--force-rccl", action="store_true",
                     help="N=1: form a real 1-rank RCCL communicator (the multi-GPU device "
                     "collective path) instead of the no-op local comm")

@@ -12,6 +12,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
@@ -23,6 +24,8 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--alpha", type=float, default=40.0)
     ap.add_argument("--reg", type=float, default=0.01)
+    ap.add_argument("--cpu-ratings", type=int, default=2_000_000,
+                    help="ratings of the fp64 host-engine CPU-proxy baseline (0: skip)")
     ap.add_argument("--force-rccl", action="store_true",
                     help="1 GPU: a real 1-rank RCCL communicator (device shuffle, comm-stream "
                     "Gramian allreduce, chunked factor broadcasts) instead of the local comm")
@@ -48,12 +51,26 @@ def main():
     out = N.als_fit(w.ctx, w.comm, u, it, r, a.rank, a.iters, a.reg, a.alpha, True, 0)
     w.barrier()
     wall = time.time() - t0
+    cpu = None
+    if w.rank == 0 and a.cpu_ratings > 0:
+        # labelled CPU proxy — the fp64 host engine on a ratings subsample of the
+        # same generator (users and items scaled down with it), scaled to the full ratings
+        from cpu_baseline import als_proxy
+
+        m = min(a.cpu_ratings, n_loc)
+        fu = max(1, int(a.users * m / a.ratings))
+        fi = max(1, int(a.items * m / a.ratings))
+        cpu = als_proxy(N, (u[:m] % fu).astype(np.int32), (it[:m] % fi).astype(np.int32), r[:m],
+                        a.rank, a.alpha, a.reg, a.ratings)
     if w.rank == 0:
         it_ms = list(out["iter_ms"])
         steady = it_ms[1:] if len(it_ms) > 1 else it_ms
         print(json.dumps({
             "metric": "als_iteration_s", "value": sum(steady) / len(steady) / 1e3, "unit": "s",
             "n_gpus": w.size, "higher_is_better": False,
+            # CPU-proxy seconds per iteration over the GPU's (extra.cpu_baseline)
+            "vs_baseline": (cpu["s_per_iter_scaled"] / (sum(steady) / len(steady) / 1e3)
+                            if cpu else None),
             "dtype": ("fp32 factors; Gramian: fp32 MFMA (rows <= 64 ratings), split-fp16 "
                       "hi+lo MFMA with fp32 accumulation (longer rows); fp32 Cholesky"),
             "data": "synthetic implicit counts (uniform users, power-law items)",
@@ -68,7 +85,8 @@ def main():
                       "factor_bcast_ms_total": out["bcast_ms"],
                       "factor_bcast_recv_bytes": out["bcast_recv_bytes"],
                       "factor_bcast_gbps": (out["bcast_recv_bytes"] / out["bcast_ms"] / 1e6
-                                            if out["bcast_ms"] > 0 else None)}}))
+                                            if out["bcast_ms"] > 0 else None),
+                      "cpu_baseline": cpu}}))
     O.shutdown_world()
 
 

@@ -13,6 +13,7 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
@@ -21,6 +22,8 @@ def main():
     ap.add_argument("--dim", type=int, default=1000)
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cpu-rows", type=int, default=500_000,
+                    help="rows of the fp64 numpy CPU-proxy baseline (0: skip; vs_baseline null)")
     ap.add_argument("--precision", default="both", choices=["exact", "fast", "fast4", "both"],
                     help="exact: fp64 products + sums (fp64 MFMA, the reference's precision); "
                     "fast: bf16x3 split products; fast4: bf16x4; both: exact (headline) + fast")
@@ -68,6 +71,12 @@ def main():
         extra = dict(res[head][0])
         extra["ingest_synth_s"] = ingest
         extra["precision"] = head
+        cpu = None
+        if a.cpu_rows > 0:  # labelled fp64 CPU proxy on this host's cores
+            from cpu_baseline import pca_proxy
+
+            cpu = pca_proxy(t.to_numpy(w.ctx, 0, min(a.cpu_rows, n_loc)), a.k, a.rows)
+            extra["cpu_baseline"] = cpu
         for m in modes[1:]:
             extra[m + "_mode"] = res[m][0]
             ev_a = np.asarray(res[head][1]["explained_variance"])
@@ -76,6 +85,8 @@ def main():
         print(json.dumps({
             "metric": "pca_fit_wall_s", "value": res[head][0]["fit_wall_s"], "unit": "s",
             "n_gpus": w.size, "higher_is_better": False, "dtype": dtype,
+            # CPU-proxy fit time over the GPU fit time (extra.cpu_baseline)
+            "vs_baseline": (cpu["fit_s_scaled"] / res[head][0]["fit_wall_s"]) if cpu else None,
             "data": "synthetic (gaussian blobs, on-device)",
             "config": {"model": "pca top-%d" % a.k, "rows": a.rows, "dim": a.dim},
             "extra": extra}))

@@ -50,7 +50,7 @@ void register_als(py::module_& m) {
          py::array_t<int32_t, py::array::c_style | py::array::forcecast> items,
          py::array_t<float, py::array::c_style | py::array::forcecast> ratings, int rank,
          int max_iter, double reg, double alpha, bool implicit, uint64_t seed,
-         py::object init_ids, py::object init_factors) {
+         py::object init_ids, py::object init_factors, bool host_engine, bool nonnegative) {
         const int64_t n = users.size();
         if (items.size() != n || ratings.size() != n)
           throw ConfigError("users, items and ratings must have the same length");
@@ -61,6 +61,8 @@ void register_als(py::module_& m) {
         p.alpha = alpha;
         p.implicit = implicit;
         p.seed = seed;
+        p.host_engine = host_engine;
+        p.nonnegative = nonnegative;
         py::array_t<int32_t, py::array::c_style | py::array::forcecast> iid;
         py::array_t<float, py::array::c_style | py::array::forcecast> ifac;
         if (!init_ids.is_none()) {
@@ -113,6 +115,7 @@ void register_als(py::module_& m) {
       py::arg("ctx"), py::arg("comm"), py::arg("users"), py::arg("items"), py::arg("ratings"),
       py::arg("rank") = 10, py::arg("max_iter") = 10, py::arg("reg") = 0.1,
       py::arg("alpha") = 1.0, py::arg("implicit") = true, py::arg("seed") = 0,
-      py::arg("init_ids") = py::none(), py::arg("init_factors") = py::none());
+      py::arg("init_ids") = py::none(), py::arg("init_factors") = py::none(),
+      py::arg("host_engine") = false, py::arg("nonnegative") = false);
   m.def("als_max_rank", &kern::als_max_rank);
 }

@@ -519,6 +519,7 @@ PYBIND11_MODULE(_native, m) {
         out["deferred_rows"] = r.deferred_rows;
         out["moved_rows"] = r.moved_rows;
         out["image_passes"] = r.image_passes;
+        out["pruned_rows"] = r.pruned_rows;
         out["image_bytes"] = r.image_bytes;
         return out;
       },

@@ -296,6 +296,25 @@ void comm_allreduce_host(Context& ctx, Comm& comm, void* host, size_t count, DTy
   comm.wait(s);
 }
 
+void comm_allgather_host(Context& ctx, Comm& comm, const void* send, void* recv, size_t count,
+                         DType dt) {
+  const size_t bytes = count * dtype_size(dt);
+  if (comm.trivial()) {
+    if (bytes) std::memmove(recv, send, bytes);
+    return;
+  }
+  if (!comm.on_device()) {
+    comm.allgather(send, recv, count, dt, nullptr);
+    return;
+  }
+  Buffer ds = ctx.alloc(bytes), dr = ctx.alloc(bytes * comm.size());
+  hipStream_t s = ctx.comm_stream();
+  OAP_HIP_CHECK(hipMemcpyAsync(ds.data(), send, bytes, hipMemcpyHostToDevice, s));
+  comm.allgather(ds.data(), dr.data(), count, dt, s);
+  OAP_HIP_CHECK(hipMemcpyAsync(recv, dr.data(), bytes * comm.size(), hipMemcpyDeviceToHost, s));
+  comm.wait(s);
+}
+
 void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
                          const std::vector<size_t>& send_counts, void* recv,
                          const std::vector<size_t>& recv_counts, DType dt) {

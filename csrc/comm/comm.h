@@ -119,6 +119,9 @@ void comm_bcast(Context& ctx, Comm& comm, void* buf, size_t count, DType dt, int
 // Host memory in, host memory out, whatever memory the comm works on.
 void comm_allreduce_host(Context& ctx, Comm& comm, void* host, size_t count, DType dt,
                          ReduceOp op);
+// allgather of HOST buffers over any comm (device comms stage through HBM).
+void comm_allgather_host(Context& ctx, Comm& comm, const void* send, void* recv, size_t count,
+                         DType dt);
 // Variable-size exchange of HOST buffers over any comm (device comms stage through HBM).
 void comm_alltoallv_host(Context& ctx, Comm& comm, const void* send,
                          const std::vector<size_t>& send_counts, void* recv,

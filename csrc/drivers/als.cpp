@@ -284,6 +284,80 @@ bool chol_solve(std::vector<double>& A, std::vector<double>& b, int r) {
   return true;
 }
 
+// Non-negative least squares on the normal equations: min 1/2 x^T A x - b^T x subject to x >= 0
+// (A = lower triangle of an SPD r x r matrix, row-major), by the Lawson-Hanson active set: the
+// strictly convex problem has one minimiser, the one Spark's projected-CG NNLS
+// (mllib/optimization/NNLS.scala, ALS.scala:1718-1800 with nonnegative = true) converges to.
+// Each passive-set solve is a Cholesky of the passive block.  x gets the solution; false when a
+// passive block is not SPD.
+bool nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int r,
+                std::vector<double>& x) {
+  auto a = [&](int i, int j) { return i >= j ? A[size_t(i) * r + j] : A[size_t(j) * r + i]; };
+  x.assign(r, 0.0);
+  std::vector<char> passive(r, 0);
+  std::vector<int> idx;
+  std::vector<double> sub, z(r), rhs;
+  double amax = 0.0;
+  for (int i = 0; i < r; ++i) amax = std::max(amax, std::fabs(a(i, i)));
+  const double tol = 1e-12 * std::max(amax, 1e-300) * (1.0 + std::fabs(*std::max_element(
+      b.begin(), b.end(), [](double u, double v) { return std::fabs(u) < std::fabs(v); })));
+  auto solve_passive = [&]() -> bool {  // z_P = A_PP^-1 b_P, z elsewhere 0
+    idx.clear();
+    for (int i = 0; i < r; ++i)
+      if (passive[i]) idx.push_back(i);
+    const int m = int(idx.size());
+    sub.assign(size_t(m) * m, 0.0);
+    rhs.assign(m, 0.0);
+    for (int i = 0; i < m; ++i) {
+      rhs[i] = b[idx[i]];
+      for (int j = 0; j <= i; ++j) sub[size_t(i) * m + j] = a(idx[i], idx[j]);
+    }
+    if (!chol_solve(sub, rhs, m)) return false;
+    std::fill(z.begin(), z.end(), 0.0);
+    for (int i = 0; i < m; ++i) z[idx[i]] = rhs[i];
+    return true;
+  };
+  for (int outer = 0; outer < 3 * r + 10; ++outer) {
+    // gradient of the objective's negative: w = b - A x; the best free coordinate enters
+    int jbest = -1;
+    double wbest = tol;
+    for (int j = 0; j < r; ++j) {
+      if (passive[j]) continue;
+      double w = b[j];
+      for (int i = 0; i < r; ++i) w -= a(j, i) * x[i];
+      if (w > wbest) {
+        wbest = w;
+        jbest = j;
+      }
+    }
+    if (jbest < 0) return true;
+    passive[jbest] = 1;
+    for (int inner = 0; inner < 3 * r + 10; ++inner) {
+      if (!solve_passive()) return false;
+      double alpha = 1.0;
+      bool feasible = true;
+      for (int i = 0; i < r; ++i)
+        if (passive[i] && z[i] <= 0.0) {
+          feasible = false;
+          const double den = x[i] - z[i];
+          if (den > 0.0) alpha = std::min(alpha, x[i] / den);
+        }
+      if (feasible) {
+        x = z;
+        break;
+      }
+      for (int i = 0; i < r; ++i) {
+        x[i] += alpha * (z[i] - x[i]);
+        if (passive[i] && x[i] <= 0.0) {
+          passive[i] = 0;
+          x[i] = 0.0;
+        }
+      }
+    }
+  }
+  return true;
+}
+
 // Rows of X (global user order, stride ld) whose id appears in the caller's initial factors
 // (ids sorted ascending, rank columns) are overwritten with them — the resume path.
 void overlay_init(const std::vector<int32_t>& ids, int r, int ld, const AlsParams& p,
@@ -320,7 +394,10 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   kern::AlsDistSetup dist_setup;
   bool on_device = false;
   kern::AlsDeviceCsr *dev_ucsr = nullptr, *dev_icsr = nullptr;
-  if (ctx.is_gpu() && !std::getenv("OAP_ALS_HOST_SETUP")) {
+  // (host_engine: the fp64 host solver on a GPU world, e.g. ranks beyond the GPU kernels; the
+  // GPU context only stages the collectives)
+  const bool gpu_engine = ctx.is_gpu() && !p.host_engine && !p.nonnegative;
+  if (gpu_engine && !std::getenv("OAP_ALS_HOST_SETUP")) {
     ctx.activate();
     if (local)
       on_device = kern::als_device_setup(ctx, users, items, ratings, n, ctx.compute(), &dev_setup);
@@ -440,7 +517,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
 
   std::vector<float> Xh, Yh;  // final factors (host, [n][ld])
   auto t_train = std::chrono::steady_clock::now();
-  if (ctx.is_gpu()) {
+  if (gpu_engine) {
     OAP_CHECK(r <= kern::als_max_rank(), "GPU ALS supports rank <= " << kern::als_max_rank()
                                                                       << " (use the CPU engine)");
     ctx.activate();
@@ -842,7 +919,12 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
           const double lam = p.reg * double(nexp);
           for (int i = 0; i < r; ++i) A[size_t(i) * r + i] += lam;
           float* out = &mine[size_t(row) * ld];
-          if (chol_solve(A, bv, r)) {
+          if (p.nonnegative) {
+            if (nnls_solve(A, bv, r, y))
+              for (int f = 0; f < r; ++f) out[f] = float(y[f]);
+            else
+              ++fail_part[ci];
+          } else if (chol_solve(A, bv, r)) {
             for (int f = 0; f < r; ++f) out[f] = float(bv[f]);
           } else {
             ++fail_part[ci];
@@ -859,7 +941,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         for (int q = 0; q < P; ++q) mx = std::max(mx, Dst.cnt[q]);
         mine.resize(size_t(mx) * ld, 0.f);
         std::vector<float> all(size_t(mx) * ld * P);
-        comm_allgather(ctx, comm, mine.data(), all.data(), size_t(mx) * ld, DType::F32, nullptr);
+        comm_allgather_host(ctx, comm, mine.data(), all.data(), size_t(mx) * ld, DType::F32);
         for (int q = 0; q < P; ++q)
           std::copy(all.begin() + size_t(q) * mx * ld,
                     all.begin() + size_t(q) * mx * ld + size_t(Dst.cnt[q]) * ld,

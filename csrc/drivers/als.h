@@ -35,6 +35,12 @@ struct AlsParams {
   const int32_t* init_ids = nullptr;
   const float* init_factors = nullptr;
   int64_t n_init = 0;
+  // fp64 host engine (thread pool, per-row Cholesky) even on a GPU context: the distributed
+  // fallback for what the GPU kernels do not take (rank > kern::als_max_rank()); the ratings
+  // stay sharded (same owner shuffle), only the factor slices are exchanged
+  bool host_engine = false;
+  // non-negative factors (Spark's nonnegative = true): NNLS per row, host engine
+  bool nonnegative = false;
 };
 
 struct AlsResult {

@@ -261,6 +261,9 @@ struct AssignReq {
   int img_kernel = -1;      // -1: OAP_KMEANS_IMG_KERNEL (default on), 0 kmeans_lloyd, 1 lean_img
   int img_cfg = -1;         // oap_kmeans_lean_img configuration (-1: OAP_KMEANS_IMG_CFG / default)
   bool skip_exact = false;  // timing probes: the lean pass only
+  // image passes after a row-level scan (kmeans_lean_scan_rows): the rows it could not prune
+  const int32_t* img_rows = nullptr;
+  const unsigned* img_row_count = nullptr;
 };
 
 // The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
@@ -389,6 +392,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.ximg = req.ximg;
     a.img_beta = req.img_beta;
     a.img_mode = req.img_mode;
+    a.img_rows = req.img_mode == 2 ? req.img_rows : nullptr;
+    a.img_row_count = req.img_mode == 2 ? req.img_row_count : nullptr;
     if (req.delta) {  // delta accumulation; over the scan's tile list when there is one
       OAP_CHECK(req.labels && req.labels_valid,
                 "kmeans delta accumulation needs the previous iteration's labels");
@@ -415,8 +420,11 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
         f.img_mode = 3;
         kern::kmeans_lloyd(f, grid, lv, s);
       }
-      t_assign_path = req.tile_list ? "lean_img_kernel_delta_scan" : "lean_img_kernel_delta";
+      t_assign_path = a.img_rows       ? "lean_img_kernel_delta_rowscan"
+                      : req.tile_list ? "lean_img_kernel_delta_scan"
+                                      : "lean_img_kernel_delta";
     } else {
+      OAP_CHECK(!a.img_rows, "kmeans: a row-list image pass needs the image kernel");
       kern::kmeans_lloyd(a, grid, lv, s);
     }
     if (req.skip_exact) return 0;
@@ -432,6 +440,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.tile_list = nullptr;
     b.tile_count = nullptr;
     b.xnorm = nullptr;
+    b.img_rows = nullptr;
+    b.img_row_count = nullptr;
     b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
     kern::kmeans_exact_rows(b, grid, s);
     return a.cost_slab ? 2 * grid : 0;
@@ -1285,6 +1295,23 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     req.xnorm = xnorm_b.as<float>();
   }
   if (delta) cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
+  // Row-level scan (image passes): per row, the Hamerly test the tile scan applies to whole
+  // 32-row tiles; the image kernel then gathers only the rows it could not prune.  On overlapping
+  // clusters a tile almost always holds a row near a boundary, while most rows are far from one
+  // (headline data: tiles 0-13% prunable, rows up to 93%: profiles/r4/row_prune_potential.jsonl).
+  // Bounds are then written by every pass.  OAP_KMEANS_ROW_SCAN=0 keeps the tile scan.
+  Buffer rlist_b, rpruned_b;
+  const char* rs_env = std::getenv("OAP_KMEANS_ROW_SCAN");
+  const bool row_scan = scan && !chunked && !(rs_env && *rs_env == '0');
+  if (row_scan) {
+    rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
+                        sizeof(unsigned) * size_t(lgrid) + 64);
+    rpruned_b = ctx.alloc(sizeof(u64));
+    ctx.memset(rpruned_b.data(), 0, sizeof(u64), s);
+  }
+  unsigned* rcount = row_scan ? reinterpret_cast<unsigned*>(rlist_b.as<int32_t>() +
+                                                            size_t(lgrid) * size_t(ltiles) * 32)
+                              : nullptr;
   unsigned* dcount =
       scan ? reinterpret_cast<unsigned*>(dlist_b.as<int32_t>() + size_t(lgrid) * size_t(ltiles))
            : nullptr;
@@ -1324,6 +1351,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       img_beta_b = ctx.alloc(sizeof(float) * 4);
       res.image_bytes = static_cast<int64_t>(ib);
     }
+  }
+  // (row-scan mode needs the image and the image kernel at this shape; rank-uniform in practice:
+  // every rank decides from the same shape, and a rank without rows scans nothing)
+  bool row_scan_ok = false;
+  if (row_scan && img_b.data() && img_kernel_default()) {
+    const int lv = lean_variant(d, g.kpad);
+    row_scan_ok = lv != 3 && lv != 10 &&
+                  kern::kmeans_lean_img_supported(d, k, kern::kmeans_lloyd_waves(lv));
   }
   // with the adaptive scan off, full passes write the per-row bounds (8 B/row) only where a
   // following iteration may scan, and the per-tile max |x|^2 (constant) once
@@ -1397,7 +1432,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (a probe batch scans its first iteration only: the next batch decides from it)
       // (the first batch scans its third iteration only: one right after the init's large
       // move rarely prunes)
-      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on &&
+      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on && !row_scan_ok &&
                                (!probing || b == 0);  // rank-uniform
       const bool scan_it = scan_it_all && scan;
       last_scanned = scan_it_all;
@@ -1420,7 +1455,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         const bool next_may_scan =
             it >= 1 && (b < nb_it - 1 ? delta_on && !probing
                                       : delta_on || delta_probe + 1 >= probe_gap);
-        req.bounds = (scan_it || next_may_scan) ? bounds_full : nullptr;
+        req.bounds = (scan_it || next_may_scan || row_scan_ok) ? bounds_full : nullptr;
         req.xnorm = xnorm_ready ? nullptr : xnorm_full;
       }
       if (prune) {
@@ -1449,6 +1484,20 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       } else if (!chunked) {
         req.tile_list = nullptr;
         req.tile_count = nullptr;
+      }
+      // row-level scan ahead of an image pass (the drift finalize wrote for the previous step)
+      const bool row_scan_it = row_scan_ok && delta_it && it > 1 && img_ready && !cost_it &&
+                               req.fast1 && !req.tile_list;
+      req.img_rows = nullptr;
+      req.img_row_count = nullptr;
+      if (row_scan_it) {
+        OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
+        kern::kmeans_lean_scan_rows(x.rows, k, d, lgrid, bounds_full, req.labels, xnorm_full,
+                                    drift_b.as<float>(), drift_b.as<float>() + k,
+                                    g.cstat.as<float>(), rlist_b.as<int32_t>(), rcount,
+                                    rpruned_b.as<u64>(), s);
+        req.img_rows = rlist_b.as<int32_t>();
+        req.img_row_count = rcount;
       }
       // operand image: written by the first full lean pass, read by costless delta passes
       req.ximg = img_b.data();
@@ -1654,6 +1703,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     u64 pt = 0;
     ctx.copy_to_host(&pt, pruned_d.data(), sizeof(u64), s);
     res.pruned_tiles = static_cast<int64_t>(pt);
+  }
+  if (rpruned_b.data()) {
+    u64 pr = 0;
+    ctx.copy_to_host(&pr, rpruned_b.data(), sizeof(u64), s);
+    res.pruned_rows = static_cast<int64_t>(pr);
   }
   if (ldstat_b.data()) {
     u64 dr[3] = {0, 0, 0};

@@ -60,6 +60,7 @@ struct KMeansResult {
   int64_t pruned_tiles = 0;  // 32-row tile passes whose distance work the bounds skipped
   int64_t deferred_rows = 0;  // rows the lean tier-1 pass left to the exact re-decision
   int64_t moved_rows = 0;     // rows the lean delta passes moved between clusters
+  int64_t pruned_rows = 0;    // rows the row-level scan proved unchanged (summed over passes)
   int image_passes = 0;       // lean passes that took their operands from the fp16 row image
   int64_t image_bytes = 0;    // HBM of that image (0: not allocated)
   std::string assign_path = "cpu";  // the distance kernel path of the last iteration (GPU)

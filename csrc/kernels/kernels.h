@@ -111,6 +111,10 @@ struct KMeansAssignArgs {
   // row's previous label.
   const int32_t* row_list = nullptr;
   const unsigned* row_count = nullptr;  // [grid][16]: rows per sub-segment
+  // Row-list image pass (kmeans_lean_img): the rows the row scan left, [grid][32 tiles/block]
+  // in row order, count [grid] (kmeans_lean_scan_rows)
+  const int32_t* img_rows = nullptr;
+  const unsigned* img_row_count = nullptr;
   int64_t row_seg_cap = 0;
   int row_subs = 1;  // sub-segments per workgroup segment (each row_seg_cap / row_subs long)
   // Lean tier-1 kernel output: rows whose tier-1 top-2 gap is inside the tier's error bound are
@@ -137,8 +141,8 @@ struct KMeansAssignArgs {
   int kglob = 0;
   int32_t* lean_keys = nullptr;
   float* xstate = nullptr;
-  // Resident fp16 operand image of f32 rows (lean kernel, single launch): [ceil(n/32)][KS][64]
-  // fragments of 8 halves (kmeans_lloyd_image_bytes), the MFMA B operand of each 32-row tile
+  // Resident fp16 operand image of f32 rows (lean kernel, single launch): row-major
+  // [32 ceil(n/32)][16 KS] halves (kmeans_lloyd_image_bytes), the MFMA B operand of each row
   // with its bias slots, at the scale *img_beta.  img_mode 1: this full pass writes image and
   // scale; 2: this pass takes its operands from the image (f32 rows only for accumulation).
   void* ximg = nullptr;
@@ -170,6 +174,15 @@ size_t kmeans_lloyd_image_bytes(int64_t n, int d);
 // current centers the kernel does nothing; kmeans_lloyd with img_mode 3 then runs the pass.
 bool kmeans_lean_img_supported(int d, int k, int waves);
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s);
+// Row-level bound scan for the image passes: every row of lean workgroup b's range gets the
+// Hamerly test of kmeans_lean_scan (u + drift[label] against l - max drift, with the tile's
+// max |x|^2 in the margin); pruned rows have their bounds advanced in place (no write once no
+// center moves), the others are appended in row order to b's segment of row_list
+// ([lean_grid][32 tiles_per_block], count row_count[b]).  *pruned_rows (optional) counts.
+void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
+                           const int32_t* labels, const float* xnorm, const float* drift,
+                           const float* drift_max, const float* cstat, int32_t* row_list,
+                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s);
 // Largest centroid chunks (multiples of 32) of the chunked lean pass at dimension d: the lean
 // kernel's fp16 plane and the exact kernel's fp32 centers (0: d not supported).
 int kmeans_lloyd_chunk_kmax(int d);

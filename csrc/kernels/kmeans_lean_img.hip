@@ -46,7 +46,7 @@ constexpr float kBias = 16.f;  // the bias features' unit (kmeans_lloyd.hip kBia
 constexpr int kMv = 64;        // per-wave LDS slots of staged moved rows
 
 struct ImgArgs {
-  const f16x8* img;  // [tiles][KS][64] fragments
+  const f16x8* img;  // row-major [32 tiles][2 KS] fragments (k-step s, half h at 2 s + h)
   const float* img_beta;
   const float* x;  // f32 rows [n][ld] (moved rows only)
   const float* centers;
@@ -62,6 +62,8 @@ struct ImgArgs {
   int32_t* defer_rows;
   unsigned* defer_row_count;
   u64* stat;  // optional [deferred rows, moved rows, image passes]
+  const int32_t* rows;  // row-list passes: [grid][32 tiles_per_block] rows in order, count [grid]
+  const unsigned* row_count;
   int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
 };
@@ -89,6 +91,17 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves) 
   return m;
 }
 
+// set bits of a wave mask below this lane (v_mbcnt_lo + v_mbcnt_hi: no per-lane mask register)
+__device__ inline unsigned lanes_below(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
+                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
+}
+
+// a kernel-uniform float in an SGPR (v_readfirstlane of its bits)
+__device__ inline float ufl(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 __device__ inline void split_h(float v, _Float16& hi, _Float16& lo) {
   hi = static_cast<_Float16>(v);
   lo = static_cast<_Float16>(v - static_cast<float>(hi));
@@ -96,11 +109,13 @@ __device__ inline void split_h(float v, _Float16& hi, _Float16& lo) {
 
 // CFG: bit 0 software-pipelined chunk loop; bit 1 operands two tiles ahead (else one); bits 2+
 // timing ablations (probe builds only): 4 no epilogue, 8 no MFMA, 16 no plane reads, 32 no image
-// loads, 64 no moved-row accumulation, 128 no per-row stores
-template <int KS, int WAVES, int CFG>
+// loads, 64 no moved-row accumulation, 128 no per-row stores.
+// LIST: the tiles are 32 consecutive entries of this workgroup's row list (the rows the row
+// scan could not prune), gathered from the row-major image; else 32 consecutive rows.
+template <int KS, int WAVES, int CFG, bool LIST>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) {
   constexpr bool PIPE = (CFG & 1) != 0;
-  constexpr int PD = (CFG & 2) ? 2 : 1;
+  constexpr int PD = (LIST || !(CFG & 2)) ? 1 : 2;
   constexpr bool NO_EPI = (CFG & 4) != 0, NO_MFMA = (CFG & 8) != 0, NO_LDS = (CFG & 16) != 0;
   constexpr bool NO_LOAD = (CFG & 32) != 0, NO_ACC = (CFG & 64) != 0, NO_ST = (CFG & 128) != 0;
   constexpr int DP = 16 * KS, NT = WAVES * 64, RS = DP + 1;
@@ -117,7 +132,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   int* cnt_l = reinterpret_cast<int*>(smem + L.cnt);
   const int tid = threadIdx.x;
   const float a2 = alpha * alpha;
-  const float inv_a2 = 1.f / a2;  // (a power of two)
+  const float inv_a2 = ufl(1.f / a2);  // (a power of two)
   // ---- the plane c' = [-2 alpha c, 0 .., hi, lo (alpha^2 |c|^2 / 16), 16, 16] (kmeans_lloyd.hip)
   for (int idx = tid; idx < kpad * DP; idx += NT) {
     const int c = idx / DP, f = idx - c * DP;
@@ -142,16 +157,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const int r = lane & 31, h = lane >> 5;
   int2* mv_l = reinterpret_cast<int2*>(smem + L.mv) + wave * kMv;
   // tier-1 bound (kmeans_lloyd.hip, f32 rows): cross term, subnormals, bias pairs, accumulation
-  const float cm_s = alpha * cmax;
-  const float thr_c = 0.0040f * cm_s;
-  const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
-  const float mrel = 4e-7f * float(d + 8);
+  // (kernel-uniform values pinned to SGPRs: a VGPR copy each would cost the pipelined loop
+  // its register headroom)
+  const float cm_s = ufl(alpha * cmax);
+  const float thr_c = ufl(0.0040f * cm_s);
+  const float thr_k = ufl(6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f);
+  const float mrel = ufl(4e-7f * float(d + 8));
+  const float mg_c = ufl(mrel * cm_s * cm_s);
   const int64_t ntiles_all = (a.n + 31) / 32;
   const bool listed = a.tile_list != nullptr;
   const int64_t T = a.tiles_per_block;
   const int64_t t0 = int64_t(blockIdx.x) * T;
-  const int64_t npos = listed ? int64_t(a.tile_count[blockIdx.x])
-                              : (t0 < ntiles_all ? (ntiles_all - t0 < T ? ntiles_all - t0 : T) : 0);
+  const unsigned lcnt = LIST ? a.row_count[blockIdx.x] : 0u;  // (row-list passes)
+  const int32_t* rseg = LIST ? a.rows + blockIdx.x * (T * 32) : nullptr;
+  const int64_t dense_pos = t0 < ntiles_all ? (ntiles_all - t0 < T ? ntiles_all - t0 : T) : 0;
+  const int64_t npos = LIST     ? (int64_t(lcnt) + 31) / 32
+                       : listed ? int64_t(a.tile_count[blockIdx.x])
+                                : dense_pos;
   const int32_t* seg = listed ? a.tile_list + blockIdx.x * T : nullptr;
   constexpr int64_t stride = WAVES;
   const int64_t sub_cap = a.seg_cap / WAVES;
@@ -163,6 +185,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const __amdgpu_buffer_rsrc_t rs_bnd =
       buf_rsrc(a.bounds ? a.bounds + row0 : nullptr, a.bounds ? uint32_t(wrows * 8) : 0u);
   const __amdgpu_buffer_rsrc_t rs_def = buf_rsrc(dseg, uint32_t(sub_cap * 4));
+  // this workgroup's image rows (32 ceil(wrows / 32) records, < 4 GiB) and f32 rows
+  const __amdgpu_buffer_rsrc_t rs_img =
+      buf_rsrc(a.img + row0 * (2 * KS), uint32_t((wrows + 31) / 32 * 32 * (32 * KS)));
+  const __amdgpu_buffer_rsrc_t rs_x = buf_rsrc(a.x + row0 * a.ld, uint32_t(wrows * a.ld * 4));
   const bool want_bounds = a.bounds != nullptr;
   // last chunk: its real 8-centroid groups (the earlier chunks are all real: kpad = 32 ceil(k/32))
   const int c_last = kpad - 32;
@@ -176,12 +202,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     const int64_t tl = int64_t(((seg_cptr)(seg))[q]);
     return tl < 0 ? 0 : (tl < ntiles_all ? tl : ntiles_all - 1);
   };
-  auto load_img = [&](int64_t tile, f16x8(&dst)[KS]) OAP_AI {
+  // one row's operand fragments (row-major image: 2 KS fragments per row) through a buffer
+  // resource over this workgroup's rows: a 32-bit offset per lane instead of a 64-bit pointer
+  // (the pipelined loop has no VGPRs to spare)
+  auto load_img_row = [&](int64_t row, f16x8(&dst)[KS]) OAP_AI {
     if constexpr (!NO_LOAD) {
-      const f16x8* p = a.img + tile * (KS * 64) + lane;
+      const uint32_t off = uint32_t(row - row0) * uint32_t(32 * KS) + 16u * uint32_t(h);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) dst[s] = p[s * 64];
+      for (int s = 0; s < KS; ++s)
+        dst[s] = __builtin_bit_cast(
+            f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_img, off + 32u * s, 0, 0));
     }
+  };
+  // row-list passes: this lane's row of list tile q (-1 past the count)
+  auto rid_of = [&](int64_t q) OAP_AI -> int32_t {
+    const int64_t i = q * 32 + r;
+    return i < int64_t(lcnt) ? rseg[i] : -1;
   };
 
   // ---- moved rows: staged (row, new | old << 16) in the wave's LDS slots, accumulated 32 at a
@@ -195,18 +231,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     const int2 e = mv_l[on ? r : 0];
     float xv[KS][8];
     {
-      const float* p = a.x + int64_t(e.x) * a.ld + 8 * h;
+      // (an offset past the row's ld reads zeros: features beyond ld are padding)
+      const uint32_t rb = uint32_t(int64_t(e.x) - row0) * uint32_t(a.ld) * 4u;
 #pragma unroll
       for (int s = 0; s < KS; ++s)
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           const int f = 16 * s + 8 * h + 4 * q;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (s < KS - 1 || f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
-          xv[s][4 * q + 0] = v.x;
-          xv[s][4 * q + 1] = v.y;
-          xv[s][4 * q + 2] = v.z;
-          xv[s][4 * q + 3] = v.w;
+          const uint32_t off = (s < KS - 1 || f < a.ld) ? rb + uint32_t(f) * 4u : kBufOff;
+          const f32x4 v = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs_x, off, 0, 0));
+          xv[s][4 * q + 0] = v[0];
+          xv[s][4 * q + 1] = v[1];
+          xv[s][4 * q + 2] = v[2];
+          xv[s][4 * q + 3] = v[3];
         }
     }
     if (on) {
@@ -243,19 +281,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   };
 
   // ---- one tile: X holds its operands (landed or in flight), pf receives tile pos + PD stride
-  auto body = [&](const int64_t pos, f16x8(&X)[KS], f16x8(&pf)[KS]) OAP_AI {
+  // row: this lane's row (-1: none); pf_row: the row whose operands go to pf (a real row)
+  // rid_next: row-list passes — the list entry of tile pos + 2 stride, loaded here (ahead of
+  // this tile's own loads, so waiting for it never waits for them)
+  auto body = [&](const int64_t pos, const int64_t row, const int64_t pf_row, int32_t* rid_next,
+                  f16x8(&X)[KS], f16x8(&pf)[KS]) OAP_AI {
     if constexpr (!NO_ACC) {
       if (n_mv >= 32) {  // (before this tile's loads are issued)
         flush(n_mv);
         n_mv -= 32;
       }
     }
-    const int64_t tile = tile_of(pos);
-    const int64_t row = tile * 32 + r;
-    const bool valid = pos < npos && row < a.n;
+    if constexpr (LIST) *rid_next = rid_of(pos + 2 * stride);
+    const bool valid = pos < npos && row >= 0 && row < a.n;
     const uint32_t roff = uint32_t(row - row0);
     int old = buf_load_b32(rs_lab, roff * 4, valid);
-    load_img(tile_of(pos + PD * stride), pf);
+    load_img_row(pf_row, pf);
     // alpha^2 |x|^2 from the bias pair (h = 1 lanes' slots 6, 7 of the last k-step)
     const float mine =
         kBias * (static_cast<float>(X[KS - 1][6]) + static_cast<float>(X[KS - 1][7]));
@@ -372,7 +413,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     const bool unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
     // ---- defer unsure rows (wave-private sub-segment, in tile order)
     const unsigned long long um = __ballot(unsure && h == 0);
-    buf_store_b32(rs_def, (n_def + __popcll(um & ((1ull << lane) - 1ull))) * 4u,
+    buf_store_b32(rs_def, (n_def + lanes_below(um)) * 4u,
                   static_cast<int32_t>(row), !NO_ST && unsure && h == 0);
     n_def += static_cast<unsigned>(__popcll(um));
     const bool done = valid && !unsure;
@@ -383,7 +424,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       const unsigned long long mm = __ballot(moved && h == 0);
       if (mm) {
         if (moved && h == 0)
-          mv_l[n_mv + __popcll(mm & ((1ull << lane) - 1ull))] =
+          mv_l[n_mv + lanes_below(mm)] =
               make_int2(static_cast<int>(row), b | (min(old, k - 1) << 16));
         n_mv += static_cast<unsigned>(__popcll(mm));
       }
@@ -394,7 +435,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     // every other one >= b2 - tt
     float2 bnd = make_float2(0.f, 0.f);
     if (want_bounds) {
-      const float mg = mrel * (nx2_s + cm_s * cm_s);
+      const float mg = fmaf(mrel, nx2_s, mg_c);
       const float up = (b1 + tt + mg) * inv_a2, lo = (b2 - (tt + mg)) * inv_a2;
       bnd = make_float2(__builtin_amdgcn_sqrtf(fmaxf(up, 0.f)) * (1.f + 1e-6f) + 1e-30f,
                         __builtin_amdgcn_sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
@@ -403,32 +444,46 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   };
 
   int64_t t = wave;
-  if constexpr (PD == 1) {
+  auto trow = [&](int64_t q) OAP_AI -> int64_t { return tile_of(q) * 32 + r; };  // (dense)
+  if constexpr (LIST) {
+    // rows of tiles t, t + stride in ra, rb; each body loads the list entry two tiles ahead
+    const int64_t rfix = row0;  // (a real row of this workgroup: the operands of padding lanes)
+    int32_t ra = rid_of(t), rb = rid_of(t + stride), rc = -1;
     f16x8 xa[KS], xb[KS];
-    load_img(tile_of(t), xa);
+    load_img_row(ra >= 0 ? ra : rfix, xa);
+    for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
+      body(t, ra, rb >= 0 ? rb : rfix, &rc, xa, xb);
+      ra = rc;  // (tile t + 2 stride)
+      if (t + stride >= npos) break;
+      body(t + stride, rb, ra >= 0 ? ra : rfix, &rc, xb, xa);
+      rb = rc;  // (tile t + 3 stride)
+    }
+  } else if constexpr (PD == 1) {
+    f16x8 xa[KS], xb[KS];
+    load_img_row(trow(t), xa);
     if constexpr (NO_LOAD) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) xa[s] = xb[s] = f16x8{};
     }
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      body(t, xa, xb);
+      body(t, trow(t), trow(t + stride), nullptr, xa, xb);
       if (t + stride >= npos) break;
-      body(t + stride, xb, xa);
+      body(t + stride, trow(t + stride), trow(t + 2 * stride), nullptr, xb, xa);
     }
   } else {
     f16x8 xa[KS], xb[KS], xc[KS];
-    load_img(tile_of(t), xa);
-    load_img(tile_of(t + stride), xb);
+    load_img_row(trow(t), xa);
+    load_img_row(trow(t + stride), xb);
     if constexpr (NO_LOAD) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) xa[s] = xb[s] = xc[s] = f16x8{};
     }
     for (; t < npos; t += 3 * stride) {
-      body(t, xa, xc);
+      body(t, trow(t), trow(t + 2 * stride), nullptr, xa, xc);
       if (t + stride >= npos) break;
-      body(t + stride, xb, xa);
+      body(t + stride, trow(t + stride), trow(t + 3 * stride), nullptr, xb, xa);
       if (t + 2 * stride >= npos) break;
-      body(t + 2 * stride, xc, xb);
+      body(t + 2 * stride, trow(t + 2 * stride), trow(t + 4 * stride), nullptr, xc, xb);
     }
   }
   if constexpr (!NO_ACC) {
@@ -455,19 +510,32 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   }
 }
 
-template <int KS, int WAVES, int CFG>
-void launch_img(const ImgArgs& a, int grid, hipStream_t s) {
+template <int KS, int WAVES, int CFG, bool LIST>
+void launch_img_l(const ImgArgs& a, int grid, hipStream_t s) {
   const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_lean_img<KS, WAVES, CFG>),
+        reinterpret_cast<const void*>(&oap_kmeans_lean_img<KS, WAVES, CFG, LIST>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_lean_img<KS, WAVES, CFG>), dim3(grid), dim3(WAVES * 64), L.total,
-                     s, a);
+  hipLaunchKernelGGL((oap_kmeans_lean_img<KS, WAVES, CFG, LIST>), dim3(grid), dim3(WAVES * 64),
+                     L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
+}
+
+template <int KS, int WAVES, int CFG>
+void launch_img(const ImgArgs& a, int grid, hipStream_t s) {
+  if constexpr ((CFG & ~1) == 0) {  // (row-list passes: the production configurations only)
+    if (a.rows) {
+      launch_img_l<KS, WAVES, CFG, true>(a, grid, s);
+      return;
+    }
+  } else {
+    OAP_CHECK(!a.rows, "kmeans_lean_img: row-list passes take configuration 0 or 1");
+  }
+  launch_img_l<KS, WAVES, CFG, false>(a, grid, s);
 }
 
 constexpr int kImgDefaultCfg = 1;  // pipelined chunk loop, operands one tile ahead
@@ -516,7 +584,90 @@ void launch_img_w(const ImgArgs& a, int grid, int cfg, hipStream_t s) {
   }
 }
 
+// ---------------------------------------------------------------- row-level bound scan
+// Lean workgroup b's rows, 1024 per step, one block per lean workgroup: the Hamerly test of
+// kmeans_lean_scan (kmeans_lloyd.hip) per ROW.  A pruned row keeps its label (the exact-fp32
+// argmin cannot change: its stored upper bound plus its center's drift stays below its lower
+// bound minus the largest drift, with the fp32 evaluation margin) and has its bounds advanced in
+// place, rounded outward; the other rows are appended in row order to b's segment (wave ballots
+// + one LDS prefix per step: deterministic, no atomics on the list).
+constexpr int kScanRowThreads = 1024;
+
+__global__ __launch_bounds__(kScanRowThreads) void oap_kmeans_lean_scan_rows(
+    int64_t n, int k, int d, int64_t tiles_per_block, float2* __restrict__ bounds,
+    const int32_t* __restrict__ labels, const float* __restrict__ xnorm,
+    const float* __restrict__ drift, const float* __restrict__ drift_max,
+    const float* __restrict__ cstat, int32_t* __restrict__ row_list,
+    unsigned* __restrict__ row_count, unsigned long long* __restrict__ pruned) {
+  constexpr int W = kScanRowThreads / 64;
+  __shared__ float dr[1024];
+  __shared__ unsigned wcnt[2][W];
+  __shared__ unsigned long long bpr;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int j = tid; j < k && j < 1024; j += kScanRowThreads) dr[j] = drift[j];
+  if (tid == 0) bpr = 0;
+  const float dmax = drift_max[0];
+  const float cmax = cstat[0];
+  const float mrel = 4e-7f * float(d + 8);
+  const int64_t span = tiles_per_block * 32;
+  const int64_t r0 = int64_t(blockIdx.x) * span;
+  const int64_t r1 = r0 + span < n ? r0 + span : n;
+  int32_t* seg = row_list + int64_t(blockIdx.x) * span;
+  unsigned base = 0;  // (block-uniform) entries written so far
+  unsigned long long npr = 0;
+  __syncthreads();
+  int par = 0;
+  for (int64_t c = r0; c < r1; c += kScanRowThreads, par ^= 1) {  // block-uniform trip count
+    const int64_t row = c + tid;
+    bool active = false;
+    if (row < r1) {
+      const float2 b = bounds[row];
+      const int lab = min(max(labels[row], 0), k - 1);
+      const float u = b.x + dr[lab];
+      const float lk = b.y - dmax;
+      const bool ok =
+          lk > 0.f && (lk - u) * (lk + u) > mrel * (xnorm[row >> 5] + cmax * cmax);
+      if (ok) {
+        ++npr;
+        if (dmax > 0.f) bounds[row] = make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f));
+      } else {
+        active = true;
+      }
+    }
+    const unsigned long long m = __ballot(active);
+    if (lane == 0) wcnt[par][wave] = static_cast<unsigned>(__popcll(m));
+    __syncthreads();  // (wcnt alternates by step parity: one barrier per step)
+    unsigned off = base, tot = 0;
+    for (int w = 0; w < W; ++w) {
+      const unsigned cw = wcnt[par][w];
+      off += w < wave ? cw : 0u;
+      tot += cw;
+    }
+    if (active) seg[off + lanes_below(m)] = static_cast<int32_t>(row);
+    base += tot;
+  }
+  if (npr) atomicAdd(&bpr, npr);
+  __syncthreads();
+  if (tid == 0) {
+    row_count[blockIdx.x] = base;
+    if (pruned && bpr) atomicAdd(pruned, bpr);
+  }
+}
+
 }  // namespace
+
+void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
+                           const int32_t* labels, const float* xnorm, const float* drift,
+                           const float* drift_max, const float* cstat, int32_t* row_list,
+                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s) {
+  OAP_CHECK(k <= 1024 && lean_grid >= 1, "kmeans_lean_scan_rows: k <= 1024");
+  if (n <= 0) return;
+  hipLaunchKernelGGL(oap_kmeans_lean_scan_rows, dim3(lean_grid), dim3(kScanRowThreads), 0, s, n, k,
+                     d, kmeans_lloyd_tiles_per_block(n, lean_grid),
+                     reinterpret_cast<float2*>(bounds), labels, xnorm, drift, drift_max, cstat,
+                     row_list, row_count, pruned_rows);
+  OAP_HIP_CHECK(hipGetLastError());
+}
 
 bool kmeans_lean_img_supported(int d, int k, int waves) {
   if (d + 4 > 128 || k < 1 || (waves != 12 && waves != 16)) return false;
@@ -533,7 +684,8 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
                 a.sums_too && a.defer_rows && a.defer_row_count && a.cstat && !a.xnorm &&
                 !a.cost_slab && !a.mindist && !a.centers_all && a.chunk_mode == 0 &&
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, waves) &&
-                a.ld == kmeans_ld(a.d, false) && (!a.tile_list || a.tile_count),
+                a.ld == kmeans_ld(a.d, false) && (!a.tile_list || a.tile_count) &&
+                (!a.img_rows || (a.img_row_count && !a.tile_list)),
             "kmeans_lean_img: unsupported arguments");
   if (a.n == 0) return;
   ImgArgs l;
@@ -553,6 +705,8 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.defer_rows = a.defer_rows;
   l.defer_row_count = a.defer_row_count;
   l.stat = a.deferred_rows;
+  l.rows = a.img_rows;
+  l.row_count = a.img_row_count;
   l.n = a.n;
   l.seg_cap = a.row_seg_cap;
   l.tiles_per_block = kmeans_lloyd_tiles_per_block(a.n, grid);

@@ -338,9 +338,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     const int64_t row = tile * 32 + r;
     load_row(row < a.n ? row : a.n - 1, dst);
   };
-  // image layout: [tile][k-step][lane][8 halves] — every load is one contiguous 1 KB per wave
+  // image layout: row-major [row][16 KS halves] (the MFMA B operand of each row: k-step s,
+  // half h at halves 16 s + 8 h) — a row is one 16 KS-half record, so a listed (gathered) row
+  // costs whole cache lines (kmeans_lean_img.hip's row-list passes)
   auto img_frag = [&](int64_t tile, int s) OAP_AI -> f16x8* {
-    return reinterpret_cast<f16x8*>(a.ximg) + (tile * KS + s) * 64 + lane;
+    return reinterpret_cast<f16x8*>(a.ximg) + (tile * 32 + r) * (2 * KS) + 2 * s + h;
   };
   auto load_img = [&](int64_t tile, f16x8 (&dst)[KS]) OAP_AI {
 #pragma unroll

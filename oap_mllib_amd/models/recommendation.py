@@ -2,8 +2,9 @@
 
 Mirrors the reference's shadow ``ALS`` (mllib-dal/src/main/scala/org/apache/spark-3.1.1/ml/
 recommendation/ALS.scala): Params and defaults (:241-245, blockSize :130), integer-id checks
-(``checkedCast``, :89-113), dispatch — accelerated iff ``implicitPrefs`` (:922-926; the
-reference's oneDAL path) — otherwise the vanilla Spark algorithm, ``ALSModel.transform`` with
+(``checkedCast``, :89-113), dispatch (the reference accelerates only ``implicitPrefs``,
+:922-926, and falls back to Spark's distributed ALS otherwise, :971-1114; here every
+configuration runs natively with the ratings sharded — see below), ``ALSModel.transform`` with
 ``coldStartStrategy`` nan/drop (:303-334), ``recommendForAll*`` / ``recommendFor*Subset``
 (:365-505) and persistence: metadata with an extra ``rank`` field plus ``userFactors`` /
 ``itemFactors`` parquet of (id: int, features: array<float>) (:522-553).
@@ -13,8 +14,13 @@ ALSDALImpl.cpp: id-owner alltoallv shuffle with dense re-indexing, replicated fp
 HBM, MFMA Gramian + allreduce, per-row normal equations + Cholesky on the GPU
 (kernels/als.hip), one allgather per half-iteration.
 
-Deviation (documented): ``implicitPrefs`` with ``nonnegative=True`` takes the vanilla NNLS path
-— the reference's oneDAL path silently ignored ``nonnegative``.
+Explicit feedback takes the same GPU kernels (``A = sum y y^T + lambda n I``, Spark's
+``computeFactors`` semantics, ALS.scala:1777-1795).  Ranks beyond the GPU kernels
+(``als_max_rank()``) and ``nonnegative=True`` run the driver's fp64 host solver over the same
+distributed shuffle (per-row Cholesky; Lawson-Hanson NNLS for non-negative factors — the
+minimiser Spark's NNLS converges to; the reference's oneDAL path silently ignored
+``nonnegative``).  Only the ``vanilla`` backend (no native library) runs the single-process
+numpy fallback.
 """
 from __future__ import annotations
 
@@ -146,13 +152,15 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
         u, i, r = self._ratings(dataset)
         rank = self.getOrDefault("rank")
         implicit = self.getOrDefault("implicitPrefs")
-        native_ok = implicit and not self.getOrDefault("nonnegative")
-        engine = choose_engine(native_ok, w)
-        if engine == "gpu" and rank > _loader.load().als_max_rank():
-            engine = "vanilla"
+        nonneg = self.getOrDefault("nonnegative")
+        # every configuration runs natively and distributed (ratings stay sharded): explicit and
+        # implicit feedback on the GPU kernels; ranks beyond them and non-negative factors
+        # (NNLS) on the fp64 host solver of the same driver, over the same world
+        engine = choose_engine(True, w)
+        host_solver = engine == "gpu" and (nonneg or rank > _loader.load().als_max_rank())
         seed = self.getOrDefault("seed") & 0xFFFFFFFFFFFFFFFF
         t0 = time.time()
-        extra: dict = {"engine": engine}
+        extra: dict = {"engine": engine, "host_solver": host_solver or engine == "cpu"}
         if engine == "vanilla":
             if w.distributed:  # the fallback is single-process: gather every rank's ratings
                 parts = w.allgather_obj((u, i, r))
@@ -167,7 +175,7 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
             N = _loader.load()
             ck = checkpoint.for_fit(w, self, (len(u),)) \
                 if self.getOrDefault("checkpointInterval") > 0 else None
-            out = self._fit_native(N, w, u, i, r, rank, implicit, seed, ck)
+            out = self._fit_native(N, w, u, i, r, rank, implicit, seed, ck, host_solver, nonneg)
             uid, uf = np.asarray(out["user_ids"]), np.asarray(out["user_factors"])
             iid, itf = np.asarray(out["item_ids"]), np.asarray(out["item_factors"])
             extra.update({k: out[k] for k in ("nnz", "setup_ms", "train_ms", "iter_ms", "gram_ms",
@@ -181,13 +189,15 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
         return model
 
 
-    def _fit_native(self, N, w, u, i, r, rank, implicit, seed, ck):
+    def _fit_native(self, N, w, u, i, r, rank, implicit, seed, ck, host_solver=False,
+                    nonneg=False):
         """Native fit; with a checkpointer, in checkpointInterval-sized segments that save
         (and resume from) the user factors."""
         max_iter = self.getOrDefault("maxIter")
         args = (self.getOrDefault("regParam"), self.getOrDefault("alpha"), implicit, seed)
+        kw = {"host_engine": host_solver, "nonnegative": nonneg}
         if ck is None:
-            return N.als_fit(w.ctx, w.comm, u, i, r, rank, max_iter, *args)
+            return N.als_fit(w.ctx, w.comm, u, i, r, rank, max_iter, *args, **kw)
         interval = self.getOrDefault("checkpointInterval")
         done, ids, fac = 0, None, None
         state = ck.load()
@@ -197,7 +207,7 @@ class ALS(_ALSParams, Estimator, DefaultParamsPersistence):
         out = None
         while out is None or done < max_iter:
             seg = min(interval, max_iter - done)
-            out = N.als_fit(w.ctx, w.comm, u, i, r, rank, max(seg, 0), *args, ids, fac)
+            out = N.als_fit(w.ctx, w.comm, u, i, r, rank, max(seg, 0), *args, ids, fac, **kw)
             done += max(seg, 0)
             ids = np.asarray(out["user_ids"])
             order = np.argsort(ids, kind="stable")

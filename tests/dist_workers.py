@@ -95,7 +95,8 @@ def pca_native(n=3000, d=12, k=4, seed=5, device="cpu", use_rccl=True, device_id
     return out
 
 
-def als_native(seed=3, device="cpu", use_rccl=True, rank=3, device_id=0):
+def als_native(seed=3, device="cpu", use_rccl=True, rank=3, device_id=0, implicit=True,
+               nonnegative=False):
     import oap_mllib_amd as O
     from test_als import gen_implicit
 
@@ -103,7 +104,10 @@ def als_native(seed=3, device="cpu", use_rccl=True, rank=3, device_id=0):
                                              device_id=device_id))
     tr, _ = gen_implicit(30, 50, 2, 0.01, seed)
     mine = {k: v[w.rank::w.size] for k, v in tr.items()}  # a strided (non-range) partition
-    m = O.ALS(rank=rank, maxIter=4, regParam=0.01, implicitPrefs=True, seed=0).fit(mine)
+    if w.distributed:  # the native path never gathers the ratings (only the vanilla one did)
+        w.allgather_obj = None
+    m = O.ALS(rank=rank, maxIter=4, regParam=0.01, implicitPrefs=implicit, seed=0,
+              nonnegative=nonnegative).fit(mine)
     out = {"engine": m.fit_info["engine"], "uid": m.userFactors["id"].tolist(),
            "uf": np.stack(m.userFactors["features"].to_list()).tolist(),
            "if": np.stack(m.itemFactors["features"].to_list()).tolist()}

@@ -96,7 +96,8 @@ def test_exact_rank1_explicit(world, request):
     # hash-keyed init the same target needs a few sweeps (parity of the init stream unpinned)
     for rank in (1, 2):
         m = _fit(tr, rank=rank, maxIter=5, regParam=1e-5)
-        assert m.fit_info["engine"] == "vanilla"  # explicit feedback is never accelerated
+        # explicit feedback runs natively (the reference fell back to Spark's ALS)
+        assert m.fit_info["engine"] == ("cpu" if world == "cpu_world" else "vanilla")
         assert _rmse(m, te, False) < 0.001
 
 
@@ -123,9 +124,10 @@ def test_native_cpu_equals_oracle(native):
     i = (rng.integers(0, 45, 900) * 3 + 5).astype(np.int32)
     r = rng.integers(-2, 6, 900).astype(np.float32)              # negatives and zeros
     ctx, comm = native.Context(-1, 1.0, 3), native.LocalComm()
-    for rank, alpha in ((1, 1.0), (4, 40.0), (17, 0.5)):
-        out = native.als_fit(ctx, comm, u, i, r, rank, 3, 0.05, alpha, True, 123)
-        ref = als_vanilla.fit(u, i, r, rank, 3, 0.05, True, alpha, False, 123)
+    for rank, alpha, implicit in ((1, 1.0, True), (4, 40.0, True), (17, 0.5, True),
+                                  (3, 1.0, False), (9, 1.0, False)):
+        out = native.als_fit(ctx, comm, u, i, r, rank, 3, 0.05, alpha, implicit, 123)
+        ref = als_vanilla.fit(u, i, r, rank, 3, 0.05, implicit, alpha, False, 123)
         assert np.array_equal(out["user_ids"], ref.user_ids)
         assert np.array_equal(out["item_ids"], ref.item_ids)
         np.testing.assert_allclose(out["user_factors"], ref.user_factors, rtol=1e-5, atol=1e-6)
@@ -191,11 +193,30 @@ def test_recommend_for_all(cpu_world):
     assert all(len(x) == len(I) for x in big["recommendations"])
 
 
-def test_nonnegative_takes_vanilla(cpu_world):
+def test_nonnegative_native_nnls(cpu_world):
+    """nonnegative=True runs the native host solver (Lawson-Hanson NNLS per row): factors are
+    non-negative and each user row is the NNLS minimiser of its normal equations against the
+    final item factors (scipy.optimize.nnls on the Cholesky form as the oracle)."""
+    from scipy.optimize import nnls
+
     tr, te = gen_explicit(10, 20, 2)
     m = _fit(tr, rank=2, maxIter=3, implicitPrefs=True, nonnegative=True)
-    assert m.fit_info["engine"] == "vanilla"
+    assert m.fit_info["engine"] == "cpu" and m.fit_info["host_solver"]
     assert np.all(np.stack(m.userFactors["features"].to_list()) >= 0)
+    reg, rank = 0.05, 4
+    m = _fit(tr, rank=rank, maxIter=4, regParam=reg, nonnegative=True)
+    U = dict(zip(m.userFactors["id"], np.stack(m.userFactors["features"].to_list())))
+    V = dict(zip(m.itemFactors["id"], np.stack(m.itemFactors["features"].to_list())))
+    assert min(f.min() for f in U.values()) >= 0 and min(f.min() for f in V.values()) >= 0
+    users, items, ratings = tr["user"], tr["item"], tr["rating"]
+    for uid in list(U)[:6]:
+        sel = users == uid
+        Y = np.stack([V[i] for i in items[sel]]).astype(np.float64)
+        M = Y.T @ Y + reg * sel.sum() * np.eye(rank)
+        c = Y.T @ ratings[sel].astype(np.float64)
+        L = np.linalg.cholesky(M)
+        x, _ = nnls(L.T, np.linalg.solve(L, c))
+        np.testing.assert_allclose(U[uid], x, rtol=2e-4, atol=2e-5)
 
 
 def test_read_write(tmp_path, cpu_world):
@@ -223,16 +244,20 @@ def test_read_write(tmp_path, cpu_world):
     assert os.path.isdir(tmp_path / "model" / "itemFactors")
 
 
-@pytest.mark.parametrize("nproc", [2, 3])
-def test_distributed_matches_single(nproc):
+@pytest.mark.parametrize("nproc,implicit,nonneg", [(2, True, False), (3, True, False),
+                                                   (2, False, False), (2, True, True)])
+def test_distributed_matches_single(nproc, implicit, nonneg):
+    """2-3 rank CPU worlds (explicit and non-negative fits included) equal the 1-rank fit; the
+    ratings stay sharded (the workers disable allgather_obj)."""
     from mp_util import run_world
 
     from dist_workers import als_native
 
-    rc, outs = run_world("dist_workers", "als_native", nproc=nproc, device="cpu")
+    rc, outs = run_world("dist_workers", "als_native", nproc=nproc, device="cpu",
+                         implicit=implicit, nonnegative=nonneg)
     assert rc == 0, outs
     O.shutdown_world()
-    ref = als_native(device="cpu")
+    ref = als_native(device="cpu", implicit=implicit, nonnegative=nonneg)
     O.shutdown_world()
     for o in outs:
         assert o["engine"] == "cpu"

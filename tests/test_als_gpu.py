@@ -181,3 +181,43 @@ def test_device_gram_eig_matches_numpy(native, gpu_world, r):
     np.testing.assert_allclose(np.sort(e[:r]), np.sort(np.linalg.eigvalsh(G)),
                                rtol=0, atol=1e-6 * np.max(np.abs(G)))
     assert np.all(e[r:] == 1.0) and np.all(Q[r:, r:] == np.eye(ld - r))
+
+
+def test_direct_split_fp16_rows_match_fp64_oracle(native, gpu_world):
+    """Rows of 129-4096 ratings (the direct solve on the split-fp16 hi + lo Gramian, both halves
+    of the iteration) stay within 1e-4 of the fp64 oracle, relative to the largest factor."""
+    rng = np.random.default_rng(11)
+    nu, ni, rank = 600, 900, 100
+    per = rng.integers(150, 700, nu)
+    u = np.repeat(np.arange(nu), per).astype(np.int32)
+    i = np.concatenate([rng.choice(ni, p, replace=False) for p in per]).astype(np.int32)
+    r = rng.integers(1, 6, len(u)).astype(np.float32)
+    cu, ci = np.bincount(u), np.bincount(i, minlength=ni)
+    assert cu.min() > 128 and cu.max() <= 4096 and ci.min() > 128 and ci.max() <= 4096
+    out = native.als_fit(gpu_world.ctx, gpu_world.comm, u, i, r, rank, 1, 0.05, 2.0, True, 7)
+    ref = als_vanilla.fit(u, i, r, rank, 1, 0.05, True, 2.0, False, 7)
+    assert out["failed_rows"] == 0
+    for key, rk in (("item_factors", ref.item_factors), ("user_factors", ref.user_factors)):
+        err = np.abs(out[key] - rk).max() / np.abs(rk).max()
+        print(f"{key}: max |gpu - fp64| / max |fp64| = {err:.2e}")
+        assert err <= 1e-4
+
+
+def test_every_configuration_runs_natively(native, gpu_world):
+    """Explicit feedback takes the GPU kernels; a rank beyond them and nonnegative=True take the
+    driver's fp64 host solver over the same world (equal to the CPU engine's fit)."""
+    u, i, r = _data(60, 40, 1200, 4)
+    data = {"user": u, "item": i, "rating": r}
+    m = O.ALS(rank=4, maxIter=2, regParam=0.1, seed=0).fit(data)
+    assert m.fit_info["engine"] == "gpu" and not m.fit_info["host_solver"]
+    big = native.als_max_rank() + 22
+    m = O.ALS(rank=big, maxIter=2, regParam=0.1, implicitPrefs=True, seed=0).fit(data)
+    assert m.fit_info["engine"] == "gpu" and m.fit_info["host_solver"]
+    ref = native.als_fit(native.Context(-1, 1.0, 4), native.LocalComm(), u, i, r, big, 2, 0.1,
+                         1.0, True, 0)
+    F = np.stack(m.userFactors["features"].to_list())
+    order = np.argsort(np.asarray(ref["user_ids"]))
+    np.testing.assert_allclose(F, np.asarray(ref["user_factors"])[order], rtol=1e-5, atol=1e-6)
+    m = O.ALS(rank=3, maxIter=2, regParam=0.1, nonnegative=True, seed=0).fit(data)
+    assert m.fit_info["host_solver"]
+    assert np.stack(m.userFactors["features"].to_list()).min() >= 0

@@ -79,3 +79,18 @@ def test_presets_match_baseline_configs(monkeypatch):
     with pytest.raises(SystemExit):
         b.main(["--config", "kmeans", "--rows", "1000", "--k", "7"])
     assert seen["rows"] == 1000 and seen["k"] == 7 and seen["dim"] == 50
+
+
+def test_cpu_baseline_proxies_report_rates():
+    """The CPU-proxy baselines (benchmarks/cpu_baseline.py) return labelled, positive rates."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    from cpu_baseline import kmeans_proxy, pca_proxy
+
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(20000, 8))
+    km = kmeans_proxy(X, X[:5].copy(), iters=2)
+    assert km["samples_per_sec"] > 0 and km["rows"] == 20000 and "proxy" in km["note"]
+    pc = pca_proxy(X, 3, full_rows=1_000_000)
+    assert pc["fit_s_scaled"] > 0 and pc["rows_scaled_to"] == 1_000_000
