@@ -110,6 +110,7 @@ void register_als(py::module_& m) {
         out["bcast_ms"] = r.bcast_ms;
         out["bcast_recv_bytes"] = r.bcast_recv_bytes;
         out["failed_rows"] = r.failed_rows;
+        out["eig_unconverged"] = r.eig_unconverged;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("users"), py::arg("items"), py::arg("ratings"),

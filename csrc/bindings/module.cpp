@@ -12,6 +12,7 @@
 
 #include "bindings/bindings.h"
 #include "comm/comm.h"
+#include "comm/tcp_comm.h"
 #include "drivers/kmeans.h"
 #include "kernels/kernels.h"
 #include "runtime/context.h"
@@ -322,6 +323,18 @@ PYBIND11_MODULE(_native, m) {
            }),
            py::arg("unique_id"), py::arg("world"), py::arg("rank"), py::arg("device"),
            py::arg("timeout_s") = 600.0);
+  // the KVS-rendezvous host comm (JNI / C ABI worlds), for tests of its collectives
+  py::class_<TcpComm, Comm, std::shared_ptr<TcpComm>>(m, "TcpComm")
+      .def(py::init([](const std::string& address, int world, int rank, double timeout) {
+             std::string ip;
+             int port = 0;
+             OAP_CHECK(parse_kvs_address(address, &ip, &port),
+                       "TcpComm: address must be ip_port or ip:port");
+             py::gil_scoped_release r;
+             return std::make_shared<TcpComm>(
+                 std::make_shared<TcpStore>(ip, port, world, rank, timeout));
+           }),
+           py::arg("address"), py::arg("world"), py::arg("rank"), py::arg("timeout_s") = 60.0);
   py::class_<HostComm, Comm, std::shared_ptr<HostComm>>(m, "HostComm")
       .def(py::init<py::object, int, int>(), py::arg("impl"), py::arg("rank"), py::arg("world"));
 

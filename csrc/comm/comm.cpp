@@ -137,7 +137,13 @@ void RcclComm::alltoallv(const void* send, const std::vector<size_t>& send_count
   // per peer): bounded transfers per send/recv pair and per group.  Both sides of a pair agree
   // on the counts, hence on the number of rounds; p2p ops match in order per pair, so ranks may
   // run different numbers of rounds.
-  constexpr size_t kChunk = size_t(1) << 28;  // 256 MiB
+  // (OAP_RCCL_A2A_CHUNK_BYTES overrides the 256 MiB round size: tests drive several rounds
+  // with small uneven counts)
+  const size_t kChunk = [] {  // (read per call: tests set it mid-process)
+    const char* e = std::getenv("OAP_RCCL_A2A_CHUNK_BYTES");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? size_t(v) : size_t(1) << 28;
+  }();
   const size_t chunk = std::max<size_t>(1, kChunk / es);
   size_t most = 0;
   for (int p = 0; p < world_; ++p) most = std::max({most, send_counts[p], recv_counts[p]});

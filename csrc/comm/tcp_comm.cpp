@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -266,59 +267,70 @@ void TcpComm::bcast(void* buf, size_t count, DType dt, int root, hipStream_t) {
 
 void TcpComm::alltoallv(const void* send, const std::vector<size_t>& send_counts, void* recv,
                         const std::vector<size_t>& recv_counts, DType dt, hipStream_t) {
+  // Star-routed, but streamed: for each source rank in order, rank 0 receives that source's
+  // segment for one destination at a time, in pieces of at most kPiece bytes, and forwards
+  // each piece before reading the next — rank 0 holds one piece, never the world's exchange.
+  // Every rank follows the same (source, destination) order, so the blocking sockets cannot
+  // deadlock; a rank's segment to itself never leaves the rank.
   const int P = size(), me = rank();
   OAP_CHECK(int(send_counts.size()) == P && int(recv_counts.size()) == P,
             "alltoallv: counts must have one entry per rank");
   const size_t es = dtype_size(dt);
-  std::vector<uint64_t> sc(send_counts.begin(), send_counts.end());
-  size_t stot = 0, rtot = 0;
-  for (auto c : send_counts) stot += c;
-  for (auto c : recv_counts) rtot += c;
-  if (P == 1) {
-    OAP_CHECK(stot == rtot, "alltoallv: world of one with mismatched counts");
-    if (stot) std::memmove(recv, send, stot * es);
-    return;
-  }
-  if (me != 0) {  // my counts + my whole send buffer to rank 0, then my routed receive buffer
-    store_->send_to(0, sc.data(), sc.size() * 8);
-    if (stot) store_->send_to(0, send, stot * es);
-    if (rtot) store_->recv_from(0, recv, rtot * es);
-    return;
-  }
-  // rank 0 routes: segment (src -> dst) at the src's prefix offset, dst buffers in src order
-  std::vector<std::vector<uint64_t>> cnt(P);
-  std::vector<std::vector<char>> data(P);
-  cnt[0] = sc;
-  for (int p = 1; p < P; ++p) {
-    cnt[p].resize(P);
-    store_->recv_from(p, cnt[p].data(), size_t(P) * 8);
-    size_t n = 0;
-    for (auto c : cnt[p]) n += c;
-    data[p].resize(n * es);
-    if (n) store_->recv_from(p, data[p].data(), n * es);
-  }
-  auto src_ptr = [&](int p) {
-    return p == 0 ? static_cast<const char*>(send) : data[p].data();
-  };
+  // (OAP_TCP_PIECE_BYTES overrides the 64 MiB forwarding piece: tests drive several pieces)
+  const size_t kPiece = [] {  // (read per call: tests set it mid-process)
+    const char* e = std::getenv("OAP_TCP_PIECE_BYTES");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? size_t(v) : size_t(64) << 20;
+  }();
+  std::vector<size_t> soff(P + 1, 0), roff(P + 1, 0);
   for (int q = 0; q < P; ++q) {
-    std::vector<char> outq;
-    char* dst = q == 0 ? static_cast<char*>(recv) : nullptr;
-    size_t need = 0;
-    for (int p = 0; p < P; ++p) need += cnt[p][q];
-    if (q == 0) {
-      OAP_CHECK(need == rtot, "alltoallv: receive counts disagree with the senders");
-    } else {
-      outq.resize(need * es);
-      dst = outq.data();
+    soff[q + 1] = soff[q] + send_counts[q];
+    roff[q + 1] = roff[q] + recv_counts[q];
+  }
+  const char* sb = static_cast<const char*>(send);
+  char* rb = static_cast<char*>(recv);
+  OAP_CHECK(send_counts[me] == recv_counts[me], "alltoallv: own segment counts disagree");
+  if (send_counts[me]) std::memmove(rb + roff[me] * es, sb + soff[me] * es, send_counts[me] * es);
+  if (P == 1) return;
+  // rank 0 learns every (source, destination) count (one small gather)
+  std::vector<uint64_t> mine(send_counts.begin(), send_counts.end());
+  std::vector<uint64_t> all;
+  if (me == 0) {
+    all.resize(size_t(P) * P);
+    std::copy(mine.begin(), mine.end(), all.begin());
+    for (int p = 1; p < P; ++p) store_->recv_from(p, all.data() + size_t(p) * P, size_t(P) * 8);
+  } else {
+    store_->send_to(0, mine.data(), size_t(P) * 8);
+  }
+  std::vector<char> piece;
+  for (int src = 0; src < P; ++src) {
+    if (me == 0) {
+      for (int q = 0; q < P; ++q) {
+        if (q == src) continue;
+        const size_t n = size_t(all[size_t(src) * P + q]) * es;
+        if (q == 0) {  // a peer's segment to rank 0
+          OAP_CHECK(n == recv_counts[src] * es, "alltoallv: receive counts disagree");
+          if (n) store_->recv_from(src, rb + roff[src] * es, n);
+          continue;
+        }
+        if (src == 0) {  // rank 0's own segment to a peer
+          if (n) store_->send_to(q, sb + soff[q] * es, n);
+          continue;
+        }
+        for (size_t done = 0; done < n;) {  // peer -> peer, piece by piece
+          const size_t m = std::min(kPiece, n - done);
+          piece.resize(m);
+          store_->recv_from(src, piece.data(), m);
+          store_->send_to(q, piece.data(), m);
+          done += m;
+        }
+      }
+    } else if (src == me) {  // my segments to every other rank, in destination order
+      for (int q = 0; q < P; ++q)
+        if (q != me && send_counts[q]) store_->send_to(0, sb + soff[q] * es, send_counts[q] * es);
+    } else if (recv_counts[src]) {  // the segment from src, through rank 0
+      store_->recv_from(0, rb + roff[src] * es, recv_counts[src] * es);
     }
-    size_t off = 0;
-    for (int p = 0; p < P; ++p) {
-      size_t soff = 0;
-      for (int j = 0; j < q; ++j) soff += cnt[p][j];
-      if (cnt[p][q]) std::memcpy(dst + off * es, src_ptr(p) + soff * es, cnt[p][q] * es);
-      off += cnt[p][q];
-    }
-    if (q != 0 && need) store_->send_to(q, outq.data(), need * es);
   }
 }
 

@@ -688,8 +688,10 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
         OAP_HIP_CHECK(hipStreamSynchronize(s));
       }
     }
-    Buffer ctr = ctx.alloc(64);
-    ctx.memset(ctr.data(), 0, 64);
+    // [0, 8): solve work queues (als.hip / als_lowrank.hip slots), [2] failed rows;
+    // [12]: Gramian eigensolves that missed the tolerance
+    Buffer ctr = ctx.alloc(128);
+    ctx.memset(ctr.data(), 0, 128);
     // low-rank path state: eigenbasis of the source Gramian, computed on the device
     // (kernels/als_eig.hip) straight from the allreduced fp64 Gramian — no host round trip
     Buffer lrQ = ctx.alloc(size_t(ld) * ld * 4), lrQT = ctx.alloc(size_t(ld) * ld * 4),
@@ -738,7 +740,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       for (const auto& o : dD.lro) lr_on = lr_on || o[4] > o[0];
       if (lr_on) {
         kern::als_gram_eig(gram64.as<double>(), r, ld, eig_scratch.as<double>(), lrQ.as<float>(),
-                           lrQT.as<float>(), lrEig.as<float>(), s);
+                           lrQT.as<float>(), lrEig.as<float>(), s, 30, 1e-14,
+                           ctr.as<unsigned long long>() + 12);
         if (!dS.rot.data()) dS.rot = ctx.alloc(std::max<size_t>(size_t(Src.n) * ld * 4, 256));
         kern::als_rotate(dS.f.as<float>(), nullptr, dS.rot.as<float>(), nullptr, Src.n,
                          lrQ.as<float>(), ld, cus, s);
@@ -843,6 +846,14 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     }
     unsigned long long fails = 0;
     ctx.copy_to_host(&fails, ctr.as<unsigned long long>() + 2, 8);
+    unsigned long long eig_uncv = 0;
+    ctx.copy_to_host(&eig_uncv, ctr.as<unsigned long long>() + 12, 8);
+    res.eig_unconverged = int64_t(eig_uncv);
+    if (eig_uncv && me == 0)
+      Logger::instance().log(LogLevel::Warn, "als/eig_unconverged",
+                             "\"solves\":" + std::to_string(eig_uncv) +
+                                 ",\"note\":\"Jacobi sweeps hit max_sweeps (30) above tol 1e-14; "
+                                 "low-rank solves used the last basis\"");
     res.failed_rows = int64_t(comm_allreduce_scalar(ctx, comm, double(fails), ReduceOp::Sum));
     // the result handoff (the reference copies each factor row into a Java array,
     // ALSDALImpl.cpp:500-576): pitched 2D copies drop the ld padding on the GPU side into pinned

@@ -56,6 +56,7 @@ struct AlsResult {
   double bcast_ms = 0.0;
   int64_t bcast_recv_bytes = 0;
   int64_t failed_rows = 0;                        // rows whose system was not SPD
+  int64_t eig_unconverged = 0;  // Gramian eigensolves that stopped at max_sweeps (low-rank path)
 };
 
 // users/items/ratings: this rank's share of the ratings (any partition).

@@ -37,7 +37,8 @@ __global__ __launch_bounds__(kEigThreads) void oap_als_jacobi_eig(const double* 
                                                                    float* __restrict__ Q,
                                                                    float* __restrict__ QT,
                                                                    float* __restrict__ eig,
-                                                                   int max_sweeps, double tol) {
+                                                                   int max_sweeps, double tol,
+                                                                   unsigned long long* status) {
   extern __shared__ double sm[];
   const int n = r + (r & 1), S = n + 1, np = n / 2;
   const int tid = threadIdx.x;
@@ -51,6 +52,7 @@ __global__ __launch_bounds__(kEigThreads) void oap_als_jacobi_eig(const double* 
     V[i * S + j] = i == j ? 1.0 : 0.0;
   }
   __syncthreads();
+  bool converged = false;
   for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     // convergence: off-diagonal vs total Frobenius mass
     double off = 0.0, tot = 0.0;
@@ -74,7 +76,10 @@ __global__ __launch_bounds__(kEigThreads) void oap_als_jacobi_eig(const double* 
       off += red[2 * w];
       tot += red[2 * w + 1];
     }
-    if (off <= tol * tol * tot) break;  // (uniform: every thread read the same partials)
+    if (off <= tol * tol * tot) {  // (uniform: every thread read the same partials)
+      converged = true;
+      break;
+    }
     __syncthreads();                     // red is rewritten next sweep
     for (int t = 0; t < n - 1; ++t) {
       if (tid < np) {  // rotation of pair tid: zeroes A[p][q] (sym.schur2)
@@ -122,6 +127,9 @@ __global__ __launch_bounds__(kEigThreads) void oap_als_jacobi_eig(const double* 
     QT[j * ld + k] = v;
   }
   for (int j = tid; j < ld; j += kEigThreads) eig[j] = j < r ? float(fmax(A[j * S + j], 0.0)) : 1.f;
+  // solves whose basis missed the tolerance within max_sweeps (the host reads it at its
+  // per-iteration sync and reports it)
+  if (tid == 0 && status && !converged) atomicAdd(status, 1ull);
 }
 
 size_t eig_lds_bytes(int r, bool vlds) {
@@ -137,7 +145,8 @@ size_t als_gram_eig_scratch_bytes(int r) {
 }
 
 void als_gram_eig(const double* gram, int r, int ld, double* scratch, float* Q, float* QT,
-                  float* eig, hipStream_t s, int max_sweeps, double tol) {
+                  float* eig, hipStream_t s, int max_sweeps, double tol,
+                  unsigned long long* status) {
   OAP_CHECK(r >= 1 && r <= 128 && ld >= r && ld <= 128, "als_gram_eig: r <= ld <= 128");
   const bool vlds = eig_lds_bytes(r, true) <= 160 * 1024;
   const size_t lds = eig_lds_bytes(r, vlds);
@@ -150,7 +159,7 @@ void als_gram_eig(const double* gram, int r, int ld, double* scratch, float* Q, 
       attr = true;
     }
     hipLaunchKernelGGL(oap_als_jacobi_eig<true>, dim3(1), dim3(kEigThreads), lds, s, gram, r, ld,
-                       nullptr, Q, QT, eig, max_sweeps, tol);
+                       nullptr, Q, QT, eig, max_sweeps, tol, status);
   } else {
     static bool attr = false;
     if (!attr) {
@@ -160,7 +169,7 @@ void als_gram_eig(const double* gram, int r, int ld, double* scratch, float* Q, 
       attr = true;
     }
     hipLaunchKernelGGL(oap_als_jacobi_eig<false>, dim3(1), dim3(kEigThreads), lds, s, gram, r,
-                       ld, scratch, Q, QT, eig, max_sweeps, tol);
+                       ld, scratch, Q, QT, eig, max_sweeps, tol, status);
   }
   OAP_HIP_CHECK(hipGetLastError());
 }

@@ -367,8 +367,10 @@ void als_absmax(const float* x, int64_t n, unsigned* out, hipStream_t s);
 // identity padding), eig: float [ld] (max(lambda, 0), padding 1).  scratch: device bytes of
 // als_gram_eig_scratch_bytes(r) (fp64 V when it does not fit in LDS next to A).
 size_t als_gram_eig_scratch_bytes(int r);
+// status (optional): incremented when the sweeps stop at max_sweeps short of the tolerance.
 void als_gram_eig(const double* gram, int r, int ld, double* scratch, float* Q, float* QT,
-                  float* eig, hipStream_t s, int max_sweeps = 30, double tol = 1e-14);
+                  float* eig, hipStream_t s, int max_sweeps = 30, double tol = 1e-14,
+                  unsigned long long* status = nullptr);
 
 // cov = (S - c c^T / n) / (n - 1) from pca_reduce's [S | c] output, on the device
 void pca_cov(const double* stats, int d, int64_t n, double* cov, hipStream_t s);

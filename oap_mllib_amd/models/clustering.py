@@ -259,16 +259,20 @@ def streamed_decision(w, X: np.ndarray, engine: str) -> bool:
     return streamed
 
 
+def hbm_budget(w) -> int:
+    """Bytes of rows a rank may keep resident (Config.hbm_budget_bytes; automatic: 60% of the
+    device memory)."""
+    budget = int(w.config.hbm_budget_bytes)
+    return budget if budget > 0 else int(0.6 * w.ctx.info["total_mem"])
+
+
 def _streamed(w, X: np.ndarray) -> bool:
     """K-Means rows of this rank exceed the HBM budget (Config.hbm_budget_bytes, automatic:
     60% of the device memory): stream them from host memory instead of uploading."""
     if X.ndim != 2 or w.config.storage_dtype != "f32":
         return False
-    budget = int(w.config.hbm_budget_bytes)
-    if budget <= 0:
-        budget = int(0.6 * w.ctx.info["total_mem"])
     ld = (X.shape[1] + 3) // 4 * 4
-    return X.shape[0] * ld * 4 > budget
+    return X.shape[0] * ld * 4 > hbm_budget(w)
 
 
 def upload_table(w, X: np.ndarray, layout: str = "kmeans"):
@@ -280,7 +284,9 @@ def upload_table(w, X: np.ndarray, layout: str = "kmeans"):
         st = w.config.storage_dtype
         if layout == "kmeans":
             ld = N.kmeans_ld(d, st)
-        elif layout == "pca_exact" and X.dtype == np.float64:
+        elif layout == "pca_exact" and X.dtype == np.float64 and X.nbytes <= hbm_budget(w):
+            # (f64 rows take twice the HBM of f32 ones; beyond the budget the rows go up as
+            # f32 and the exact kernel still forms fp64 products of them)
             st, ld = "f64", d
         else:
             st, ld = "f32", d  # PCA reads f32 rows

@@ -77,10 +77,12 @@ class PCA(_PCAParams, Estimator, DefaultParamsPersistence):
 
             N = _loader.load()
             exact = w.config.pca_precision != "fast"
-            # f32 rows whatever storage_dtype says; exact mode keeps f64 input rows f64
+            # f32 rows whatever storage_dtype says; exact mode keeps f64 input rows f64 while
+            # they fit the HBM budget (upload_table), else uploads them as f32
             table = upload_table(w, X, layout="pca_exact" if exact else "pca")
             r = N.pca_fit(w.ctx, w.comm, table, k, False, exact=exact)
             extra["precision"] = "exact" if exact else "fast"
+            extra["device_rows_dtype"] = table.dtype
             pc, ev = np.asarray(r["pc"]), np.asarray(r["explained_variance"])
             extra.update({k_: r[k_] for k_ in ("stats_ms", "allreduce_ms", "eig_ms", "total_ms")})
         model = PCAModel(uid=self.uid, pc=DenseMatrix.from_array(pc),

@@ -113,3 +113,35 @@ def als_native(seed=3, device="cpu", use_rccl=True, rank=3, device_id=0, implici
            "if": np.stack(m.itemFactors["features"].to_list()).tolist()}
     O.shutdown_world()
     return out
+
+
+def tcp_alltoallv(port, piece=0):
+    """Uneven alltoallv / allreduce / allgather over the KVS TcpComm (streamed star routing);
+    piece > 0 forces several forwarding pieces per segment."""
+    import numpy as np
+
+    from oap_mllib_amd import _loader
+
+    if piece:
+        os.environ["OAP_TCP_PIECE_BYTES"] = str(piece)
+    N = _loader.load()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    comm = N.TcpComm(f"127.0.0.1_{port}", world, rank, 60.0)
+    ctx = N.Context(-1, 0.5, 1)
+
+    def cnt(p, q):  # elements p sends q (uneven, some empty)
+        return 0 if (p + q) % 4 == 3 else (p + 1) * (q + 2) * 7 + (5 if p == q else 0)
+
+    def seg(p, q):
+        return p * 1e6 + q * 1e3 + np.arange(cnt(p, q), dtype=np.float64)
+
+    send = [cnt(rank, q) for q in range(world)]
+    recv = [cnt(p, rank) for p in range(world)]
+    data = np.concatenate([seg(rank, q) for q in range(world)])
+    out = comm.exchange_f64(ctx, "alltoallv", data, send, recv)
+    want = np.concatenate([seg(p, rank) for p in range(world)])
+    red = comm.exchange_f64(ctx, "allreduce", np.full(5, float(rank + 1)))
+    gat = comm.exchange_f64(ctx, "allgather", np.array([float(rank)]))
+    return {"a2a": bool(np.array_equal(out, want)),
+            "allreduce": bool(np.all(red == world * (world + 1) / 2)),
+            "allgather": gat.tolist() == [float(p) for p in range(world)]}

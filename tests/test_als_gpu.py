@@ -153,6 +153,7 @@ def test_lowrank_path_matches_direct_and_oracle(native, gpu_world, monkeypatch, 
     args = (u, i, r, rank, 2, 0.05, 8.0, True, 4)
     monkeypatch.setenv("OAP_ALS_LOWRANK", "1")
     lr = native.als_fit(gpu_world.ctx, gpu_world.comm, *args)
+    assert lr["eig_unconverged"] == 0  # the device Jacobi met its tolerance every time
     monkeypatch.setenv("OAP_ALS_LOWRANK", "0")
     direct = native.als_fit(gpu_world.ctx, gpu_world.comm, *args)
     monkeypatch.delenv("OAP_ALS_LOWRANK")

@@ -46,6 +46,19 @@ def test_rccl_one_rank_collectives(rccl1_world):
     assert w.comm.name == "rccl" and not w.comm.trivial
 
 
+def test_rccl_chunked_alltoallv_rounds(rccl1_world, monkeypatch):
+    """The multi-round path of RcclComm::alltoallv (segments above the round size move in
+    several grouped send/recv rounds, offsets advancing per round): a 24-byte round size makes
+    a 1000-element exchange take 334 rounds; equal to the single-round result."""
+    w = rccl1_world
+    a = np.random.default_rng(3).normal(size=1000)
+    one = w.comm.exchange_f64(w.ctx, "alltoallv", a, send_counts=[1000], recv_counts=[1000])
+    monkeypatch.setenv("OAP_RCCL_A2A_CHUNK_BYTES", "24")
+    many = w.comm.exchange_f64(w.ctx, "alltoallv", a, send_counts=[1000], recv_counts=[1000])
+    np.testing.assert_array_equal(one, a)
+    np.testing.assert_array_equal(many, a)
+
+
 def test_local_comm_is_trivial(gpu_world):
     assert gpu_world.comm.trivial and gpu_world.comm.name == "local"
 

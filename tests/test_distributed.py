@@ -65,3 +65,20 @@ def test_fault_injection_no_hang():
     rc, _ = run_world("dist_workers", "fault_injection", nproc=2, timeout=120,
                       env={"OAP_MLLIB_FAULT": "1:kmeans_iter:0"})
     assert rc not in (0, 124), rc
+
+
+@pytest.mark.parametrize("nproc,piece", [(3, 0), (4, 64), (2, 40)])
+def test_tcp_comm_streamed_alltoallv(nproc, piece):
+    """The KVS TcpComm (JNI / C ABI worlds) routes alltoallv through rank 0 one bounded piece at
+    a time (never the world's whole exchange): uneven and empty segments, 2-4 ranks, pieces of
+    a few elements, plus allreduce / allgather on the same sockets."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    rc, outs = run_world("dist_workers", "tcp_alltoallv", nproc=nproc, port=port, piece=piece)
+    assert rc == 0, outs
+    for o in outs:
+        assert o == {"a2a": True, "allreduce": True, "allgather": True}, outs

@@ -157,3 +157,24 @@ def test_exact_with_bf16_storage_config(gpu_world):
         assert m.fit_info["engine"] == "gpu"
     finally:
         O.set_config(O.get_config().replace(storage_dtype="f32"))
+
+
+def test_exact_f64_rows_beyond_budget_go_up_as_f32(gpu_world):
+    """f64 input rows take twice the HBM: within the budget they stay f64 on the device, beyond
+    it (Config.hbm_budget_bytes) they are uploaded as f32 and the exact kernel still forms fp64
+    products of them (the covariance of the f32-rounded rows, to fp64 accuracy)."""
+    rng = np.random.default_rng(21)
+    X = rng.normal(size=(8000, 32)) * np.geomspace(4, 0.3, 32) + 1.0
+    m = O.PCA(k=3, inputCol="features").fit(X)
+    assert m.fit_info["device_rows_dtype"] == "f64"
+    O.set_config(O.get_config().replace(hbm_budget_bytes=X.nbytes // 2))
+    try:
+        O.shutdown_world()
+        O.init_world(O.get_config().replace(device="gpu", device_id=0))
+        f = O.PCA(k=3, inputCol="features").fit(X)
+        assert f.fit_info["device_rows_dtype"] == "f32" and f.fit_info["precision"] == "exact"
+        X32 = X.astype(np.float32).astype(np.float64)
+        wr = np.sort(np.linalg.eigvalsh(np.cov(X32.T, ddof=1)))[::-1]
+        np.testing.assert_allclose(f.explainedVariance.toArray(), wr[:3] / wr.sum(), rtol=1e-10)
+    finally:
+        O.set_config(O.get_config().replace(hbm_budget_bytes=0))
