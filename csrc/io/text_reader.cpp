@@ -52,7 +52,9 @@ std::vector<size_t> line_ranges(const Mapped& m, int parts) {
   for (int t = 1; t < parts; ++t) {
     size_t pos = m.n * t / parts;
     if (pos < cut[t - 1]) pos = cut[t - 1];
-    while (pos < m.n && m.p[pos - 1] != '\n') ++pos;
+    // (pos 0 is a line start: a file shorter than the thread count puts early cuts there —
+    // reading m.p[-1] would touch the page before the mapping)
+    while (pos > 0 && pos < m.n && m.p[pos - 1] != '\n') ++pos;
     cut[t] = pos;
   }
   return cut;

@@ -118,6 +118,16 @@ static void test_readers(const std::string& dir) {
   }
   oap::RatingsText r = oap::read_ratings(rat, "::", pool);
   EXPECT(r.users.size() == 100 && r.items[10] == 11 && r.ratings[8] == 2.0f);
+  // files shorter than the thread count: early line cuts fall on byte 0 (the splitter must not
+  // read the byte before the mapping — ASan catches it here)
+  oap::ThreadPool wide(8);
+  const std::string tiny = dir + "/tiny.csv";
+  {
+    std::ofstream f(tiny);
+    f << "1,2\n";
+  }
+  oap::DenseText tt = oap::read_csv_dense(tiny, ',', wide);
+  EXPECT(tt.rows == 1 && tt.cols == 2 && tt.values[1] == 2.0);
   bool threw = false;
   try {
     oap::read_csv_dense(dir + "/does-not-exist.csv", ',', pool);
