@@ -975,10 +975,14 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   if (!Xh.empty() || !Yh.empty()) {  // (host engine: repack [n][ld] -> [n][r] on the pool)
     res.user_factors = HostArray<float>::alloc(size_t(U.n) * r);
     res.item_factors = HostArray<float>::alloc(size_t(I.n) * r);
-    ctx.download_rows(res.user_factors.data(), size_t(r) * 4, Xh.data(), size_t(ld) * 4,
-                      size_t(r) * 4, U.n);
-    ctx.download_rows(res.item_factors.data(), size_t(r) * 4, Yh.data(), size_t(ld) * 4,
-                      size_t(r) * 4, I.n);
+    auto repack = [&](float* dst, const std::vector<float>& src, int64_t rows) {
+      ctx.pool().parallel_for(rows, [&](int, int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i)
+          std::memcpy(dst + size_t(i) * r, src.data() + size_t(i) * ld, size_t(r) * 4);
+      });
+    };
+    repack(res.user_factors.data(), Xh, U.n);
+    repack(res.item_factors.data(), Yh, I.n);
   }
   if (me == 0 && Logger::instance().level() <= LogLevel::Info)
     Logger::instance().log(LogLevel::Info, "als/fit",

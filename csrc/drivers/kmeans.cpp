@@ -1379,8 +1379,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   u64 pruned_seen = 0;
 
   kern::KMeansFinalizeArgs fa;
-  fa.sums = sums;
-  fa.counts = counts;
+  // a single-rank delta fit finalizes straight from its local statistics (no copy into the
+  // allreduce buffer: there is no allreduce)
+  const bool fin_direct = delta && comm.trivial();
+  u64* const fin_counts = fin_direct ? loc_b.as<u64>() + kd : counts;
+  fa.sums = fin_direct ? loc_b.as<u64>() : sums;
+  fa.counts = fin_counts;
   fa.inv_scale = inv_scale.as<double>();
   fa.centers64 = c64.as<double>();
   fa.centers32 = g.c32.as<float>();
@@ -1516,15 +1520,19 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                      hipMemcpyDeviceToDevice, s));
       if (req.xnorm && !req.tile_list) xnorm_ready = true;
       if (delta) {
-        OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
-                                     hipMemcpyDeviceToDevice, s));
-        OAP_HIP_CHECK(hipMemcpyAsync(cbak_b.data(), g.c32.data(),
-                                     sizeof(float) * size_t(g.kpad) * g.dp,
-                                     hipMemcpyDeviceToDevice, s));
+        if (!fin_direct)
+          OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
+                                       hipMemcpyDeviceToDevice, s));
+        // the centers this iteration assigned against, for the final exact-cost pass — only
+        // when it may follow this iteration (a convergence test, or the last iteration)
+        if (p.tol >= 0 || it == p.max_iter - 1)
+          OAP_HIP_CHECK(hipMemcpyAsync(cbak_b.data(), g.c32.data(),
+                                       sizeof(float) * size_t(g.kpad) * g.dp,
+                                       hipMemcpyDeviceToDevice, s));
       }
       if (nb > 0)
         kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
-      else
+      else if (cost_it || !comm.trivial())  // (a costless iteration's cost is not reported)
         OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
       ev[b].e1.record(s);
       if (!comm.trivial()) {
@@ -1546,7 +1554,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       roctx_pop();
     }
     OAP_HIP_CHECK(
-        hipMemcpyAsync(counts_h.data(), counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
+        hipMemcpyAsync(counts_h.data(), fin_counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
     if (ldstat_b.data())
