@@ -10,6 +10,7 @@
 
 #include "bindings/bindings.h"
 #include "drivers/als.h"
+#include "drivers/recommend.h"
 #include "kernels/kernels.h"
 
 namespace py = pybind11;
@@ -119,4 +120,35 @@ void register_als(py::module_& m) {
       py::arg("init_ids") = py::none(), py::arg("init_factors") = py::none(),
       py::arg("host_engine") = false, py::arg("nonnegative") = false);
   m.def("als_max_rank", &kern::als_max_rank);
+  // recommendForAll*: fused score + top-k (kernels/als_recommend.hip); no score matrix stored
+  m.def("als_recommend_max_num", &als_recommend_max_num);
+  m.def(
+      "als_recommend",
+      [](std::shared_ptr<Context> ctx,
+         py::array_t<float, py::array::c_style | py::array::forcecast> src,
+         py::array_t<float, py::array::c_style | py::array::forcecast> dst, int num,
+         int64_t slab_rows) {
+        if (src.ndim() != 2 || dst.ndim() != 2 || src.shape(1) != dst.shape(1))
+          throw ConfigError("als_recommend: src [n, rank] and dst [m, rank] needed");
+        const int64_t n = src.shape(0), m = dst.shape(0);
+        const int rank = int(src.shape(1));
+        py::array_t<int32_t> idx({n, int64_t(num)});
+        py::array_t<float> val({n, int64_t(num)});
+        RecTiming t;
+        {
+          py::gil_scoped_release rel;
+          als_recommend(*ctx, src.data(), n, dst.data(), m, rank, num, idx.mutable_data(),
+                        val.mutable_data(), slab_rows, &t);
+        }
+        py::dict info;
+        info["pack_dst_s"] = t.pack_dst_s;
+        info["upload_s"] = t.upload_s;
+        info["topk_s"] = t.topk_s;
+        info["download_s"] = t.download_s;
+        info["wall_s"] = t.wall_s;
+        info["slabs"] = t.slabs;
+        info["slab_rows"] = t.slab_rows;
+        return py::make_tuple(idx, val, info);
+      },
+      py::arg("ctx"), py::arg("src"), py::arg("dst"), py::arg("num"), py::arg("slab_rows") = 0);
 }

@@ -264,6 +264,10 @@ struct AssignReq {
   // image passes after a row-level scan (kmeans_lean_scan_rows): the rows it could not prune
   const int32_t* img_rows = nullptr;
   const unsigned* img_row_count = nullptr;
+  // image passes with the row scan fused into the image kernel (KMeansAssignArgs::img_scan_*)
+  const float* img_scan_xnorm = nullptr;
+  const float* img_scan_drift = nullptr;
+  u64* img_scan_pruned = nullptr;
 };
 
 // The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
@@ -279,6 +283,17 @@ int img_cfg_default() {
   static const int c = [] {
     const char* e = std::getenv("OAP_KMEANS_IMG_CFG");
     return e ? std::atoi(e) : -1;
+  }();
+  return c;
+}
+
+// configuration of the fused row-scan passes (OAP_KMEANS_SCAN_CFG): 0, the chunk loop without
+// software pipelining — the scan's prefetched bounds fit its registers (105 VGPRs, no spill)
+// where the pipelined loop would spill 64 B per lane (r4h: 4.66 vs 5.14 ms/step)
+int scan_cfg_default() {
+  static const int c = [] {
+    const char* e = std::getenv("OAP_KMEANS_SCAN_CFG");
+    return e ? std::atoi(e) : 0;
   }();
   return c;
 }
@@ -394,6 +409,9 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.img_mode = req.img_mode;
     a.img_rows = req.img_mode == 2 ? req.img_rows : nullptr;
     a.img_row_count = req.img_mode == 2 ? req.img_row_count : nullptr;
+    a.img_scan_xnorm = req.img_mode == 2 ? req.img_scan_xnorm : nullptr;
+    a.img_scan_drift = req.img_mode == 2 ? req.img_scan_drift : nullptr;
+    a.img_scan_pruned = req.img_mode == 2 ? req.img_scan_pruned : nullptr;
     if (req.delta) {  // delta accumulation; over the scan's tile list when there is one
       OAP_CHECK(req.labels && req.labels_valid,
                 "kmeans delta accumulation needs the previous iteration's labels");
@@ -413,18 +431,23 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     const bool img_k = req.img_kernel >= 0 ? req.img_kernel == 1 : img_kernel_default();
     // (variants 3 / 10 have no image branch: their img_mode 3 would not be a fallback only)
     if (req.img_mode == 2 && img_k && lv != 3 && lv != 10 &&
-        kern::kmeans_lean_img_supported(x.cols, g.k, lw)) {
-      kern::kmeans_lean_img(a, grid, lw, req.img_cfg >= 0 ? req.img_cfg : img_cfg_default(), s);
+        kern::kmeans_lean_img_supported(x.cols, g.k, lw, a.img_scan_xnorm != nullptr)) {
+      const int cfg = req.img_cfg >= 0                         ? req.img_cfg
+                      : a.img_scan_xnorm && scan_cfg_default() >= 0 ? scan_cfg_default()
+                                                                    : img_cfg_default();
+      kern::kmeans_lean_img(a, grid, lw, cfg, s);
       if (req.img_fallback) {
         kern::KMeansAssignArgs f = a;
         f.img_mode = 3;
         kern::kmeans_lloyd(f, grid, lv, s);
       }
-      t_assign_path = a.img_rows       ? "lean_img_kernel_delta_rowscan"
-                      : req.tile_list ? "lean_img_kernel_delta_scan"
-                                      : "lean_img_kernel_delta";
+      t_assign_path = a.img_scan_xnorm ? "lean_img_kernel_delta_fused_rowscan"
+                      : a.img_rows     ? "lean_img_kernel_delta_rowscan"
+                      : req.tile_list  ? "lean_img_kernel_delta_scan"
+                                       : "lean_img_kernel_delta";
     } else {
-      OAP_CHECK(!a.img_rows, "kmeans: a row-list image pass needs the image kernel");
+      OAP_CHECK(!a.img_rows && !a.img_scan_xnorm,
+                "kmeans: a row-list / row-scan image pass needs the image kernel");
       kern::kmeans_lloyd(a, grid, lv, s);
     }
     if (req.skip_exact) return 0;
@@ -442,6 +465,9 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.xnorm = nullptr;
     b.img_rows = nullptr;
     b.img_row_count = nullptr;
+    b.img_scan_xnorm = nullptr;
+    b.img_scan_drift = nullptr;
+    b.img_scan_pruned = nullptr;
     b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
     kern::kmeans_exact_rows(b, grid, s);
     return a.cost_slab ? 2 * grid : 0;
@@ -1299,19 +1325,18 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // 32-row tiles; the image kernel then gathers only the rows it could not prune.  On overlapping
   // clusters a tile almost always holds a row near a boundary, while most rows are far from one
   // (headline data: tiles 0-13% prunable, rows up to 93%: profiles/r4/row_prune_potential.jsonl).
-  // Bounds are then written by every pass.  OAP_KMEANS_ROW_SCAN=0 keeps the tile scan.
+  // Bounds are then written by every pass.  The scan runs inside the image kernel (each wave
+  // tests its own rows and queues the unpruned ones in LDS) where the kernel's LDS plan has room
+  // for it; OAP_KMEANS_ROW_SCAN=2 takes the separate scan kernel + row list through HBM instead,
+  // =0 the tile scan.
   Buffer rlist_b, rpruned_b;
   const char* rs_env = std::getenv("OAP_KMEANS_ROW_SCAN");
   const bool row_scan = scan && !chunked && !(rs_env && *rs_env == '0');
+  bool row_scan_fused = row_scan && !(rs_env && *rs_env == '2');
   if (row_scan) {
-    rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
-                        sizeof(unsigned) * size_t(lgrid) + 64);
     rpruned_b = ctx.alloc(sizeof(u64));
     ctx.memset(rpruned_b.data(), 0, sizeof(u64), s);
   }
-  unsigned* rcount = row_scan ? reinterpret_cast<unsigned*>(rlist_b.as<int32_t>() +
-                                                            size_t(lgrid) * size_t(ltiles) * 32)
-                              : nullptr;
   unsigned* dcount =
       scan ? reinterpret_cast<unsigned*>(dlist_b.as<int32_t>() + size_t(lgrid) * size_t(ltiles))
            : nullptr;
@@ -1357,9 +1382,18 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   bool row_scan_ok = false;
   if (row_scan && img_b.data() && img_kernel_default()) {
     const int lv = lean_variant(d, g.kpad);
-    row_scan_ok = lv != 3 && lv != 10 &&
-                  kern::kmeans_lean_img_supported(d, k, kern::kmeans_lloyd_waves(lv));
+    const int lw = kern::kmeans_lloyd_waves(lv);
+    row_scan_ok = lv != 3 && lv != 10 && kern::kmeans_lean_img_supported(d, k, lw);
+    row_scan_fused =
+        row_scan_fused && row_scan_ok && kern::kmeans_lean_img_supported(d, k, lw, true);
   }
+  if (row_scan_ok && !row_scan_fused)
+    rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
+                        sizeof(unsigned) * size_t(lgrid) + 64);
+  unsigned* rcount =
+      rlist_b.data()
+          ? reinterpret_cast<unsigned*>(rlist_b.as<int32_t>() + size_t(lgrid) * size_t(ltiles) * 32)
+          : nullptr;
   // with the adaptive scan off, full passes write the per-row bounds (8 B/row) only where a
   // following iteration may scan, and the per-tile max |x|^2 (constant) once
   float* const bounds_full = req.bounds;
@@ -1494,7 +1528,15 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                req.fast1 && !req.tile_list;
       req.img_rows = nullptr;
       req.img_row_count = nullptr;
-      if (row_scan_it) {
+      req.img_scan_xnorm = nullptr;
+      req.img_scan_drift = nullptr;
+      req.img_scan_pruned = nullptr;
+      if (row_scan_it && row_scan_fused) {
+        OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
+        req.img_scan_xnorm = xnorm_full;
+        req.img_scan_drift = drift_b.as<float>();
+        req.img_scan_pruned = rpruned_b.as<u64>();
+      } else if (row_scan_it) {
         OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
         kern::kmeans_lean_scan_rows(x.rows, k, d, lgrid, bounds_full, req.labels, xnorm_full,
                                     drift_b.as<float>(), drift_b.as<float>() + k,

@@ -115,6 +115,13 @@ struct KMeansAssignArgs {
   // in row order, count [grid] (kmeans_lean_scan_rows)
   const int32_t* img_rows = nullptr;
   const unsigned* img_row_count = nullptr;
+  // Row-scan image pass (kmeans_lean_img, fused): the kernel applies the row scan's Hamerly test
+  // to every row itself and runs only the rows it cannot prune.  img_scan_xnorm: per-tile max
+  // |x|^2 (set: the fused scan is on); img_scan_drift: the centers' drift [k] and its maximum at
+  // [k]; img_scan_pruned (optional): counter of pruned rows.
+  const float* img_scan_xnorm = nullptr;
+  const float* img_scan_drift = nullptr;
+  unsigned long long* img_scan_pruned = nullptr;
   int64_t row_seg_cap = 0;
   int row_subs = 1;  // sub-segments per workgroup segment (each row_seg_cap / row_subs long)
   // Lean tier-1 kernel output: rows whose tier-1 top-2 gap is inside the tier's error bound are
@@ -172,7 +179,7 @@ size_t kmeans_lloyd_image_bytes(int64_t n, int d);
 // img_mode 2).  `waves` must be the lean variant's (kmeans_lloyd_waves: the deferral
 // sub-segments), cfg < 0 the default configuration.  When the image's scale cannot hold the
 // current centers the kernel does nothing; kmeans_lloyd with img_mode 3 then runs the pass.
-bool kmeans_lean_img_supported(int d, int k, int waves);
+bool kmeans_lean_img_supported(int d, int k, int waves, bool scan = false);
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s);
 // Row-level bound scan for the image passes: every row of lean workgroup b's range gets the
 // Hamerly test of kmeans_lean_scan (u + drift[label] against l - max drift, with the tile's

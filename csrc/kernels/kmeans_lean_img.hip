@@ -19,7 +19,11 @@
 //   chunk c's epilogue, into a second accumulator, so the matrix pipe works under the wave's
 //   own VALU as well as under the other waves';
 // * the last chunk folds only its real centroid groups (k = 200: 4 of 16 keys per lane);
-// * labels are stored only for rows that moved (the others already hold theirs).
+// * labels are stored only for rows that moved (the others already hold theirs);
+// * row-scan passes (RM 2) test every row's Hamerly bounds in the kernel itself: each wave scans
+//   its own tiles two at a time, advances the pruned rows' bounds in place and queues the others
+//   in a per-wave LDS ring, from which it forms 32-row tiles — no separate scan kernel, no row
+//   list through HBM, and a pass that prunes nothing costs one 8-byte bound read per row.
 // When the plane at the image's scale is not representable (beta max|c| > 2^9) the kernel does
 // nothing and oap_kmeans_lloyd_t1 (img_mode 3) runs the f32-row pass instead: both test the same
 // device values, so exactly one of them runs.
@@ -44,6 +48,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 constexpr float kBias = 16.f;  // the bias features' unit (kmeans_lloyd.hip kBiasUnit)
 constexpr int kMv = 64;        // per-wave LDS slots of staged moved rows
+constexpr int kRing = 128;     // per-wave LDS ring of unpruned rows (row-scan passes)
 
 struct ImgArgs {
   const f16x8* img;  // row-major [32 tiles][2 KS] fragments (k-step s, half h at 2 s + h)
@@ -64,17 +69,22 @@ struct ImgArgs {
   u64* stat;  // optional [deferred rows, moved rows, image passes]
   const int32_t* rows;  // row-list passes: [grid][32 tiles_per_block] rows in order, count [grid]
   const unsigned* row_count;
+  // row-scan passes: per-tile max |x|^2 (global tile index), the centers' drift [k] and its
+  // maximum at [k], and the counter of pruned rows
+  const float* scan_xnorm;
+  const float* drift;
+  u64* pruned;
   int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
 };
 
 struct ImgSmem {
-  size_t plane, sc, acc, cnt, mv, total;
+  size_t plane, sc, acc, cnt, mv, dr, ring, total;
 };
 
 // fp16 plane; fixed-point accumulator rows of DP + 1 doubles (odd: conflict-free ds_add_f64; the
 // padded features add zeros into their own columns, so the moved-row adds need no predicate)
-__host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves) {
+__host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, bool scan) {
   ImgSmem m;
   size_t off = 0;
   m.plane = 0;
@@ -87,6 +97,10 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves) 
   off = round16(off + size_t(k) * 4);
   m.mv = off;
   off += size_t(waves) * kMv * 8;
+  m.dr = off;  // (row-scan passes: the drift, then the rings)
+  off = scan ? round16(off + size_t(k) * 4) : off;
+  m.ring = off;
+  off += scan ? size_t(waves) * kRing * 4 : 0;
   m.total = round16(off);
   return m;
 }
@@ -110,10 +124,12 @@ __device__ inline void split_h(float v, _Float16& hi, _Float16& lo) {
 // CFG: bit 0 software-pipelined chunk loop; bit 1 operands two tiles ahead (else one); bits 2+
 // timing ablations (probe builds only): 4 no epilogue, 8 no MFMA, 16 no plane reads, 32 no image
 // loads, 64 no moved-row accumulation, 128 no per-row stores.
-// LIST: the tiles are 32 consecutive entries of this workgroup's row list (the rows the row
-// scan could not prune), gathered from the row-major image; else 32 consecutive rows.
-template <int KS, int WAVES, int CFG, bool LIST>
+// RM (row mode): 0 dense tiles of 32 consecutive rows; 1 (LIST) 32 consecutive entries of this
+// workgroup's row list (the rows kmeans_lean_scan_rows could not prune), gathered from the
+// row-major image; 2 (SCAN) the fused row scan: 32 consecutive entries of the wave's LDS ring.
+template <int KS, int WAVES, int CFG, int RM>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) {
+  constexpr bool LIST = RM == 1, SCAN = RM == 2;
   constexpr bool PIPE = (CFG & 1) != 0;
   constexpr int PD = (LIST || !(CFG & 2)) ? 1 : 2;
   constexpr bool NO_EPI = (CFG & 4) != 0, NO_MFMA = (CFG & 8) != 0, NO_LDS = (CFG & 16) != 0;
@@ -124,7 +140,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const float alpha = a.img_beta[0];
   if (!(alpha * cmax <= 512.f)) return;  // (kmeans_lloyd img_mode 3 takes this pass)
   const int k = a.k, kpad = a.kpad, d = a.d;
-  const ImgSmem L = img_plan(DP, kpad, k, WAVES);
+  const ImgSmem L = img_plan(DP, kpad, k, WAVES, SCAN);
   const int sb = stride_bf16(DP);
   _Float16* ph = reinterpret_cast<_Float16*>(smem + L.plane);
   float* sc_l = reinterpret_cast<float*>(smem + L.sc);
@@ -151,6 +167,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   for (int f = tid; f < DP; f += NT) sc_l[f] = f < d ? a.scale[f] : 0.f;
   for (int i = tid; i < k * RS; i += NT) acc_l[i] = 0.0;
   for (int i = tid; i < k; i += NT) cnt_l[i] = 0;
+  float* dr_l = reinterpret_cast<float*>(smem + L.dr);
+  if constexpr (SCAN)
+    for (int i = tid; i < k; i += NT) dr_l[i] = a.drift[i];
   __syncthreads();
 
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -444,6 +463,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   };
 
   int64_t t = wave;
+  unsigned n_pruned = 0;  // (row-scan passes; wave-uniform)
   auto trow = [&](int64_t q) OAP_AI -> int64_t { return tile_of(q) * 32 + r; };  // (dense)
   if constexpr (LIST) {
     // rows of tiles t, t + stride in ra, rb; each body loads the list entry two tiles ahead
@@ -457,6 +477,77 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       if (t + stride >= npos) break;
       body(t + stride, rb, ra >= 0 ? ra : rfix, &rc, xb, xa);
       rb = rc;  // (tile t + 3 stride)
+    }
+  } else if constexpr (SCAN) {
+    // The wave's dense tiles (t = wave + j stride) are scanned two at a time (h = 0 lanes the
+    // first, h = 1 the second): the Hamerly test of kmeans_lean_scan_rows per row.  A pruned
+    // row keeps its label and has its bounds advanced in place (rounded outward; no write once
+    // no center moves); the others enter the ring in row order.  The ring holds [head, tail):
+    // the current tile and the next one (whose operands are prefetched under the current one)
+    // are complete before the current tile runs, except at the end of the wave's rows.
+    int* ring = reinterpret_cast<int*>(smem + L.ring) + wave * kRing;
+    const float dmax = ufl(a.drift[k]);
+    const float cm2 = ufl(cmax * cmax);
+    const __amdgpu_buffer_rsrc_t rs_xn = buf_rsrc(a.scan_xnorm + t0, uint32_t(dense_pos * 4));
+    unsigned head = 0, tail = 0;  // wave-uniform ring positions
+    int64_t sq = wave;            // the next tile pair to scan (wave-uniform)
+    // the scan of tile pair sq reads bounds, label and tile norm one step ahead: issued when the
+    // previous pair is consumed, in flight under the tiles in between (an unpredicated issue:
+    // offsets past the wave's rows read zeros)
+    u32x2 pbw;
+    int plab;
+    float pxn;
+    auto issue = [&]() OAP_AI {
+      const int64_t q = sq + h * stride;
+      const uint32_t roff = uint32_t(q * 32 + r);
+      const bool in = q < dense_pos && int64_t(roff) < wrows;
+      pbw = __builtin_bit_cast(
+          u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, in ? roff * 8u : kBufOff, 0, 0));
+      plab = buf_load_b32(rs_lab, roff * 4u, in);
+      pxn = __int_as_float(buf_load_b32(rs_xn, uint32_t(q) * 4u, in));
+    };
+    auto refill = [&]() OAP_AI {
+      while (tail - head < 64u && sq < dense_pos) {
+        const int64_t q = sq + h * stride;
+        const uint32_t roff = uint32_t(q * 32 + r);
+        const bool in = q < dense_pos && int64_t(roff) < wrows;
+        const float u = __uint_as_float(pbw[0]) + dr_l[min(max(plab, 0), k - 1)];
+        const float lk = __uint_as_float(pbw[1]) - dmax;
+        const bool ok = in && lk > 0.f && (lk - u) * (lk + u) > mrel * (pxn + cm2);
+        buf_store_f2(rs_bnd, roff * 8u, make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f)),
+                     ok && dmax > 0.f);
+        const bool act = in && !ok;
+        const unsigned long long m = __ballot(act);
+        if (act) ring[(tail + lanes_below(m)) & (kRing - 1)] = static_cast<int>(roff);
+        tail += static_cast<unsigned>(__popcll(m));
+        n_pruned += static_cast<unsigned>(__popcll(__ballot(ok)));
+        sq += 2 * stride;
+        issue();
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    issue();
+    // this lane's row of the tile starting at ring position i (-1 past the tail)
+    auto ring_row = [&](unsigned i) OAP_AI -> int64_t {
+      const int e = ring[(i + unsigned(r)) & (kRing - 1)];
+      return i + unsigned(r) < tail ? row0 + e : int64_t(-1);
+    };
+    const int64_t rfix = row0;
+    f16x8 xa[KS], xb[KS];
+    refill();
+    int64_t ra = ring_row(head), rb = -1;
+    load_img_row(ra >= 0 ? ra : rfix, xa);
+    while (head < tail) {  // (wave-uniform)
+      refill();
+      rb = ring_row(head + 32u);
+      body(0, ra, rb >= 0 ? rb : rfix, nullptr, xa, xb);
+      head = tail - head > 32u ? head + 32u : tail;
+      if (head == tail) break;
+      refill();
+      ra = ring_row(head + 32u);
+      body(0, rb, ra >= 0 ? ra : rfix, nullptr, xb, xa);
+      head = tail - head > 32u ? head + 32u : tail;
     }
   } else if constexpr (PD == 1) {
     f16x8 xa[KS], xb[KS];
@@ -497,6 +588,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     a.defer_row_count[blockIdx.x * kDeferSubs + wave] = n_def;
     if (a.stat && n_def) atomicAdd(a.stat, u64(n_def));
     if (a.stat && moved_total) atomicAdd(a.stat + 1, moved_total);
+    if (SCAN && a.pruned && n_pruned) atomicAdd(a.pruned, u64(n_pruned));
   }
   __syncthreads();
   for (int i = tid; i < k * d; i += NT) {
@@ -510,32 +602,37 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   }
 }
 
-template <int KS, int WAVES, int CFG, bool LIST>
+template <int KS, int WAVES, int CFG, int RM>
 void launch_img_l(const ImgArgs& a, int grid, hipStream_t s) {
-  const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES);
+  const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES, RM == 2);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_lean_img<KS, WAVES, CFG, LIST>),
+        reinterpret_cast<const void*>(&oap_kmeans_lean_img<KS, WAVES, CFG, RM>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_lean_img<KS, WAVES, CFG, LIST>), dim3(grid), dim3(WAVES * 64),
+  hipLaunchKernelGGL((oap_kmeans_lean_img<KS, WAVES, CFG, RM>), dim3(grid), dim3(WAVES * 64),
                      L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
 template <int KS, int WAVES, int CFG>
 void launch_img(const ImgArgs& a, int grid, hipStream_t s) {
-  if constexpr ((CFG & ~1) == 0) {  // (row-list passes: the production configurations only)
+  if constexpr ((CFG & ~1) == 0) {  // (row-list / row-scan passes: production configurations)
     if (a.rows) {
-      launch_img_l<KS, WAVES, CFG, true>(a, grid, s);
+      launch_img_l<KS, WAVES, CFG, 1>(a, grid, s);
+      return;
+    }
+    if (a.scan_xnorm) {
+      launch_img_l<KS, WAVES, CFG, 2>(a, grid, s);
       return;
     }
   } else {
-    OAP_CHECK(!a.rows, "kmeans_lean_img: row-list passes take configuration 0 or 1");
+    OAP_CHECK(!a.rows && !a.scan_xnorm,
+              "kmeans_lean_img: row-list / row-scan passes take configuration 0 or 1");
   }
-  launch_img_l<KS, WAVES, CFG, false>(a, grid, s);
+  launch_img_l<KS, WAVES, CFG, 0>(a, grid, s);
 }
 
 constexpr int kImgDefaultCfg = 1;  // pipelined chunk loop, operands one tile ahead
@@ -669,23 +766,25 @@ void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-bool kmeans_lean_img_supported(int d, int k, int waves) {
+bool kmeans_lean_img_supported(int d, int k, int waves, bool scan) {
   if (d + 4 > 128 || k < 1 || (waves != 12 && waves != 16)) return false;
   const int dp = (d + 4 + 15) / 16 * 16;
   if (dp != kmeans_dp(d)) return false;
   const int kpad = (k + 31) / 32 * 32;
   if (kpad > 1024) return false;
-  return img_plan(dp, kpad, k, waves).total <= kLdsLimit;
+  return img_plan(dp, kpad, k, waves, scan).total <= kLdsLimit;
 }
 
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s) {
-  OAP_CHECK(kmeans_lean_img_supported(a.d, a.k, waves) && !a.xbf16 && a.ximg && a.img_beta &&
+  const bool scan = a.img_scan_xnorm != nullptr;
+  OAP_CHECK(kmeans_lean_img_supported(a.d, a.k, waves, scan) && !a.xbf16 && a.ximg && a.img_beta &&
                 a.delta && a.labels && a.scale && a.sums && a.counts && a.accumulate &&
                 a.sums_too && a.defer_rows && a.defer_row_count && a.cstat && !a.xnorm &&
                 !a.cost_slab && !a.mindist && !a.centers_all && a.chunk_mode == 0 &&
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, waves) &&
                 a.ld == kmeans_ld(a.d, false) && (!a.tile_list || a.tile_count) &&
-                (!a.img_rows || (a.img_row_count && !a.tile_list)),
+                (!a.img_rows || (a.img_row_count && !a.tile_list)) &&
+                (!scan || (a.img_scan_drift && a.bounds && !a.img_rows && !a.tile_list)),
             "kmeans_lean_img: unsupported arguments");
   if (a.n == 0) return;
   ImgArgs l;
@@ -707,6 +806,9 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.stat = a.deferred_rows;
   l.rows = a.img_rows;
   l.row_count = a.img_row_count;
+  l.scan_xnorm = a.img_scan_xnorm;
+  l.drift = a.img_scan_drift;
+  l.pruned = a.img_scan_pruned;
   l.n = a.n;
   l.seg_cap = a.row_seg_cap;
   l.tiles_per_block = kmeans_lloyd_tiles_per_block(a.n, grid);

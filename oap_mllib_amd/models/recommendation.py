@@ -430,16 +430,36 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
 def _blocked_topk(S: np.ndarray, D: np.ndarray, num: int, block: int = 4096):
     """Top-`num` (index, score) per row of S @ D^T, descending; ties by lower index.
 
-    On a GPU world the scoring runs through torch on the MI355X (rocBLAS GEMM + topk); otherwise
-    numpy in row blocks.
+    Sharded by rank (Spark's blocked recommendForAll, ALS.scala:365-505, is distributed over the
+    source blocks): each rank takes a contiguous slab of S, then the slabs are allgathered.  On
+    a GPU world a slab runs through the fused score + top-k kernel (kernels/als_recommend.hip:
+    split-fp16 MFMA scores kept in registers, no score matrix anywhere) when num fits its
+    per-row lists; otherwise torch (rocBLAS GEMM + topk over row blocks), or numpy on CPU.
     """
+    n = len(S)
+    w = get_world()
+    lo, hi = (n * w.rank) // w.size, (n * (w.rank + 1)) // w.size
+    idx, val = _local_topk(S[lo:hi], D, num, w, block)
+    if w.size > 1:
+        parts = w.allgather_obj((idx, val))
+        idx = np.concatenate([p[0] for p in parts]) if n else idx
+        val = np.concatenate([p[1] for p in parts]) if n else val
+    return idx, val
+
+
+def _local_topk(S: np.ndarray, D: np.ndarray, num: int, w, block: int):
     n = len(S)
     idx = np.zeros((n, num), dtype=np.int64)
     val = np.zeros((n, num), dtype=np.float32)
     if n == 0 or num == 0:
         return idx, val
-    w = get_world()
     if w.is_gpu:
+        N = _loader.load()
+        rank = S.shape[1] if S.ndim == 2 else 0
+        if 1 <= rank and num <= N.als_recommend_max_num(rank) and len(D) > 0:
+            i32, v, _ = N.als_recommend(w.ctx, np.ascontiguousarray(S, dtype=np.float32),
+                                        np.ascontiguousarray(D, dtype=np.float32), num)
+            return i32.astype(np.int64), v
         import torch
 
         dev = torch.device("cuda", w.device)

@@ -281,12 +281,18 @@ def test_pruning_is_exact(native, monkeypatch, d, k, dtype, n):
     # (f32 fits with the operand image prune per row: kmeans_lean_scan_rows)
     assert ru["pruned_tiles"] == 0 and ru["pruned_rows"] == 0 and rn["pruned_tiles"] > 0
     assert rp["pruned_tiles"] + rp["pruned_rows"] > 0
-    if dtype == "f32" and d == 50:  # the tile-level scan (OAP_KMEANS_ROW_SCAN=0) still exact
+    if dtype == "f32" and k == 200:  # the tile-level scan (OAP_KMEANS_ROW_SCAN=0) still exact
         monkeypatch.setenv("OAP_KMEANS_ROW_SCAN", "0")
         rt = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
         assert rt["pruned_rows"] == 0 and rt["pruned_tiles"] > 0 and rp["pruned_rows"] > 0
         assert rt["last_counts"] == ru["last_counts"]
         assert np.array_equal(rt["centers"], ru["centers"])
+        # the separate scan kernel + row list (=2) prunes exactly the rows the fused scan does
+        monkeypatch.setenv("OAP_KMEANS_ROW_SCAN", "2")
+        r2 = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
+        assert r2["pruned_rows"] == rp["pruned_rows"] and r2["pruned_tiles"] == 0
+        assert r2["last_counts"] == ru["last_counts"]
+        assert np.array_equal(r2["centers"], ru["centers"])
     for r in (rp, rn):
         assert r["last_counts"] == ru["last_counts"]
         assert np.array_equal(r["centers"], ru["centers"])
