@@ -115,6 +115,36 @@ def als_native(seed=3, device="cpu", use_rccl=True, rank=3, device_id=0, implici
     return out
 
 
+def recommend_sharded(n=301, m=57, rank=6, num=7, seed=9):
+    """recommendForAllUsers on a 2-rank CPU world: each rank scores its own slab of users (the
+    local top-k sees only its rows), then the slabs are allgathered in rank order."""
+    import oap_mllib_amd as O
+    from oap_mllib_amd.models import recommendation as rec
+
+    w = O.init_world(O.get_config().replace(device="cpu"))
+    rng = np.random.default_rng(seed)
+    U = rng.normal(size=(n, rank)).astype(np.float32)
+    V = rng.normal(size=(m, rank)).astype(np.float32)
+    seen = []
+    local = rec._local_topk
+
+    def spy(S, D, k, world, block):
+        seen.append(len(S))
+        return local(S, D, k, world, block)
+
+    rec._local_topk = spy
+    try:
+        idx, val = rec._blocked_topk(U, V, num)
+    finally:
+        rec._local_topk = local
+    model = O.ALSModel(rank=rank, user_arrays=(np.arange(n), U), item_arrays=(np.arange(m), V))
+    first = [r[0]["item"] for r in model.recommendForAllUsers(num)["recommendations"].tolist()]
+    out = {"rank": w.rank, "rows_scored": seen, "idx": idx.tolist(), "val": val.tolist(),
+           "first": first}
+    O.shutdown_world()
+    return out
+
+
 def tcp_alltoallv(port, piece=0):
     """Uneven alltoallv / allreduce / allgather over the KVS TcpComm (streamed star routing);
     piece > 0 forces several forwarding pieces per segment."""

@@ -82,3 +82,25 @@ def test_tcp_comm_streamed_alltoallv(nproc, piece):
     assert rc == 0, outs
     for o in outs:
         assert o == {"a2a": True, "allreduce": True, "allgather": True}, outs
+
+
+def test_recommend_for_all_sharded_by_rank():
+    """Each rank of a 2-rank world scores only its own slab of users (the result is the
+    single-process one on every rank)."""
+    rc, outs = run_world("dist_workers", "recommend_sharded", nproc=2)
+    assert rc == 0
+    from oap_mllib_amd.models.recommendation import _local_topk
+
+    rng = np.random.default_rng(9)
+    U = rng.normal(size=(301, 6)).astype(np.float32)
+    V = rng.normal(size=(57, 6)).astype(np.float32)
+
+    class W:
+        is_gpu = False
+
+    idx, val = _local_topk(U, V, 7, W(), 4096)
+    assert outs[0]["rows_scored"] == [150] and outs[1]["rows_scored"] == [151]
+    for o in outs:
+        assert np.array_equal(np.array(o["idx"]), idx)
+        np.testing.assert_array_equal(np.array(o["val"], dtype=np.float32), val)
+        assert o["first"] == idx[:, 0].tolist()
