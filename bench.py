@@ -59,8 +59,9 @@ def _barrier_sync(w):
 def _timed_fit(args, w, N, table, init, steps, prune=True):
     _barrier_sync(w)
     t0 = time.perf_counter()
+    # (one event pair per batch of iterations: per-phase events put ~10 us gaps in the stream)
     r = N.kmeans_fit(w.ctx, w.comm, table, init, args.k, steps, -1.0, precise=args.precise,
-                     prune=prune)
+                     prune=prune, phase_events=False)
     _barrier_sync(w)
     el = float(w.allreduce_np(np.array([time.perf_counter() - t0]), "max")[0])
     assert r["num_iter"] == steps, r["num_iter"]
@@ -127,8 +128,12 @@ def bench_kmeans(args, w):
     if args.warmup > 0:
         N.kmeans_fit(w.ctx, w.comm, table, init, k, args.warmup, -1.0, precise=args.precise,
                      prune=not args.no_prune)
-    w.ctx.reset_metrics()
     r, el_max = _timed_fit(args, w, N, table, init, args.steps, prune=not args.no_prune)
+    # the phase breakdown (assign / allreduce / rest per iteration): the same fit again with
+    # per-phase events, untimed
+    w.ctx.reset_metrics()
+    N.kmeans_fit(w.ctx, w.comm, table, init, args.k, args.steps, -1.0, precise=args.precise,
+                 prune=not args.no_prune, phase_events=True)
     m = w.ctx.metrics()["phases"]
     # the same timed run with every distance evaluated (no bound-based pruning), for reference
     ms_unpruned = None
@@ -182,6 +187,10 @@ def bench_kmeans(args, w):
                                          "it could not prune (gathered from the row-major "
                                          "operand image) + exact fp32 re-decision; delta "
                                          "accumulation of moved rows",
+        "lean_img_kernel_delta_fused_rowscan": "image kernel with the row-level Hamerly scan "
+                                               "fused in (per-wave LDS ring of the rows it "
+                                               "cannot prune) + exact fp32 re-decision; delta "
+                                               "accumulation of moved rows",
         "tiered_bf16_mfma": "tiered bf16 MFMA distances (exact-fp32 re-decision of near ties)",
         "tiered_bf16_mfma_chunked": "centroid-chunked tiered bf16 MFMA distances",
         "exact_fp32_mfma": "fp32-exact MFMA (v_mfma_f32_32x32x2_f32)",
@@ -332,13 +341,18 @@ def main(argv=None):
     if ws != args.gpus:
         print(f"--gpus {args.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
         return 2
+    # native libraries write to fd 1 too (RCCL's version banner at communicator init): fd 1 goes
+    # to stderr while the world runs, so rank 0's stdout carries exactly the one JSON line
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
     import oap_mllib_amd as O
 
     dev = os.environ.get("OAP_BENCH_DEVICE", "gpu")  # "cpu": CPU-engine rehearsal (tests)
     w = O.init_world(O.get_config().replace(device=dev, force_device_comm=args.force_rccl))
     out = bench_kmeans(args, w)
     if w.rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     O.shutdown_world()
     return 0
 

@@ -484,11 +484,13 @@ PYBIND11_MODULE(_native, m) {
       "kmeans_fit",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
          py::object init_centers, int k, int max_iter, double tol, const std::string& init_mode,
-         int init_steps, uint64_t seed, bool precise, bool prune, bool delta) {
+         int init_steps, uint64_t seed, bool precise, bool prune, bool delta,
+         bool phase_events) {
         KMeansParams p;
         p.precise = precise;
         p.prune = prune;
         p.delta = delta;
+        p.phase_events = phase_events;
         p.k = k;
         p.max_iter = max_iter;
         p.tol = tol;
@@ -539,7 +541,8 @@ PYBIND11_MODULE(_native, m) {
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),
       py::arg("k") = 2, py::arg("max_iter") = 20, py::arg("tol") = 1e-4,
       py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1,
-      py::arg("precise") = false, py::arg("prune") = true, py::arg("delta") = true);
+      py::arg("precise") = false, py::arg("prune") = true, py::arg("delta") = true,
+      py::arg("phase_events") = true);
   m.def(
       "kmeans_fit_streamed",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,

@@ -111,6 +111,26 @@ void RcclComm::check_async() {
     OAP_THROW(CommError, "RCCL async error: " << ncclGetErrorString(r));
 }
 
+void Comm::allreduce_oop(const void* send, void* recv, size_t count, DType dt, ReduceOp op,
+                         hipStream_t s) {
+  const size_t bytes = count * dtype_size(dt);
+  if (bytes && send != recv) {
+    if (on_device())
+      OAP_HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+    else
+      std::memcpy(recv, send, bytes);
+  }
+  allreduce(recv, count, dt, op, s);
+}
+
+void RcclComm::allreduce_oop(const void* send, void* recv, size_t count, DType dt, ReduceOp op,
+                             hipStream_t s) {
+  check_async();
+  if (count == 0) return;
+  OAP_NCCL_CHECK(ncclAllReduce(send, recv, count, to_nccl(dt), to_nccl(op),
+                               static_cast<ncclComm_t>(comm_), s));
+}
+
 void RcclComm::allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t s) {
   check_async();
   if (count == 0) return;

@@ -38,6 +38,10 @@ class Comm {
 
   // In-place allreduce.
   virtual void allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t s) = 0;
+  // Out-of-place allreduce (send and recv distinct); the default copies send into recv (on the
+  // device when on_device(), else on the host) and reduces in place.
+  virtual void allreduce_oop(const void* send, void* recv, size_t count, DType dt, ReduceOp op,
+                             hipStream_t s);
   // recv holds size()*count elements, rank-major.
   virtual void allgather(const void* send, void* recv, size_t count, DType dt, hipStream_t s) = 0;
   // Variable-size exchange; counts are in elements, displacements are packed (prefix sums).
@@ -84,6 +88,8 @@ class RcclComm final : public Comm {
   const char* name() const override { return "rccl"; }
   bool trivial() const override { return false; }
   void allreduce(void* buf, size_t count, DType dt, ReduceOp op, hipStream_t s) override;
+  void allreduce_oop(const void* send, void* recv, size_t count, DType dt, ReduceOp op,
+                     hipStream_t s) override;
   void allgather(const void* send, void* recv, size_t count, DType dt, hipStream_t s) override;
   void alltoallv(const void* send, const std::vector<size_t>& send_counts, void* recv,
                  const std::vector<size_t>& recv_counts, DType dt, hipStream_t s) override;

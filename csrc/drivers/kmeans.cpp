@@ -1212,7 +1212,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer cost_d = ctx.alloc(sizeof(double));
   Buffer scale = ctx.alloc(sizeof(float) * (round_up(d, 4) + 4));
   Buffer inv_scale = ctx.alloc(sizeof(double) * d);
-  Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags));
+  // one flags slot per iteration of a batch (read back once per batch), the finalize's
+  // last-block counter, the cost accumulator (zeroed by the finalize that reads it)
+  Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags) * 8);
+  Buffer fin_done = ctx.alloc(sizeof(unsigned));
+  ctx.memset(fin_done.data(), 0, sizeof(unsigned), s);
+  ctx.memset(cost_d.data(), 0, sizeof(double), s);
   Buffer refine_d = ctx.alloc(2 * sizeof(u64));  // [exact re-decisions, tier-3 re-runs]
   Buffer counts_h = ctx.alloc_pinned(sizeof(u64) * k);
   Buffer refine_h = ctx.alloc_pinned(2 * sizeof(u64));
@@ -1387,6 +1392,16 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     row_scan_fused =
         row_scan_fused && row_scan_ok && kern::kmeans_lean_img_supported(d, k, lw, true);
   }
+  // the same decision from the shape alone (rank-uniform: it may change which iterations compute
+  // a cost, and so which collectives run)
+  bool row_scan_shape = false;
+  if (scan_all && !chunked && !(rs_env && *rs_env == '0') && x.dtype == DType::F32 &&
+      img_kernel_default()) {
+    const char* e = std::getenv("OAP_KMEANS_IMAGE");
+    const int lv = lean_variant(d, g.kpad);
+    row_scan_shape = !(e && *e == '0') && lv != 3 && lv != 10 &&
+                     kern::kmeans_lean_img_supported(d, k, kern::kmeans_lloyd_waves(lv));
+  }
   if (row_scan_ok && !row_scan_fused)
     rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
                         sizeof(unsigned) * size_t(lgrid) + 64);
@@ -1429,10 +1444,16 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   fa.dp = g.dp;
   fa.tol = p.tol;
   fa.cost_in = cost_d.as<double>();
+  fa.cost_reset = cost_d.as<double>();
   fa.flags = flags_d.data();
   Buffer fin_scratch = ctx.alloc(sizeof(double) * 2 * std::max(k, 1));
   fa.scratch = fin_scratch.as<double>();
+  fa.done = fin_done.as<unsigned>();
   if (prune) fa.drift = drift_b.as<float>();
+  // per-phase events (assign / allreduce / rest) in every iteration, or only one pair per
+  // batch: an event record is a gap of ~10 us in the stream, a measurable share of an
+  // iteration on a 12.5M-row shard
+  const bool pev = p.phase_events;
 
   u64 tier2_seen = 0;
   RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
@@ -1442,7 +1463,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // kBatch iterations are enqueued back to back (kernels + collective, no host round trip in
   // between) and their flags / timings are read once per batch — the host re-checks the
   // adaptive distance tier at every batch boundary.
-  constexpr int kBatch = 8;
+  constexpr int kBatch = 8;  // (flags_d slots)
   const int B = p.tol < 0 ? kBatch : 1;
   struct IterEvents {
     Event e0, e1, e2, e3;
@@ -1464,7 +1485,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       const int it = it0 + b;
       maybe_inject_fault(comm.rank(), "kmeans_iter", it);
       roctx_push("kmeans/iteration");
-      ev[b].e0.record(s);
+      if (pev || b == 0) ev[b].e0.record(s);
       // (req.fast1: the lean kernel runs; only it does delta accumulation)
       const bool delta_it = delta && it > 0 && req.fast1;
       // (a probe batch scans its first iteration only: the next batch decides from it)
@@ -1507,8 +1528,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // lean iterations compute the exact cost only where it is reported: the first and a
       // known last iteration (fixed count); otherwise the final cost comes from one exact pass
       // over the labels after the loop
+      // (with the row scan, a known last iteration is a scan pass too: the exact cost pass over
+      // the labels after the loop reads the f32 rows once, cheaper than a full f32 cost pass)
       const bool cost_it = !req.fast1 || !delta_all || it == 0 ||
-                           (p.tol < 0 && it == p.max_iter - 1);
+                           (p.tol < 0 && it == p.max_iter - 1 && !row_scan_shape);
       req.cost_slab = cost_it ? slab.as<double>() : nullptr;
       it_costless[b] = !cost_it || scan_it_all;
       last_costless = it_costless[b];
@@ -1561,8 +1584,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), cloc_b.data(), sizeof(u64) * (kd + k),
                                      hipMemcpyDeviceToDevice, s));
       if (req.xnorm && !req.tile_list) xnorm_ready = true;
+      // (a device communicator reduces the local statistics out of place into stats)
+      const bool stats_oop = delta && !fin_direct && comm.on_device();
       if (delta) {
-        if (!fin_direct)
+        if (!fin_direct && !stats_oop)
           OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
                                        hipMemcpyDeviceToDevice, s));
         // the centers this iteration assigned against, for the final exact-cost pass — only
@@ -1572,15 +1597,18 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                        sizeof(float) * size_t(g.kpad) * g.dp,
                                        hipMemcpyDeviceToDevice, s));
       }
-      if (nb > 0)
-        kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
-      else if (cost_it || !comm.trivial())  // (a costless iteration's cost is not reported)
-        OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
-      ev[b].e1.record(s);
+      // (otherwise cost_d holds the zero the last finalize left: a costless iteration's cost
+      // is not reported)
+      if (nb > 0) kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
+      if (pev) ev[b].e1.record(s);
       if (!comm.trivial()) {
         if (comm.on_device()) {
           if (rccl) rccl->group_start();
-          comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
+          if (stats_oop)
+            comm.allreduce_oop(loc_b.data(), stats.data(), kd + k, DType::I64, ReduceOp::Sum,
+                               s);
+          else
+            comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
           comm.allreduce(cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
           if (rccl) rccl->group_end();
         } else {
@@ -1588,13 +1616,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
         }
       }
-      ev[b].e2.record(s);
+      if (pev) ev[b].e2.record(s);
+      fa.flags = flags_d.as<kern::KMeansFlags>() + b;
       kern::kmeans_finalize(fa, s);
-      OAP_HIP_CHECK(hipMemcpyAsync(flh + b, flags_d.data(), sizeof(kern::KMeansFlags),
-                                   hipMemcpyDeviceToHost, s));
-      ev[b].e3.record(s);
+      if (pev || b == nb_it - 1) ev[b].e3.record(s);
       roctx_pop();
     }
+    OAP_HIP_CHECK(hipMemcpyAsync(flh, flags_d.data(), sizeof(kern::KMeansFlags) * nb_it,
+                                 hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(
         hipMemcpyAsync(counts_h.data(), fin_counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
@@ -1607,13 +1636,16 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       OAP_HIP_CHECK(hipMemcpyAsync(&pruned_now, pruned_d.data(), sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     comm.wait(s);
+    const float ms_batch = pev ? 0.f : Event::elapsed_ms(ev[0].e0, ev[nb_it - 1].e3);
     for (int b = 0; b < nb_it; ++b) {
       const int it = it0 + b;
-      const float ms_assign = Event::elapsed_ms(ev[b].e0, ev[b].e1),
-                  ms_comm = Event::elapsed_ms(ev[b].e1, ev[b].e2),
-                  ms_all = Event::elapsed_ms(ev[b].e0, ev[b].e3);
-      M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.bytes()));
-      M.add("kmeans/allreduce", ms_comm * 1e3, int64_t(kd + k) * 8 + 8);
+      const float ms_assign = pev ? Event::elapsed_ms(ev[b].e0, ev[b].e1) : 0.f,
+                  ms_comm = pev ? Event::elapsed_ms(ev[b].e1, ev[b].e2) : 0.f,
+                  ms_all = pev ? Event::elapsed_ms(ev[b].e0, ev[b].e3) : ms_batch / nb_it;
+      if (pev) {
+        M.add("kmeans/assign_kernel", ms_assign * 1e3, int64_t(x.bytes()));
+        M.add("kmeans/allreduce", ms_comm * 1e3, int64_t(kd + k) * 8 + 8);
+      }
       M.add("kmeans/iteration", ms_all * 1e3);
       const kern::KMeansFlags& fl = flh[b];
       if (Logger::instance().level() <= LogLevel::Info) {

@@ -39,6 +39,9 @@ struct KMeansParams {
   // per-iteration costs are then computed only on full passes, the final cost by an exact
   // pass over the labels (cost_history holds NaN for the delta iterations before the last)
   bool delta = true;
+  // per-iteration phase events (kmeans/assign_kernel and kmeans/allreduce metrics); off: one
+  // event pair per batch of iterations (kmeans/iteration only), no event gaps between phases
+  bool phase_events = true;
 };
 
 struct KMeansResult {

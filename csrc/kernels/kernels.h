@@ -283,6 +283,11 @@ struct KMeansFinalizeArgs {
   double* scratch = nullptr;        // [2k]: enables the multi-block finalize (else 1 block)
   // optional [k + 1] out: |centers32_new - centers32_old| per center (rounded up), [k] = max
   float* drift = nullptr;
+  // multi-block finalize in ONE launch: the last cluster block to finish (this zero-initialised
+  // counter, reset by it) reduces the flags — no second kernel
+  unsigned* done = nullptr;
+  // optional: zeroed once its value is in the flags (the next iteration's cost accumulator)
+  double* cost_reset = nullptr;
 };
 struct KMeansFlags {
   int converged;

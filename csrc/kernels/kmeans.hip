@@ -583,65 +583,14 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
     fl->nonempty = s_nonempty;
     fl->cost = a.cost_in ? a.cost_in[0] : 0.0;
     fl->max_shift2 = mx;
+    if (a.cost_reset) a.cost_reset[0] = 0.0;
     if (a.cstat) a.cstat[0] = nm * 1.0000001f;
     if (a.drift) a.drift[a.k] = dm;
   }
 }
 
-// Multi-block finalize (one wave per cluster): new centers + per-cluster shift / norm into
-// scratch; oap_kmeans_finalize_flags reduces them.  The fp64 sums keep the single-block
-// kernel's sequential feature order (lane 0), so results are bitwise unchanged.
-__global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinalizeArgs a) {
-  __shared__ double s_df[4][256];
-  __shared__ float s_dv[4][256];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + w;
-  if (c >= a.k) return;
-  const long long cntv = static_cast<long long>(a.counts[c]);
-  double* c64 = a.centers64 + size_t(c) * a.d;
-  double dr2 = 0.0;  // lane 0: squared movement of the fp32 center
-  for (int f0 = 0; f0 < a.d; f0 += 256) {
-    const int nf = min(256, a.d - f0);
-    for (int f = lane; f < nf; f += 64) {
-      double df = 0.0;
-      float dv = 0.f;
-      if (cntv > 0) {
-        const long long sv = static_cast<long long>(a.sums[size_t(c) * a.d + f0 + f]);
-        const double nv = double(sv) * a.inv_scale[f0 + f] / double(cntv);  // == CPU formula
-        df = nv - c64[f0 + f];
-        dv = static_cast<float>(nv) - static_cast<float>(c64[f0 + f]);
-        c64[f0 + f] = nv;
-      }
-      const float v = static_cast<float>(c64[f0 + f]);
-      a.centers32[size_t(c) * a.dp + f0 + f] = v;
-      s_df[w][f] = df;
-      s_dv[w][f] = dv;
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (lane == 0) {
-      double sh = f0 == 0 ? 0.0 : a.scratch[c];
-      for (int f = 0; f < nf; ++f) {
-        sh += s_df[w][f] * s_df[w][f];
-        dr2 += double(s_dv[w][f]) * double(s_dv[w][f]);
-      }
-      a.scratch[c] = sh;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  if (lane == 0 && a.drift) a.drift[c] = static_cast<float>(sqrt(dr2) * (1.0 + 1e-6));
-  if (lane == 0) {
-    double nrm = 0.0;
-    for (int f = 0; f < a.d; ++f) {
-      const double v = double(static_cast<float>(c64[f]));
-      nrm += v * v;
-    }
-    a.cnorm[c] = static_cast<float>(nrm);
-    a.scratch[a.k + c] = double(sqrtf(static_cast<float>(nrm)));
-    if (cntv <= 0) a.scratch[c] = -1.0;  // empty: keeps its center, not part of the test
-  }
-}
-
-__global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeArgs a) {
+// The flags of a multi-block finalize from the per-cluster scratch (one block of 256 threads).
+__device__ void finalize_flags_block(const KMeansFinalizeArgs& a) {
   __shared__ double s_shift[256];
   __shared__ float s_norm[256], s_drift[256];
   __shared__ int s_conv, s_nonempty;
@@ -680,8 +629,80 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeA
     fl->nonempty = s_nonempty;
     fl->cost = a.cost_in ? a.cost_in[0] : 0.0;
     fl->max_shift2 = mx;
+    if (a.cost_reset) a.cost_reset[0] = 0.0;
     if (a.cstat) a.cstat[0] = nm * 1.0000001f;
   }
+}
+
+// Multi-block finalize (one wave per cluster): new centers + per-cluster shift / norm into
+// scratch; the flags from them (the last block to finish when a.done is set, else
+// oap_kmeans_finalize_flags).  The fp64 sums keep the single-block kernel's sequential feature
+// order (lane 0), so results are bitwise unchanged.
+__global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinalizeArgs a) {
+  __shared__ double s_df[4][256];
+  __shared__ float s_dv[4][256];
+  __shared__ bool s_last;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + w;
+  if (c < a.k) {
+    const long long cntv = static_cast<long long>(a.counts[c]);
+    double* c64 = a.centers64 + size_t(c) * a.d;
+    double dr2 = 0.0;  // lane 0: squared movement of the fp32 center
+    for (int f0 = 0; f0 < a.d; f0 += 256) {
+      const int nf = min(256, a.d - f0);
+      for (int f = lane; f < nf; f += 64) {
+        double df = 0.0;
+        float dv = 0.f;
+        if (cntv > 0) {
+          const long long sv = static_cast<long long>(a.sums[size_t(c) * a.d + f0 + f]);
+          const double nv = double(sv) * a.inv_scale[f0 + f] / double(cntv);  // == CPU formula
+          df = nv - c64[f0 + f];
+          dv = static_cast<float>(nv) - static_cast<float>(c64[f0 + f]);
+          c64[f0 + f] = nv;
+        }
+        const float v = static_cast<float>(c64[f0 + f]);
+        a.centers32[size_t(c) * a.dp + f0 + f] = v;
+        s_df[w][f] = df;
+        s_dv[w][f] = dv;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        double sh = f0 == 0 ? 0.0 : a.scratch[c];
+        for (int f = 0; f < nf; ++f) {
+          sh += s_df[w][f] * s_df[w][f];
+          dr2 += double(s_dv[w][f]) * double(s_dv[w][f]);
+        }
+        a.scratch[c] = sh;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane == 0 && a.drift) a.drift[c] = static_cast<float>(sqrt(dr2) * (1.0 + 1e-6));
+    if (lane == 0) {
+      double nrm = 0.0;
+      for (int f = 0; f < a.d; ++f) {
+        const double v = double(static_cast<float>(c64[f]));
+        nrm += v * v;
+      }
+      a.cnorm[c] = static_cast<float>(nrm);
+      a.scratch[a.k + c] = double(sqrtf(static_cast<float>(nrm)));
+      if (cntv <= 0) a.scratch[c] = -1.0;  // empty: keeps its center, not part of the test
+    }
+  }
+  if (!a.done) return;
+  // last block: every other block's scratch / drift writes are visible (release before the
+  // count, acquire after it)
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  finalize_flags_block(a);
+  if (threadIdx.x == 0) a.done[0] = 0u;
+}
+
+__global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeArgs a) {
+  finalize_flags_block(a);
 }
 
 __global__ void oap_kmeans_prepare_centers(const double* c64, int k, int d, int dp, float* c32,
@@ -1088,7 +1109,7 @@ void kmeans_finalize(const KMeansFinalizeArgs& a, hipStream_t s) {
   if (a.scratch) {
     hipLaunchKernelGGL(oap_kmeans_finalize_clusters, dim3((a.k + 3) / 4), dim3(256), 0, s, a);
     OAP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(oap_kmeans_finalize_flags, dim3(1), dim3(256), 0, s, a);
+    if (!a.done) hipLaunchKernelGGL(oap_kmeans_finalize_flags, dim3(1), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL(oap_kmeans_finalize, dim3(1), dim3(256), 0, s, a);
   }
