@@ -382,7 +382,14 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   // a trivial comm (world of one, no communicator) skips every exchange; any other comm — a
   // 1-rank RCCL communicator included — runs the multi-rank code path end to end
   const bool local = comm.trivial();
-  const int r = p.rank, ld = int(round_up(size_t(r), 16));
+  // factor row pitch = the solves' padded width (multiple of 16 >= rank); OAP_ALS_LD overrides
+  // it upward (timing experiments: whole 128-byte lines per gathered row)
+  const int r = p.rank;
+  int ld = int(round_up(size_t(r), 16));
+  if (const char* e = std::getenv("OAP_ALS_LD")) {
+    const int v = std::atoi(e);
+    if (v >= ld && v % 16 == 0 && v <= 128) ld = v;
+  }
   AlsResult res;
   res.rank = r;
   auto t_setup = std::chrono::steady_clock::now();

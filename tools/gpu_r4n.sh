@@ -1,0 +1,8 @@
+# usage (GPU box): bash tools/gpu_r4n.sh <tag>: config-5 bench + ALS 1B kernel trace
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+T=${1:-r4n}
+fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2: stopping"; exit $1;; esac; }
+timeout -k 10 600 python bench.py --config kmeans_bf16 --cpu-rows 0 --no-estimator --skip-unpruned > gpurun_out/bench_cfg5_$T.json 2> gpurun_out/bench_cfg5_$T.err
+rc=$?; echo cfg5_rc=$rc; fatal $rc cfg5
+bash tools/gpu_als_prof.sh alsprof_$T
+echo done
