@@ -870,7 +870,12 @@ void launch_lean_xb(const LeanArgs& a, int grid, int variant, bool cost, hipStre
 // exact cost, labels / mindist / bounds, fixed-point statistics (LDS fp64 accumulator when it
 // fits, else global int64 atomics).  Rows: the lean workgroup's deferral sub-segments in order
 // (deterministic).
-constexpr int kExactWaves = 8;
+// waves per workgroup: 16 (4 per SIMD with the one workgroup the LDS plan allows per CU) where
+// the kernel fits 128 VGPRs, else 8 — the pass is latency bound, not MFMA bound
+constexpr int kExactWaves = 16;  // (the most: LDS slots)
+__host__ __device__ constexpr int exact_waves(int ks, bool xb) {
+  return (xb ? ks <= 5 : ks <= 4) ? 16 : 8;
+}
 
 struct ExactSmem {
   size_t ct, cn, sc, acc, cnt, wc, pref, total;
@@ -905,7 +910,9 @@ __host__ __device__ inline ExactSmem exact_plan(int kpad, int k, int d, bool acc
 }
 
 template <int KS, bool XB>
-__global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeansAssignArgs a) {
+__global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_rows(
+    KMeansAssignArgs a) {
+  constexpr int EW = exact_waves(KS, XB);
   constexpr int DP = 16 * KS;
   constexpr int CS = DP + 4;
   using F = Frag<KS, XB>;
@@ -927,7 +934,7 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
   unsigned* pref = reinterpret_cast<unsigned*>(smem + L.pref);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  constexpr int NT = kExactWaves * 64;
+  constexpr int NT = EW * 64;
   if (tid == 0) {
     pref[0] = 0u;
     for (int w = 0; w < a.row_subs; ++w)
@@ -1017,12 +1024,12 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
   F xa, xb;
   int64_t g = wave;
   load_rows(g, xa);
-  for (; g < ngroups; g += kExactWaves) {  // wave-uniform
+  for (; g < ngroups; g += EW) {  // wave-uniform
     const int64_t i = g * 32 + r;
     const bool valid = i < int64_t(total);
     const int64_t row = row_at(i);
     F& x = xa;
-    load_rows(g + kExactWaves, xb);  // next group: in flight under this one's MFMAs
+    load_rows(g + EW, xb);  // next group: in flight under this one's MFMAs
     // exact argmin with the best and second-best exact distances (the second for the bounds)
     float best = INFINITY, second = INFINITY;
     int bidx = 0x7fffffff;
@@ -1118,7 +1125,7 @@ __global__ __launch_bounds__(kExactWaves * 64) void oap_kmeans_exact_rows(KMeans
   __syncthreads();
   if (tid == 0 && a.cost_slab) {
     double tot = 0.0;
-    for (int w = 0; w < kExactWaves; ++w) tot += wc[w];
+    for (int w = 0; w < EW; ++w) tot += wc[w];
     a.cost_slab[blockIdx.x] = tot;
   }
   if (L.lds_acc) {
@@ -1144,8 +1151,8 @@ void launch_exact(const KMeansAssignArgs& a, int grid, hipStream_t s) {
                                       static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_exact_rows<KS, XB>), dim3(grid), dim3(kExactWaves * 64), L.total,
-                     s, a);
+  hipLaunchKernelGGL((oap_kmeans_exact_rows<KS, XB>), dim3(grid), dim3(exact_waves(KS, XB) * 64),
+                     L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
