@@ -14,6 +14,7 @@
 #include <unordered_map>
 
 #include "kernels/kernels.h"
+#include "kernels/kmeans_init.h"
 #include "kernels/kmeans_wide.h"
 
 namespace oap {
@@ -739,6 +740,29 @@ void check_gpu_table(const DenseTable& x) {
 // OAP_KMEANS_INIT_PRECISE=1 keeps the previous path for A/B runs.
 bool init_fast() { return std::getenv("OAP_KMEANS_INIT_PRECISE") == nullptr; }
 
+// Candidate sets beyond one LDS plan take super-chunks of at most 1024 candidates on the lean
+// pass (the centroid-chunked one where a super-chunk still exceeds the plan), the per-row exact
+// answers merged by distance (kmeans_merge_argmin), instead of the general chunked kernel's
+// bf16x3 tiers: config 5's ~2000-4000 candidates.  OAP_KMEANS_INIT_SUPER=0: the previous path.
+// (debug: =1 cost updates only, =2 candidate counts only)
+bool init_super(const DenseTable& x, int m, int which) {
+  const char* e = std::getenv("OAP_KMEANS_INIT_SUPER");
+  if (e && (*e == '0' || (*e == '1' && which != 1) || (*e == '2' && which != 2))) return false;
+  return init_fast() && x.cols <= 128 && x.rows > 0 &&
+         int(round_up(size_t(m), 32)) > kern::kmeans_lds_kmax(x.cols, false) &&
+         kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
+}
+
+// super-chunk [base, base + size) of m candidates: sizes of at most 1024, multiples of 32
+int super_size(int m) {
+  const int n = (m + 1023) / 1024;
+  return int(round_up(size_t((m + n - 1) / n), 32));
+}
+
+std::vector<double> centers_slice(const std::vector<double>& c, int d, int base, int size) {
+  return std::vector<double>(c.begin() + size_t(base) * d, c.begin() + size_t(base + size) * d);
+}
+
 // Operations the initialisers need, on either backend.
 class InitOps {
  public:
@@ -757,7 +781,19 @@ class InitOps {
   // costs = min(costs, dist^2 to `centers`)
   void update_costs(const std::vector<double>& centers, int m) {
     if (m == 0 || x_.rows == 0) return;
-    if (ctx_.is_gpu()) {
+    if (ctx_.is_gpu() && init_super(x_, m, 1)) {
+      const int ss = super_size(m), d = x_.cols;
+      for (int base = 0; base < m; base += ss) {
+        const int sz = std::min(ss, m - base);
+        GpuCenters g = upload_centers(ctx_, centers_slice(centers, d, base, sz), sz, d);
+        AssignReq req;
+        req.mindist = tmp_.as<float>();
+        req.fast1 = true;
+        gpu_assign(ctx_, x_, g, req, ctx_.compute());
+        kern::elementwise_min(costs_.as<float>(), tmp_.as<float>(), x_.rows, ctx_.compute());
+        OAP_HIP_CHECK(hipStreamSynchronize(ctx_.compute()));  // (g is freed on return)
+      }
+    } else if (ctx_.is_gpu()) {
       GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
       AssignReq req;
       if (x_.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x_.cols, false)) {
@@ -850,6 +886,31 @@ class InitOps {
   std::vector<int64_t> count_closest(const std::vector<double>& centers, int m) {
     std::vector<int64_t> cnt(m, 0);
     if (x_.rows == 0) return cnt;
+    if (ctx_.is_gpu() && init_super(x_, m, 2)) {
+      const int ss = super_size(m), d = x_.cols;
+      Buffer lab_b = ctx_.alloc(sizeof(int32_t) * x_.rows);
+      Buffer lab_s = ctx_.alloc(sizeof(int32_t) * x_.rows);
+      Buffer best = ctx_.alloc(sizeof(float) * x_.rows);  // the running nearest distance
+      for (int base = 0; base < m; base += ss) {
+        const int sz = std::min(ss, m - base);
+        GpuCenters g = upload_centers(ctx_, centers_slice(centers, d, base, sz), sz, d);
+        AssignReq req;
+        req.labels = lab_s.as<int32_t>();
+        req.mindist = tmp_.as<float>();
+        req.fast1 = true;
+        gpu_assign(ctx_, x_, g, req, ctx_.compute());
+        kern::kmeans_merge_argmin(best.as<float>(), lab_b.as<int32_t>(), tmp_.as<float>(),
+                                  lab_s.as<int32_t>(), base, x_.rows, base == 0, ctx_.compute());
+        OAP_HIP_CHECK(hipStreamSynchronize(ctx_.compute()));
+      }
+      Buffer dc = ctx_.alloc(sizeof(u64) * m);
+      ctx_.memset(dc.data(), 0, sizeof(u64) * m);
+      kern::kmeans_accumulate(x_.data.data(), x_.dtype == DType::BF16, x_.rows,
+                              static_cast<int>(x_.ld), x_.cols, lab_b.as<int32_t>(), m, nullptr,
+                              nullptr, dc.as<u64>(), ctx_.compute());
+      ctx_.copy_to_host(cnt.data(), dc.data(), sizeof(u64) * m);
+      return cnt;
+    }
     if (ctx_.is_gpu()) {
       GpuCenters g = upload_centers(ctx_, centers, m, x_.cols);
       Buffer dc = ctx_.alloc(sizeof(u64) * m);

@@ -79,6 +79,33 @@ def test_gpu_init_matches_cpu_engine(native):
         np.testing.assert_array_equal(cg, cc)
 
 
+def test_gpu_init_super_chunks(native, monkeypatch):
+    """k-means|| with candidate sets beyond one LDS plan (d = 100, k = 400: 800 candidates a
+    round, ~1600 counted) on super-chunks of the lean pass, merged by exact distance.  With ~40
+    near-equidistant candidates per blob, exact-fp32 forms (direct vs expanded) and fp64 differ
+    for a few rows' nearest candidate, so the inits are compared by what they must share:
+    deterministic, the cost updates exactly the general chunked kernel's (OAP_KMEANS_INIT_SUPER=1
+    uses the super-chunks for those only), and an init cost within 2% of the general path's."""
+    X = f32_blobs(30000, 100, 40, seed=5, sigma=1.0)
+    g = native.Context(0, 0.5, 0)
+    t = native.upload_dense(g, X, "f32", native.kmeans_ld(100))
+
+    def init():
+        return native.kmeans_init(g, native.LocalComm(True), t, 400, "k-means||", 2, 13)
+
+    def cost(C):
+        return sum(float(((X[i:i + 2000, None, :] - C[None]) ** 2).sum(-1).min(1).sum())
+                   for i in range(0, len(X), 2000))
+
+    cs = init()
+    assert np.array_equal(cs, init())
+    monkeypatch.setenv("OAP_KMEANS_INIT_SUPER", "0")
+    cp = init()
+    monkeypatch.setenv("OAP_KMEANS_INIT_SUPER", "1")
+    assert np.array_equal(init(), cp)
+    assert abs(cost(cs) - cost(cp)) <= 0.02 * cost(cp)
+
+
 def test_api_uses_gpu_engine(gpu_world):
     X = f32_blobs(10000, 16, 6, seed=9)
     m = O.KMeans(k=6, seed=3).fit(X)
