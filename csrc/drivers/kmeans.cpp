@@ -1432,6 +1432,18 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // when the image fits beside the arena's other buffers with a quarter of its budget to spare.
   Buffer img_b, img_beta_b;
   bool img_ready = false;
+  // (the fallback check: the image scale read back into pinned memory)
+  Buffer imgchk_h = ctx.alloc_pinned(sizeof(float));
+  bool imgchk_pending = false;
+  double row_norm_cap = 0.0;  // >= every row's |x| on every rank (global column maxima)
+  for (int f = 0; f < d; ++f) row_norm_cap += absmax[f] * absmax[f];
+  row_norm_cap = std::isfinite(row_norm_cap) ? std::sqrt(row_norm_cap) : 1e300;
+  double init_cmax = 0.0;  // the largest |c| of the initial centers
+  for (int c = 0; c < k; ++c) {
+    double s2 = 0.0;
+    for (int f = 0; f < d; ++f) s2 += centers[size_t(c) * d + f] * centers[size_t(c) * d + f];
+    init_cmax = std::max(init_cmax, std::sqrt(s2));
+  }
   {
     const char* e = std::getenv("OAP_KMEANS_IMAGE");
     const size_t ib = kern::kmeans_lloyd_image_bytes(x.rows, x.cols);
@@ -1640,7 +1652,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           req.img_mode = 2;
       }
       int nb = gpu_assign(ctx, x, g, req, s);
-      if (req.img_mode == 1) img_ready = true;
+      if (req.img_mode == 1) {
+        img_ready = true;
+        // the image's scale, read back with the batch: whether the f32 fallback launch
+        // after every image pass can be retired (below)
+        OAP_HIP_CHECK(hipMemcpyAsync(imgchk_h.data(), img_beta_b.data(), sizeof(float),
+                                     hipMemcpyDeviceToHost, s));
+        imgchk_pending = true;
+      }
       if (cdelta)
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), cloc_b.data(), sizeof(u64) * (kd + k),
                                      hipMemcpyDeviceToDevice, s));
@@ -1697,6 +1716,16 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       OAP_HIP_CHECK(hipMemcpyAsync(&pruned_now, pruned_d.data(), sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     comm.wait(s);
+    if (imgchk_pending) {
+      // every later center is a mean of rows (of any rank) or a center that never moved, so
+      // its norm stays below the larger of the global column-max bound on the rows' norms and
+      // the initial centers' largest (margin for the fp32 means): then the image's scale holds
+      // every later plane and kmeans_lloyd's img_mode-3 fallback (a launch that would exit at
+      // once) is not needed
+      imgchk_pending = false;
+      if (double(imgchk_h.as<float>()[0]) * std::max(row_norm_cap, init_cmax) * 1.001 <= 512.0)
+        req.img_fallback = false;
+    }
     const float ms_batch = pev ? 0.f : Event::elapsed_ms(ev[0].e0, ev[nb_it - 1].e3);
     for (int b = 0; b < nb_it; ++b) {
       const int it = it0 + b;
