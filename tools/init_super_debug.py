@@ -22,7 +22,8 @@ for mode in ("0", "1", "2", "3"):
     out[mode] = N.kmeans_init(g, N.LocalComm(True), tg, 400, "k-means||", 2, 13)
 ref = N.kmeans_init(cc, N.LocalComm(False), tc, 400, "k-means||", 2, 13)
 for mode, v in out.items():
-    print(mode, "eq_precise", bool(np.array_equal(v, out["0"])), "eq_cpu", bool(np.array_equal(v, ref)))
+    print(mode, "eq_precise", bool(np.array_equal(v, out["0"])),
+          "eq_cpu", bool(np.array_equal(v, ref)))
 # the lean chunked pass's labels / distances against numpy for 800 centers
 C = X[rng.choice(n, 800, replace=False)] + 1e-3
 lab, dist = N.kmeans_predict(g, tg, C)
