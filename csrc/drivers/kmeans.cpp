@@ -1275,7 +1275,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer inv_scale = ctx.alloc(sizeof(double) * d);
   // one flags slot per iteration of a batch (read back once per batch), the finalize's
   // last-block counter, the cost accumulator (zeroed by the finalize that reads it)
-  Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags) * 16);
+  Buffer flags_d = ctx.alloc(sizeof(kern::KMeansFlags) * 32);
   Buffer fin_done = ctx.alloc(sizeof(unsigned));
   ctx.memset(fin_done.data(), 0, sizeof(unsigned), s);
   ctx.memset(cost_d.data(), 0, sizeof(double), s);
@@ -1536,9 +1536,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // kBatch iterations are enqueued back to back (kernels + collective, no host round trip in
   // between) and their flags / timings are read once per batch — the host re-checks the
   // adaptive distance tier at every batch boundary.
-  // (16: a 20-iteration fit has 3 batch boundaries — each a host round trip, ~130 us with its
-  // read-backs — instead of 4; flags_d slots)
-  constexpr int kBatch = 16;
+  // (32: a 20-iteration fit has 2 batch boundaries — each a host round trip, ~130 us with its
+  // read-backs; flags_d slots)
+  constexpr int kBatch = 32;
   const int B = p.tol < 0 ? kBatch : 1;
   struct IterEvents {
     Event e0, e1, e2, e3;

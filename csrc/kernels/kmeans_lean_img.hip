@@ -488,7 +488,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     int* ring = reinterpret_cast<int*>(smem + L.ring) + wave * kRing;
     const float dmax = ufl(a.drift[k]);
     const float cm2 = ufl(cmax * cmax);
-    const __amdgpu_buffer_rsrc_t rs_xn = buf_rsrc(a.scan_xnorm + t0, uint32_t(dense_pos * 4));
+    // (the tile norms of a pair are wave-uniform: scalar loads, held in SGPRs across the tiles
+    // in between, so the prefetch costs the pipelined loop only its three vector registers)
+    typedef const float __attribute__((address_space(4)))* xn_cptr;
+    const xn_cptr xn_seg = (xn_cptr)(a.scan_xnorm + t0);
     unsigned head = 0, tail = 0;  // wave-uniform ring positions
     int64_t sq = wave;            // the next tile pair to scan (wave-uniform)
     // the scan of tile pair sq reads bounds, label and tile norm one step ahead: issued when the
@@ -496,7 +499,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     // offsets past the wave's rows read zeros)
     u32x2 pbw;
     int plab;
-    float pxn;
+    float pxn0, pxn1;
     auto issue = [&]() OAP_AI {
       const int64_t q = sq + h * stride;
       const uint32_t roff = uint32_t(q * 32 + r);
@@ -504,7 +507,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       pbw = __builtin_bit_cast(
           u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, in ? roff * 8u : kBufOff, 0, 0));
       plab = buf_load_b32(rs_lab, roff * 4u, in);
-      pxn = __int_as_float(buf_load_b32(rs_xn, uint32_t(q) * 4u, in));
+      const int64_t q0 = sq < dense_pos ? sq : dense_pos - 1;
+      const int64_t q1 = sq + stride < dense_pos ? sq + stride : dense_pos - 1;
+      pxn0 = xn_seg[q0 < 0 ? 0 : q0];
+      pxn1 = xn_seg[q1 < 0 ? 0 : q1];
     };
     auto refill = [&]() OAP_AI {
       while (tail - head < 64u && sq < dense_pos) {
@@ -513,7 +519,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
         const bool in = q < dense_pos && int64_t(roff) < wrows;
         const float u = __uint_as_float(pbw[0]) + dr_l[min(max(plab, 0), k - 1)];
         const float lk = __uint_as_float(pbw[1]) - dmax;
-        const bool ok = in && lk > 0.f && (lk - u) * (lk + u) > mrel * (pxn + cm2);
+        const float xn = h ? pxn1 : pxn0;
+        const bool ok = in && lk > 0.f && (lk - u) * (lk + u) > mrel * (xn + cm2);
         buf_store_f2(rs_bnd, roff * 8u, make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f)),
                      ok && dmax > 0.f);
         const bool act = in && !ok;
@@ -533,20 +540,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       const int e = ring[(i + unsigned(r)) & (kRing - 1)];
       return i + unsigned(r) < tail ? row0 + e : int64_t(-1);
     };
+    // (the rows of the current tile are re-read from the ring rather than carried across a
+    // tile: after a refill the current tile is complete unless the scan is exhausted, so its
+    // slots — whose operands were prefetched — are unchanged)
     const int64_t rfix = row0;
     f16x8 xa[KS], xb[KS];
     refill();
-    int64_t ra = ring_row(head), rb = -1;
-    load_img_row(ra >= 0 ? ra : rfix, xa);
+    {
+      const int64_t r0v = ring_row(head);
+      load_img_row(r0v >= 0 ? r0v : rfix, xa);
+    }
     while (head < tail) {  // (wave-uniform)
       refill();
-      rb = ring_row(head + 32u);
-      body(0, ra, rb >= 0 ? rb : rfix, nullptr, xa, xb);
+      {
+        const int64_t nx = ring_row(head + 32u);
+        body(0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xa, xb);
+      }
       head = tail - head > 32u ? head + 32u : tail;
       if (head == tail) break;
       refill();
-      ra = ring_row(head + 32u);
-      body(0, rb, ra >= 0 ? ra : rfix, nullptr, xb, xa);
+      {
+        const int64_t nx = ring_row(head + 32u);
+        body(0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xb, xa);
+      }
       head = tail - head > 32u ? head + 32u : tail;
     }
   } else if constexpr (PD == 1) {
