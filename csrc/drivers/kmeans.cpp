@@ -1320,6 +1320,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // chunked lean pass with delta accumulation: local statistics persist, the labels alternate
   // between two buffers so the previous assignment is at hand (moved rows only)
   const bool cdelta = lean_chunked && p.delta && x.rows > 0;
+  // (rank-uniform form) chunked lean iterations compute the cost only where it is reported, as
+  // the single-launch delta path does: the first and a known last iteration, otherwise one
+  // exact pass over the labels after the loop (a costless last chunk runs the kernel without
+  // the per-row f32 distance: ~12% of the pass at 1B rows, k = 1000)
+  const bool cfree_all = lean_chunked && p.delta;
   Buffer cloc_b, lab_prev_b;
   int32_t* lab_prev = nullptr;
   int64_t cmoved = 0;
@@ -1386,7 +1391,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                         sizeof(unsigned) * size_t(lgrid) + 64);
     req.xnorm = xnorm_b.as<float>();
   }
-  if (delta) cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
+  if (delta || cdelta) cbak_b = ctx.alloc(sizeof(float) * size_t(g.kpad) * g.dp);
   // Row-level scan (image passes): per row, the Hamerly test the tile scan applies to whole
   // 32-row tiles; the image kernel then gathers only the rows it could not prune.  On overlapping
   // clusters a tile almost always holds a row near a boundary, while most rows are far from one
@@ -1605,7 +1610,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // over the labels after the loop
       // (with the row scan, a known last iteration is a scan pass too: the exact cost pass over
       // the labels after the loop reads the f32 rows once, cheaper than a full f32 cost pass)
-      const bool cost_it = !req.fast1 || !delta_all || it == 0 ||
+      const bool cost_it = !req.fast1 || !(delta_all || cfree_all) || it == 0 ||
                            (p.tol < 0 && it == p.max_iter - 1 && !row_scan_shape);
       req.cost_slab = cost_it ? slab.as<double>() : nullptr;
       it_costless[b] = !cost_it || scan_it_all;
@@ -1653,6 +1658,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         else if (img_ready && delta_it && !req.cost_slab && !req.mindist && !req.xnorm)
           req.img_mode = 2;
       }
+      // (the lean chunked pass keeps its running state in its own buffers: no per-row distance
+      // unless a cost is asked for; the general chunked path re-seeds its own each iteration)
+      if (lean_chunked && x.rows > 0) req.mindist = req.fast1 ? nullptr : mind_keep.as<float>();
       int nb = gpu_assign(ctx, x, g, req, s);
       if (req.img_mode == 1) {
         img_ready = true;
@@ -1662,9 +1670,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                                      hipMemcpyDeviceToHost, s));
         imgchk_pending = true;
       }
-      if (cdelta)
+      if (cdelta) {
         OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), cloc_b.data(), sizeof(u64) * (kd + k),
                                      hipMemcpyDeviceToDevice, s));
+        if (p.tol >= 0 || it == p.max_iter - 1)  // (the final exact-cost pass's centers)
+          OAP_HIP_CHECK(hipMemcpyAsync(cbak_b.data(), g.c32.data(),
+                                       sizeof(float) * size_t(g.kpad) * g.dp,
+                                       hipMemcpyDeviceToDevice, s));
+      }
       if (req.xnorm && !req.tile_list) xnorm_ready = true;
       // (a device communicator reduces the local statistics out of place into stats)
       const bool stats_oop = delta && !fin_direct && comm.on_device();
@@ -1831,12 +1844,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
     }
   }
-  if (delta_all && last_costless && res.num_iter > 1) {
+  if ((delta_all || cfree_all) && last_costless && res.num_iter > 1) {
     // exact cost of a last scan iteration: every row against the centers it was assigned to,
     // with the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
     TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
     Buffer md;  // outlives the copy_to_host below (which synchronizes the stream)
-    if (!delta) {
+    if (!delta && !cdelta) {
       OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
     } else {
       kern::KMeansAssignArgs ca;
@@ -1851,10 +1864,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       ca.labels = req.labels;
       int nb = kern::kmeans_label_cost(ca, slab.as<double>(), std::min(nslab, 2048), s);
       if (nb < 0) {  // centers beyond LDS: per-row costs through the seed kernel
-        md = ctx.alloc(sizeof(float) * x.rows);
-        ca.mindist = md.as<float>();
+        if (!mind_keep.data()) md = ctx.alloc(sizeof(float) * x.rows);
+        ca.mindist = mind_keep.data() ? mind_keep.as<float>() : md.as<float>();
         kern::kmeans_seed_mindist(ca, s);
-        nb = kern::reduce_sum_f32(md.as<float>(), x.rows, slab.as<double>(), s);
+        nb = kern::reduce_sum_f32(ca.mindist, x.rows, slab.as<double>(), s);
       }
       kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
     }
