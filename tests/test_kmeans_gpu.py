@@ -514,6 +514,29 @@ def test_lean_chunked_large_k_bitwise(native, monkeypatch, d, k, sigma, dtype):
     assert (lab == ref_lab).mean() > 0.9999
 
 
+def test_lean_chunked_cost_only_where_reported(native):
+    """Chunked lean iterations compute the cost only at the first and a known last pass; with a
+    tolerance (last pass unknown) the final cost comes from one exact pass over the labels after
+    the loop.  Same centers either way, the final cost equal to the in-pass one (per-row fp32,
+    summed in fp64 in another order) and to the exact-fp32 fit's."""
+    n, d, k = 60000, 100, 1000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d, "bf16"), 0, k, 10.0, 6.0, 9, "bf16")
+    init = bf16_round(t.to_numpy(g, 0, k) + 0.25)
+    comm = native.LocalComm(True)
+    rf = native.kmeans_fit(g, comm, t, init, k, 4, -1.0)  # fixed count: last pass costed
+    rt = native.kmeans_fit(g, comm, t, init, k, 4, 0.0)  # tol 0: final pass after the loop
+    rp = native.kmeans_fit(g, comm, t, init, k, 4, -1.0, precise=True)
+    assert rf["num_iter"] == rt["num_iter"] == 4
+    for r in (rt, rp):
+        assert np.array_equal(r["centers"], rf["centers"])
+    hf = np.array(rf["cost_history"])
+    assert np.isfinite(hf[0]) and np.isfinite(hf[-1]) and np.isnan(hf[1:-1]).all()
+    assert np.isfinite(rt["cost"])
+    assert abs(rt["cost"] - rf["cost"]) <= 1e-12 * rf["cost"]
+    assert abs(rf["cost"] - rp["cost"]) <= 1e-9 * rp["cost"]
+
+
 
 @pytest.mark.parametrize("d,k,sigma", [(50, 200, 8.0), (20, 37, 4.0), (12, 7, 4.0), (60, 100, 6.0),
                                        (100, 50, 5.0), (40, 230, 4.0), (26, 160, 3.0)])
