@@ -105,7 +105,7 @@ __global__ void oap_kmeans_accumulate_global(const T* x, int64_t n, int ld, int 
 // change a bit).  Table layout: cluster stride `rs` (odd), segment stride EPS + 1 doubles, so
 // the SEG lanes of one row hit distinct banks.  One global int64 atomic per (cluster, feature)
 // per block at the end.  Replaces a global atomic per row element.
-constexpr int kAccThreads = 1024;  // one workgroup per CU (LDS): 4 waves per SIMD in flight
+constexpr int kAccThreads = 512;  // (1024: 60 -> 63 ms at 1B rows, k = 1000)
 constexpr int kAccU = 4;
 template <typename T>
 __global__ __launch_bounds__(kAccThreads) void oap_kmeans_accumulate_owned(
