@@ -526,8 +526,8 @@ __global__ __launch_bounds__(kBinThreads) void oap_kmeans_bin_scatter_e(const in
 
 __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a) {
   __shared__ int s_conv, s_nonempty;
-  __shared__ double s_shift[256];
-  __shared__ float s_norm[256], s_drift[256];
+  __shared__ double s_shift[4];
+  __shared__ float s_norm[4], s_drift[4];
   if (threadIdx.x == 0) {
     s_conv = 1;
     s_nonempty = 0;
@@ -566,14 +566,23 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
     a.cnorm[c] = static_cast<float>(nrm);
     my_nmax = fmaxf(my_nmax, sqrtf(static_cast<float>(nrm)));
   }
-  s_shift[threadIdx.x] = my_max;
-  s_norm[threadIdx.x] = my_nmax;
-  s_drift[threadIdx.x] = my_drift;
+  // wave maxima by shuffles, then the block's 4 waves (a serial loop over 256 LDS slots was
+  // most of the finalize's ~16 us)
+  for (int m = 32; m >= 1; m >>= 1) {
+    my_max = fmax(my_max, __shfl_xor(my_max, m, 64));
+    my_nmax = fmaxf(my_nmax, __shfl_xor(my_nmax, m, 64));
+    my_drift = fmaxf(my_drift, __shfl_xor(my_drift, m, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_shift[threadIdx.x >> 6] = my_max;
+    s_norm[threadIdx.x >> 6] = my_nmax;
+    s_drift[threadIdx.x >> 6] = my_drift;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     double mx = 0.0;
     float nm = 0.f, dm = 0.f;
-    for (int i = 0; i < int(blockDim.x); ++i) {
+    for (int i = 0; i < int(blockDim.x) / 64; ++i) {
       mx = fmax(mx, s_shift[i]);
       nm = fmaxf(nm, s_norm[i]);
       dm = fmaxf(dm, s_drift[i]);
@@ -591,8 +600,8 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
 
 // The flags of a multi-block finalize from the per-cluster scratch (one block of 256 threads).
 __device__ void finalize_flags_block(const KMeansFinalizeArgs& a) {
-  __shared__ double s_shift[256];
-  __shared__ float s_norm[256], s_drift[256];
+  __shared__ double s_shift[4];
+  __shared__ float s_norm[4], s_drift[4];
   __shared__ int s_conv, s_nonempty;
   if (threadIdx.x == 0) {
     s_conv = 1;
@@ -611,14 +620,23 @@ __device__ void finalize_flags_block(const KMeansFinalizeArgs& a) {
     my_nmax = fmaxf(my_nmax, static_cast<float>(a.scratch[a.k + c]));
     if (a.drift) my_drift = fmaxf(my_drift, a.drift[c]);
   }
-  s_shift[threadIdx.x] = my_max;
-  s_norm[threadIdx.x] = my_nmax;
-  s_drift[threadIdx.x] = my_drift;
+  // wave maxima by shuffles, then the block's 4 waves (a serial loop over 256 LDS slots was
+  // most of the finalize's ~16 us)
+  for (int m = 32; m >= 1; m >>= 1) {
+    my_max = fmax(my_max, __shfl_xor(my_max, m, 64));
+    my_nmax = fmaxf(my_nmax, __shfl_xor(my_nmax, m, 64));
+    my_drift = fmaxf(my_drift, __shfl_xor(my_drift, m, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_shift[threadIdx.x >> 6] = my_max;
+    s_norm[threadIdx.x >> 6] = my_nmax;
+    s_drift[threadIdx.x >> 6] = my_drift;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     double mx = 0.0;
     float nm = 0.f, dm = 0.f;
-    for (int i = 0; i < int(blockDim.x); ++i) {
+    for (int i = 0; i < int(blockDim.x) / 64; ++i) {
       mx = fmax(mx, s_shift[i]);
       nm = fmaxf(nm, s_norm[i]);
       dm = fmaxf(dm, s_drift[i]);
@@ -640,14 +658,16 @@ __device__ void finalize_flags_block(const KMeansFinalizeArgs& a) {
 // order (lane 0), so results are bitwise unchanged.
 __global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinalizeArgs a) {
   __shared__ double s_df[4][256];
-  __shared__ float s_dv[4][256];
+  __shared__ float s_dv[4][256], s_v[4][256];
   __shared__ bool s_last;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * 4 + w;
   if (c < a.k) {
     const long long cntv = static_cast<long long>(a.counts[c]);
     double* c64 = a.centers64 + size_t(c) * a.d;
-    double dr2 = 0.0;  // lane 0: squared movement of the fp32 center
+    // lane 0: the shift, the squared movement of the fp32 center and |c|^2 (fp32 values), each
+    // summed in feature order from this wave's LDS rows (no serial global reads)
+    double sh = 0.0, dr2 = 0.0, nrm = 0.0;
     for (int f0 = 0; f0 < a.d; f0 += 256) {
       const int nf = min(256, a.d - f0);
       for (int f = lane; f < nf; f += 64) {
@@ -664,28 +684,24 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinali
         a.centers32[size_t(c) * a.dp + f0 + f] = v;
         s_df[w][f] = df;
         s_dv[w][f] = dv;
+        s_v[w][f] = v;
       }
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) {
-        double sh = f0 == 0 ? 0.0 : a.scratch[c];
+#pragma unroll 8
         for (int f = 0; f < nf; ++f) {
           sh += s_df[w][f] * s_df[w][f];
           dr2 += double(s_dv[w][f]) * double(s_dv[w][f]);
+          nrm += double(s_v[w][f]) * double(s_v[w][f]);
         }
-        a.scratch[c] = sh;
       }
       __builtin_amdgcn_wave_barrier();
     }
-    if (lane == 0 && a.drift) a.drift[c] = static_cast<float>(sqrt(dr2) * (1.0 + 1e-6));
     if (lane == 0) {
-      double nrm = 0.0;
-      for (int f = 0; f < a.d; ++f) {
-        const double v = double(static_cast<float>(c64[f]));
-        nrm += v * v;
-      }
+      if (a.drift) a.drift[c] = static_cast<float>(sqrt(dr2) * (1.0 + 1e-6));
       a.cnorm[c] = static_cast<float>(nrm);
       a.scratch[a.k + c] = double(sqrtf(static_cast<float>(nrm)));
-      if (cntv <= 0) a.scratch[c] = -1.0;  // empty: keeps its center, not part of the test
+      a.scratch[c] = cntv <= 0 ? -1.0 : sh;  // empty: keeps its center, not part of the test
     }
   }
   if (!a.done) return;
