@@ -536,6 +536,7 @@ PYBIND11_MODULE(_native, m) {
         out["image_passes"] = r.image_passes;
         out["pruned_rows"] = r.pruned_rows;
         out["image_bytes"] = r.image_bytes;
+        out["final_cost_path"] = r.final_cost_path;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

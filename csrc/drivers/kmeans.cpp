@@ -1185,6 +1185,58 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
 }
 
 // ------------------------------------------------------------------------------- fit
+// The exact cost of the last assignment from the fit's own statistics, without a pass over
+// the rows:  sum_i |x_i - c_l(i)|^2 = sum_i |x_i|^2 - 2 sum_c c.S_c + sum_c n_c |c|^2, with
+// sum_i |x_i|^2 cached on the table (fp64, exact squares: one pass per table, like the column
+// maxima), S_c and n_c the global fixed-point statistics the last finalize used and c the fp32
+// centers that assignment used.  The rigorous error bound — fixed-point quantisation of S_c
+// (|S~ - S| <= n_c q_f / 2 per feature) plus fp64 rounding — must stay within 1e-9 of the
+// result, else (rows far from the origin, a table layout without the norm kernel) it returns
+// false and the caller runs the per-row pass.  Rank-uniform: every input is global (the norm
+// sum is allreduced), so every rank takes the same branch.
+static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const u64* sums_d,
+                           const u64* counts_d, const float* centers_d, int k, int d, int dp,
+                           const std::vector<double>& inv_scale, double* cost) {
+  double t_err = 0.0;
+  double T = local_row_sqnorm(ctx, x, &t_err);
+  double terr_abs = std::isfinite(T) ? t_err * T : std::numeric_limits<double>::quiet_NaN();
+  if (!comm.trivial()) {
+    T = comm_allreduce_scalar(ctx, comm, T, ReduceOp::Sum);
+    terr_abs = comm_allreduce_scalar(ctx, comm, terr_abs, ReduceOp::Sum);
+  }
+  if (!std::isfinite(T) || !std::isfinite(terr_abs)) return false;
+  const size_t kd = size_t(k) * d;
+  std::vector<u64> sh(kd), nh(k);
+  std::vector<float> ch(size_t(k) * dp);
+  ctx.copy_to_host(sh.data(), sums_d, sizeof(u64) * kd);
+  ctx.copy_to_host(nh.data(), counts_d, sizeof(u64) * k);
+  ctx.copy_to_host(ch.data(), centers_d, sizeof(float) * ch.size());
+  double A = 0.0, A_abs = 0.0, B = 0.0, q_err = 0.0;
+  for (int c = 0; c < k; ++c) {
+    const double n = double(static_cast<long long>(nh[c]));
+    double a = 0.0, aa = 0.0, b = 0.0, qe = 0.0;
+    for (int f = 0; f < d; ++f) {
+      const double cf = ch[size_t(c) * dp + f];
+      const double s = double(static_cast<long long>(sh[size_t(c) * d + f])) * inv_scale[f];
+      a += cf * s;
+      aa += std::fabs(cf * s);
+      b += cf * cf;
+      qe += std::fabs(cf) * inv_scale[f];
+    }
+    A += a;
+    A_abs += aa;
+    B += n * b;
+    q_err += n * qe;  // 2 |c| (n q / 2)
+  }
+  const double v = T - 2.0 * A + B;
+  const double u = 1.12e-16;
+  const double err = terr_abs + q_err + double(kd + k + 8) * u * (2.0 * A_abs + B) +
+                     4.0 * u * (T + 2.0 * A_abs + B);
+  if (!(v > 0.0) || err > 1e-9 * v) return false;
+  *cost = v;
+  return true;
+}
+
 KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                         const std::vector<double>& init_centers, const KMeansParams& p) {
   OAP_CHECK(p.k > 1 || p.init == KMeansInit::Given, "k must be > 1");
@@ -1849,36 +1901,48 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     // with the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
     TraceRange tc(&M, "kmeans/final_cost", int64_t(x.bytes()));
     Buffer md;  // outlives the copy_to_host below (which synchronizes the stream)
-    if (!delta && !cdelta) {
-      OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+    // (rank-uniform: the dtype, the shape and the env are; the helper's inputs are global)
+    double c_stats = 0.0;
+    const char* fc_env = std::getenv("OAP_KMEANS_FINAL_COST");  // "rows": the per-row pass
+    const bool try_stats = delta_all && x.dtype == DType::F32 && !(fc_env && *fc_env == 'r');
+    if (try_stats && final_cost_from_stats(ctx, comm, x, fa.sums, fa.counts, cbak_b.as<float>(),
+                                           k, d, g.dp, fp.inv_scale, &c_stats)) {
+      res.cost = c_stats;
+      res.cost_history.back() = c_stats;
+      res.final_cost_path = "stats";
     } else {
-      kern::KMeansAssignArgs ca;
-      ca.x = x.data.data();
-      ca.xbf16 = x.dtype == DType::BF16;
-      ca.n = x.rows;
-      ca.ld = static_cast<int>(x.ld);
-      ca.d = x.cols;
-      ca.centers = cbak_b.as<float>();
-      ca.k = k;
-      ca.kpad = g.kpad;
-      ca.labels = req.labels;
-      int nb = kern::kmeans_label_cost(ca, slab.as<double>(), std::min(nslab, 2048), s);
-      if (nb < 0) {  // centers beyond LDS: per-row costs through the seed kernel
-        if (!mind_keep.data()) md = ctx.alloc(sizeof(float) * x.rows);
-        ca.mindist = mind_keep.data() ? mind_keep.as<float>() : md.as<float>();
-        kern::kmeans_seed_mindist(ca, s);
-        nb = kern::reduce_sum_f32(ca.mindist, x.rows, slab.as<double>(), s);
+      res.final_cost_path = "rows";
+      if (!delta && !cdelta) {
+        OAP_HIP_CHECK(hipMemsetAsync(cost_d.data(), 0, sizeof(double), s));
+      } else {
+        kern::KMeansAssignArgs ca;
+        ca.x = x.data.data();
+        ca.xbf16 = x.dtype == DType::BF16;
+        ca.n = x.rows;
+        ca.ld = static_cast<int>(x.ld);
+        ca.d = x.cols;
+        ca.centers = cbak_b.as<float>();
+        ca.k = k;
+        ca.kpad = g.kpad;
+        ca.labels = req.labels;
+        int nb = kern::kmeans_label_cost(ca, slab.as<double>(), std::min(nslab, 2048), s);
+        if (nb < 0) {  // centers beyond LDS: per-row costs through the seed kernel
+          if (!mind_keep.data()) md = ctx.alloc(sizeof(float) * x.rows);
+          ca.mindist = mind_keep.data() ? mind_keep.as<float>() : md.as<float>();
+          kern::kmeans_seed_mindist(ca, s);
+          nb = kern::reduce_sum_f32(ca.mindist, x.rows, slab.as<double>(), s);
+        }
+        kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
       }
-      kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
+      if (!comm.trivial()) {
+        comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+        if (comm.on_device()) comm.wait(s);  // the watchdog covers this collective too
+      }
+      double c = 0.0;
+      ctx.copy_to_host(&c, cost_d.data(), sizeof(double), s);
+      res.cost = c;
+      res.cost_history.back() = c;
     }
-    if (!comm.trivial()) {
-      comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
-      if (comm.on_device()) comm.wait(s);  // the watchdog covers this collective too
-    }
-    double c = 0.0;
-    ctx.copy_to_host(&c, cost_d.data(), sizeof(double), s);
-    res.cost = c;
-    res.cost_history.back() = c;
   }
   res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);
   res.centers.resize(kd);

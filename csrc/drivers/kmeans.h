@@ -67,6 +67,10 @@ struct KMeansResult {
   int image_passes = 0;       // lean passes that took their operands from the fp16 row image
   int64_t image_bytes = 0;    // HBM of that image (0: not allocated)
   std::string assign_path = "cpu";  // the distance kernel path of the last iteration (GPU)
+  // how a last assignment that computed no cost in its pass got one: "stats" (from the fit's
+  // statistics, kmeans.cpp final_cost_from_stats), "rows" (a pass over the labels), "" (none
+  // needed: the last pass computed it)
+  std::string final_cost_path;
 };
 
 // Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for

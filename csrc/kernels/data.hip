@@ -70,6 +70,34 @@ __global__ __launch_bounds__(256) void oap_column_absmax4(const float4* x, int64
   }
 }
 
+// Per-block fp64 partial sums of |x|^2 over the rows (features < cols), the same flat float4
+// stream: K-Means takes the exact cost of its last assignment from its own statistics,
+// sum_i |x_i - c|^2 = sum_i |x_i|^2 - 2 c.S + n |c|^2 (drivers/kmeans.cpp), which needs this
+// sum once per table.  Squares of fp32 values are exact in fp64; a fixed grid and per-thread row
+// order make the partials (summed in order by the caller) deterministic.
+__global__ __launch_bounds__(256) void oap_row_sqnorm_partials4(const float4* x, int64_t rows,
+                                                               int ld4, int cols, double* part) {
+  __shared__ double red[4];
+  const int per_block = (256 / ld4) * ld4;
+  const int t = threadIdx.x;
+  double acc = 0.0;
+  if (t < per_block) {
+    const int cg = t % ld4, c0 = 4 * cg;
+    const double m0 = c0 < cols ? 1.0 : 0.0, m1 = c0 + 1 < cols ? 1.0 : 0.0;
+    const double m2 = c0 + 2 < cols ? 1.0 : 0.0, m3 = c0 + 3 < cols ? 1.0 : 0.0;
+    const int64_t rstride = int64_t(gridDim.x) * (per_block / ld4);
+    for (int64_t r = int64_t(blockIdx.x) * (per_block / ld4) + t / ld4; r < rows; r += rstride) {
+      const float4 v = x[r * ld4 + cg];
+      const double a = double(v.x), b = double(v.y), c = double(v.z), e = double(v.w);
+      acc += (a * a * m0 + b * b * m1) + (c * c * m2 + e * e * m3);
+    }
+  }
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if ((t & 63) == 0) red[t >> 6] = acc;
+  __syncthreads();
+  if (t == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // bf16 rows with ld % 8 == 0: the same flat-stream scheme with 16-byte groups of 8 columns.
 __global__ __launch_bounds__(256) void oap_column_absmax8_bf16(const bf16x8* x, int64_t rows,
                                                                int ld8, int cols, float* out) {
@@ -246,6 +274,17 @@ void column_absmax(const void* xv, DType t, int64_t rows, int cols, int64_t ld, 
   hipLaunchKernelGGL(oap_column_absmax<float>, dim3(grid), dim3(256), 0, s, x, rows, cols, ld,
                      out);
   OAP_HIP_CHECK(hipGetLastError());
+}
+
+int row_sqnorm_partials(const float* x, int64_t rows, int cols, int64_t ld, double* part,
+                        hipStream_t s) {
+  const bool aligned = reinterpret_cast<uintptr_t>(x) % 16 == 0;
+  if (rows <= 0 || ld % 4 != 0 || ld / 4 > 256 || !aligned) return -1;
+  hipLaunchKernelGGL(oap_row_sqnorm_partials4, dim3(kSqnormBlocks), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(x), rows, static_cast<int>(ld / 4), cols,
+                     part);
+  OAP_HIP_CHECK(hipGetLastError());
+  return kSqnormBlocks;
 }
 
 void synth_blobs(void* x, DType t, int64_t rows, int cols, int64_t ld, int64_t row0, int ncenters,

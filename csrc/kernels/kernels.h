@@ -23,6 +23,12 @@ void convert_pad(const void* src, DType src_t, int64_t rows, int cols, int64_t s
 // x is f32 or bf16 (t).
 void column_absmax(const void* x, DType t, int64_t rows, int cols, int64_t ld, float* out,
                    hipStream_t s);
+// sum_i |x_i|^2 of f32 rows [rows][ld] (first `cols` columns) as kSqnormBlocks fp64 partials
+// (deterministic; the caller sums them in order).  Returns the partial count, or -1 when the
+// layout is not supported (ld % 4 != 0, ld > 1024, rows not 16-byte aligned) or rows == 0.
+constexpr int kSqnormBlocks = 2048;
+int row_sqnorm_partials(const float* x, int64_t rows, int cols, int64_t ld, double* part,
+                        hipStream_t s);
 // Deterministic synthetic Gaussian blobs (hash RNG): rows [row0, row0+rows) of a global dataset,
 // x = center[label] + sigma * N(0,1) with centers uniform in [-box, box]^cols, stored as f32 or
 // bf16 (t; bf16 = the f32 value rounded to nearest even).

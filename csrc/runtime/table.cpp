@@ -2,6 +2,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <limits>
 
 #include "kernels/kernels.h"
 
@@ -203,6 +204,34 @@ std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t
     }
   }
   return mx;
+}
+
+double local_row_sqnorm(Context& ctx, DenseTable& t, double* rel_err) {
+  *rel_err = 0.0;
+  if (t.rows == 0) return 0.0;
+  if (t.local_sqnorm >= 0.0) {
+    *rel_err = t.local_sqnorm_rel_err;
+    return t.local_sqnorm;
+  }
+  if (!ctx.is_gpu() || t.dtype != DType::F32) return std::numeric_limits<double>::quiet_NaN();
+  Buffer part = ctx.alloc(sizeof(double) * kern::kSqnormBlocks);
+  const int nb = kern::row_sqnorm_partials(t.data.as<float>(), t.rows, t.cols, t.ld,
+                                           part.as<double>(), ctx.compute());
+  if (nb < 0) return std::numeric_limits<double>::quiet_NaN();
+  std::vector<double> h(nb);
+  ctx.copy_to_host(h.data(), part.data(), sizeof(double) * nb);
+  double sum = 0.0;
+  for (double v : h) sum += v;
+  // longest addition chain of any square: its thread's loop (one add per row group, 3 inside
+  // the 4-term expression), 6 shuffle levels, 2 in the block, nb on the host; each add of
+  // non-negative terms errs by at most u of the running (<= final) sum
+  const int64_t per_block = (256 / (t.ld / 4)) * (t.ld / 4);
+  const int64_t rstride = int64_t(nb) * (per_block / (t.ld / 4));
+  const double chain = double((t.rows + rstride - 1) / rstride + 3 + 6 + 2 + nb);
+  t.local_sqnorm = sum;
+  t.local_sqnorm_rel_err = chain * 1.12e-16;
+  *rel_err = t.local_sqnorm_rel_err;
+  return sum;
 }
 
 std::vector<double> table_rows_f64(Context& ctx, const DenseTable& t, int64_t r0, int64_t n) {

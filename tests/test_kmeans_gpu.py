@@ -149,8 +149,9 @@ def test_fast_path_bitwise_equals_precise(native, d, k):
     assert rf["tier3_tiles"] + rf["deferred_rows"] > 0
     assert rf["last_counts"] == rp["last_counts"]
     assert np.array_equal(rf["centers"], rp["centers"])
-    # identical per-row fp32 costs; the fp64 sum runs over a different row partition
-    assert abs(rf["cost"] - rp["cost"]) <= 1e-12 * rp["cost"]
+    # per-row fp32 costs (precise) vs the statistics identity of a costless last pass (within
+    # 1e-9 of the fp64 cost): both within the fp32 per-row rounding of each other
+    assert abs(rf["cost"] - rp["cost"]) <= 1e-7 * rp["cost"]
 
 
 def test_refinement_triggers_on_near_ties(native):
@@ -333,8 +334,10 @@ def test_pruning_is_exact(native, monkeypatch, d, k, dtype, n):
     fin = np.isfinite(hp) & np.isfinite(hu)
     assert fin[0] and np.isfinite(hp[-1]) and np.isfinite(hu[-1])
     np.testing.assert_allclose(hp[fin][:-1], hu[fin][:-1], rtol=1e-12)
-    assert abs(hp[-1] - hu[-1]) <= 1e-12 * hu[-1]
-    assert abs(rp["cost"] - ru["cost"]) <= 1e-12 * ru["cost"]
+    # (a costless last pass takes its cost from the statistics, within 1e-9 of the fp64 cost;
+    # the unpruned fit's last pass sums per-row fp32 costs)
+    assert abs(hp[-1] - hu[-1]) <= 1e-7 * hu[-1]
+    assert abs(rp["cost"] - ru["cost"]) <= 1e-7 * ru["cost"]
 
 
 @pytest.mark.parametrize("d,k,sigma,dtype", [(50, 200, 8.0, "f32"), (20, 64, 6.0, "f32"),
@@ -359,7 +362,7 @@ def test_lean_pass_bitwise_equals_precise_on_overlapping_data(native, d, k, sigm
         assert r["last_counts"] == rp["last_counts"]
         assert np.array_equal(r["centers"], rp["centers"])
     assert abs(rf["cost"] - rp["cost"]) <= 1e-12 * rp["cost"]
-    assert abs(rl["cost"] - rp["cost"]) <= 1e-12 * rp["cost"]
+    assert abs(rl["cost"] - rp["cost"]) <= 1e-7 * rp["cost"]  # (statistics identity)
     # deterministic: the deferral list is filled in tile order per wave
     rf2 = native.kmeans_fit(t_g, comm, t, init, k, 6, -1.0, prune=False)
     assert rf2["cost"] == rf["cost"] and rf2["deferred_rows"] == rf["deferred_rows"]
@@ -384,7 +387,37 @@ def test_operand_image_bitwise(native, monkeypatch, d, k, sigma, tol):
     for r in (ri, rr):
         assert r["last_counts"] == rp["last_counts"]
         assert np.array_equal(r["centers"], rp["centers"])
-        assert abs(r["cost"] - rp["cost"]) <= 1e-12 * rp["cost"]
+        assert abs(r["cost"] - rp["cost"]) <= 1e-7 * rp["cost"]
+
+
+def test_final_cost_from_statistics(native, monkeypatch):
+    """A last pass that computed no cost (row-scan fits) takes it from the fit's statistics:
+    sum |x|^2 - 2 c.S + n |c|^2 with a rigorous bound of 1e-9.  Checked against the fp64 cost of
+    the nearest-center assignment to the previous fit's centers (the last assignment's), and
+    the per-row pass taken instead for rows far from the origin (the bound fails)."""
+    n, d, k, it = 150000, 50, 200, 8
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, 8.0, 23)
+    X = t.to_numpy(g)
+    init = X[:k] + 0.25
+    comm = native.LocalComm(True)
+    r = native.kmeans_fit(g, comm, t, init, k, it, -1.0)
+    assert r["final_cost_path"] == "stats"
+    prev = native.kmeans_fit(g, comm, t, init, k, it - 1, -1.0)["centers"]
+    C = prev.astype(np.float32).astype(np.float64)  # the fp32 centers the last pass used
+    D = (X * X).sum(1)[:, None] + (C * C).sum(1)[None, :] - 2.0 * X @ C.T  # fp64
+    oracle = np.maximum(D.min(1), 0.0).sum()
+    assert abs(r["cost"] - oracle) <= 2e-9 * oracle
+    monkeypatch.setenv("OAP_KMEANS_FINAL_COST", "rows")
+    rr = native.kmeans_fit(g, comm, t, init, k, it, -1.0)
+    assert rr["final_cost_path"] == "rows" and np.array_equal(rr["centers"], r["centers"])
+    assert abs(rr["cost"] - oracle) <= 1e-7 * oracle
+    monkeypatch.delenv("OAP_KMEANS_FINAL_COST")
+    # rows far from the origin: the statistics bound fails (or the fit's last pass is costed
+    # itself): never the identity
+    t2 = native.upload_dense(g, X + 4096.0, "f32", native.kmeans_ld(d))
+    r2 = native.kmeans_fit(g, comm, t2, init + 4096.0, k, it, -1.0)
+    assert r2["final_cost_path"] != "stats" and np.isfinite(r2["cost"])
 
 
 def test_operand_image_scale_fallback(native):
