@@ -134,6 +134,8 @@ def test_gpu_world_two_ranks_host_comm_bitwise():
     for o in outs:
         assert o["engine"] == "gpu" and o["comm"] == "host"
         assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
+        # (the final cost's collectives: the statistics form allreduces sum |x|^2)
+        assert abs(o["cost"] - ref["cost"]) <= 1e-9 * ref["cost"]
 
 
 @pytest.mark.parametrize("d,k", [(50, 200), (16, 64), (100, 30)])
