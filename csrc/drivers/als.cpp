@@ -317,12 +317,16 @@ bool nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int 
     for (int i = 0; i < m; ++i) z[idx[i]] = rhs[i];
     return true;
   };
-  for (int outer = 0; outer < 3 * r + 10; ++outer) {
+  // (Lawson-Hanson safeguard: a coordinate whose entry was undone at once — its passive solve
+  // gave z_j <= 0 from x_j = 0, so it left again in the first inner step — is not offered again
+  // until the passive set changes otherwise; without that the same j would re-enter forever)
+  std::vector<char> blocked(r, 0);
+  for (int outer = 0; outer < 8 * r + 32; ++outer) {
     // gradient of the objective's negative: w = b - A x; the best free coordinate enters
     int jbest = -1;
     double wbest = tol;
     for (int j = 0; j < r; ++j) {
-      if (passive[j]) continue;
+      if (passive[j] || blocked[j]) continue;
       double w = b[j];
       for (int i = 0; i < r; ++i) w -= a(j, i) * x[i];
       if (w > wbest) {
@@ -354,8 +358,13 @@ bool nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int 
         }
       }
     }
+    if (!passive[jbest]) {
+      blocked[jbest] = 1;  // its entry was undone: skip it until the passive set moves
+    } else {
+      std::fill(blocked.begin(), blocked.end(), 0);
+    }
   }
-  return true;
+  return false;  // iteration cap: not reported as converged (the caller counts a failed row)
 }
 
 // Rows of X (global user order, stride ld) whose id appears in the caller's initial factors

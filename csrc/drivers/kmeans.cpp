@@ -1623,8 +1623,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (a probe batch scans its first iteration only: the next batch decides from it)
       // (the first batch scans its third iteration only: one right after the init's large
       // move rarely prunes)
-      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on && !row_scan_ok &&
-                               (!probing || b == 0);  // rank-uniform
+      // (rank-uniform: row_scan_shape, not row_scan_ok — the latter also needs this rank's rows
+      // and its image allocation, so a rank without rows or without room for the image would
+      // count tile-scan iterations its peers do not, and the per-batch collectives below that
+      // scan_iters gates would pair up differently across ranks)
+      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on && !row_scan_shape &&
+                               (!probing || b == 0);
       const bool scan_it = scan_it_all && scan;
       last_scanned = scan_it_all;
       it_scanned[b] = scan_it_all;

@@ -155,8 +155,11 @@ void Context::download_rows(void* dst, size_t dst_pitch, const void* src, size_t
   hipStream_t st = s ? s : compute();
   constexpr size_t kStage = size_t(64) << 20;
   const int64_t per = std::max<int64_t>(1, int64_t(kStage / width));
-  if (stage_[0].empty()) {
-    stage_[0] = Buffer::pinned(std::max(kStage, width));
+  // (one Context's staging pair: download_rows is not thread-safe per Context — callers
+  // serialise on the Context, as every driver does on its compute stream)
+  std::lock_guard<std::mutex> lk(stage_mu_);
+  if (stage_[0].empty() || stage_[0].bytes() < std::max(kStage, width)) {
+    stage_[0] = Buffer::pinned(std::max(kStage, width));  // (regrown for a wider row)
     stage_[1] = Buffer::pinned(std::max(kStage, width));
   }
   const int64_t nch = (rows + per - 1) / per;

@@ -106,7 +106,8 @@ class Context {
   std::unique_ptr<Stream> compute_, comm_, h2d_;
   std::unique_ptr<ThreadPool> pool_;
   Metrics metrics_;
-  Buffer stage_[2];  // download_rows staging (allocated on first use)
+  Buffer stage_[2];  // download_rows staging (allocated on first use, regrown for wider rows)
+  std::mutex stage_mu_;
 };
 
 // Number of visible HIP devices (0 when no GPU / no driver).

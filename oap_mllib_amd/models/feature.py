@@ -81,7 +81,17 @@ class PCA(_PCAParams, Estimator, DefaultParamsPersistence):
             # they fit the HBM budget (upload_table), else uploads them as f32
             table = upload_table(w, X, layout="pca_exact" if exact else "pca")
             r = N.pca_fit(w.ctx, w.comm, table, k, False, exact=exact)
-            extra["precision"] = "exact" if exact else "fast"
+            precision = "exact" if exact else "fast"
+            if exact and X.dtype == np.float64 and table.dtype != "f64":
+                # f64 input beyond the HBM budget went up as f32 rows: the statistics are exact
+                # fp64 products of ROUNDED rows (~1e-7 relative input error) — say so
+                precision = "exact_f32_rows"
+                import warnings
+
+                warnings.warn("PCA exact mode: the float64 rows exceed the HBM budget and were "
+                              "rounded to float32 on upload (fit_info['precision'] = "
+                              "'exact_f32_rows')", RuntimeWarning, stacklevel=2)
+            extra["precision"] = precision
             extra["device_rows_dtype"] = table.dtype
             pc, ev = np.asarray(r["pc"]), np.asarray(r["explained_variance"])
             extra.update({k_: r[k_] for k_ in ("stats_ms", "allreduce_ms", "eig_ms", "total_ms")})

@@ -328,13 +328,14 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
         return float(np.dot(Fu[0], Fi[0])) if fu[0] and fi[0] else float("nan")
 
     # ---- recommendations ---------------------------------------------------------------
-    def _topk(self, src_ids, S, dst_ids, D, num: int, dst_col: str, src_col: str):
+    def _topk(self, src_ids, S, dst_ids, D, num: int, dst_col: str, src_col: str,
+              replicated: bool = True):
         import pandas as pd
 
         import pyarrow as pa
 
         num = max(0, min(int(num), len(dst_ids)))
-        recs_idx, recs_val = _blocked_topk(S, D, num)
+        recs_idx, recs_val = _blocked_topk(S, D, num, replicated=replicated)
         # array<struct<dst: int, rating: float>> per source row, as ONE Arrow list array
         dst = np.asarray(dst_ids, dtype=np.int32)[recs_idx.reshape(-1)] if recs_idx.size else \
             np.zeros(0, np.int32)
@@ -364,7 +365,7 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
         found, U = self._lookup("user", keys)
         iids, I = self._mat("item")
         return self._topk(keys[found], U[found], iids, I, numItems, self.getOrDefault("itemCol"),
-                          self.getOrDefault("userCol"))
+                          self.getOrDefault("userCol"), replicated=False)
 
     def recommendForItemSubset(self, dataset, numUsers: int):  # noqa: N802,N803
         keys = np.unique(checked_cast(_frame(dataset)[self.getOrDefault("itemCol")].to_numpy(),
@@ -372,7 +373,7 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
         found, I = self._lookup("item", keys)
         uids, U = self._mat("user")
         return self._topk(keys[found], I[found], uids, U, numUsers, self.getOrDefault("userCol"),
-                          self.getOrDefault("itemCol"))
+                          self.getOrDefault("itemCol"), replicated=False)
 
     def copy(self, extra: dict | None = None) -> "ALSModel":
         m = super().copy(extra)
@@ -427,23 +428,27 @@ class ALSModel(_ALSModelParams, Model, MLWritable, MLReadable):
         return m
 
 
-def _blocked_topk(S: np.ndarray, D: np.ndarray, num: int, block: int = 4096):
+def _blocked_topk(S: np.ndarray, D: np.ndarray, num: int, block: int = 4096,
+                  replicated: bool = True):
     """Top-`num` (index, score) per row of S @ D^T, descending; ties by lower index.
 
-    Sharded by rank (Spark's blocked recommendForAll, ALS.scala:365-505, is distributed over the
-    source blocks): each rank takes a contiguous slab of S, then the slabs are allgathered.  On
-    a GPU world a slab runs through the fused score + top-k kernel (kernels/als_recommend.hip:
-    split-fp16 MFMA scores kept in registers, no score matrix anywhere) when num fits its
-    per-row lists; otherwise torch (rocBLAS GEMM + topk over row blocks), or numpy on CPU.
+    ``replicated`` (recommendForAll*: S is the model's factor matrix, the same on every rank):
+    sharded by rank as Spark's blocked recommendForAll is over the source blocks
+    (ALS.scala:365-505) — each rank takes a contiguous slab of S, then the slabs are
+    allgathered as typed int32 / fp32 row slabs.  Otherwise (the subset calls: S comes from this
+    rank's own dataset shard) every row is scored locally and nothing is exchanged.  On a GPU
+    world the scoring runs through the fused score + top-k kernel (kernels/als_recommend.hip:
+    split-fp16 MFMA scores kept in registers, no score matrix anywhere), numpy on CPU.
     """
     n = len(S)
     w = get_world()
-    lo, hi = (n * w.rank) // w.size, (n * (w.rank + 1)) // w.size
-    idx, val = _local_topk(S[lo:hi], D, num, w, block)
-    if w.size > 1:
-        parts = w.allgather_obj((idx, val))
-        idx = np.concatenate([p[0] for p in parts]) if n else idx
-        val = np.concatenate([p[1] for p in parts]) if n else val
+    if not replicated or w.size == 1:
+        return _local_topk(S, D, num, w, block)
+    bounds = [(n * r) // w.size for r in range(w.size + 1)]
+    counts = [bounds[r + 1] - bounds[r] for r in range(w.size)]
+    idx, val = _local_topk(S[bounds[w.rank]:bounds[w.rank + 1]], D, num, w, block)
+    idx = w.allgather_rows(idx.astype(np.int32), counts).astype(np.int64)
+    val = w.allgather_rows(val.astype(np.float32), counts)
     return idx, val
 
 

@@ -33,6 +33,36 @@ def kmeans_native(n=4000, d=6, k=5, seed=7, device="cpu", use_rccl=True, init_mo
     return out
 
 
+def kmeans_uneven(n=200000, d=16, k=20, seed=11, sigma=3.0, max_iter=12, tol=0.0,
+                  empty_rank=-1, no_image_rank=-1, device="gpu", use_rccl=False):
+    """Ranks that differ in what the row scan needs: one rank without rows (empty_rank) or one
+    without the fp16 operand image (no_image_rank: OAP_KMEANS_IMAGE=0 there), with tol >= 0 so
+    every iteration is its own batch and every per-batch collective must pair up across ranks."""
+    import oap_mllib_amd as O
+    from oap_mllib_amd import _loader
+
+    if no_image_rank >= 0 and int(os.environ.get("RANK", "0")) == no_image_rank:
+        os.environ["OAP_KMEANS_IMAGE"] = "0"
+    N = _loader.load()
+    w = O.init_world(O.get_config().replace(device=device, use_rccl=use_rccl))
+    X = _blobs(n, d, k, seed, sigma).astype(np.float32)
+    if w.size == 1:
+        local = X
+    elif w.rank == empty_rank:
+        local = X[:0]
+    else:
+        rest = [r for r in range(w.size) if r != empty_rank]
+        local = _shard(X, rest.index(w.rank), len(rest))
+    init = X[np.random.default_rng(seed).choice(n, k, replace=False)].astype(np.float64)
+    t = N.upload_dense(w.ctx, np.ascontiguousarray(local), "f32", N.kmeans_ld(d))
+    r = N.kmeans_fit(w.ctx, w.comm, t, init.ravel(), k, max_iter, tol)
+    out = {"rank": w.rank, "centers": np.asarray(r["centers"]).tolist(), "cost": r["cost"],
+           "iters": r["num_iter"], "comm": w.comm.name if w.comm is not None else None}
+    del t
+    O.shutdown_world()
+    return out
+
+
 def kmeans_vanilla(n=2000, d=4, k=3, seed=3):
     import oap_mllib_amd as O
 
@@ -143,6 +173,26 @@ def recommend_sharded(n=301, m=57, rank=6, num=7, seed=9):
            "first": first}
     O.shutdown_world()
     return out
+
+
+def recommend_subset(n=120, m=40, rank=5, num=6, seed=4):
+    """recommendForUserSubset with a DIFFERENT subset on each rank (each rank's own dataset
+    shard): every rank gets the recommendations of its own users, computed locally."""
+    import pandas as pd
+
+    import oap_mllib_amd as O
+
+    w = O.init_world(O.get_config().replace(device="cpu"))
+    rng = np.random.default_rng(seed)
+    U = rng.normal(size=(n, rank)).astype(np.float32)
+    V = rng.normal(size=(m, rank)).astype(np.float32)
+    model = O.ALSModel(rank=rank, user_arrays=(np.arange(n), U), item_arrays=(np.arange(m), V))
+    mine = np.arange(w.rank, n, 7 + w.rank)  # uneven subsets, different sizes per rank
+    out = model.recommendForUserSubset(pd.DataFrame({"user": mine}), num)
+    recs = {int(u): [int(r["item"]) for r in rs] for u, rs in
+            zip(out["user"].tolist(), out["recommendations"].tolist())}
+    O.shutdown_world()
+    return {"rank": w.rank, "users": mine.tolist(), "recs": {str(k): v for k, v in recs.items()}}
 
 
 def tcp_alltoallv(port, piece=0):

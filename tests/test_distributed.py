@@ -32,6 +32,23 @@ def test_kmeans_native_cpu_world_matches_single_process(nproc):
         np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-12)
 
 
+def test_kmeans_rank_without_rows_cpu():
+    """A rank that holds no rows still joins every collective of the fit (tol >= 0)."""
+    from dist_workers import kmeans_uneven
+
+    kw = dict(n=30000, d=8, k=9, device="cpu")
+    rc, outs = run_world("dist_workers", "kmeans_uneven", nproc=2, empty_rank=0, **kw)
+    assert rc == 0, outs
+    import oap_mllib_amd as O
+
+    O.shutdown_world()
+    ref = kmeans_uneven(**kw)
+    O.shutdown_world()
+    for o in outs:
+        assert o["iters"] == ref["iters"]
+        assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
+
+
 def test_kmeans_random_init_world_size_independent():
     rc, outs = run_world("dist_workers", "kmeans_native", nproc=2, device="cpu",
                          init_mode="random")
@@ -82,6 +99,22 @@ def test_tcp_comm_streamed_alltoallv(nproc, piece):
     assert rc == 0, outs
     for o in outs:
         assert o == {"a2a": True, "allreduce": True, "allgather": True}, outs
+
+
+def test_recommend_for_user_subset_per_rank():
+    """Subset calls score each rank's own keys locally (no cross-rank slab exchange), so ranks
+    with different subsets each get exactly their users' recommendations."""
+    rc, outs = run_world("dist_workers", "recommend_subset", nproc=2)
+    assert rc == 0, outs
+    rng = np.random.default_rng(4)
+    U = rng.normal(size=(120, 5)).astype(np.float32)
+    V = rng.normal(size=(40, 5)).astype(np.float32)
+    sc = U @ V.T
+    for o in outs:
+        assert sorted(int(u) for u in o["recs"]) == sorted(o["users"])
+        for u, items in o["recs"].items():
+            want = np.lexsort((np.arange(40), -sc[int(u)]))[:6].tolist()
+            assert items == want, (u, items, want)
 
 
 def test_recommend_for_all_sharded_by_rank():

@@ -138,6 +138,22 @@ def test_gpu_world_two_ranks_host_comm_bitwise():
         assert abs(o["cost"] - ref["cost"]) <= 1e-9 * ref["cost"]
 
 
+@pytest.mark.parametrize("case", [{"empty_rank": 1}, {"no_image_rank": 1}])
+def test_two_ranks_uneven_scan_state(case):
+    """A rank without rows, or without room for the operand image, takes different per-row
+    scan paths than its peer; the per-batch collectives must still pair up (tol >= 0: one
+    iteration per batch) and the fit must equal the one-rank fit of the same rows."""
+    from dist_workers import kmeans_uneven
+
+    rc, outs = run_world("dist_workers", "kmeans_uneven", nproc=2, timeout=240, **case)
+    assert rc == 0, outs
+    O.shutdown_world()
+    ref = kmeans_uneven()
+    for o in outs:
+        assert o["comm"] == "host" and o["iters"] == ref["iters"]
+        assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
+
+
 @pytest.mark.parametrize("d,k", [(50, 200), (16, 64), (100, 30)])
 def test_fast_path_bitwise_equals_precise(native, d, k):
     """bf16-split + refinement must reproduce the exact-fp32 kernel's assignments exactly."""
