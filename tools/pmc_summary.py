@@ -1,4 +1,4 @@
-"""Per-kernel PMC summary of rocprofv3 counter passes (tools/pmc_lean.sh, tools/pmc_img.sh):
+"""Per-kernel PMC summary of rocprofv3 counter passes (tools/gpu.sh pmc:<probe>:<pass> steps):
 counter totals of the named kernel's last dispatch in each pass, per-tile instruction counts,
 and busy fractions normalised by THAT dispatch's own duration (its Start/End_Timestamp in the
 counter CSV) — not by GRBM_GUI_ACTIVE alone, which the profiler accumulates over more than the
