@@ -537,6 +537,7 @@ PYBIND11_MODULE(_native, m) {
         out["pruned_rows"] = r.pruned_rows;
         out["image_bytes"] = r.image_bytes;
         out["final_cost_path"] = r.final_cost_path;
+        out["scale_source"] = r.scale_source;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

@@ -101,6 +101,41 @@ FixedPoint fixed_point_scales(const std::vector<double>& absmax, int64_t global_
   return fp;
 }
 
+// The fixed point's per-column bounds.  Provisional bounds from the initial centers,
+// B_f = 2^(ceil(log2 max_c |c_f|) + 3) (identical on every rank and engine: the centers are), are
+// taken whenever every row satisfies |x_f| < B_f; otherwise the global column maxima.  The rule
+// needs no pass over the rows up front: the GPU fit's first full pass checks a sufficient
+// condition (every |x_f| below min_f B_f: max3 chains, 16 VALU per 32-row tile) and only a
+// flagged row costs the column-maxima pass (then the rule is evaluated exactly on them).
+// Either way the scale is a function of (init centers, global column maxima), so the CPU engine,
+// the out-of-core fit and every world size derive the same integers.
+std::vector<double> center_bounds(const std::vector<double>& centers, int k, int d) {
+  std::vector<double> b(d, 0.0);
+  for (int f = 0; f < d; ++f) {
+    double m = 0.0;
+    for (int c = 0; c < k; ++c) m = std::max(m, std::fabs(centers[size_t(c) * d + f]));
+    b[f] = (m > 0.0 && std::isfinite(m)) ? std::ldexp(1.0, int(std::ceil(std::log2(m))) + 3) : 0.0;
+  }
+  return b;
+}
+
+// The provisional bounds cost up to 3 bits of the fixed point's resolution against the column
+// maxima; they apply only where the pass they save is worth it: datasets of at least
+// OAP_KMEANS_PROVISIONAL_MIN elements (global rows x features, default 2^28 — 1 GiB of f32).
+bool provisional_allowed(int64_t global_rows, int d) {
+  const char* e = std::getenv("OAP_KMEANS_PROVISIONAL_MIN");  // (read per fit: tests set it)
+  const double lim = e ? std::atof(e) : double(int64_t(1) << 28);
+  return double(global_rows) * double(d) >= lim;
+}
+
+std::vector<double> fit_bounds(const std::vector<double>& cb, const std::vector<double>& absmax,
+                               int64_t global_rows, bool* from_centers) {
+  bool ok = provisional_allowed(global_rows, int(cb.size()));
+  for (size_t f = 0; f < cb.size(); ++f) ok = ok && absmax[f] < cb[f];
+  *from_centers = ok;
+  return ok ? cb : absmax;
+}
+
 inline double table_at(const DenseTable& t, int64_t r, int c) {
   return t.dtype == DType::F64 ? t.data.as<double>()[size_t(r) * t.ld + c]
                                : double(t.data.as<float>()[size_t(r) * t.ld + c]);
@@ -269,6 +304,10 @@ struct AssignReq {
   const float* img_scan_xnorm = nullptr;
   const float* img_scan_drift = nullptr;
   u64* img_scan_pruned = nullptr;
+  // lean full pass: per-workgroup sum |x|^2 and the provisional-bound check (KMeansAssignArgs)
+  double* sq_slab = nullptr;
+  unsigned* bound_flag = nullptr;
+  float bound_inf = 0.f;
 };
 
 // The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
@@ -413,6 +452,9 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.img_scan_xnorm = req.img_mode == 2 ? req.img_scan_xnorm : nullptr;
     a.img_scan_drift = req.img_mode == 2 ? req.img_scan_drift : nullptr;
     a.img_scan_pruned = req.img_mode == 2 ? req.img_scan_pruned : nullptr;
+    a.sq_slab = req.sq_slab;
+    a.bound_flag = req.bound_flag;
+    a.bound_inf = req.bound_inf;
     if (req.delta) {  // delta accumulation; over the scan's tile list when there is one
       OAP_CHECK(req.labels && req.labels_valid,
                 "kmeans delta accumulation needs the previous iteration's labels");
@@ -469,6 +511,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.img_scan_xnorm = nullptr;
     b.img_scan_drift = nullptr;
     b.img_scan_pruned = nullptr;
+    b.sq_slab = nullptr;
+    b.bound_flag = nullptr;
     b.cost_slab = a.cost_slab ? a.cost_slab + grid : nullptr;
     kern::kmeans_exact_rows(b, grid, s);
     return a.cost_slab ? 2 * grid : 0;
@@ -1196,9 +1240,13 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
 // sum is allreduced), so every rank takes the same branch.
 static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const u64* sums_d,
                            const u64* counts_d, const float* centers_d, int k, int d, int dp,
-                           const std::vector<double>& inv_scale, double* cost) {
+                           const std::vector<double>& inv_scale, const double* fused_T,
+                           double* cost) {
   double t_err = 0.0;
-  double T = local_row_sqnorm(ctx, x, &t_err);
+  // sum |x|^2: fused into the fit's first pass when it ran the lean kernel (fused_T = {sum,
+  // relative bound}), else one pass over the rows now
+  double T = fused_T ? fused_T[0] : local_row_sqnorm(ctx, x, &t_err);
+  if (fused_T) t_err = fused_T[1];
   double terr_abs = std::isfinite(T) ? t_err * T : std::numeric_limits<double>::quiet_NaN();
   if (!comm.trivial()) {
     T = comm_allreduce_scalar(ctx, comm, T, ReduceOp::Sum);
@@ -1262,10 +1310,21 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   res.init_seconds = seconds_since(t_init);
   res.k = k;
 
-  auto absmax = global_column_absmax(ctx, comm, x);
+  // fixed-point scales (fit_bounds): provisional bounds from the initial centers, or the global
+  // column maxima where a pass over the rows has to decide
+  const std::vector<double> cbound = center_bounds(centers, k, d);
   const int64_t max_local =
       static_cast<int64_t>(comm_allreduce_scalar(ctx, comm, double(x.rows), ReduceOp::Max));
-  FixedPoint fp = fixed_point_scales(absmax, x.global_rows, max_local);
+  std::vector<double> absmax;  // the global column maxima, once a pass computed them
+  FixedPoint fp;
+  auto bounds_from_absmax = [&]() {
+    absmax = global_column_absmax(ctx, comm, x);
+    bool fc = false;
+    fp = fixed_point_scales(fit_bounds(cbound, absmax, x.global_rows, &fc), x.global_rows,
+                            max_local);
+    res.scale_source = fc ? "centers_checked" : "absmax";
+  };
+  if (!ctx.is_gpu()) bounds_from_absmax();
   const size_t kd = size_t(k) * d;
   auto t_iter = std::chrono::steady_clock::now();
   Metrics& M = ctx.metrics();
@@ -1337,8 +1396,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   ctx.memset(scale.data(), 0, sizeof(float) * (round_up(d, 4) + 4), s);
   ctx.memset(refine_d.data(), 0, 2 * sizeof(u64), s);
   ctx.copy_to_backend(c64.data(), centers.data(), sizeof(double) * kd, s);
-  ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d, s);
-  ctx.copy_to_backend(inv_scale.data(), fp.inv_scale.data(), sizeof(double) * d, s);
   kern::kmeans_prepare_centers(c64.as<double>(), k, d, g.dp, g.c32.as<float>(),
                                g.cnorm.as<float>(), g.cstat.as<float>(), g.kpad, s);
   u64* sums = stats.as<u64>();
@@ -1428,8 +1485,35 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     lab_keep = ctx.alloc(sizeof(int32_t) * x.rows);
     req.labels = lab_keep.as<int32_t>();
   }
+  // Provisional fixed-point bounds (fit_bounds): the lean single-launch fit's first full pass
+  // checks every row against them (and sums |x|^2 for the final cost), so no pass over the rows
+  // runs before the first iteration.  Decided from the shape and parameters (rank-uniform).
+  const char* am_env = std::getenv("OAP_KMEANS_ABSMAX_PASS");
+  const bool provisional = !p.absmax_pass && !(am_env && *am_env == '1') && delta_all &&
+                           provisional_allowed(x.global_rows, d) &&
+                           x.dtype == DType::F32 && lean_applies(x, k, g.kpad, req);
+  double cb_min = std::numeric_limits<double>::infinity();
+  for (int f = 0; f < d; ++f) cb_min = std::min(cb_min, cbound[f]);
+  Buffer bflag_b, bflag_h, sq_slab_b;
+  if (provisional) {
+    fp = fixed_point_scales(cbound, x.global_rows, max_local);
+    res.scale_source = "centers";
+    bflag_b = ctx.alloc(2 * sizeof(unsigned));  // [flag, largest fp32 |x|^2 (bits)]
+    bflag_h = ctx.alloc_pinned(2 * sizeof(unsigned));
+    ctx.memset(bflag_b.data(), 0, 2 * sizeof(unsigned), s);
+  } else {
+    bounds_from_absmax();
+  }
+  ctx.copy_to_backend(scale.data(), fp.scale.data(), sizeof(float) * d, s);
+  ctx.copy_to_backend(inv_scale.data(), fp.inv_scale.data(), sizeof(double) * d, s);
+  bool prov_pending = provisional;  // the first batch's check is still to be read
   Buffer loc_b, xnorm_b, dlist_b, cbak_b;
   const int lgrid = kern::kmeans_lloyd_grid(x.rows, ctx.info().cu_count);
+  // sum |x|^2 of the local rows, fused into the first full pass (the final cost's statistics
+  // form): one fp64 partial per lean workgroup
+  if (delta_all && x.rows > 0 && x.dtype == DType::F32 && lean_applies(x, k, g.kpad, req))
+    sq_slab_b = ctx.alloc(sizeof(double) * lgrid);
+  bool sq_ready = false;
   const int64_t ltiles = kern::kmeans_lloyd_tiles_per_block(x.rows, lgrid);
   if (delta) {
     loc_b = ctx.alloc(sizeof(u64) * (kd + k));
@@ -1492,9 +1576,14 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // (the fallback check: the image scale read back into pinned memory)
   Buffer imgchk_h = ctx.alloc_pinned(sizeof(float));
   bool imgchk_pending = false;
-  double row_norm_cap = 0.0;  // >= every row's |x| on every rank (global column maxima)
-  for (int f = 0; f < d; ++f) row_norm_cap += absmax[f] * absmax[f];
-  row_norm_cap = std::isfinite(row_norm_cap) ? std::sqrt(row_norm_cap) : 1e300;
+  // >= every row's |x| on every rank: the global column maxima's norm, or (provisional bounds)
+  // the smallest bound, which the first pass's check proves above every row's norm
+  auto norm_cap_of = [](const std::vector<double>& am) {
+    double c = 0.0;
+    for (double v : am) c += v * v;
+    return std::isfinite(c) ? std::sqrt(c) : 1e300;
+  };
+  double row_norm_cap = provisional ? norm_cap_of(cbound) : norm_cap_of(absmax);
   double init_cmax = 0.0;  // the largest |c| of the initial centers
   for (int c = 0; c < k; ++c) {
     double s2 = 0.0;
@@ -1522,16 +1611,16 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     row_scan_fused =
         row_scan_fused && row_scan_ok && kern::kmeans_lean_img_supported(d, k, lw, true);
   }
-  // the same decision from the shape alone (rank-uniform: it may change which iterations compute
-  // a cost, and so which collectives run)
-  bool row_scan_shape = false;
-  if (scan_all && !chunked && !(rs_env && *rs_env == '0') && x.dtype == DType::F32 &&
-      img_kernel_default()) {
-    const char* e = std::getenv("OAP_KMEANS_IMAGE");
-    const int lv = lean_variant(d, g.kpad);
-    row_scan_shape = !(e && *e == '0') && lv != 3 && lv != 10 &&
-                     kern::kmeans_lean_img_supported(d, k, kern::kmeans_lloyd_waves(lv));
-  }
+  // the same decision for the whole world (it changes which iterations compute a cost and
+  // scan tiles, and so which collectives run): every rank with rows must have the image and the
+  // kernel (a rank without rows abstains) — one scalar Min-allreduce per fit; a rank whose own
+  // image is there still leaves the row scan off when a peer's is not
+  double rs_vote = (x.rows == 0 || row_scan_ok) ? 1.0 : 0.0;
+  if (!comm.trivial()) rs_vote = comm_allreduce_scalar(ctx, comm, rs_vote, ReduceOp::Min);
+  const bool row_scan_all = scan_all && !chunked && rs_vote > 0.5 &&
+                            (row_scan_ok || x.rows == 0 || !comm.trivial());
+  row_scan_ok = row_scan_ok && row_scan_all;
+  row_scan_fused = row_scan_fused && row_scan_ok;
   if (row_scan_ok && !row_scan_fused)
     rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
                         sizeof(unsigned) * size_t(lgrid) + 64);
@@ -1604,6 +1693,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   Buffer flags_hb = ctx.alloc_pinned(sizeof(kern::KMeansFlags) * B);
   auto* flh = flags_hb.as<kern::KMeansFlags>();
   bool stop = false;
+  bool restart = false;  // the provisional fixed-point bounds failed (see prov_pending)
   int scan_iters = 0;  // scan passes in the current batch
   std::vector<char> it_scanned(B, 0), it_costless(B, 0);
   bool last_costless = false;  // the last iteration computed no cost (rank-uniform)
@@ -1623,11 +1713,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (a probe batch scans its first iteration only: the next batch decides from it)
       // (the first batch scans its third iteration only: one right after the init's large
       // move rarely prunes)
-      // (rank-uniform: row_scan_shape, not row_scan_ok — the latter also needs this rank's rows
+      // (rank-uniform: row_scan_all, not row_scan_ok — the latter also needs this rank's rows
       // and its image allocation, so a rank without rows or without room for the image would
       // count tile-scan iterations its peers do not, and the per-batch collectives below that
       // scan_iters gates would pair up differently across ranks)
-      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on && !row_scan_shape &&
+      const bool scan_it_all = scan_all && it > 1 && req.fast1 && delta_on && !row_scan_all &&
                                (!probing || b == 0);
       const bool scan_it = scan_it_all && scan;
       last_scanned = scan_it_all;
@@ -1667,7 +1757,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (with the row scan, a known last iteration is a scan pass too: the exact cost pass over
       // the labels after the loop reads the f32 rows once, cheaper than a full f32 cost pass)
       const bool cost_it = !req.fast1 || !(delta_all || cfree_all) || it == 0 ||
-                           (p.tol < 0 && it == p.max_iter - 1 && !row_scan_shape);
+                           (p.tol < 0 && it == p.max_iter - 1 && !row_scan_all);
       req.cost_slab = cost_it ? slab.as<double>() : nullptr;
       it_costless[b] = !cost_it || scan_it_all;
       last_costless = it_costless[b];
@@ -1717,7 +1807,18 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // (the lean chunked pass keeps its running state in its own buffers: no per-row distance
       // unless a cost is asked for; the general chunked path re-seeds its own each iteration)
       if (lean_chunked && x.rows > 0) req.mindist = req.fast1 ? nullptr : mind_keep.as<float>();
+      // the first full pass: sum |x|^2 (final cost) and the provisional-bound check
+      const bool first_full = it == 0 && !req.tile_list && !req.delta && req.fast1;
+      req.sq_slab = first_full && sq_slab_b.data() ? sq_slab_b.as<double>() : nullptr;
+      req.bound_flag = first_full && prov_pending ? bflag_b.as<unsigned>() : nullptr;
+      req.bound_inf = float(cb_min);  // (a power of two, or 0 / inf)
+      OAP_CHECK(!(it == 0 && prov_pending && x.rows > 0) ||
+                    (req.bound_flag && lean_applies(x, k, g.kpad, req)),
+                "kmeans: the provisional fixed-point bounds need the lean first pass");
       int nb = gpu_assign(ctx, x, g, req, s);
+      if (req.sq_slab) sq_ready = true;
+      req.sq_slab = nullptr;
+      req.bound_flag = nullptr;
       if (req.img_mode == 1) {
         img_ready = true;
         // the image's scale, read back with the batch: whether the f32 fallback launch
@@ -1786,7 +1887,37 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     if (scan)
       OAP_HIP_CHECK(hipMemcpyAsync(&pruned_now, pruned_d.data(), sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
+    if (prov_pending)
+      OAP_HIP_CHECK(hipMemcpyAsync(bflag_h.data(), bflag_b.data(), 2 * sizeof(unsigned),
+                                   hipMemcpyDeviceToHost, s));
     comm.wait(s);
+    if (prov_pending) {
+      // the first pass's check of the provisional bounds (rank-uniform: allreduced); a flagged
+      // row costs one column-maxima pass, which evaluates the rule exactly — the bounds either
+      // hold (continue) or the fit restarts from its initial centers with the column maxima
+      prov_pending = false;
+      double fl = double(bflag_h.as<unsigned>()[0]);
+      float nmax = 0.f;
+      std::memcpy(&nmax, bflag_h.as<unsigned>() + 1, sizeof(float));
+      // every row's norm on every rank: the largest fp32 |x|^2 (relative error <= (d + 1) 2^-24)
+      double ncap = std::sqrt(double(nmax) * (1.0 + 1e-5));
+      if (!comm.trivial()) {
+        fl = comm_allreduce_scalar(ctx, comm, fl, ReduceOp::Max);
+        ncap = comm_allreduce_scalar(ctx, comm, ncap, ReduceOp::Max);
+      }
+      if (std::isfinite(ncap)) row_norm_cap = std::min(row_norm_cap, ncap);
+      if (fl > 0.0) {
+        absmax = global_column_absmax(ctx, comm, x);
+        bool fc = false;
+        (void)fit_bounds(cbound, absmax, x.global_rows, &fc);
+        if (!fc) {
+          restart = true;
+          break;
+        }
+        res.scale_source = "centers_checked";
+        row_norm_cap = norm_cap_of(absmax);
+      }
+    }
     if (imgchk_pending) {
       // every later center is a mean of rows (of any rank) or a center that never moved, so
       // its norm stays below the larger of the global column-max bound on the rows' norms and
@@ -1900,6 +2031,23 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
     }
   }
+  if (restart) {
+    // a row beyond the provisional bounds: the first batch's integers may have wrapped — the
+    // fit runs again from its initial centers with the column maxima's scales (rare: rows
+    // far outside every initial center's coordinate range)
+    OAP_HIP_CHECK(hipStreamSynchronize(s));
+    img_b.reset();
+    ldefer_b.reset();
+    bounds_b.reset();
+    lab_keep.reset();
+    KMeansParams q = p;
+    q.absmax_pass = true;
+    q.init = KMeansInit::Given;
+    KMeansResult r = kmeans_fit(ctx, comm, x, centers, q);
+    r.init_seconds = res.init_seconds;
+    r.scale_source = "restart";
+    return r;
+  }
   if ((delta_all || cfree_all) && last_costless && res.num_iter > 1) {
     // exact cost of a last scan iteration: every row against the centers it was assigned to,
     // with the assign kernel's per-row fp32 arithmetic (kmeans_label_cost), summed in fp64
@@ -1909,8 +2057,21 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     double c_stats = 0.0;
     const char* fc_env = std::getenv("OAP_KMEANS_FINAL_COST");  // "rows": the per-row pass
     const bool try_stats = delta_all && x.dtype == DType::F32 && !(fc_env && *fc_env == 'r');
+    double fused_T[2] = {0.0, 0.0};  // {sum |x|^2 of the local rows, its relative bound}
+    const bool fused = sq_ready || x.rows == 0;
+    if (sq_ready) {
+      std::vector<double> h(lgrid);
+      ctx.copy_to_host(h.data(), sq_slab_b.data(), sizeof(double) * lgrid, s);
+      for (double v : h) fused_T[0] += v;  // (fixed order)
+      // longest chain of additions of non-negative terms: a lane's fma chain (<= 8 x 8 values
+      // a row), one add per tile it ran (>= 8 waves per workgroup), the wave's shuffle tree,
+      // the workgroup's waves, the host's workgroups
+      const double chain = double(64 + (ltiles + 7) / 8 + 6 + 16 + lgrid + 2);
+      fused_T[1] = chain * 1.12e-16;
+    }
     if (try_stats && final_cost_from_stats(ctx, comm, x, fa.sums, fa.counts, cbak_b.as<float>(),
-                                           k, d, g.dp, fp.inv_scale, &c_stats)) {
+                                           k, d, g.dp, fp.inv_scale, fused ? fused_T : nullptr,
+                                           &c_stats)) {
       res.cost = c_stats;
       res.cost_history.back() = c_stats;
       res.final_cost_path = "stats";
@@ -2059,7 +2220,11 @@ KMeansResult kmeans_fit_streamed(Context& ctx, Comm& comm, const float* host, in
       for (int f = 0; f < d; ++f) absmax[f] = std::max(absmax[f], m[f]);
     comm_allreduce_host(ctx, comm, absmax.data(), size_t(d), DType::F64, ReduceOp::Max);
   }
-  FixedPoint fp = fixed_point_scales(absmax, g_rows, max_local);
+  bool from_centers = false;  // (the resident fit's rule: bitwise its integers)
+  FixedPoint fp = fixed_point_scales(fit_bounds(center_bounds(centers, k, d), absmax, g_rows,
+                                                &from_centers),
+                                     g_rows, max_local);
+  res.scale_source = from_centers ? "centers_checked" : "absmax";
   auto t_iter = std::chrono::steady_clock::now();
 
   // two device chunk buffers, filled by pitched DMA from the (registered) host rows on the H2D

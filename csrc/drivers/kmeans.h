@@ -42,6 +42,9 @@ struct KMeansParams {
   // per-iteration phase events (kmeans/assign_kernel and kmeans/allreduce metrics); off: one
   // event pair per batch of iterations (kmeans/iteration only), no event gaps between phases
   bool phase_events = true;
+  // internal: the fixed-point bounds come from a column-maxima pass up front (set on the
+  // restart after a failed provisional check, see kmeans.cpp fit_bounds)
+  bool absmax_pass = false;
 };
 
 struct KMeansResult {
@@ -71,6 +74,11 @@ struct KMeansResult {
   // statistics, kmeans.cpp final_cost_from_stats), "rows" (a pass over the labels), "" (none
   // needed: the last pass computed it)
   std::string final_cost_path;
+  // where the fixed-point column bounds came from: "centers" (provisional bounds from the
+  // initial centers, verified by the first pass), "centers_checked" (verified by a column-maxima
+  // pass after the first pass flagged a row), "absmax" (the column maxima), "restart" (the
+  // provisional bounds failed: the fit was restarted with the column maxima)
+  std::string scale_source;
 };
 
 // Initial centers (k_eff x d) for `params.init` in {Random, Parallel}.  Identical result for

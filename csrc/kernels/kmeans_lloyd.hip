@@ -92,10 +92,15 @@ struct LeanArgs {
   _Float16* ximg;
   float* img_beta;
   int img_mode;
+  // full passes over the rows: per-workgroup sum |x|^2 (fp64, exact squares) and the
+  // provisional fixed-point bound check (KMeansAssignArgs::sq_slab / bound_flag / bound_inf)
+  double* sq_slab;
+  unsigned* bound_flag;
+  float bound_inf;
 };
 
 struct LeanSmem {
-  size_t plane, sc, acc, cnt, mv, wcost, total;
+  size_t plane, sc, acc, cnt, mv, wcost, wsq, total;
 };
 
 constexpr int kMoveCap = 64;  // per-wave staging slots for moved rows (delta passes)
@@ -117,6 +122,8 @@ __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bo
   m.mv = off;  // delta: per wave kMoveCap (row, new | old << 16) pairs
   if (acc && delta) off += size_t(waves) * kMoveCap * 8;
   m.wcost = off;
+  off += size_t(waves) * 8;
+  m.wsq = off;
   off += size_t(waves) * 8;
   m.total = round16(off);
   return m;
@@ -174,6 +181,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
   int2* mv_l = reinterpret_cast<int2*>(smem + L.mv) + (threadIdx.x >> 6) * kMoveCap;
   double* wcost = reinterpret_cast<double*>(smem + L.wcost);
+  double* wsq = reinterpret_cast<double*>(smem + L.wsq);
   const int tid = threadIdx.x;
   const float cmax = a.cstat[0];
   float alpha = lean_alpha(cmax);
@@ -282,6 +290,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const __amdgpu_buffer_rsrc_t rs_xn =
       buf_rsrc(a.xnorm ? a.xnorm + t0 : nullptr, a.xnorm ? uint32_t((wrows + 31) / 32 * 4) : 0u);
   double my_cost = 0.0;
+  double my_sq = 0.0;  // sum |x|^2 of this lane's values of its rows (sq_slab)
+  float my_nx2max = 0.f;  // largest fp32 |x|^2 of its rows (bound_flag[1])
 
   auto tile_of = [&](int64_t q) OAP_AI -> int64_t {
     if (npos == 0) return 0;  // (prefetch of an empty range: any real tile)
@@ -470,6 +480,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += xor32_f(nx2);
+      if (a.sq_slab && valid) {  // exact squares in fp64 (24-bit mantissas: 48-bit products)
+        double q = 0.0;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const double v = static_cast<double>(x.at(s, j));
+            q = fma(v, v, q);
+          }
+        my_sq += q;
+      }
+      // provisional fixed-point bounds: a value at or beyond the smallest column bound makes
+      // the host check the column maxima (max3 chains with |.| modifiers: 16 VALU a tile)
+      if (a.bound_flag) {
+        float m = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; j += 2)
+            m = fmaxf(m, fmaxf(fabsf(x.at(s, j)), fabsf(x.at(s, j + 1))));
+        if (valid && !(m < a.bound_inf)) atomicOr(a.bound_flag, 1u);
+        my_nx2max = fmaxf(my_nx2max, valid ? nx2 : 0.f);
+      }
       // per-tile max |x|^2 (the delta scan's pruning margin): the reduction only where it is
       // asked for, the store predicated by offset (issued on every path, see buf_rsrc)
       float tmax = nx2;
@@ -760,8 +793,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   if (n_mv) flush_moved(n_mv);
   // ---- deterministic per-block cost (fixed shuffle tree, waves in index order), flushes
   const double wsum = wave_sum_f64(my_cost);
+  const double wsq_sum = a.sq_slab ? wave_sum_f64(my_sq) : 0.0;
+  if (a.bound_flag) {  // the rows' largest norm (non-negative floats order as their bits)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) my_nx2max = fmaxf(my_nx2max, __shfl_xor(my_nx2max, m, 64));
+    if (lane == 0 && my_nx2max > 0.f) atomicMax(a.bound_flag + 1, __float_as_uint(my_nx2max));
+  }
   if (lane == 0) {
     wcost[wave] = wsum;
+    wsq[wave] = wsq_sum;
     a.defer_row_count[blockIdx.x * kDeferSubs + wave] = n_def;
     if (a.deferred_rows && n_def) atomicAdd(a.deferred_rows, u64(n_def));
     if (a.deferred_rows && moved_total) atomicAdd(a.deferred_rows + 1, moved_total);
@@ -771,6 +811,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     double tot = 0.0;
     for (int w = 0; w < WAVES; ++w) tot += wcost[w];
     a.cost_slab[blockIdx.x] = tot;
+  }
+  if (tid == 0 && a.sq_slab) {
+    double tot = 0.0;
+    for (int w = 0; w < WAVES; ++w) tot += wsq[w];
+    a.sq_slab[blockIdx.x] = tot;
   }
   if (accumulate) {
     for (int i = tid; a.sums_too && i < k * d; i += NT) {
@@ -1369,6 +1414,13 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.ximg = static_cast<_Float16*>(a.ximg);
   l.img_beta = a.img_beta;
   l.img_mode = a.ximg ? a.img_mode : 0;
+  // (full passes over the rows only: the image passes never see every row's f32 values)
+  const bool rows_pass = !(l.img_mode == 2 || l.img_mode == 3) && !a.tile_list && !a.delta;
+  OAP_CHECK((!a.sq_slab && !a.bound_flag) || (rows_pass && a.chunk_mode <= 1),
+            "kmeans_lloyd: sum |x|^2 / bound check need a full pass over the rows");
+  l.sq_slab = a.sq_slab;
+  l.bound_flag = a.bound_flag;
+  l.bound_inf = a.bound_inf;
   // the exact per-row cost is computed when a cost or mindist is asked for
   const bool cost = a.cost_slab != nullptr || a.mindist != nullptr;
   if (a.xbf16)

@@ -166,9 +166,7 @@ void assign_global_offsets(Context& ctx, Comm& comm, DenseTable& t) {
 
 std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t) {
   std::vector<double> mx(t.cols, 0.0);
-  if (!t.local_absmax.empty()) {
-    mx = t.local_absmax;
-  } else if (ctx.is_gpu()) {
+  if (ctx.is_gpu()) {
     Buffer d = ctx.alloc(sizeof(float) * t.cols);
     ctx.memset(d.data(), 0, sizeof(float) * t.cols);
     kern::column_absmax(t.data.data(), t.dtype, t.rows, t.cols, t.ld, d.as<float>(),
@@ -190,7 +188,6 @@ std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t
     for (auto& p : part)
       for (int c = 0; c < t.cols; ++c) mx[c] = std::max(mx[c], p[c]);
   }
-  t.local_absmax = mx;
   if (!comm.trivial()) {
     if (comm.on_device() && ctx.is_gpu()) {
       Buffer d = ctx.alloc(sizeof(double) * t.cols);
@@ -209,10 +206,6 @@ std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t
 double local_row_sqnorm(Context& ctx, DenseTable& t, double* rel_err) {
   *rel_err = 0.0;
   if (t.rows == 0) return 0.0;
-  if (t.local_sqnorm >= 0.0) {
-    *rel_err = t.local_sqnorm_rel_err;
-    return t.local_sqnorm;
-  }
   if (!ctx.is_gpu() || t.dtype != DType::F32) return std::numeric_limits<double>::quiet_NaN();
   Buffer part = ctx.alloc(sizeof(double) * kern::kSqnormBlocks);
   const int nb = kern::row_sqnorm_partials(t.data.as<float>(), t.rows, t.cols, t.ld,
@@ -228,9 +221,7 @@ double local_row_sqnorm(Context& ctx, DenseTable& t, double* rel_err) {
   const int64_t per_block = (256 / (t.ld / 4)) * (t.ld / 4);
   const int64_t rstride = int64_t(nb) * (per_block / (t.ld / 4));
   const double chain = double((t.rows + rstride - 1) / rstride + 3 + 6 + 2 + nb);
-  t.local_sqnorm = sum;
-  t.local_sqnorm_rel_err = chain * 1.12e-16;
-  *rel_err = t.local_sqnorm_rel_err;
+  *rel_err = chain * 1.12e-16;
   return sum;
 }
 

@@ -23,9 +23,7 @@ struct DenseTable {
   Backend backend = Backend::CPU;
   int64_t global_offset = -1;  // global row index of local row 0 (-1 = not yet known)
   int64_t global_rows = -1;
-  std::vector<double> local_absmax;  // cached per-column max |x| over the local rows
-  double local_sqnorm = -1.0;        // cached sum_i |x_i|^2 over the local rows (< 0: not yet)
-  double local_sqnorm_rel_err = 0.0;  // its fp64 rounding bound, relative
+  // (no per-table statistics are cached across fits: every fit pays for what it reads)
 
   size_t bytes() const { return size_t(rows) * size_t(ld) * dtype_size(dtype); }
 };
@@ -45,12 +43,11 @@ DenseTable synth_blobs_table(Context& ctx, int64_t rows, int cols, int64_t ld, i
 // Fills global_offset / global_rows with an allgather of local row counts.
 void assign_global_offsets(Context& ctx, Comm& comm, DenseTable& t);
 
-// Per-column max |x| over the GLOBAL dataset (local kernel + allreduce MAX).
-// The local pass runs once per table (cached in t.local_absmax).
+// Per-column max |x| over the GLOBAL dataset (local kernel + allreduce MAX), one pass per call.
 std::vector<double> global_column_absmax(Context& ctx, Comm& comm, DenseTable& t);
 
-// sum_i |x_i|^2 over the LOCAL rows in fp64 (exact squares, fixed summation order), computed
-// once per table and cached; *rel_err receives its rounding bound relative to the sum.  NaN when
+// sum_i |x_i|^2 over the LOCAL rows in fp64 (exact squares, fixed summation order), one pass per
+// call; *rel_err receives its rounding bound relative to the sum.  NaN when
 // no kernel covers the table's layout (GPU f32 rows with ld % 4 == 0 and ld <= 1024 only).
 double local_row_sqnorm(Context& ctx, DenseTable& t, double* rel_err);
 
