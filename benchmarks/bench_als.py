@@ -3,7 +3,12 @@
 Each rank generates its shard of (user, item, count) triples (uniform users, power-law item
 popularity), then runs the native ALS fit.  Reported: seconds per iteration (both halves:
 Gramian + normal equations/Cholesky + factor allgather), setup (shuffle + CSR) separately.
-Run: python benchmarks/bench_als.py [--ratings N] [--users U] [--items I] [--rank R] [--iters K]
+Run: python benchmarks/bench_als.py [--gpus N] [--ratings N] [--users U] [--items I] [--rank R]
+     [--iters K]
+With --gpus N (N > 1) and no launcher environment the script starts N rank processes itself
+(bench_common.self_launch).  The ratings are ONE global synthetic set for any N — fixed blocks of
+2^22 triples, each drawn from its own generator, each rank taking its contiguous share — so N
+changes only the sharding (strong scaling).
 """
 import argparse
 import json
@@ -15,8 +20,33 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
+def gen_ratings(lo, hi, total, users, items, seed=1000, block=1 << 22):
+    """Triples [lo, hi) of the global synthetic set: uniform users, power-law item popularity
+    (a Pareto transform, ids scrambled), counts 1-5; block b drawn by default_rng([seed, b])."""
+    import numpy as np
+
+    u = np.empty(hi - lo, np.int32)
+    it = np.empty(hi - lo, np.int32)
+    r = np.empty(hi - lo, np.float32)
+    for b in range(lo // block, (hi - 1) // block + 1 if hi > lo else lo // block):
+        b0 = b * block
+        n = min(block, total - b0)
+        rng = np.random.default_rng([seed, b])
+        bu = rng.integers(0, users, n, dtype=np.int32)
+        bi = np.minimum((rng.pareto(1.2, n) * items / 50).astype(np.int64), items - 1)
+        bi = ((bi * 2654435761) % items).astype(np.int32)
+        br = rng.integers(1, 6, n).astype(np.float32)
+        s0, s1 = max(lo, b0) - b0, min(hi, b0 + n) - b0
+        u[b0 + s0 - lo:b0 + s1 - lo] = bu[s0:s1]
+        it[b0 + s0 - lo:b0 + s1 - lo] = bi[s0:s1]
+        r[b0 + s0 - lo:b0 + s1 - lo] = br[s0:s1]
+    return u, it, r
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--ratings", type=int, default=1_000_000_000)
     ap.add_argument("--users", type=int, default=20_000_000)
     ap.add_argument("--items", type=int, default=2_000_000)
@@ -29,22 +59,25 @@ def main():
     ap.add_argument("--force-rccl", action="store_true",
                     help="1 GPU: a real 1-rank RCCL communicator (device shuffle, comm-stream "
                     "Gramian allreduce, chunked factor broadcasts) instead of the local comm")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    from bench_common import init_world, self_launch, shard
+
+    rc = self_launch(__file__, argv, a.gpus)
+    if rc is not None:
+        return rc
+    sys.stdout.flush()
+    out_fd = os.dup(1)  # (native banners go to stderr; stdout carries the one JSON line)
+    os.dup2(2, 1)
     import numpy as np
 
     import oap_mllib_amd as O
     from oap_mllib_amd import _loader
 
     N = _loader.load()
-    w = O.init_world(O.get_config().replace(device="gpu", force_device_comm=a.force_rccl))
-    n_loc = a.ratings // w.size + (1 if w.rank < a.ratings % w.size else 0)
+    w = init_world(a.force_rccl)
+    n_loc, r0 = shard(a.ratings, w.rank, w.size)
     t0 = time.time()
-    rng = np.random.default_rng(1000 + w.rank)
-    u = rng.integers(0, a.users, n_loc, dtype=np.int32)
-    # power-law item popularity (Zipf-like via a Pareto transform), ids scrambled
-    it = np.minimum((rng.pareto(1.2, n_loc) * a.items / 50).astype(np.int64), a.items - 1)
-    it = ((it * 2654435761) % a.items).astype(np.int32)
-    r = rng.integers(1, 6, n_loc).astype(np.float32)
+    u, it, r = gen_ratings(r0, r0 + n_loc, a.ratings, a.users, a.items)
     gen_s = time.time() - t0
     w.barrier()
     t0 = time.time()
@@ -65,7 +98,7 @@ def main():
     if w.rank == 0:
         it_ms = list(out["iter_ms"])
         steady = it_ms[1:] if len(it_ms) > 1 else it_ms
-        print(json.dumps({
+        os.write(out_fd, (json.dumps({
             "metric": "als_iteration_s", "value": sum(steady) / len(steady) / 1e3, "unit": "s",
             "n_gpus": w.size, "higher_is_better": False,
             # CPU-proxy seconds per iteration over the GPU's (extra.cpu_baseline)
@@ -75,7 +108,8 @@ def main():
                       "hi+lo MFMA with fp32 accumulation (longer rows); fp32 Cholesky"),
             "data": "synthetic implicit counts (uniform users, power-law items)",
             "config": {"model": "als implicit rank %d" % a.rank, "ratings": int(out["nnz"]),
-                       "users": len(out["user_ids"]), "items": len(out["item_ids"])},
+                       "users": len(out["user_ids"]), "items": len(out["item_ids"]),
+                       "parallelism": "dp%d" % w.size},
             "extra": {"iter_ms": it_ms, "setup_s": out["setup_ms"] / 1e3,
                       "fit_wall_s": wall, "gram_ms_total": out["gram_ms"],
                       "solve_ms_total": out["solve_ms"], "comm_ms_total": out["comm_ms"],
@@ -86,9 +120,16 @@ def main():
                       "factor_bcast_recv_bytes": out["bcast_recv_bytes"],
                       "factor_bcast_gbps": (out["bcast_recv_bytes"] / out["bcast_ms"] / 1e6
                                             if out["bcast_ms"] > 0 else None),
-                      "cpu_baseline": cpu}}))
+                      "cpu_baseline": cpu,
+                      # (for the world-size tests: the fit's factors, summarised)
+                      "user_factor_sum": float(np.abs(np.asarray(out["user_factors"])).sum()),
+                      "item_factor_sum": float(np.abs(np.asarray(out["item_factors"])).sum()),
+                      "factor_head": np.asarray(out["user_factors"])[
+                          np.argsort(np.asarray(out["user_ids"]))[:3], :4].tolist()}})
+                      + "\n").encode())
     O.shutdown_world()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

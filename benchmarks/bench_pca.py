@@ -3,8 +3,11 @@
 Rows are generated on the device (synthetic Gaussian blobs, row-sharded over ranks); reported:
 fit wall clock (covariance SYRK + allreduce + eigensolver), SYRK device time and its TFLOP/s
 (useful flops n*d*(d+1) of the symmetric product), allreduce and eigensolver times.
-Run: python benchmarks/bench_pca.py [--rows N] [--dim D] [--k K] [--reps R]
+Run: python benchmarks/bench_pca.py [--gpus N] [--rows N] [--dim D] [--k K] [--reps R]
      [--precision exact|fast|fast4|both]
+With --gpus N (N > 1) and no launcher environment the script starts N rank processes itself
+(one per GPU, bench_common.self_launch); the rows are the same global dataset for any N (each
+rank generates its contiguous shard), so N changes only the sharding (strong scaling).
 """
 import argparse
 import json
@@ -16,8 +19,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
-def main():
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=1000)
     ap.add_argument("--k", type=int, default=50)
@@ -27,17 +32,23 @@ def main():
     ap.add_argument("--precision", default="both", choices=["exact", "fast", "fast4", "both"],
                     help="exact: fp64 products + sums (fp64 MFMA, the reference's precision); "
                     "fast: bf16x3 split products; fast4: bf16x4; both: exact (headline) + fast")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    from bench_common import init_world, self_launch, shard
+
+    rc = self_launch(__file__, argv, a.gpus)
+    if rc is not None:
+        return rc
+    sys.stdout.flush()
+    out_fd = os.dup(1)  # (native banners go to stderr; stdout carries the one JSON line)
+    os.dup2(2, 1)
     import numpy as np
 
     import oap_mllib_amd as O
     from oap_mllib_amd import _loader
 
     N = _loader.load()
-    w = O.init_world(O.get_config().replace(device="gpu"))
-    base, rem = divmod(a.rows, w.size)
-    n_loc = base + (1 if w.rank < rem else 0)
-    row0 = w.rank * base + min(w.rank, rem)
+    w = init_world()
+    n_loc, row0 = shard(a.rows, w.rank, w.size)
     t0 = time.time()
     t = N.synth_blobs(w.ctx, n_loc, a.dim, N.kmeans_ld(a.dim), row0, 64, 10.0, 1.0, 1234)
     t.set_global(row0, a.rows)
@@ -71,6 +82,10 @@ def main():
         extra = dict(res[head][0])
         extra["ingest_synth_s"] = ingest
         extra["precision"] = head
+        extra["world_size"] = w.size
+        extra["comm"] = w.comm.name if w.comm is not None else "none"
+        extra["explained_variance"] = list(res[head][1]["explained_variance"])
+        extra["pc_abs_sum"] = float(np.abs(np.asarray(res[head][1]["pc"])).sum())
         cpu = None
         if a.cpu_rows > 0:  # labelled fp64 CPU proxy on this host's cores
             from cpu_baseline import pca_proxy
@@ -82,16 +97,18 @@ def main():
             ev_a = np.asarray(res[head][1]["explained_variance"])
             ev_b = np.asarray(res[m][1]["explained_variance"])
             extra[m + "_mode"]["max_abs_ev_diff_vs_" + head] = float(np.max(np.abs(ev_a - ev_b)))
-        print(json.dumps({
+        os.write(out_fd, (json.dumps({
             "metric": "pca_fit_wall_s", "value": res[head][0]["fit_wall_s"], "unit": "s",
             "n_gpus": w.size, "higher_is_better": False, "dtype": dtype,
             # CPU-proxy fit time over the GPU fit time (extra.cpu_baseline)
             "vs_baseline": (cpu["fit_s_scaled"] / res[head][0]["fit_wall_s"]) if cpu else None,
             "data": "synthetic (gaussian blobs, on-device)",
-            "config": {"model": "pca top-%d" % a.k, "rows": a.rows, "dim": a.dim},
-            "extra": extra}))
+            "config": {"model": "pca top-%d" % a.k, "rows": a.rows, "dim": a.dim,
+                       "parallelism": "dp%d" % w.size},
+            "extra": extra}) + "\n").encode())
     O.shutdown_world()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())
