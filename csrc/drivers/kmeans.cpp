@@ -86,7 +86,10 @@ FixedPoint fixed_point_scales(const std::vector<double>& absmax, int64_t global_
   fp.inv_scale.resize(d);
   auto clog2 = [](double v) { return static_cast<int>(std::ceil(std::log2(std::max(v, 2.0)))); };
   const int ln = clog2(double(global_rows));
-  const int lb = clog2(double(kern::kmeans_rows_per_block_bound(max_local_rows)));
+  // (the per-block bound of the GLOBAL row count, not this world's largest shard: a bound for
+  // every sharding, so the scales — and the integers — are the same for any world size)
+  const int lb = clog2(double(kern::kmeans_rows_per_block_bound(
+      std::max(max_local_rows, global_rows))));
   const int budget = std::min(61 - ln, 52 - lb);
   for (int f = 0; f < d; ++f) {
     int e = 0;
@@ -1231,13 +1234,17 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
 // ------------------------------------------------------------------------------- fit
 // The exact cost of the last assignment from the fit's own statistics, without a pass over
 // the rows:  sum_i |x_i - c_l(i)|^2 = sum_i |x_i|^2 - 2 sum_c c.S_c + sum_c n_c |c|^2, with
-// sum_i |x_i|^2 cached on the table (fp64, exact squares: one pass per table, like the column
-// maxima), S_c and n_c the global fixed-point statistics the last finalize used and c the fp32
-// centers that assignment used.  The rigorous error bound — fixed-point quantisation of S_c
-// (|S~ - S| <= n_c q_f / 2 per feature) plus fp64 rounding — must stay within 1e-9 of the
-// result, else (rows far from the origin, a table layout without the norm kernel) it returns
-// false and the caller runs the per-row pass.  Rank-uniform: every input is global (the norm
+// sum_i |x_i|^2 summed by the fit's first pass (the rows' fp32 norms, fp64 sum; a pass of its
+// own when the first pass was not the lean kernel), S_c and n_c the global fixed-point
+// statistics the last finalize used and c the fp32 centers that assignment used.  The rigorous
+// error bound — the norms' fp32 rounding, fixed-point quantisation of S_c (|S~ - S| <= n_c q_f / 2
+// per feature) plus fp64 rounding — must stay within kStatsCostRel of the result, else (rows far
+// from the origin, a table layout without the norm kernel) it returns false and the caller runs
+// the per-row pass.  Rank-uniform: every input is global (the norm
 // sum is allreduced), so every rank takes the same branch.
+// (accepted when its rigorous bound is within 1e-5 of the result: the per-row fp32 cost pass it
+// replaces carries (d + 1) 2^-24 per row — ~3e-6 at d = 50 — in the worst case too)
+constexpr double kStatsCostRel = 1e-5;
 static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const u64* sums_d,
                            const u64* counts_d, const float* centers_d, int k, int d, int dp,
                            const std::vector<double>& inv_scale, const double* fused_T,
@@ -1280,7 +1287,7 @@ static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const
   const double u = 1.12e-16;
   const double err = terr_abs + q_err + double(kd + k + 8) * u * (2.0 * A_abs + B) +
                      4.0 * u * (T + 2.0 * A_abs + B);
-  if (!(v > 0.0) || err > 1e-9 * v) return false;
+  if (!(v > 0.0) || err > kStatsCostRel * v) return false;
   *cost = v;
   return true;
 }
@@ -2063,11 +2070,13 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       std::vector<double> h(lgrid);
       ctx.copy_to_host(h.data(), sq_slab_b.data(), sizeof(double) * lgrid, s);
       for (double v : h) fused_T[0] += v;  // (fixed order)
-      // longest chain of additions of non-negative terms: a lane's fma chain (<= 8 x 8 values
-      // a row), one add per tile it ran (>= 8 waves per workgroup), the wave's shuffle tree,
-      // the workgroup's waves, the host's workgroups
-      const double chain = double(64 + (ltiles + 7) / 8 + 6 + 16 + lgrid + 2);
-      fused_T[1] = chain * 1.12e-16;
+      // each row's fp32 |x|^2 errs by <= (8 KS + 1) 2^-24 of itself (its fma chain over a half
+      // row, the two halves' add; KS <= 8); then fp64 additions of non-negative terms: one per
+      // tile a lane ran (>= 8 waves per workgroup), the wave's shuffle tree, the workgroup's
+      // waves, the host's workgroups
+      const double chain = double((ltiles + 7) / 8 + 6 + 16 + lgrid + 2);
+      fused_T[1] = double(8 * ((d + 4 + 15) / 16) + 1) * 5.97e-8 * (1.0 + 1e-6) +
+                   chain * 1.12e-16;
     }
     if (try_stats && final_cost_from_stats(ctx, comm, x, fa.sums, fa.counts, cbak_b.as<float>(),
                                            k, d, g.dp, fp.inv_scale, fused ? fused_T : nullptr,

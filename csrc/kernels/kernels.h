@@ -163,7 +163,7 @@ struct KMeansAssignArgs {
   int img_mode = 0;
   const float* centers_all = nullptr;
   // Lean kernel, full passes over the f32 / bf16 rows (kmeans_lloyd): sq_slab [grid] receives
-  // each workgroup's sum of |x|^2 over its rows in fp64 from exact squares (the final cost's
+  // each workgroup's sum of its rows' fp32 |x|^2, summed in fp64 (the final cost's
   // sum_i |x_i|^2, fused into the fit's first pass); bound_flag (optional) gets 1 or'ed in when
   // a row has a value |x_f| >= bound_inf — the fit's provisional fixed-point bounds may not hold
   // — and bound_flag[1] receives the largest fp32 |x|^2 of the rows (float bits, atomicMax).

@@ -290,7 +290,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const __amdgpu_buffer_rsrc_t rs_xn =
       buf_rsrc(a.xnorm ? a.xnorm + t0 : nullptr, a.xnorm ? uint32_t((wrows + 31) / 32 * 4) : 0u);
   double my_cost = 0.0;
-  double my_sq = 0.0;  // sum |x|^2 of this lane's values of its rows (sq_slab)
+  double my_sq = 0.0;  // sum of the fp32 |x|^2 of this lane's rows (sq_slab)
   float my_nx2max = 0.f;  // largest fp32 |x|^2 of its rows (bound_flag[1])
 
   auto tile_of = [&](int64_t q) OAP_AI -> int64_t {
@@ -480,17 +480,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 #pragma unroll
         for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
       nx2 += xor32_f(nx2);
-      if (a.sq_slab && valid) {  // exact squares in fp64 (24-bit mantissas: 48-bit products)
-        double q = 0.0;
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const double v = static_cast<double>(x.at(s, j));
-            q = fma(v, v, q);
-          }
-        my_sq += q;
-      }
+      // the row's fp32 |x|^2 (a chain of <= 8 KS + 1 roundings) summed in fp64: the final cost's
+      // sum_i |x_i|^2 at the per-row accuracy of the cost pass it replaces, for one add a tile
+      // (exact fp64 squares cost this pass ~10%: +1 ms at the headline)
+      if (a.sq_slab && valid && h == 0) my_sq += static_cast<double>(nx2);
       // provisional fixed-point bounds: a value at or beyond the smallest column bound makes
       // the host check the column maxima (max3 chains with |.| modifiers: 16 VALU a tile)
       if (a.bound_flag) {

@@ -410,7 +410,9 @@ def test_operand_image_bitwise(native, monkeypatch, d, k, sigma, tol):
 
 def test_final_cost_from_statistics(native, monkeypatch):
     """A last pass that computed no cost (row-scan fits) takes it from the fit's statistics:
-    sum |x|^2 - 2 c.S + n |c|^2 with a rigorous bound of 1e-9.  Checked against the fp64 cost of
+    sum |x|^2 - 2 c.S + n |c|^2 (sum |x|^2 from the first pass's fp32 row norms) with a rigorous
+    bound within 1e-5, the class of the per-row fp32 cost pass it replaces.  Checked against the
+    fp64 cost of
     the nearest-center assignment to the previous fit's centers (the last assignment's), and
     the per-row pass taken instead for rows far from the origin (the bound fails)."""
     n, d, k, it = 150000, 50, 200, 8
@@ -425,7 +427,7 @@ def test_final_cost_from_statistics(native, monkeypatch):
     C = prev.astype(np.float32).astype(np.float64)  # the fp32 centers the last pass used
     D = (X * X).sum(1)[:, None] + (C * C).sum(1)[None, :] - 2.0 * X @ C.T  # fp64
     oracle = np.maximum(D.min(1), 0.0).sum()
-    assert abs(r["cost"] - oracle) <= 2e-9 * oracle
+    assert abs(r["cost"] - oracle) <= 1e-7 * oracle  # (the rows path's own accuracy, below)
     monkeypatch.setenv("OAP_KMEANS_FINAL_COST", "rows")
     rr = native.kmeans_fit(g, comm, t, init, k, it, -1.0)
     assert rr["final_cost_path"] == "rows" and np.array_equal(rr["centers"], r["centers"])
