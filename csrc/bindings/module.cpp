@@ -538,6 +538,8 @@ PYBIND11_MODULE(_native, m) {
         out["image_bytes"] = r.image_bytes;
         out["final_cost_path"] = r.final_cost_path;
         out["scale_source"] = r.scale_source;
+        out["mover_rows"] = r.mover_rows;
+        out["mover_listed_rows"] = r.mover_listed_rows;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

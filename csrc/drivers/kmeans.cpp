@@ -307,6 +307,9 @@ struct AssignReq {
   const float* img_scan_xnorm = nullptr;
   const float* img_scan_drift = nullptr;
   u64* img_scan_pruned = nullptr;
+  // fused row-scan image passes: the mover stage (KMeansAssignArgs::img_movers)
+  bool img_movers = false;
+  int32_t* img_mover_list = nullptr;
   // lean full pass: per-workgroup sum |x|^2 and the provisional-bound check (KMeansAssignArgs)
   double* sq_slab = nullptr;
   unsigned* bound_flag = nullptr;
@@ -455,6 +458,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.img_scan_xnorm = req.img_mode == 2 ? req.img_scan_xnorm : nullptr;
     a.img_scan_drift = req.img_mode == 2 ? req.img_scan_drift : nullptr;
     a.img_scan_pruned = req.img_mode == 2 ? req.img_scan_pruned : nullptr;
+    a.img_movers = req.img_mode == 2 && req.img_scan_xnorm && req.img_movers;
+    a.img_mover_list = req.img_mover_list;
     a.sq_slab = req.sq_slab;
     a.bound_flag = req.bound_flag;
     a.bound_inf = req.bound_inf;
@@ -477,7 +482,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     const bool img_k = req.img_kernel >= 0 ? req.img_kernel == 1 : img_kernel_default();
     // (variants 3 / 10 have no image branch: their img_mode 3 would not be a fallback only)
     if (req.img_mode == 2 && img_k && lv != 3 && lv != 10 &&
-        kern::kmeans_lean_img_supported(x.cols, g.k, lw, a.img_scan_xnorm != nullptr)) {
+        kern::kmeans_lean_img_supported(x.cols, g.k, lw, a.img_scan_xnorm != nullptr,
+                                        a.img_movers)) {
       const int cfg = req.img_cfg >= 0                         ? req.img_cfg
                       : a.img_scan_xnorm && scan_cfg_default() >= 0 ? scan_cfg_default()
                                                                     : img_cfg_default();
@@ -487,7 +493,8 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
         f.img_mode = 3;
         kern::kmeans_lloyd(f, grid, lv, s);
       }
-      t_assign_path = a.img_scan_xnorm ? "lean_img_kernel_delta_fused_rowscan"
+      t_assign_path = a.img_movers       ? "lean_img_kernel_delta_rowscan_movers"
+                      : a.img_scan_xnorm ? "lean_img_kernel_delta_fused_rowscan"
                       : a.img_rows     ? "lean_img_kernel_delta_rowscan"
                       : req.tile_list  ? "lean_img_kernel_delta_scan"
                                        : "lean_img_kernel_delta";
@@ -1567,9 +1574,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   }
   if (x.rows > 0 && (req.defer_rows || lean_chunked)) {
     // [deferred rows, moved rows staged, passes that read the operand image]
-    ldstat_b = ctx.alloc(3 * sizeof(u64));
-    ldstat_h = ctx.alloc_pinned(3 * sizeof(u64));
-    ctx.memset(ldstat_b.data(), 0, 3 * sizeof(u64), s);
+    // (+ [3] rows into the mover stage, [4] rows it listed for the full pass)
+    ldstat_b = ctx.alloc(5 * sizeof(u64));
+    ldstat_h = ctx.alloc_pinned(5 * sizeof(u64));
+    ctx.memset(ldstat_b.data(), 0, 5 * sizeof(u64), s);
     req.deferred_rows = ldstat_b.as<u64>();
   }
   u64 deferred_seen = 0, moved_seen = 0;
@@ -1628,6 +1636,24 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
                             (row_scan_ok || x.rows == 0 || !comm.trivial());
   row_scan_ok = row_scan_ok && row_scan_all;
   row_scan_fused = row_scan_fused && row_scan_ok;
+  // the mover stage of the fused row scan (OAP_KMEANS_MOVERS=1: on; a local choice — it
+  // changes no collective and no result, only which rows take the full pass).  Off by default:
+  // at the headline it bounds 81M rows a pass and lists 26M for the full pass (64% of the rows
+  // pruned instead of 25%), but the extra image read of every bounded row and the looser bounds
+  // it leaves make the fit slower: 5.52 vs 4.38 ms/step (profiles/r5/bench_movers_r5f.json)
+  {
+    const char* e = std::getenv("OAP_KMEANS_MOVERS");
+    const int lw = kern::kmeans_lloyd_waves(lean_variant(d, g.kpad));
+    req.img_movers = row_scan_fused && (e && *e == '1') &&
+                     kern::kmeans_lean_img_supported(d, k, lw, true, true);
+  }
+  Buffer mlist_b;  // the mover stage's per-wave row lists ([grid][seg_cap], like the deferrals)
+  if (req.img_movers) {
+    const int64_t scap = kern::kmeans_lloyd_seg_cap(
+        x.rows, lgrid, kern::kmeans_lloyd_waves(lean_variant(d, g.kpad)));
+    mlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(scap) + 64);
+    req.img_mover_list = mlist_b.as<int32_t>();
+  }
   if (row_scan_ok && !row_scan_fused)
     rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
                         sizeof(unsigned) * size_t(lgrid) + 64);
@@ -1888,7 +1914,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
     if (ldstat_b.data())
-      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), 3 * sizeof(u64),
+      OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), 5 * sizeof(u64),
                                    hipMemcpyDeviceToHost, s));
     u64 pruned_now = 0;
     if (scan)
@@ -2135,8 +2161,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     res.pruned_rows = static_cast<int64_t>(pr);
   }
   if (ldstat_b.data()) {
-    u64 dr[3] = {0, 0, 0};
-    ctx.copy_to_host(dr, ldstat_b.data(), 3 * sizeof(u64), s);
+    u64 dr[5] = {0, 0, 0, 0, 0};
+    ctx.copy_to_host(dr, ldstat_b.data(), 5 * sizeof(u64), s);
+    res.mover_rows = static_cast<int64_t>(dr[3]);
+    res.mover_listed_rows = static_cast<int64_t>(dr[4]);
     res.deferred_rows = static_cast<int64_t>(dr[0]);
     res.moved_rows = static_cast<int64_t>(dr[1]) + cmoved;
     res.image_passes = static_cast<int>(dr[2]);  // counted by the passes that read the image
@@ -2421,8 +2449,8 @@ double kmeans_assign_timing(Context& ctx, const DenseTable& x, const std::vector
     req.counts = a.counts;
     req.cost_slab = (ablate & 4) ? nullptr : a.cost_slab;  // 4: the Lloyd pass without a cost
     req.fast1 = true;
-    Buffer dr = ctx.alloc(3 * sizeof(u64));
-    ctx.memset(dr.data(), 0, 3 * sizeof(u64), s);
+    Buffer dr = ctx.alloc(5 * sizeof(u64));
+    ctx.memset(dr.data(), 0, 5 * sizeof(u64), s);
     req.deferred_rows = dr.as<u64>();
     OAP_CHECK(lean_applies(x, k, g.kpad, req), "lean path not applicable");
     gpu_assign(ctx, x, g, req, s);  // warm
@@ -2475,9 +2503,9 @@ ImageTiming kmeans_image_timing(Context& ctx, const DenseTable& x,
   const size_t ib = kern::kmeans_lloyd_image_bytes(x.rows, d);
   OAP_CHECK(ib > 0, "kmeans_image_timing: no operand image at d=" << d);
   Buffer img = ctx.alloc(ib), beta = ctx.alloc(sizeof(float) * 4);
-  Buffer dr = ctx.alloc(3 * sizeof(u64));
+  Buffer dr = ctx.alloc(5 * sizeof(u64));
   ctx.memset(stats.data(), 0, sizeof(u64) * nst, s);
-  ctx.memset(dr.data(), 0, 3 * sizeof(u64), s);
+  ctx.memset(dr.data(), 0, 5 * sizeof(u64), s);
   AssignReq req;
   req.accumulate = true;
   req.sums_too = true;
@@ -2514,7 +2542,7 @@ ImageTiming kmeans_image_timing(Context& ctx, const DenseTable& x,
                                    hipMemcpyDeviceToDevice, s));
       OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), stats0.data(), sizeof(u64) * nst,
                                    hipMemcpyDeviceToDevice, s));
-      ctx.memset(dr.data(), 0, 3 * sizeof(u64), s);
+      ctx.memset(dr.data(), 0, 5 * sizeof(u64), s);
       e0.record(s);
       gpu_assign(ctx, x, gb, req, s);
       e1.record(s);

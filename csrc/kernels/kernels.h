@@ -128,6 +128,11 @@ struct KMeansAssignArgs {
   const float* img_scan_xnorm = nullptr;
   const float* img_scan_drift = nullptr;
   unsigned long long* img_scan_pruned = nullptr;
+  // row-scan image passes: the mover stage (kmeans_lean_img.hip RM 3) — rows the scan cannot
+  // prune are first bounded against the 32 centers that moved most (one MFMA chunk); only the
+  // rows that bound cannot decide take the full pass
+  bool img_movers = false;
+  int32_t* img_mover_list = nullptr;  // [grid][row_seg_cap] rows (the mover stage's lists)
   int64_t row_seg_cap = 0;
   int row_subs = 1;  // sub-segments per workgroup segment (each row_seg_cap / row_subs long)
   // Lean tier-1 kernel output: rows whose tier-1 top-2 gap is inside the tier's error bound are
@@ -193,7 +198,7 @@ size_t kmeans_lloyd_image_bytes(int64_t n, int d);
 // img_mode 2).  `waves` must be the lean variant's (kmeans_lloyd_waves: the deferral
 // sub-segments), cfg < 0 the default configuration.  When the image's scale cannot hold the
 // current centers the kernel does nothing; kmeans_lloyd with img_mode 3 then runs the pass.
-bool kmeans_lean_img_supported(int d, int k, int waves, bool scan = false);
+bool kmeans_lean_img_supported(int d, int k, int waves, bool scan = false, bool movers = false);
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s);
 // Row-level bound scan for the image passes: every row of lean workgroup b's range gets the
 // Hamerly test of kmeans_lean_scan (u + drift[label] against l - max drift, with the tile's

