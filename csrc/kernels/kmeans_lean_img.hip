@@ -825,7 +825,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       if (t + stride >= npos) break;
       body(std::true_type{}, t + stride, trow(t + stride), trow(t + 3 * stride), nullptr, xb, xa);
       if (t + 2 * stride >= npos) break;
-      body(std::true_type{}, t + 2 * stride, trow(t + 2 * stride), trow(t + 4 * stride), nullptr, xc, xb);
+      body(std::true_type{}, t + 2 * stride, trow(t + 2 * stride), trow(t + 4 * stride), nullptr,
+           xc, xb);
     }
   }
   if constexpr (!NO_ACC) {
