@@ -411,6 +411,312 @@ __global__ __launch_bounds__(kEigThreads) void oap_eig_bisect(const double* d, c
   if (lane == 0) out[idx] = 0.5 * (lo + hi);
 }
 
+// Gershgorin bracket of the tridiagonal and the Sturm-count pivot floor (LAPACK dstebz
+// conventions), on the device: out = [lo - pad, hi + pad, pivmin, ||T||_inf].  One block.
+__global__ __launch_bounds__(kEigThreads) void oap_eig_gersh(const double* d, const double* e,
+                                                             int n, double* out) {
+  __shared__ double red[4][4];
+  double lo = INFINITY, hi = -INFINITY, tn = 0.0, em = 0.0;
+  for (int i = threadIdx.x; i < n; i += kEigThreads) {
+    const double r = (i > 0 ? fabs(e[i - 1]) : 0.0) + (i + 1 < n ? fabs(e[i]) : 0.0);
+    lo = fmin(lo, d[i] - r);
+    hi = fmax(hi, d[i] + r);
+    tn = fmax(tn, fabs(d[i]) + r);
+    if (i + 1 < n) em = fmax(em, e[i] * e[i]);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, o, 64));
+    hi = fmax(hi, __shfl_xor(hi, o, 64));
+    tn = fmax(tn, __shfl_xor(tn, o, 64));
+    em = fmax(em, __shfl_xor(em, o, 64));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+    red[2][w] = tn;
+    red[3][w] = em;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < kEigThreads / 64; ++q) {
+      lo = fmin(lo, red[0][q]);
+      hi = fmax(hi, red[1][q]);
+      tn = fmax(tn, red[2][q]);
+      em = fmax(em, red[3][q]);
+    }
+    lo = fmin(lo, red[0][0]);
+    hi = fmax(hi, red[1][0]);
+    tn = fmax(tn, red[2][0]);
+    em = fmax(em, red[3][0]);
+    const double pivmin = 2.2250738585072014e-308 * fmax(1.0, em);
+    const double pad = 2.0 * 2.2204460492503131e-16 * tn + 4.0 * pivmin;
+    out[0] = lo - pad;
+    out[1] = hi + pad;
+    out[2] = pivmin;
+    out[3] = tn;
+  }
+}
+
+// The `keep` eigenvalues of largest magnitude in stable order (ties: lower index — the host
+// path's stable sort of the bisection's ascending output), the clusters of close ones (LAPACK
+// dstein: |lambda_j - lambda_{j-1}| < 1e-3 ||T||, exact multiples separated by 10 eps ||T||):
+// sel [keep], cstart [keep] (index of the cluster's first member).  One block.
+__global__ __launch_bounds__(kEigThreads) void oap_eig_select(const double* lam, int n, int keep,
+                                                              const double* bracket, double* sel,
+                                                              int* cstart) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  unsigned char* used = reinterpret_cast<unsigned char*>(smem);
+  __shared__ double bv[4];
+  __shared__ int bi[4];
+  __shared__ int pick;
+  for (int i = threadIdx.x; i < n; i += kEigThreads) used[i] = 0;
+  __syncthreads();
+  for (int t = 0; t < keep; ++t) {
+    double v = -1.0;
+    int ix = 0x7fffffff;
+    for (int i = threadIdx.x; i < n; i += kEigThreads) {
+      const double a = fabs(lam[i]);
+      if (!used[i] && (a > v || (a == v && i < ix))) {
+        v = a;
+        ix = i;
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double ov = __shfl_xor(v, o, 64);
+      const int oi = __shfl_xor(ix, o, 64);
+      if (ov > v || (ov == v && oi < ix)) {
+        v = ov;
+        ix = oi;
+      }
+    }
+    if ((threadIdx.x & 63) == 0) {
+      bv[threadIdx.x >> 6] = v;
+      bi[threadIdx.x >> 6] = ix;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double b = bv[0];
+      int j = bi[0];
+      for (int q = 1; q < kEigThreads / 64; ++q)
+        if (bv[q] > b || (bv[q] == b && bi[q] < j)) {
+          b = bv[q];
+          j = bi[q];
+        }
+      used[j] = 1;
+      pick = j;
+      sel[t] = lam[j];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double tn = bracket[3] == 0.0 ? 1.0 : bracket[3];
+    const double ortol = 1e-3 * tn, pert = 10.0 * 2.2204460492503131e-16 * tn;
+    for (int j = 0; j < keep; ++j) {
+      if (j > 0 && fabs(sel[j] - sel[j - 1]) < ortol) {
+        if (fabs(sel[j] - sel[j - 1]) < pert)
+          sel[j] = sel[j - 1] + (sel[j] <= sel[j - 1] ? -pert : pert);
+        cstart[j] = cstart[j - 1];
+      } else {
+        cstart[j] = j;
+      }
+    }
+  }
+}
+
+// Eigenvectors of the tridiagonal for sel[] by inverse iteration (the host path's recipe,
+// linalg/eigen.cpp tridiag_inverse_iteration): one block per cluster head; thread 0 factors
+// T - lambda I (LU with partial pivoting, in LDS) and runs the 4 solves, the block does the
+// Gram-Schmidt against the cluster's earlier vectors and the normalisation.  z: n x keep
+// row-major (column j for sel[j]).
+__global__ __launch_bounds__(kEigThreads) void oap_eig_invit(const double* d, const double* e,
+                                                             int n, int keep, const double* sel,
+                                                             const int* cstart,
+                                                             const double* bracket, double* z) {
+#pragma clang fp contract(off)
+  const int j0 = blockIdx.x;
+  if (cstart[j0] != j0) return;  // (block-uniform: only cluster heads work)
+  int j1 = j0 + 1;
+  while (j1 < keep && cstart[j1] != j1) ++j1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* dd = reinterpret_cast<double*>(smem);
+  double* du = dd + n;
+  double* du2 = du + n;
+  double* dl = du2 + n;
+  double* b = dl + n;
+  unsigned char* swp = reinterpret_cast<unsigned char*>(b + n);
+  __shared__ double red[4];
+  const double tn = bracket[3] == 0.0 ? 1.0 : bracket[3];
+  const double tiny = 2.2204460492503131e-16 * tn;
+  const int tid = threadIdx.x;
+  for (int j = j0; j < j1; ++j) {
+    const double lambda = sel[j];
+    if (tid == 0) {
+      for (int i = 0; i < n; ++i) {
+        dd[i] = d[i] - lambda;
+        du[i] = i + 1 < n ? e[i] : 0.0;
+        dl[i] = i + 1 < n ? e[i] : 0.0;
+        du2[i] = 0.0;
+        swp[i] = 0;
+      }
+      for (int i = 0; i + 1 < n; ++i) {
+        if (fabs(dd[i]) >= fabs(dl[i])) {
+          if (dd[i] == 0.0) dd[i] = tiny;
+          const double f = dl[i] / dd[i];
+          dl[i] = f;
+          dd[i + 1] -= f * du[i];
+        } else {
+          const double f = dd[i] / dl[i];
+          dd[i] = dl[i];
+          dl[i] = f;
+          const double t = du[i];
+          du[i] = dd[i + 1];
+          dd[i + 1] = t - f * dd[i + 1];
+          if (i + 2 < n) {
+            du2[i] = du[i + 1];
+            du[i + 1] = -f * du[i + 1];
+          }
+          swp[i] = 1;
+        }
+      }
+      if (dd[n - 1] == 0.0) dd[n - 1] = tiny;
+      for (int i = 0; i < n; ++i)
+        if (fabs(dd[i]) < tiny) dd[i] = copysign(tiny, dd[i] == 0.0 ? 1.0 : dd[i]);
+      uint64_t st = 0x9e3779b97f4a7c15ull * uint64_t(j + 1);  // deterministic start vector
+      for (int i = 0; i < n; ++i) {
+        st ^= st << 13;
+        st ^= st >> 7;
+        st ^= st << 17;
+        b[i] = double(st >> 11) * (1.0 / 9007199254740992.0) - 0.5;
+      }
+    }
+    __syncthreads();
+    for (int it = 0; it < 4; ++it) {
+      if (tid == 0) {
+        for (int i = 0; i + 1 < n; ++i) {
+          if (swp[i]) {
+            const double t = b[i];
+            b[i] = b[i + 1];
+            b[i + 1] = t;
+          }
+          b[i + 1] -= dl[i] * b[i];
+        }
+        b[n - 1] /= dd[n - 1];
+        if (n >= 2) b[n - 2] = (b[n - 2] - du[n - 2] * b[n - 1]) / dd[n - 2];
+        for (int i = n - 3; i >= 0; --i)
+          b[i] = (b[i] - du[i] * b[i + 1] - du2[i] * b[i + 2]) / dd[i];
+      }
+      __syncthreads();
+      for (int q = j0; q < j; ++q) {  // MGS against the cluster's vectors
+        double part = 0.0;
+        for (int i = tid; i < n; i += kEigThreads) part += z[size_t(i) * keep + q] * b[i];
+        const double dot = block_reduce(part, red);
+        __syncthreads();
+        for (int i = tid; i < n; i += kEigThreads) b[i] -= dot * z[size_t(i) * keep + q];
+        __syncthreads();
+      }
+      double part = 0.0;
+      for (int i = tid; i < n; i += kEigThreads) part += b[i] * b[i];
+      const double nrm = sqrt(block_reduce(part, red));
+      __syncthreads();
+      if (nrm == 0.0) {
+        for (int i = tid; i < n; i += kEigThreads) b[i] = i == j % n ? 1.0 : 0.0;
+      } else {
+        for (int i = tid; i < n; i += kEigThreads) b[i] /= nrm;
+      }
+      __syncthreads();
+    }
+    for (int i = tid; i < n; i += kEigThreads) z[size_t(i) * keep + j] = b[i];
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
+// Sign convention: each column's largest-magnitude component (first among equals) positive.
+// One block per column.
+__global__ __launch_bounds__(kEigThreads) void oap_eig_signs(double* z, int n, int keep) {
+  __shared__ double bv[4];
+  __shared__ int bi[4];
+  __shared__ double sgn;
+  const int c = blockIdx.x;
+  double v = -1.0;
+  int ix = 0x7fffffff;
+  for (int i = threadIdx.x; i < n; i += kEigThreads) {
+    const double a = fabs(z[size_t(i) * keep + c]);
+    if (a > v) {  // (ascending i per thread: the first of equals)
+      v = a;
+      ix = i;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(ix, o, 64);
+    if (ov > v || (ov == v && oi < ix)) {
+      v = ov;
+      ix = oi;
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    bv[threadIdx.x >> 6] = v;
+    bi[threadIdx.x >> 6] = ix;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double b = bv[0];
+    int j = bi[0];
+    for (int q = 1; q < kEigThreads / 64; ++q)
+      if (bv[q] > b || (bv[q] == b && bi[q] < j)) {
+        b = bv[q];
+        j = bi[q];
+      }
+    sgn = z[size_t(j) * keep + c] < 0.0 ? -1.0 : 1.0;
+  }
+  __syncthreads();
+  if (sgn < 0.0)
+    for (int i = threadIdx.x; i < n; i += kEigThreads)
+      z[size_t(i) * keep + c] = -z[size_t(i) * keep + c];
+}
+
+// Bisection with the bracket on the device (oap_eig_gersh's output)
+__global__ __launch_bounds__(kEigThreads) void oap_eig_bisect_dev(const double* d, const double* e,
+                                                                  int n, const double* bracket,
+                                                                  double* out) {
+#pragma clang fp contract(off)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* sd = reinterpret_cast<double*>(smem);
+  double* se2 = sd + n;
+  for (int i = threadIdx.x; i < n; i += kEigThreads) {
+    sd[i] = d[i];
+    se2[i] = i + 1 < n ? e[i] * e[i] : 0.0;
+  }
+  __syncthreads();
+  const double pivmin = bracket[2];
+  const int lane = threadIdx.x & 63;
+  const int idx = blockIdx.x * (kEigThreads / 64) + (threadIdx.x >> 6);
+  if (idx >= n) return;  // (wave-uniform; no barrier follows)
+  double lo = bracket[0], hi = bracket[1];
+  for (int round = 0; round < 16; ++round) {
+    const double w = hi - lo;
+    if (!(w > 2.0 * 2.2204460492503131e-16 * fmax(fabs(lo), fabs(hi)) + 2.0 * pivmin)) break;
+    const double x = lo + w * (double(lane + 1) / 65.0);
+    int cnt = 0;
+    double q = sd[0] - x;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+    for (int i = 1; i < n; ++i) {
+      q = (sd[i] - x) - se2[i - 1] / q;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+    }
+    const unsigned long long below = __ballot(cnt <= idx);
+    const int L = __popcll(below);
+    const double xl = __shfl(x, L > 0 ? L - 1 : 0, 64), xh = __shfl(x, L < 64 ? L : 63, 64);
+    if (L > 0) lo = xl;
+    if (L < 64) hi = xh;
+  }
+  if (lane == 0) out[idx] = 0.5 * (lo + hi);
+}
+
 }  // namespace
 
 void eig_bisect(const double* d, const double* e, int n, double lo, double hi, double pivmin,
@@ -426,6 +732,41 @@ void eig_bisect(const double* d, const double* e, int n, double lo, double hi, d
   const int per = kEigThreads / 64;
   hipLaunchKernelGGL(oap_eig_bisect, dim3((n + per - 1) / per), dim3(kEigThreads), lds, s, d, e,
                      n, lo, hi, pivmin, out);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+size_t eig_vectors_scratch_doubles(int n, int keep) { return 4 + size_t(keep) + size_t(keep); }
+
+bool eig_vectors_supported(int n, int keep) {
+  return n >= 3 && n <= 8 * kEigThreads && keep >= 1 && keep <= n &&
+         size_t(n) * 41 + 64 <= size_t(kEigLdsCap);
+}
+
+void eig_top_vectors(const double* d, const double* e, int n, int keep, const double* vrows,
+                     const double* tau, double* lam, double* z, double* scratch, hipStream_t s) {
+  OAP_CHECK(eig_vectors_supported(n, keep), "eig_top_vectors: n=" << n << " keep=" << keep);
+  double* bracket = scratch;           // [4]
+  double* sel = scratch + 4;           // [keep]
+  int* cstart = reinterpret_cast<int*>(sel + keep);  // [keep] ints (in keep doubles)
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {reinterpret_cast<const void*>(&oap_eig_bisect_dev),
+                          reinterpret_cast<const void*>(&oap_eig_invit),
+                          reinterpret_cast<const void*>(&oap_eig_select)})
+      OAP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        kEigLdsCap));
+    attr = true;
+  }
+  hipLaunchKernelGGL(oap_eig_gersh, dim3(1), dim3(kEigThreads), 0, s, d, e, n, bracket);
+  const int per = kEigThreads / 64;
+  hipLaunchKernelGGL(oap_eig_bisect_dev, dim3((n + per - 1) / per), dim3(kEigThreads),
+                     sizeof(double) * 2 * size_t(n), s, d, e, n, bracket, lam);
+  hipLaunchKernelGGL(oap_eig_select, dim3(1), dim3(kEigThreads), size_t(n) + 16, s, lam, n, keep,
+                     bracket, sel, cstart);
+  hipLaunchKernelGGL(oap_eig_invit, dim3(keep), dim3(kEigThreads), size_t(n) * 41 + 16, s, d, e,
+                     n, keep, sel, cstart, bracket, z);
+  eig_apply_q(vrows, tau, n, keep, z, s);
+  hipLaunchKernelGGL(oap_eig_signs, dim3(keep), dim3(kEigThreads), 0, s, z, n, keep);
   OAP_HIP_CHECK(hipGetLastError());
 }
 

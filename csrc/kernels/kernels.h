@@ -425,6 +425,15 @@ void eig_bisect(const double* d, const double* e, int n, double lo, double hi, d
                 double* out, hipStream_t s);
 // Z (n x k row-major, device) <- Q Z with the reflectors of eig_tridiag.
 void eig_apply_q(const double* vrows, const double* tau, int n, int k, double* z, hipStream_t s);
+// Everything after eig_tridiag on the device, no host round trip: the Gershgorin bracket, every
+// eigenvalue by multisection (lam [n], ascending), the `keep` of largest magnitude (stable order),
+// their tridiagonal eigenvectors by inverse iteration with Gram-Schmidt inside clusters (the
+// LAPACK dstein recipe), back-transformed by Q and sign-normalised: z [n x keep] row-major.
+// scratch: eig_vectors_scratch_doubles(n, keep) doubles.
+bool eig_vectors_supported(int n, int keep);
+size_t eig_vectors_scratch_doubles(int n, int keep);
+void eig_top_vectors(const double* d, const double* e, int n, int keep, const double* vrows,
+                     const double* tau, double* lam, double* z, double* scratch, hipStream_t s);
 
 }  // namespace kern
 }  // namespace oap

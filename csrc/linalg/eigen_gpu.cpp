@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 #include <vector>
@@ -35,9 +36,40 @@ SymEig sym_eig_topk_gpu(Context& ctx, const double* a, int n, int k, hipStream_t
   kern::eig_tridiag(a, n, cus, d, e, vr.as<double>(), tau, scr.as<double>(),
                     reinterpret_cast<unsigned*>(bar.data()), s);
   e1.record(s);
+  unsigned abort_word = 0;
+  if (kern::eig_vectors_supported(n, k) && !std::getenv("OAP_EIG_HOST_INVIT")) {
+    // the rest on the device (kern::eig_top_vectors): bracket, bisection, selection, inverse
+    // iteration, back-transform and signs — only the results come back
+    Buffer zb = ctx.alloc(sizeof(double) * size_t(n) * k);
+    Buffer sb = ctx.alloc(sizeof(double) * kern::eig_vectors_scratch_doubles(n, k));
+    eb0.record(s);
+    kern::eig_top_vectors(d, e, n, k, vr.as<double>(), tau, lam, zb.as<double>(), sb.as<double>(),
+                          s);
+    eb1.record(s);
+    std::vector<double> vals(n);
+    SymEig out;
+    out.n = n;
+    out.vectors.resize(size_t(n) * k);
+    ctx.copy_to_host(vals.data(), lam, sizeof(double) * n, s);
+    ctx.copy_to_host(out.vectors.data(), zb.data(), sizeof(double) * out.vectors.size(), s);
+    ctx.copy_to_host(&abort_word, bar.data(), sizeof(unsigned), s);
+    OAP_CHECK(abort_word == 0, "eig_tridiag: exchange timed out (workgroups not co-resident)");
+    std::vector<int> perm(n);
+    for (int i = 0; i < n; ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(),
+                     [&](int x, int y) { return std::fabs(vals[x]) > std::fabs(vals[y]); });
+    out.values.resize(n);
+    for (int j = 0; j < n; ++j) out.values[j] = vals[perm[j]];
+    if (timing) {
+      timing->tridiag_ms = Event::elapsed_ms(e0, e1);
+      timing->bisect_ms = Event::elapsed_ms(eb0, eb1);  // (bisection .. signs, on the device)
+      timing->backtransform_ms = 0.0;
+      timing->host_ms = 0.0;
+    }
+    return out;
+  }
   std::vector<double> hd(2 * size_t(n));
   ctx.copy_to_host(hd.data(), d, sizeof(double) * 2 * n, s);
-  unsigned abort_word = 0;
   ctx.copy_to_host(&abort_word, bar.data(), sizeof(unsigned), s);
   OAP_CHECK(abort_word == 0, "eig_tridiag: exchange timed out (workgroups not co-resident)");
   std::vector<double> hdiag(hd.begin(), hd.begin() + n), hoff(hd.begin() + n, hd.end());

@@ -76,3 +76,26 @@ def test_pca_uses_gpu_eig(native):
                                atol=1e-10 * abs(rh["eigenvalues"][0]))
     np.testing.assert_allclose(rg["pc"], rh["pc"], rtol=0, atol=1e-9)
     np.testing.assert_allclose(rg["explained_variance"], rh["explained_variance"], rtol=1e-10)
+
+
+def test_gpu_eig_device_vectors_clusters(native, ctx, monkeypatch):
+    """The device inverse iteration (kern::eig_top_vectors: bracket, bisection, selection,
+    clusters, back-transform and signs without a host round trip) on a spectrum with a triple
+    eigenvalue and a close pair in the top k: orthonormal eigenvectors with small residuals, the
+    cluster's subspace equal to the host path's (OAP_EIG_HOST_INVIT=1)."""
+    n, k = 400, 8
+    rng = np.random.default_rng(21)
+    q, _ = np.linalg.qr(rng.normal(size=(n, n)))
+    lam = np.concatenate([[100.0, 60.0, 60.0, 60.0, 30.0, 30.0 + 1e-9, 10.0, 5.0],
+                          0.5 * 0.98 ** np.arange(n - 8)])
+    a = (q * lam) @ q.T
+    vg, Vg, _ = native.sym_eig_gpu(ctx, a, k)
+    monkeypatch.setenv("OAP_EIG_HOST_INVIT", "1")
+    vh, Vh, _ = native.sym_eig_gpu(ctx, a, k)
+    monkeypatch.delenv("OAP_EIG_HOST_INVIT")
+    np.testing.assert_allclose(vg, vh, rtol=0, atol=1e-10 * 100)
+    np.testing.assert_allclose(Vg.T @ Vg, np.eye(k), atol=1e-9)
+    r = a @ Vg - Vg * np.asarray(vg[:k])[None, :]
+    assert np.abs(r).max() <= 1e-8 * 100
+    for sl in (slice(0, 1), slice(1, 4), slice(4, 6), slice(6, 8)):  # eigenspace projectors
+        np.testing.assert_allclose(Vg[:, sl] @ Vg[:, sl].T, Vh[:, sl] @ Vh[:, sl].T, atol=1e-8)
