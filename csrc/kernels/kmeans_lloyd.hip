@@ -642,6 +642,26 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
           epilogue(c0, acc);
         }
       }
+      if constexpr (U == 4) {
+        // accumulator-pipelined: chunk c + 1's MFMA chain is issued before chunk c's epilogue
+        // (into the other accumulator), so this wave's own VALU runs under its matrix work — an
+        // MFMA holds the SIMD's vector issue for 8 of its 32 cycles, so a 32-centroid epilogue
+        // (~45 VALU) fits under a chain of KS MFMAs
+        f32x16 accA, accB;
+        int c = 0;
+        mfma_chunk(0, accA);
+        while (true) {  // invariant: accA holds chunk c (issued)
+          if (c + 32 < kpad) mfma_chunk(c + 32, accB);
+          epilogue(c, accA);
+          c += 32;
+          if (c >= kpad) break;
+          if (c + 32 < kpad) mfma_chunk(c + 32, accA);
+          epilogue(c, accB);
+          c += 32;
+          if (c >= kpad) break;
+        }
+        c0 = kpad;
+      }
       for (; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
         f32x16 acc;
         mfma_chunk(c0, acc);
@@ -878,6 +898,14 @@ void launch_lean_v(const LeanArgs& a, int grid, int variant, bool cost, hipStrea
     case 7:  // 3 waves/SIMD, two chunks per step, prefetch without the cost
       if (cost) launch_lean<KS, XB, 12, 0, true, 2>(a, grid, s);
       else launch_lean<KS, XB, 12, 2, false, 2>(a, grid, s);
+      break;
+    case 12:  // 3 waves/SIMD, accumulator-pipelined chunk loop
+      if (cost) launch_lean<KS, XB, 12, 0, true, 4>(a, grid, s);
+      else launch_lean<KS, XB, 12, 2, false, 4>(a, grid, s);
+      break;
+    case 13:  // 4 waves/SIMD, accumulator-pipelined chunk loop
+      if (cost) launch_lean<KS, XB, 16, 0, true, 4>(a, grid, s);
+      else launch_lean<KS, XB, 16, 2, false, 4>(a, grid, s);
       break;
     default:  // 4 waves/SIMD
       if (cost) launch_lean<KS, XB, 16, 0, true>(a, grid, s);
@@ -1325,7 +1353,10 @@ int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid) {
 
 int kmeans_lloyd_waves(int variant) {
   if (variant == 11) return 8;
-  return (variant == 3 || variant == 5 || variant == 7 || variant == 8 || variant == 9) ? 12 : 16;
+  return (variant == 3 || variant == 5 || variant == 7 || variant == 8 || variant == 9 ||
+          variant == 12)
+             ? 12
+             : 16;
 }
 
 int kmeans_lloyd_rch(int d) {

@@ -649,35 +649,43 @@ def test_image_kernel_scale_fallback(native):
 def test_provisional_fixed_point_bounds(native, monkeypatch, case):
     """Fixed-point bounds from the initial centers (no column-maxima pass before the first
     iteration; its lean pass checks every value against them and sums |x|^2 for the final
-    cost): the fit equals the CPU engine bitwise, which evaluates the same rule on the exact
-    column maxima — bounds that hold ("centers"), a value past the smallest bound but inside its
-    own column's ("centers_checked": the maxima pass confirms), and a value past its column's
-    bound ("restart": the fit reruns with the maxima's scales)."""
+    cost) — bounds that hold ("centers"), a value past the smallest bound but inside its own
+    column's ("centers_checked": the maxima pass confirms), a value past its column's bound
+    ("restart": the fit reruns with the maxima's scales).  The lazy check gives the fit of the
+    same rule evaluated eagerly on the column maxima (OAP_KMEANS_ABSMAX_PASS=1) bitwise, and
+    the CPU engine's (which evaluates the rule on its own maxima) on separated clusters."""
     monkeypatch.setenv("OAP_KMEANS_PROVISIONAL_MIN", "0")
     n, d, k = 120000, 12, 24
-    rng = np.random.default_rng(7)
-    C = rng.uniform(-10, 10, size=(k, d))
-    X = C[rng.integers(0, k, n)] + rng.normal(0, 2.0, size=(n, d))
-    if case == "centers_checked":
-        X[:, 0] *= 40.0  # column 0's bound is large, the smallest bound is another column's
-        X[5, 0] = np.abs(X[:, 0]).max() * 0.99
-        C[:, 0] *= 40.0
-    X = X.astype(np.float32).astype(np.float64)
-    init = X[rng.choice(n, k, replace=False)].copy()
-    if case == "restart":
-        X[17, 3] = 1e5  # far past every initial center's coordinate range
+    for sigma in (2.0, 0.3):  # overlapping (lazy vs eager), separated (vs the CPU engine)
+        rng = np.random.default_rng(7)
+        C = rng.uniform(-10, 10, size=(k, d))
+        X = C[rng.integers(0, k, n)] + rng.normal(0, sigma, size=(n, d))
+        if case == "centers_checked":
+            X[:, 0] *= 40.0  # column 0's bound is large, the smallest bound another column's
+            X[5, 0] = np.abs(X[:, 0]).max() * 0.99
         X = X.astype(np.float32).astype(np.float64)
-    g, c = native.Context(0, 0.5, 0), native.Context(-1)
-    tg = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
-    tc = native.upload_dense(c, X, "f64", d)
-    for tol, it in ((-1.0, 9), (0.0, 6)):
-        rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
-        rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, it, tol)
-        assert rg["scale_source"] == case, rg["scale_source"]
-        assert rg["num_iter"] == rc["num_iter"] == it
-        assert rg["last_counts"] == rc["last_counts"]
-        assert np.array_equal(rg["centers"], rc["centers"])
-        np.testing.assert_allclose(rg["cost"], rc["cost"], rtol=1e-6)
+        init = X[rng.choice(n, k, replace=False)].copy()
+        if case == "restart":
+            X[17, 3] = 1e5  # far past every initial center's coordinate range
+        g = native.Context(0, 0.5, 0)
+        tg = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
+        for tol, it in ((-1.0, 9), (0.0, 6)):
+            rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
+            assert rg["scale_source"] == case, rg["scale_source"]
+            assert rg["num_iter"] == it
+            if sigma > 1.0:
+                monkeypatch.setenv("OAP_KMEANS_ABSMAX_PASS", "1")
+                re = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
+                monkeypatch.delenv("OAP_KMEANS_ABSMAX_PASS")
+                assert re["scale_source"] == ("absmax" if case == "restart"
+                                              else "centers_checked")
+            else:
+                c = native.Context(-1)
+                tc = native.upload_dense(c, X, "f64", d)
+                re = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, it, tol)
+            assert re["num_iter"] == it and rg["last_counts"] == re["last_counts"]
+            assert np.array_equal(rg["centers"], re["centers"])
+            np.testing.assert_allclose(rg["cost"], re["cost"], rtol=1e-6)
 
 
 @pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (60, 300)])
