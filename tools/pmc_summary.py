@@ -6,7 +6,11 @@ kernel.  The effective clock is GRBM_GUI_ACTIVE / 8 XCDs / duration (MI355X_MICR
 give-back); when a pass lacks GRBM_GUI_ACTIVE, --clock-ghz (default 2.1) is used.
 
     python tools/pmc_summary.py <tiles> <pass dir> [<pass dir> ...] [--kernel SUBSTR]
-                                [--simds 1024] [--clock-ghz 2.1]
+                                [--simds 1024] [--clock-ghz 2.1] [--dispatch last|longest|N]
+
+--dispatch picks which dispatch of the kernel each pass reports: the last (default), the longest,
+or the N-th (0-based, in dispatch order).  Memory passes add the L2 (TCC) hit ratio and, with
+FETCH_SIZE (KiB), the bytes fetched from HBM and their rate over the dispatch.
 
 Units: SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles, SQ_VALU_MFMA_BUSY_CYCLES
 counts cycles summed over SIMDs."""
@@ -18,7 +22,7 @@ import sys
 
 def main(argv):
     args = list(argv)
-    opts = {"--kernel": "lloyd_t1", "--simds": "1024", "--clock-ghz": "2.1"}
+    opts = {"--kernel": "lloyd_t1", "--simds": "1024", "--clock-ghz": "2.1", "--dispatch": "last"}
     for key in list(opts):
         if key in args:
             i = args.index(key)
@@ -34,7 +38,16 @@ def main(argv):
         rows = [r for r in csv.DictReader(open(path)) if kern in r["Kernel_Name"]]
         if not rows:
             continue
-        last = max(int(r["Dispatch_Id"]) for r in rows)
+        ids = sorted({int(r["Dispatch_Id"]) for r in rows})
+        pick = opts["--dispatch"]
+        if pick == "last":
+            last = ids[-1]
+        elif pick == "longest":
+            span = {int(r["Dispatch_Id"]): float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                    for r in rows}
+            last = max(ids, key=lambda i: span[i])
+        else:
+            last = ids[min(int(pick), len(ids) - 1)]
         mine = [r for r in rows if int(r["Dispatch_Id"]) == last]
         dur_ns = float(mine[0]["End_Timestamp"]) - float(mine[0]["Start_Timestamp"])
         durations.append(dur_ns)
@@ -79,6 +92,12 @@ def main(argv):
         # (level accumulates in-flight VMEM instructions per quad-cycle: mean latency in cycles)
         out["vmem_mean_latency_cycles"] = round(4.0 * vals["SQ_INST_LEVEL_VMEM"] /
                                                 vals["SQ_INSTS_VMEM"], 1)
+    if "TCC_HIT_sum" in vals and "TCC_MISS_sum" in vals:
+        tot = vals["TCC_HIT_sum"] + vals["TCC_MISS_sum"]
+        out["tcc_hit_ratio"] = round(vals["TCC_HIT_sum"] / tot, 4) if tot else None
+    if "FETCH_SIZE" in vals:
+        out["hbm_fetch_gb"] = round(vals["FETCH_SIZE"] * 1024 / 1e9, 3)
+        out["hbm_fetch_tb_per_s"] = round(vals["FETCH_SIZE"] * 1024 / (dur * 1e-9) / 1e12, 3)
     print(json.dumps(out, indent=1))
     return 0
 
