@@ -16,14 +16,17 @@ double now_s() {
 }
 }  // namespace
 
-int als_recommend_max_num(int rank) { return kern::rec_max_num(rank); }
+int als_recommend_max_num(int rank) {
+  return std::max(kern::rec_max_num(rank), kern::rec_big_max_num(rank));
+}
 
 void als_recommend(Context& ctx, const float* src, int64_t n_src, const float* dst,
                    int64_t n_dst, int rank, int num, int32_t* out_idx, float* out_val,
                    int64_t slab_rows, RecTiming* timing) {
   OAP_CHECK(ctx.is_gpu(), "als_recommend needs a GPU context");
-  OAP_CHECK(rank >= 1 && num >= 1 && num <= kern::rec_max_num(rank) && n_dst >= 1,
-            "als_recommend: rank 1..256, num 1.." << kern::rec_max_num(rank));
+  OAP_CHECK(rank >= 1 && num >= 1 && num <= als_recommend_max_num(rank) && n_dst >= 1,
+            "als_recommend: rank 1..256, num 1.." << als_recommend_max_num(rank));
+  const bool big = num > kern::rec_max_num(rank);  // (lists in HBM: rec_topk_big)
   RecTiming t;
   const double w0 = now_s();
   ctx.activate();
@@ -62,6 +65,16 @@ void als_recommend(Context& ctx, const float* src, int64_t n_src, const float* d
   Buffer oidx = ctx.alloc(size_t(slab_rows) * num * 4);
   Buffer oval = ctx.alloc(size_t(slab_rows) * num * 4);
   Buffer sexp = ctx.alloc(size_t(slab_rows) * 4);
+  // big num: candidate buffers for 512 workgroups per launch (the kernel chunks the grid; at
+  // most 2 of its workgroups fit a CU's LDS, so 512 fill the chip), at most the slab's own
+  // (4 MiB per workgroup at the largest cap: 2 GiB)
+  Buffer cand;
+  size_t cand_bytes = 0;
+  if (big) {
+    const int64_t wgs = std::min<int64_t>(512, (slab_rows + gran - 1) / gran);
+    cand_bytes = size_t(wgs) * kern::rec_big_scratch_per_wg(num);
+    cand = ctx.alloc(cand_bytes);
+  }
   for (int64_t r0 = 0; r0 < n_src; r0 += slab_rows) {
     const int64_t rows = std::min(slab_rows, n_src - r0);
     const int64_t rpad = (rows + gran - 1) / gran * gran;
@@ -72,8 +85,13 @@ void als_recommend(Context& ctx, const float* src, int64_t n_src, const float* d
                    rpad, s);
     OAP_HIP_CHECK(hipStreamSynchronize(s));
     double a1 = now_s();
-    kern::rec_topk(simg.data(), sexp.as<int32_t>(), rows, dimg.data(), amax.as<unsigned>() + 1,
-                   n_dst, rank, num, oidx.as<int32_t>(), oval.as<float>(), s);
+    if (big)
+      kern::rec_topk_big(simg.data(), sexp.as<int32_t>(), rows, dimg.data(),
+                         amax.as<unsigned>() + 1, n_dst, rank, num, oidx.as<int32_t>(),
+                         oval.as<float>(), cand.data(), cand_bytes, s);
+    else
+      kern::rec_topk(simg.data(), sexp.as<int32_t>(), rows, dimg.data(), amax.as<unsigned>() + 1,
+                     n_dst, rank, num, oidx.as<int32_t>(), oval.as<float>(), s);
     OAP_HIP_CHECK(hipStreamSynchronize(s));
     double a2 = now_s();
     ctx.copy_to_host(out_idx + r0 * num, oidx.data(), size_t(rows) * num * 4, s);

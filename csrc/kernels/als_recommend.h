@@ -21,6 +21,9 @@ int rec_ks(int rank);
 int rec_row_slots(int rank);
 // largest num the kernel's per-row lists hold at this rank (0: rank not supported)
 int rec_max_num(int rank);
+// largest num of the HBM-buffer variant (rec_topk_big), and its candidate scratch per workgroup
+int rec_big_max_num(int rank);
+size_t rec_big_scratch_per_wg(int num);
 // source rows per workgroup of the top-k kernel at (rank, num): pad the source image to this
 size_t rec_src_granule(int rank, int num);
 // max |x| of rows [n][ld] (first `rank` columns) as float bits into *amax (atomicMax; zero it
@@ -40,6 +43,14 @@ void rec_pack(const float* x, int64_t n, int rank, int64_t ld, const unsigned* a
 void rec_topk(const void* src_img, const int32_t* src_exp, int64_t n_src, const void* dst_img,
               const unsigned* dst_amax, int64_t n_dst, int rank, int num, int32_t* out_idx,
               float* out_val, hipStream_t s);
+// The same for num beyond the LDS lists (rec_max_num < num <= rec_big_max_num): per-lane
+// candidate buffers in `scratch` (HBM; workgroups run in chunks of scratch_bytes /
+// rec_big_scratch_per_wg(num)), sorted by the wave when one could overflow.  src_img rows
+// padded to a multiple of rec_src_granule(rank, num).
+void rec_topk_big(const void* src_img, const int32_t* src_exp, int64_t n_src,
+                  const void* dst_img, const unsigned* dst_amax, int64_t n_dst, int rank, int num,
+                  int32_t* out_idx, float* out_val, void* scratch, size_t scratch_bytes,
+                  hipStream_t s);
 
 }  // namespace kern
 }  // namespace oap

@@ -459,23 +459,20 @@ def _local_topk(S: np.ndarray, D: np.ndarray, num: int, w, block: int):
     if n == 0 or num == 0:
         return idx, val
     if w.is_gpu:
+        # the fused score + top-k kernel for every num it holds (LDS lists up to ~24, HBM
+        # candidate buffers up to 4088: kernels/als_recommend.hip); beyond that, and for ranks
+        # above 256, the host loop below (said out loud: it is not the GPU path)
         N = _loader.load()
         rank = S.shape[1] if S.ndim == 2 else 0
         if 1 <= rank and num <= N.als_recommend_max_num(rank) and len(D) > 0:
             i32, v, _ = N.als_recommend(w.ctx, np.ascontiguousarray(S, dtype=np.float32),
                                         np.ascontiguousarray(D, dtype=np.float32), num)
             return i32.astype(np.int64), v
-        import torch
+        import warnings
 
-        dev = torch.device("cuda", w.device)
-        Dt = torch.from_numpy(np.ascontiguousarray(D, dtype=np.float32)).to(dev)
-        for b in range(0, n, block):
-            Sb = torch.from_numpy(np.ascontiguousarray(S[b:b + block], dtype=np.float32)).to(dev)
-            sc = Sb @ Dt.T
-            v, i = torch.topk(sc, num, dim=1, largest=True, sorted=True)
-            idx[b:b + block] = i.cpu().numpy()
-            val[b:b + block] = v.cpu().numpy()
-        return idx, val
+        warnings.warn(f"recommendForAll*: num={num} at rank {rank} is beyond the GPU kernel "
+                      f"(num <= {N.als_recommend_max_num(max(rank, 1))}, rank <= 256); "
+                      "scoring on the host", RuntimeWarning, stacklevel=3)
     for b in range(0, n, block):
         sc = S[b:b + block].astype(np.float32) @ D.astype(np.float32).T
         part = np.argpartition(-sc, num - 1, axis=1)[:, :num] if num < sc.shape[1] else \

@@ -61,6 +61,37 @@ def test_topk_matches_oracle(native, ctx, n, m, rank, num):
     assert info["slabs"] == 1
 
 
+@pytest.mark.parametrize("n,m,rank,num", [(300, 5000, 10, 100), (200, 3000, 64, 1000),
+                                          (150, 1400, 129, 600), (70, 4500, 8, 3000),
+                                          (97, 2100, 33, 1016)])
+def test_large_num_matches_oracle(native, ctx, n, m, rank, num):
+    """num beyond the LDS lists: the HBM candidate-buffer variant (4 waves up to num 1016, one
+    wave with the 64 KiB sort buffer above), against the same fp64 oracle."""
+    assert num > 24 and num <= native.als_recommend_max_num(rank)
+    rng = np.random.default_rng(n + m + rank + num)
+    S = rng.normal(0, 1, size=(n, rank)).astype(np.float32)
+    D = (rng.normal(0, 0.3, size=(m, rank)) + 0.1).astype(np.float32)
+    idx, val, info = native.als_recommend(ctx, S, D, num)
+    _check(S, D, idx, val, num)
+    assert info["slabs"] == 1
+
+
+def test_large_num_ties_and_padding(native, ctx):
+    """Duplicate destinations (exact ties: lower index first) and fewer destinations than num
+    in the HBM-buffer variant."""
+    rng = np.random.default_rng(5)
+    S = rng.normal(size=(90, 16)).astype(np.float32)
+    D = np.repeat(rng.normal(size=(40, 16)).astype(np.float32), 3, axis=0)  # 120 rows
+    idx, val, _ = native.als_recommend(ctx, S, D, 100)
+    _check(S, D, idx, val, 100)
+    for i in range(len(S)):  # among equal scores, indices ascend
+        same = np.nonzero(np.diff(val[i]) == 0)[0]
+        assert (idx[i][same] < idx[i][same + 1]).all()
+    idx, val, _ = native.als_recommend(ctx, S, D[:70], 100)
+    assert (idx[:, 70:] == -1).all() and np.isneginf(val[:, 70:]).all()
+    _check(S, D[:70], idx[:, :70], val[:, :70], 70)
+
+
 def test_slabs_and_scale(native, ctx):
     """Several source slabs (each with its own fp16 scale) give the one-slab answer."""
     rng = np.random.default_rng(7)
@@ -101,3 +132,18 @@ def test_model_recommend_uses_kernel(native, gpu_world):
     df = model.recommendForAllUsers(10)
     recs = df["recommendations"].tolist()
     assert [r[0]["item"] for r in recs] == [int(5 + j) for j in idx[:, 0]]
+
+
+def test_model_recommend_large_num_on_kernel(native, gpu_world):
+    """recommendForAllUsers(num=1000) stays on the kernel (no host-scoring warning)."""
+    import warnings
+
+    from oap_mllib_amd.models import recommendation as rec
+
+    rng = np.random.default_rng(12)
+    U = rng.normal(size=(150, 20)).astype(np.float32)
+    V = rng.normal(size=(2500, 20)).astype(np.float32)
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        idx, val = rec._blocked_topk(U, V, 1000)
+    _check(U, V, idx, val, 1000)
