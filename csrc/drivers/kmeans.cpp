@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -11,6 +12,7 @@
 #include <random>
 #include <set>
 #include <sstream>
+#include <string>
 #include <unordered_map>
 
 #include "kernels/kernels.h"
@@ -1252,6 +1254,30 @@ std::vector<double> kmeans_init_centers(Context& ctx, Comm& comm, DenseTable& x,
 // (accepted when its rigorous bound is within 1e-5 of the result: the per-row fp32 cost pass it
 // replaces carries (d + 1) 2^-24 per row — ~3e-6 at d = 50 — in the worst case too)
 constexpr double kStatsCostRel = 1e-5;
+// OAP_KMEANS_HOST_MARKS=1: host timestamps at the fit's phase boundaries, to stderr (where a
+// fit's wall clock goes when its kernels do not fill it: allocations, syncs, read-backs)
+namespace {
+struct HostMarks {
+  bool on = false;
+  std::chrono::steady_clock::time_point t0;
+  std::string out;
+  HostMarks() {
+    const char* e = std::getenv("OAP_KMEANS_HOST_MARKS");
+    on = e && *e == '1';
+    t0 = std::chrono::steady_clock::now();
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const double us =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    out += std::string(" ") + what + "=" + std::to_string(int64_t(us));
+  }
+  ~HostMarks() {
+    if (on) std::fprintf(stderr, "kmeans_fit host marks (us):%s\n", out.c_str());
+  }
+};
+}  // namespace
+
 static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const u64* sums_d,
                            const u64* counts_d, const float* centers_d, int k, int d, int dp,
                            const std::vector<double>& inv_scale, const double* fused_T,
@@ -1305,6 +1331,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   OAP_CHECK(p.max_iter >= 0, "maxIter must be >= 0");
   if (ctx.is_gpu()) check_gpu_table(x);
   ctx.activate();
+  HostMarks hm;
   KMeansResult res;
   const int d = x.cols;
   res.d = d;
@@ -1340,6 +1367,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   };
   if (!ctx.is_gpu()) bounds_from_absmax();
   const size_t kd = size_t(k) * d;
+  hm.mark("setup");
   auto t_iter = std::chrono::steady_clock::now();
   Metrics& M = ctx.metrics();
 
@@ -1730,6 +1758,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   int scan_iters = 0;  // scan passes in the current batch
   std::vector<char> it_scanned(B, 0), it_costless(B, 0);
   bool last_costless = false;  // the last iteration computed no cost (rank-uniform)
+  hm.mark("buffers");
   for (int it0 = 0, nb_it = 0; it0 < p.max_iter && !stop; it0 += nb_it) {
     // the first batch is short so the adaptive choices (tier, scan) are made early
     // (with the scan on, the first batch ends after the first delta iteration: its moved-row
@@ -2064,6 +2093,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       }
     }
   }
+  hm.mark("loop");
   if (restart) {
     // a row beyond the provisional bounds: the first batch's integers may have wrapped — the
     // fit runs again from its initial centers with the column maxima's scales (rare: rows
@@ -2144,6 +2174,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       res.cost_history.back() = c;
     }
   }
+  hm.mark("final_cost");
   res.last_counts.assign(counts_h.as<u64>(), counts_h.as<u64>() + k);
   res.centers.resize(kd);
   ctx.copy_to_host(res.centers.data(), c64.data(), sizeof(double) * kd, s);
@@ -2169,6 +2200,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     res.moved_rows = static_cast<int64_t>(dr[1]) + cmoved;
     res.image_passes = static_cast<int>(dr[2]);  // counted by the passes that read the image
   }
+  hm.mark("results");
   res.iter_seconds = seconds_since(t_iter);
   M.set_value("kmeans/iter_seconds", res.iter_seconds);
   M.set_value("kmeans/refine_tiles", double(res.refine_tiles));

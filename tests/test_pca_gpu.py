@@ -171,8 +171,10 @@ def test_exact_f64_rows_beyond_budget_go_up_as_f32(gpu_world):
     try:
         O.shutdown_world()
         O.init_world(O.get_config().replace(device="gpu", device_id=0))
-        f = O.PCA(k=3, inputCol="features").fit(X)
-        assert f.fit_info["device_rows_dtype"] == "f32" and f.fit_info["precision"] == "exact"
+        with pytest.warns(RuntimeWarning, match="f32"):
+            f = O.PCA(k=3, inputCol="features").fit(X)
+        assert f.fit_info["device_rows_dtype"] == "f32"
+        assert f.fit_info["precision"] == "exact_f32_rows"  # (said so, not called "exact")
         X32 = X.astype(np.float32).astype(np.float64)
         wr = np.sort(np.linalg.eigvalsh(np.cov(X32.T, ddof=1)))[::-1]
         np.testing.assert_allclose(f.explainedVariance.toArray(), wr[:3] / wr.sum(), rtol=1e-10)
