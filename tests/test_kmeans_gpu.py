@@ -653,7 +653,8 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
     column's ("centers_checked": the maxima pass confirms), a value past its column's bound
     ("restart": the fit reruns with the maxima's scales).  The lazy check gives the fit of the
     same rule evaluated eagerly on the column maxima (OAP_KMEANS_ABSMAX_PASS=1) bitwise, and
-    the CPU engine's (which evaluates the rule on its own maxima) on separated clusters."""
+    (bounds that hold, separated clusters) the CPU engine's, which evaluates the rule on its own
+    maxima.  (The other cases' outliers can sit near a tie, where fp32 and fp64 may differ.)"""
     monkeypatch.setenv("OAP_KMEANS_PROVISIONAL_MIN", "0")
     n, d, k = 120000, 12, 24
     for sigma in (2.0, 0.3):  # overlapping (lazy vs eager), separated (vs the CPU engine)
@@ -677,7 +678,7 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
             rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
             assert rg["scale_source"] == case, rg["scale_source"]
             assert rg["num_iter"] == it or (tol == 0.0 and rg["num_iter"] < it)  # (converged)
-            if sigma > 1.0:
+            if sigma > 1.0 or case != "centers":
                 monkeypatch.setenv("OAP_KMEANS_ABSMAX_PASS", "1")
                 re = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, it, tol)
                 monkeypatch.delenv("OAP_KMEANS_ABSMAX_PASS")
