@@ -35,6 +35,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 #include <type_traits>
 
@@ -1207,6 +1208,383 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
   }
 }
 
+// ---- the exact re-decision by candidates (f32 rows, single-launch passes) ------------------
+// The same decision as oap_kmeans_exact_rows, bitwise, at a fraction of its matrix work: a
+// deferred row's exact argmin can only be a center whose tier-1 distance lies within the tier's
+// pair error bound tt of the tier-1 best (the bound the lean pass deferred it by; kmeans_lloyd
+// tier-1 notes above), so this pass re-runs tier 1 for the row (fp16 MFMA, 28 products at the
+// headline's shape instead of 224 f32 ones), keeps the centers with tier-1 distance <= t1 + 2 tt,
+// and evaluates only those in fp32 on the VALU — as the fmaf chain v_mfma_f32_32x32x2_f32 computes
+// (k = 0 product first, then k = 1, over the same (s, q, component) steps and padding skips as
+// exact_argmin: bitwise the MFMA's value, tools/probes/mfma_f32_order.hip).  A row outside fp16's
+// range for tier 1 (alpha^2 |x|^2 >= 2^20) evaluates every center.  The second-best distance
+// for the Hamerly lower bound is min(the exact second among the candidates, best + tt / alpha^2),
+// a valid lower bound for every center left out.  Accumulation, labels, bounds, cost: as
+// oap_kmeans_exact_rows.
+constexpr int kCandWaves = 8;   // 2 per SIMD: the row in registers twice (own + other half)
+constexpr int kCandList = 8;    // per-lane candidate slots (LDS); more -> the lane takes all
+
+struct CandSmem {
+  size_t plane, cn, sc, acc, cnt, wc, pref, cl, total;
+  bool lds_acc;
+};
+
+__host__ __device__ inline CandSmem cand_plan(int kpad, int k, int d, bool acc, bool sums) {
+  const int dp = (d + 15) / 16 * 16;
+  CandSmem m;
+  size_t off = 0;
+  m.plane = 0;
+  off = round16(size_t(kpad) * stride_bf16(dp) * 2);
+  m.cn = off;
+  off = round16(off + size_t(kpad) * 4);
+  m.sc = off;
+  off = round16(off + size_t(dp) * 4);
+  m.wc = off;
+  off = round16(off + kCandWaves * 8);
+  m.pref = off;
+  off = round16(off + (kDeferSubs + 1) * 4);
+  m.cl = off;
+  off = round16(off + size_t(kCandWaves) * 64 * kCandList * 4);
+  m.acc = off;
+  const size_t base = off;
+  size_t accb = (acc && sums) ? size_t(k) * (d | 1) * 8 : 0;
+  size_t cntb = acc ? size_t(k) * 4 : 0;
+  m.lds_acc = acc && round16(base + accb) + round16(cntb) <= kLdsLimit - 1024;
+  if (!m.lds_acc) accb = cntb = 0;
+  off = round16(off + accb);
+  m.cnt = off;
+  off = round16(off + cntb);
+  m.total = off;
+  return m;
+}
+
+template <int KS>
+__global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansAssignArgs a) {
+  constexpr int EW = kCandWaves;
+  constexpr int DP = 16 * KS;
+  constexpr int NT = EW * 64;
+  using F = Frag<KS, false>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int k = a.k, d = a.d, kpad = a.kpad;
+  const bool accumulate = a.accumulate;
+  const CandSmem L = cand_plan(kpad, k, d, accumulate, a.sums_too);
+  const int sb = stride_bf16(DP);
+  _Float16* ph = reinterpret_cast<_Float16*>(smem + L.plane);
+  float* cn = reinterpret_cast<float*>(smem + L.cn);
+  float* sc_l = reinterpret_cast<float*>(smem + L.sc);
+  double* acc_l = reinterpret_cast<double*>(smem + L.acc);
+  unsigned* cnt_l = reinterpret_cast<unsigned*>(smem + L.cnt);
+  double* wc = reinterpret_cast<double*>(smem + L.wc);
+  unsigned* pref = reinterpret_cast<unsigned*>(smem + L.pref);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  int* cl = reinterpret_cast<int*>(smem + L.cl) + wave * 64 * kCandList + lane;  // [slot * 64]
+  if (tid == 0) {
+    pref[0] = 0u;
+    for (int w = 0; w < a.row_subs; ++w)
+      pref[w + 1] = pref[w] + a.row_count[blockIdx.x * kDeferSubs + w];
+  }
+  __syncthreads();
+  const unsigned total = pref[a.row_subs];
+  if (total == 0) {
+    if (tid == 0 && a.cost_slab) a.cost_slab[blockIdx.x] = 0.0;
+    return;
+  }
+  const float cmax = a.cstat[0];
+  const float alpha = lean_alpha(cmax);
+  const float a2 = alpha * alpha;
+  const float inv_a2 = 1.f / a2;  // (a power of two)
+  // the tier-1 plane exactly as the lean first pass stages it (c' = [-2 alpha c, .., hi, lo
+  // (alpha^2 |c|^2 / 16), 16, 16])
+  for (int idx = tid; idx < kpad * DP; idx += NT) {
+    const int c = idx / DP, f = idx - c * DP;
+    _Float16 v;
+    if (f < d) {
+      v = static_cast<_Float16>(-2.f * alpha * a.centers[idx]);
+    } else if (f == DP - 4 || f == DP - 3) {
+      _Float16 hi, lo;
+      split_f16((c < k) ? a2 * a.cnorm[c] * (1.f / kBiasUnit) : 60000.f, hi, lo);
+      v = (f == DP - 4) ? hi : lo;
+    } else {
+      v = static_cast<_Float16>(f >= DP - 2 ? kBiasUnit : 0.f);
+    }
+    ph[c * sb + f] = v;
+  }
+  for (int c = tid; c < kpad; c += NT) cn[c] = (c < k) ? a.cnorm[c] : 1e30f;
+  for (int f = tid; f < DP; f += NT) sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
+  if (L.lds_acc) {
+    if (a.sums_too)
+      for (int i = tid; i < k * (d | 1); i += NT) acc_l[i] = 0.0;
+    for (int i = tid; i < k; i += NT) cnt_l[i] = 0u;
+  }
+  __syncthreads();
+  const int64_t sub = a.row_seg_cap / a.row_subs;
+  const float cm_s = alpha * cmax;
+  const float thr_c = 0.0040f * cm_s;
+  const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
+  const float mrel = 4e-7f * float(d + 8);
+  const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);
+  const int64_t ngroups = (int64_t(total) + 31) / 32;
+  auto slot_at = [&](int64_t i) -> int64_t {
+    i = i < int64_t(total) ? i : int64_t(total) - 1;
+    int w = 0;
+    while (w + 1 < a.row_subs && int64_t(pref[w + 1]) <= i) ++w;
+    return int64_t(blockIdx.x) * a.row_seg_cap + w * sub + (i - pref[w]);
+  };
+  auto row_at = [&](int64_t i) -> int64_t { return int64_t(a.row_list[slot_at(i)]); };
+  auto load_rows = [&](int64_t g, F& dst) {
+    const int64_t row = row_at(g * 32 + r);
+    const float* p = static_cast<const float*>(a.x) + row * a.ld + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int f = 16 * s + 8 * h + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s < KS - 1 || f < a.ld) v = *reinterpret_cast<const float4*>(p + 16 * s + 4 * q);
+        dst.v[s][4 * q + 0] = v.x;
+        dst.v[s][4 * q + 1] = v.y;
+        dst.v[s][4 * q + 2] = v.z;
+        dst.v[s][4 * q + 3] = v.w;
+      }
+  };
+  auto add_row = [&](const F& xv, int b, bool neg) {
+    if (L.lds_acc) {
+      if (h == 0) atomicAdd(&cnt_l[b], neg ? 0xffffffffu : 1u);
+    } else if (h == 0) {
+      atomicAdd(&a.counts[b], neg ? ~0ull : 1ull);
+    }
+    if (!a.sums_too) return;
+    const float sgn = neg ? -1.f : 1.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = 16 * s + 8 * h + j;
+        if (f < d) {
+          const float q = sgn * rintf(xv.at(s, j) * sc_l[f]);
+          if (L.lds_acc)
+            atomicAdd(acc_l + b * (d | 1) + f, static_cast<double>(q));
+          else
+            atomicAdd(&a.sums[size_t(b) * d + f], static_cast<u64>(static_cast<long long>(q)));
+        }
+      }
+  };
+  double my_cost = 0.0;
+  F xa, xb;
+  int64_t g = wave;
+  load_rows(g, xa);
+  for (; g < ngroups; g += EW) {  // wave-uniform
+    const int64_t i = g * 32 + r;
+    const bool valid = i < int64_t(total);
+    const int64_t row = row_at(i);
+    F& x = xa;
+    load_rows(g + EW, xb);  // next group: in flight under this one
+    // the whole row in h-normalised order: x0 = features 16 s + j (j < 8), x1 = 16 s + 8 + j
+    float x0[KS][8], x1[KS][8];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float o = __shfl_xor(x.v[s][j], 32, 64);
+        x0[s][j] = h ? o : x.v[s][j];
+        x1[s][j] = h ? x.v[s][j] : o;
+      }
+    // tier-1 operand (as the lean first pass builds it) and alpha^2 |x|^2 from its bias pair
+    float nx2 = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) nx2 = fmaf(x.at(s, j), x.at(s, j), nx2);
+    nx2 += xor32_f(nx2);
+    f16x8 xh[KS];
+    {
+      _Float16 nh, nl;
+      split_f16(alpha * alpha * nx2 * (1.f / kBiasUnit), nh, nl);
+      const _Float16 unit = static_cast<_Float16>(kBiasUnit);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        f16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const f32x2 pp = f32x2{x.at(s, j), x.at(s, j + 1)} * alpha;
+          const f16x2 qq = __builtin_convertvector(pp, f16x2);
+          v[j] = qq[0];
+          v[j + 1] = qq[1];
+        }
+        if (s == KS - 1) {
+          v[4] = h ? unit : v[4];
+          v[5] = h ? unit : v[5];
+          v[6] = h ? nh : v[6];
+          v[7] = h ? nl : v[7];
+        }
+        xh[s] = v;
+      }
+    }
+    const float mine =
+        kBiasUnit * (static_cast<float>(xh[KS - 1][6]) + static_cast<float>(xh[KS - 1][7]));
+    const float other = xor32_f(mine);
+    const float nx2_s = h ? mine : other;
+    auto tier1 = [&](int c0) -> f32x16 {
+      f32x16 acc = f32x16{};
+      const _Float16* ap = ph + size_t(c0 + r) * sb + 8 * h;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+            *reinterpret_cast<const f16x8*>(ap + 16 * s), xh[s], acc, 0, 0, 0);
+      return acc;
+    };
+    // pass 1: the tier-1 best and second of the row
+    float t1 = INFINITY, t2 = INFINITY;
+    for (int c0 = 0; c0 < kpad; c0 += 32) {
+      const f32x16 acc = tier1(c0);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        t2 = fminf(t2, fmaxf(t1, acc[e]));
+        t1 = fminf(t1, acc[e]);
+      }
+    }
+    {
+      const float o1 = xor32_f(t1), o2 = xor32_f(t2);
+      t2 = fminf(fmaxf(t1, o1), fminf(t2, o2));
+      t1 = fminf(t1, o1);
+    }
+    const float tt = fmaf(thr_c, __builtin_amdgcn_sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s +
+                     2.5e-4f * fabsf(t2);
+    // (row-uniform: both halves hold t1, t2, nx2_s)
+    const bool every = !(nx2_s < 1048576.f) || !(t1 < INFINITY) || !(tt < INFINITY);
+    const float T = t1 + 2.f * tt;
+    // pass 2: this lane's candidates (centers c0 + 8 g + 4 h + q of each chunk) into its slots
+    int ncand = 0;
+    if (!every) {
+      for (int c0 = 0; c0 < kpad; c0 += 32) {
+        const f32x16 acc = tier1(c0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int c = c0 + 8 * (e >> 2) + 4 * h + (e & 3);
+          if (acc[e] <= T && c < k) {
+            if (ncand < kCandList) cl[ncand * 64] = c;
+            ++ncand;
+          }
+        }
+      }
+    }
+    const bool all_mine = every || ncand > kCandList;  // this lane evaluates all its centers
+    const int my_n = !valid ? 0 : all_mine ? 16 * (kpad / 32) : ncand;
+    // exact fp32 distances of the candidates, in each lane's ascending center order
+    float best = INFINITY, second = INFINITY;
+    int bidx = 0x7fffffff;
+    for (int j = 0; __ballot(j < my_n) != 0; ++j) {  // (wave-uniform trip count)
+      if (j < my_n) {
+        const int c = all_mine ? 32 * (j >> 4) + 8 * ((j & 15) >> 2) + 4 * h + (j & 3)
+                               : cl[j * 64];
+        if (c < k) {
+          const float4* cp = reinterpret_cast<const float4*>(a.centers + size_t(c) * DP);
+          float acc = 0.f;
+#pragma unroll
+          for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+              if (16 * s + 4 * q < d) {
+                const float4 c0v = cp[4 * s + q], c1v = cp[4 * s + 2 + q];
+                acc = fmaf(x1[s][4 * q + 0], c1v.x, fmaf(x0[s][4 * q + 0], c0v.x, acc));
+                acc = fmaf(x1[s][4 * q + 1], c1v.y, fmaf(x0[s][4 * q + 1], c0v.y, acc));
+                acc = fmaf(x1[s][4 * q + 2], c1v.z, fmaf(x0[s][4 * q + 2], c0v.z, acc));
+                acc = fmaf(x1[s][4 * q + 3], c1v.w, fmaf(x0[s][4 * q + 3], c0v.w, acc));
+              }
+            }
+          const float dist = fmaf(-2.f, acc, cn[c]);
+          if (dist < best || (dist == best && c < bidx)) {
+            second = best;
+            best = dist;
+            bidx = a.base + c;
+          } else if (dist < second) {
+            second = dist;
+          }
+        }
+      }
+    }
+    {
+      const float ob = __shfl_xor(best, 32, 64), os = __shfl_xor(second, 32, 64);
+      const int oi = __shfl_xor(bidx, 32, 64);
+      const bool take = ob < best || (ob == best && oi < bidx);
+      second = take ? fminf(best, os) : fminf(second, ob);
+      if (take) {
+        best = ob;
+        bidx = oi;
+      }
+    }
+    // centers left out: exact distance > best + tt / alpha^2
+    if (!every) second = fminf(second, best + tt * inv_a2);
+    const int b = (bidx >= 0 && bidx < k) ? bidx : 0;
+    int old = -1;
+    if (a.delta && valid) old = a.labels[row];
+    float part = 0.f, px = 0.f;
+    const float* cb = a.centers + size_t(b) * DP + 8 * h;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float e = x.at(s, j) - cb[16 * s + j];
+        part = fmaf(e, e, part);
+        px = fmaf(x.at(s, j), x.at(s, j), px);
+      }
+    const float rowcost = part + __shfl_xor(part, 32, 64);
+    const float nx2e = px + __shfl_xor(px, 32, 64);
+    if (valid && accumulate && !(a.delta && (old == b || old < 0))) {
+      add_row(x, b, false);
+      if (a.delta) add_row(x, min(old, k - 1), true);
+    }
+    if (valid && h == 0) {
+      if (a.labels) a.labels[row] = b;
+      if (a.mindist) a.mindist[row] = rowcost;
+      if (a.bounds) {
+        const float marg = mrel * (nx2e + cmax * cmax);
+        reinterpret_cast<float2*>(a.bounds)[row] =
+            make_float2(sqrtf(rowcost) * ueps + 1e-30f,
+                        sqrtf(fmaxf(second + nx2e - 2.f * marg, 0.f)) * (1.f - 1e-6f));
+      }
+      my_cost += double(rowcost);
+    }
+    xa = xb;
+  }
+  const double ws = wave_sum_f64(my_cost);
+  if (lane == 0) wc[wave] = ws;
+  __syncthreads();
+  if (tid == 0 && a.cost_slab) {
+    double tot = 0.0;
+    for (int w = 0; w < EW; ++w) tot += wc[w];
+    a.cost_slab[blockIdx.x] = tot;
+  }
+  if (L.lds_acc) {
+    for (int i = tid; a.sums_too && i < k * d; i += NT) {
+      const int c = i / d, f = i - c * d;
+      const double v = acc_l[c * (d | 1) + f];
+      if (v != 0.0) atomicAdd(&a.sums[i], static_cast<u64>(static_cast<long long>(v)));
+    }
+    for (int i = tid; i < k; i += NT) {
+      const int c = static_cast<int>(cnt_l[i]);
+      if (c) atomicAdd(&a.counts[i], static_cast<u64>(static_cast<long long>(c)));
+    }
+  }
+}
+
+template <int KS>
+void launch_cand(const KMeansAssignArgs& a, int grid, hipStream_t s) {
+  const CandSmem L = cand_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too);
+  static bool attr_set = false;
+  if (!attr_set) {
+    OAP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&oap_kmeans_exact_cand<KS>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      static_cast<int>(kLdsLimit)));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((oap_kmeans_exact_cand<KS>), dim3(grid), dim3(kCandWaves * 64), L.total, s,
+                     a);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
 template <int KS, bool XB>
 void launch_exact(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   const ExactSmem L = exact_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too);
@@ -1465,6 +1843,23 @@ void kmeans_exact_rows(const KMeansAssignArgs& a, int grid, hipStream_t s) {
   OAP_CHECK(a.chunk_mode == 0 ||
                 (a.xstate && a.centers_all && !a.accumulate && !a.delta && !a.bounds),
             "kmeans_exact_rows: chunked pass needs its running state and every center");
+  // the candidate form: f32 rows of a single-launch pass whose centers' tier-1 plane fits (the
+  // chunked and bf16 passes keep the full MFMA sweep); OAP_KMEANS_EXACT=mfma forces the sweep
+  const char* fe = std::getenv("OAP_KMEANS_EXACT");  // (read per call: tests switch it)
+  const bool force_mfma = fe && fe[0] == 'm';
+  if (!force_mfma && !a.xbf16 && a.chunk_mode == 0 && a.d + 4 <= 96 && a.base == 0 &&
+      (a.d + 4 + 15) / 16 * 16 == kmeans_dp(a.d) &&  // (the centers' row stride)
+      cand_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too).total <= kLdsLimit) {
+    switch ((a.d + 4 + 15) / 16) {
+      case 1: launch_cand<1>(a, grid, s); return;
+      case 2: launch_cand<2>(a, grid, s); return;
+      case 3: launch_cand<3>(a, grid, s); return;
+      case 4: launch_cand<4>(a, grid, s); return;
+      case 5: launch_cand<5>(a, grid, s); return;
+      case 6: launch_cand<6>(a, grid, s); return;
+      default: break;  // (KS 7, 8: the row twice in registers spills; the sweep keeps them)
+    }
+  }
   if (a.xbf16)
     launch_exact_xb<true>(a, grid, s);
   else

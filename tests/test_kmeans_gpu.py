@@ -693,7 +693,7 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
             np.testing.assert_allclose(rg["cost"], re["cost"], rtol=1e-6)
 
 
-@pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (32, 96)])
+@pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (44, 96)])
 def test_mover_stage_is_exact(native, monkeypatch, d, k):
     """The row scan's mover stage (rows the Hamerly test cannot prune are bounded against the 32
     centers that moved most, kmeans_lean_img.hip RM 3) skips full passes but never changes a
@@ -716,3 +716,28 @@ def test_mover_stage_is_exact(native, monkeypatch, d, k):
         assert r["last_counts"] == ref["last_counts"]
     assert on["pruned_rows"] >= off["pruned_rows"]
     assert abs(on["cost"] - ref["cost"]) <= 1e-7 * ref["cost"]
+
+
+@pytest.mark.parametrize("d,k,sigma", [(50, 200, 8.0), (20, 24, 3.0), (44, 96, 12.0)])
+def test_exact_candidates_equal_mfma_sweep(native, monkeypatch, d, k, sigma):
+    """The exact re-decision by candidates (tier 1 again, fp32 fmaf chains for the centers within
+    2 tt of the tier-1 best; kmeans_lloyd.hip oap_kmeans_exact_cand) decides every deferred row
+    as the full f32 MFMA sweep does: centers, counts and cost history bitwise, with and without
+    the bound-based pruning (whose lower bounds it writes differently: best + tt / alpha^2 for
+    the centers it leaves out)."""
+    n = 1_200_000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, sigma, 91)
+    comm = native.LocalComm(True)
+    init = native.kmeans_init(g, comm, t, k, "k-means||", 2, 5)
+    out = {}
+    for mode in ("cand", "mfma"):
+        monkeypatch.setenv("OAP_KMEANS_EXACT", mode)
+        out[mode] = [native.kmeans_fit(g, comm, t, init, k, 12, -1.0, prune=pr)
+                     for pr in (True, False)]
+    monkeypatch.delenv("OAP_KMEANS_EXACT")
+    for a, b in zip(out["cand"], out["mfma"]):
+        assert a["deferred_rows"] > 0
+        assert np.array_equal(a["centers"], b["centers"])
+        assert a["last_counts"] == b["last_counts"]
+        np.testing.assert_array_equal(a["cost_history"], b["cost_history"])  # (NaN: costless)
