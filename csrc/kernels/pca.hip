@@ -578,18 +578,28 @@ __global__ __launch_bounds__(kXThreads, 1) void oap_pca_syrk_f64(SyrkF64Args a) 
     const double* buf = lds + cur * (2 * kXPlane);
     double* nbuf = lds + (cur ^ 1) * (2 * kXPlane);  // last read before the previous barrier
     const bool more = r0 + kXRows < r_end;
+    // fragments one k-step ahead (two register sets): k-step ks + 1's LDS reads are in flight
+    // under k-step ks's MFMAs instead of waited for between them (the staging writes between
+    // the steps target the other stage, but the compiler cannot tell, so it never hoisted them)
+    double av[2][4], bv[2][2];
+    auto frag = [&](int ks, double (&a4)[4], double (&b2)[2]) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) a4[x] = buf[(fa + 16 * x) * kXS + 4 * ks + kr];
+#pragma unroll
+      for (int y = 0; y < 2; ++y) b2[y] = buf[boff + (fb + 16 * y) * kXS + 4 * ks + kr];
+    };
+    frag(0, av[0], bv[0]);
 #pragma unroll
     for (int ks = 0; ks < kXRows / 4; ++ks) {
-      double av[4], bv[2];
-#pragma unroll
-      for (int x = 0; x < 4; ++x) av[x] = buf[(fa + 16 * x) * kXS + 4 * ks + kr];
-#pragma unroll
-      for (int y = 0; y < 2; ++y) bv[y] = buf[boff + (fb + 16 * y) * kXS + 4 * ks + kr];
+      const int cs = ks & 1;
+      if (ks + 1 < kXRows / 4) frag(ks + 1, av[cs ^ 1], bv[cs ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);  // (the reads stay ahead of this step's MFMAs)
 #pragma unroll
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 2; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[x], bv[y], acc[x][y], 0, 0, 0);
+          acc[x][y] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(av[cs][x], bv[cs][y], acc[x][y], 0, 0, 0);
       if (more) {
 #pragma unroll
         for (int e = 0; e < kPerStep; ++e) stage_el(nbuf, r0 + kXRows, ks * kPerStep + e);
