@@ -198,6 +198,9 @@ size_t kmeans_lloyd_image_bytes(int64_t n, int d);
 // img_mode 2).  `waves` must be the lean variant's (kmeans_lloyd_waves: the deferral
 // sub-segments), cfg < 0 the default configuration.  When the image's scale cannot hold the
 // current centers the kernel does nothing; kmeans_lloyd with img_mode 3 then runs the pass.
+// the refined tier-1 deferral test of the image passes (kmeans_frag.h refined_tt): on unless
+// OAP_KMEANS_REFINE=0 (timing A/B; labels and statistics are the same either way)
+bool kmeans_refine_default();
 bool kmeans_lean_img_supported(int d, int k, int waves, bool scan = false, bool movers = false);
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s);
 // Row-level bound scan for the image passes: every row of lean workgroup b's range gets the

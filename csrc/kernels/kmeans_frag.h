@@ -111,6 +111,56 @@ __device__ inline void exact_argmin(const float* __restrict__ cbase, int stride,
   if (ob < best || (ob == best && oi < bidx)) bidx = oi;
 }
 
+// ---- Refined tier-1 deferral test (image passes; kmeans_lean_img.hip and kmeans_lloyd.hip's
+// image branch, bitwise the same).  The lean kernels' tier-1 bound tt prices the fp16 rounding of
+// both operands at its worst case: a cross term 2^-8 beta max|c| |beta x|.  The operand image
+// also carries each row's actual rounding residual |e_x| = |fp16(beta x) - beta x| (rounded up)
+// in a pad slot (DP - kResidSlotOff: the plane is 0 there, so no product sees it), and every
+// workgroup computes 2 r, r = max_c |fp16(-2 beta c) - (-2 beta c)| (plane_resid2).  With T the
+// tier-1 value and D the exact alpha^2 distance, for any center c against the pick c1
+//   |(D(c) - T(c)) - (D(c1) - T(c1))| <= 2 |e_x| |beta (c - c1)| + 2 r |X| + rest,
+//   |beta (c - c1)| <= sqrt(D(c)) + sqrt(D(c1)),   D <= T + tt,   |X| <= |beta x| + |e_x|,
+// where rest is tt without its cross term (bias pairs, accumulation, subnormals, key truncation).
+// T - 2 |e_x| sqrt(T + tt) increases with T (tt >= 5e-5 |beta x|^2 >> |e_x|^2), so the test at the
+// second-best key value b2 covers every other center.  On overlapping blobs (headline) this
+// halves the rows the worst-case test defers; only waves holding such a row evaluate it.
+constexpr int kResidSlots = 16;   // LDS: per-wave partial maxima (<= 16 waves per workgroup)
+constexpr int kResidSlotOff = 5;  // image slot DP - 5 (h = 1 lanes, element 3 of step KS - 1)
+
+// 2 max |fp16(-2 alpha c_f) - (-2 alpha c_f)|_2 over this wave's centers (c = tid, tid + nt, ..;
+// each difference is exact in fp32), rounded up; every lane gets the wave's value
+__device__ inline float plane_resid2(const float* __restrict__ centers, int dp, int k, int d,
+                                     float alpha, int tid, int nt) {
+  float m = 0.f;
+  for (int c = tid; c < k; c += nt) {
+    float e2 = 0.f;
+    for (int f = 0; f < d; ++f) {
+      const float p = -2.f * alpha * centers[size_t(c) * dp + f];
+      const float e = static_cast<float>(static_cast<_Float16>(p)) - p;
+      e2 = fmaf(e, e, e2);
+    }
+    m = fmaxf(m, e2);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  return 2.f * __builtin_amdgcn_sqrtf(m * 1.0001f) * 1.001f + 1e-30f;
+}
+
+// fp16 upper bound of a row's residual norm from its fp32 sum of squares (<= 129 roundings)
+__device__ inline _Float16 resid_f16_up(float e2) {
+  return static_cast<_Float16>(__builtin_amdgcn_sqrtf(e2 * 1.0001f) * 1.001f + 6e-8f);
+}
+
+// the refined bound (see above): b1 <= b2 the tier-1 keys' values, tt the worst-case bound, rest
+// tt without its cross term, nx2 |beta x|^2 (bias pair), exn >= |e_x|, r2 = 2 r
+__device__ inline float refined_tt(float b1, float b2, float tt, float rest, float nx2, float exn,
+                                   float r2) {
+  const float xn = __builtin_amdgcn_sqrtf(nx2) * 1.001f + exn;
+  const float s2 = __builtin_amdgcn_sqrtf(fmaxf(b2, 0.f) + tt);
+  const float s1 = __builtin_amdgcn_sqrtf(fmaxf(b1, 0.f) * 1.0005f + tt);
+  return (2.f * exn * (s1 + s2) + r2 * xn + rest) * 1.0001f;
+}
+
 template <int KS>
 __device__ inline void load_row8(const float* __restrict__ p, float (&dst)[KS][8]) {
 #pragma unroll

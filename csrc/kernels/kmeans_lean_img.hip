@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 
 #include "kernels/kmeans_frag.h"
@@ -77,6 +78,7 @@ struct ImgArgs {
   int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
   int movers;  // row-scan passes: the mover stage (RM 3)
+  int refine;  // the refined deferral test (kmeans_frag.h refined_tt; OAP_KMEANS_REFINE=0: off)
   int32_t* mlist;  // RM 3: per-wave lists of the rows the mover stage left, [grid][seg_cap]
 };
 
@@ -97,8 +99,8 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, 
   size_t off = 0;
   m.plane = 0;
   off = round16(size_t(kpad) * stride_bf16(dp) * 2);
-  m.sc = off;
-  off = round16(off + size_t(dp) * 4);
+  m.sc = off;  // scales [dp], then per-wave 2 max |e_c| (kmdev::plane_resid2)
+  off = round16(off + size_t(dp + kmdev::kResidSlots) * 4);
   m.acc = off;
   off = round16(off + size_t(k) * size_t(movers ? (d | 1) : dp + 1) * 8);
   m.cnt = off;
@@ -183,6 +185,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     ph[c * sb + f] = v;
   }
   for (int f = tid; f < DP; f += NT) sc_l[f] = f < d ? a.scale[f] : 0.f;
+  // (the refined deferral test: the plane's largest rounding residual, per wave)
+  const bool refine = a.refine && d <= DP - kResidSlotOff;
+  if (refine) {
+    const float r2w = plane_resid2(a.centers, DP, k, d, alpha, tid, NT);
+    if ((tid & 63) == 0) sc_l[DP + (tid >> 6)] = r2w;
+  }
   for (int i = tid; i < k * rs; i += NT) acc_l[i] = 0.0;
   for (int i = tid; i < k; i += NT) cnt_l[i] = 0;
   float* dr_l = reinterpret_cast<float*>(smem + L.dr);
@@ -233,6 +241,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const float thr_k = ufl(6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f);
   const float mrel = ufl(4e-7f * float(d + 8));
   const float mg_c = ufl(mrel * cm_s * cm_s);
+  float r2m = 0.f;
+  if (refine)
+    for (int w = 0; w < WAVES; ++w) r2m = fmaxf(r2m, sc_l[DP + w]);
+  const float r2max = ufl(r2m);
   const int64_t ntiles_all = (a.n + 31) / 32;
   const bool listed = a.tile_list != nullptr;
   const int64_t T = a.tiles_per_block;
@@ -481,7 +493,16 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     const float tt = fmaf(thr_c, __builtin_amdgcn_sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s +
                      2.5e-4f * fabsf(b2);
     // rows beyond fp16's comfortable range (alpha |x| >= 2^10) are always re-decided
-    const bool unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
+    bool unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
+    // the refined test on the row's own residual (kmeans_frag.h refined_tt; wave-uniform: the
+    // residual's exchange needs both halves)
+    if (refine && __ballot(unsure) != 0ull) {
+      const float em = static_cast<float>(X[KS - 1][3]);
+      const float eo = xor32_f(em);
+      const float rest = thr_k + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
+      const float tr = refined_tt(b1, b2, tt, rest, nx2_s, h ? em : eo, r2max);
+      unsure = unsure && !(b1 >= 0.f && b2 - b1 > tr && nx2_s < 1048576.f);
+    }
     // ---- defer unsure rows (wave-private sub-segment, in tile order)
     const unsigned long long um = __ballot(unsure && h == 0);
     buf_store_b32(rs_def, (n_def + lanes_below(um)) * 4u,
@@ -1024,6 +1045,11 @@ void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds
   OAP_HIP_CHECK(hipGetLastError());
 }
 
+bool kmeans_refine_default() {  // (read per launch: tests switch it within a process)
+  const char* e = std::getenv("OAP_KMEANS_REFINE");
+  return !(e && *e == '0');
+}
+
 bool kmeans_lean_img_supported(int d, int k, int waves, bool scan, bool movers) {
   if (d + 4 > 128 || k < 1 || (waves != 12 && waves != 16)) return false;
   const int dp = (d + 4 + 15) / 16 * 16;
@@ -1076,6 +1102,7 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.k = a.k;
   l.kpad = a.kpad;
   l.movers = scan && a.img_movers ? 1 : 0;
+  l.refine = kmeans_refine_default() ? 1 : 0;
   l.mlist = a.img_mover_list;
   OAP_CHECK(!l.movers || l.mlist, "kmeans_lean_img: the mover stage needs its row lists");
   if (waves == 12)

@@ -83,6 +83,7 @@ struct LeanArgs {
   int accumulate, sums_too, delta;
   int ablate;  // timing ablations only: 1 no accumulate, 2 no cost, 8 no distance, 16 no loads,
                // 32 minimal epilogue
+  int refine;  // image passes: the refined deferral test (kmeans_frag.h refined_tt)
   // centroid-chunked pass (KMeansAssignArgs::chunk_mode): running top-2 keys per row, the
   // chunk's first global center, the global k, every center (the final chunk's exact cost)
   int2* keys;
@@ -112,8 +113,8 @@ __host__ __device__ inline LeanSmem lean_plan(int dp, int kpad, int k, int d, bo
   size_t off = 0;
   m.plane = 0;
   off = round16(size_t(kpad) * stride_bf16(dp) * 2);  // fp16 plane, same 2-byte layout
-  m.sc = off;
-  off = round16(off + size_t(dp) * 4);
+  m.sc = off;  // scales [dp], then per-wave 2 max |e_c| (kmdev::plane_resid2)
+  off = round16(off + size_t(dp + kResidSlots) * 4);
   m.acc = off;
   if (acc && sums) off += size_t(k) * (d | 1) * 8;  // odd row stride: conflict-free ds_add_f64
   off = round16(off);
@@ -230,6 +231,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     ph[c * sb + f] = v;
   }
   for (int f = tid; f < DP; f += NT) sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
+  // image passes: the plane's largest rounding residual for the refined deferral test
+  // (kmeans_frag.h refined_tt), per wave
+  const bool refine = use_img && a.refine && d <= DP - kResidSlotOff;
+  if (refine) {
+    const float r2w = plane_resid2(a.centers, DP, k, d, alpha, tid, NT);
+    if ((tid & 63) == 0) sc_l[DP + (tid >> 6)] = r2w;
+  }
   if (accumulate) {
     if (a.sums_too)
       for (int i = tid; i < k * (d | 1); i += NT) acc_l[i] = 0.0;
@@ -260,6 +268,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   const float thr_c = (XB ? 0.0020f : 0.0040f) * cm_s;
   const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
   const float mrel = 4e-7f * float(d + 8);                // fp32 evaluation margin (bounds)
+  float r2max = 0.f;
+  if (refine)
+    for (int w = 0; w < WAVES; ++w) r2max = fmaxf(r2max, sc_l[DP + w]);
+  r2max = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(r2max)));
   // direct-form |x - c|^2 rounding; the bound square roots are v_sqrt_f32 (1 ulp: inside the
   // 1e-6 relative widening of both bounds)
   const float ueps = 1.f + 1e-6f + 6e-8f * float(d + 4);
@@ -512,13 +524,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
         if (a.img_mode == 1 && pos < npos) {  // write the image (every lane of a real tile)
           _Float16 nh, nl;
           split_f16(beta_w * beta_w * nx2 * (1.f / kBiasUnit), nh, nl);
+          // the row's rounding residual |fp16(beta x) - beta x| (exact differences, packed
+          // fp32 squares) into its pad slot DP - 5 for the refined deferral test
+          const bool wres = d <= DP - kResidSlotOff;
+          f32x2 e2v = {0.f, 0.f};
+          _Float16 v2 = {};  // (the last k-step's element 2: the residual's dword partner)
 #pragma unroll
           for (int s = 0; s < KS; ++s) {  // one k-step at a time (few extra live registers)
             f16x8 v;
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
-              const f16x2 q = __builtin_convertvector(f32x2{x.at(s, j), x.at(s, j + 1)} * beta_w,
-                                                      f16x2);
+              const f32x2 p = f32x2{x.at(s, j), x.at(s, j + 1)} * beta_w;
+              const f16x2 q = __builtin_convertvector(p, f16x2);
+              if (wres) {
+                const f32x2 e = __builtin_convertvector(q, f32x2) - p;
+                e2v = e * e + e2v;
+              }
               v[j] = q[0];
               v[j + 1] = q[1];
             }
@@ -527,8 +548,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
               v[5] = h ? static_cast<_Float16>(kBiasUnit) : v[5];
               v[6] = h ? nh : v[6];
               v[7] = h ? nl : v[7];
+              v2 = v[2];
             }
             *img_frag(tile, s) = v;
+          }
+          if (wres) {  // (the slot's dword rewritten: same lane, same address, program order)
+            const float e2 = e2v[0] + e2v[1];
+            const float e2r = e2 + xor32_f(e2);
+            const f16x2 w = {v2, resid_f16_up(e2r)};
+            if (h) reinterpret_cast<f16x2*>(img_frag(tile, KS - 1))[1] = w;
           }
         }
       }
@@ -683,6 +711,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
            2.5e-4f * fabsf(b2);
       // rows beyond fp16's comfortable range (alpha |x| >= 2^10) are always re-decided
       unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
+      // image passes: the refined test on the row's own residual (kmeans_frag.h refined_tt;
+      // wave-uniform: the residual's exchange needs both halves)
+      if (IMG && refine && __ballot(unsure) != 0ull) {
+        const float em = static_cast<float>(xh[KS - 1][3]);
+        const float eo = xor32_f(em);
+        const float rest = thr_k + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
+        const float tr = refined_tt(b1, b2, tt, rest, nx2_s, h ? em : eo, r2max);
+        unsure = unsure && !(b1 >= 0.f && b2 - b1 > tr && nx2_s < 1048576.f);
+      }
     } else {
       k1 = r % k;
       b2 = 3e38f;
@@ -1808,6 +1845,7 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.sums_too = a.sums_too;
   l.delta = a.delta;
   l.ablate = a.ablate;
+  l.refine = kmeans_refine_default() ? 1 : 0;
   l.keys = reinterpret_cast<int2*>(a.lean_keys);
   l.centers_all = a.centers_all;
   l.kbase = a.base;

@@ -741,3 +741,33 @@ def test_exact_candidates_equal_mfma_sweep(native, monkeypatch, d, k, sigma):
         assert np.array_equal(a["centers"], b["centers"])
         assert a["last_counts"] == b["last_counts"]
         np.testing.assert_array_equal(a["cost_history"], b["cost_history"])  # (NaN: costless)
+
+
+@pytest.mark.parametrize("d,k,sigma,scale", [(50, 200, 8.0, 1.0), (20, 24, 3.0, 1e-3),
+                                             (40, 96, 12.0, 300.0), (27, 64, 6.0, 1.0)])
+def test_refined_deferral_is_exact(native, monkeypatch, d, k, sigma, scale):
+    """The refined tier-1 deferral test of the image passes (each row's own fp16 rounding residual
+    carried in a pad slot of the operand image, the plane's largest residual; kmeans_frag.h
+    refined_tt) defers fewer rows than the worst-case bound and never changes a label: centers,
+    counts and cost history bitwise those with it off, and the exact-fp32 fit's centers.  Scales
+    1e-3 and 300 move the image scale by powers of two; d = 27 puts the residual's slot right
+    after the last feature."""
+    n = 600_000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0 * scale, sigma * scale, 23)
+    comm = native.LocalComm(True)
+    init = native.kmeans_init(g, comm, t, k, "k-means||", 2, 7)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("OAP_KMEANS_REFINE", mode)
+        out[mode] = native.kmeans_fit(g, comm, t, init, k, 10, -1.0)
+    monkeypatch.delenv("OAP_KMEANS_REFINE")
+    rp = native.kmeans_fit(g, comm, t, init, k, 10, -1.0, precise=True)
+    on, off = out["1"], out["0"]
+    print({key: (on[key], off[key]) for key in ("deferred_rows", "image_passes", "moved_rows")})
+    assert on["image_passes"] > 0
+    assert on["deferred_rows"] < off["deferred_rows"]
+    for r in (off, rp):
+        assert np.array_equal(r["centers"], on["centers"])
+        assert r["last_counts"] == on["last_counts"]
+    np.testing.assert_array_equal(on["cost_history"], off["cost_history"])
