@@ -146,9 +146,9 @@ __device__ inline float plane_resid2(const float* __restrict__ centers, int dp, 
   return 2.f * __builtin_amdgcn_sqrtf(m * 1.0001f) * 1.001f + 1e-30f;
 }
 
-// fp16 upper bound of a row's residual norm from its fp32 sum of squares (<= 129 roundings)
-__device__ inline _Float16 resid_f16_up(float e2) {
-  return static_cast<_Float16>(__builtin_amdgcn_sqrtf(e2 * 1.0001f) * 1.001f + 6e-8f);
+// fp16 upper bound of a residual norm given an fp32 upper bound of it
+__device__ inline _Float16 resid_f16_norm_up(float nrm) {
+  return static_cast<_Float16>(nrm * 1.001f + 6e-8f);
 }
 
 // the refined bound (see above): b1 <= b2 the tier-1 keys' values, tt the worst-case bound, rest

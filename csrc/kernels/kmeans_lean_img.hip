@@ -238,7 +238,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   // its register headroom)
   const float cm_s = ufl(alpha * cmax);
   const float thr_c = ufl(0.0040f * cm_s);
-  const float thr_k = ufl(6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f);
+  // (subnormals: 1.25 d 2^-14 — the image is fp16(alpha x) / 4, rounded twice where subnormal)
+  const float thr_k = ufl(6e-5f * cm_s * cm_s + float(d) * 7.8e-5f + 1e-30f);
   const float mrel = ufl(4e-7f * float(d + 8));
   const float mg_c = ufl(mrel * cm_s * cm_s);
   float r2m = 0.f;

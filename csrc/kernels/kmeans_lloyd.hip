@@ -233,7 +233,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   for (int f = tid; f < DP; f += NT) sc_l[f] = (a.scale && a.sums_too && f < d) ? a.scale[f] : 0.f;
   // image passes: the plane's largest rounding residual for the refined deferral test
   // (kmeans_frag.h refined_tt), per wave
-  const bool refine = use_img && a.refine && d <= DP - kResidSlotOff;
+  // (and the image-writing pass, at its own alpha: its residuals are computed for the image)
+  const bool refine = !XB && a.refine &&
+                      (use_img ? d <= DP - kResidSlotOff : COST && a.img_mode == 1);
   if (refine) {
     const float r2w = plane_resid2(a.centers, DP, k, d, alpha, tid, NT);
     if ((tid & 63) == 0) sc_l[DP + (tid >> 6)] = r2w;
@@ -266,7 +268,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   // out-of-range rows are covered by thr_k / deferred), so only the centers' fp16 rounding
   // enters the cross term: half the f32-row coefficient (2 x 2^-10 instead of 2 x 2 x 2^-10)
   const float thr_c = (XB ? 0.0020f : 0.0040f) * cm_s;
-  const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 6.2e-5f + 1e-30f;
+  // (subnormals: 1.25 d 2^-14 — the image is fp16(alpha x) / 4, rounded twice where subnormal)
+  const float thr_k = 6e-5f * cm_s * cm_s + float(d) * 7.8e-5f + 1e-30f;
   const float mrel = 4e-7f * float(d + 8);                // fp32 evaluation margin (bounds)
   float r2max = 0.f;
   if (refine)
@@ -473,6 +476,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     // MFMA B operand: fp16 of alpha x with the bias slots [16, 16, hi, lo (alpha^2 |x|^2 / 16)]
     f16x8 xh[KS];
     float nx2_s;
+    float e2a = 0.f;  // (image-writing passes: the row's alpha-scale rounding residual^2)
     if constexpr (IMG) {
 #pragma unroll
       for (int s = 0; s < KS; ++s) xh[s] = xi[s];
@@ -522,41 +526,44 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       build_operand(x, alpha, nx2, xh);
       if constexpr (!XB && COST) {  // (full passes compute the cost)
         if (a.img_mode == 1 && pos < npos) {  // write the image (every lane of a real tile)
-          _Float16 nh, nl;
-          split_f16(beta_w * beta_w * nx2 * (1.f / kBiasUnit), nh, nl);
-          // the row's rounding residual |fp16(beta x) - beta x| (exact differences, packed
-          // fp32 squares) into its pad slot DP - 5 for the refined deferral test
-          const bool wres = d <= DP - kResidSlotOff;
+          // The decision operand's rounding residual |fp16(alpha x) - alpha x|^2 (exact
+          // differences, packed fp32 squares; the bias slots of the last k-step excluded) refines
+          // this pass's deferral test and bounds the image's: the image is xh / 4 = fp16(beta x)
+          // exactly wherever beta x is a normal fp16 (elsewhere one more rounding, <= 2^-25 a
+          // feature), its residual norm <= |e_alpha| / 4 + d 2^-25 — into the pad slot DP - 5.
           f32x2 e2v = {0.f, 0.f};
-          _Float16 v2 = {};  // (the last k-step's element 2: the residual's dword partner)
 #pragma unroll
-          for (int s = 0; s < KS; ++s) {  // one k-step at a time (few extra live registers)
-            f16x8 v;
+          for (int s = 0; s < KS; ++s)
 #pragma unroll
             for (int j = 0; j < 8; j += 2) {
-              const f32x2 p = f32x2{x.at(s, j), x.at(s, j + 1)} * beta_w;
-              const f16x2 q = __builtin_convertvector(p, f16x2);
-              if (wres) {
-                const f32x2 e = __builtin_convertvector(q, f32x2) - p;
-                e2v = e * e + e2v;
-              }
-              v[j] = q[0];
-              v[j + 1] = q[1];
+              const f32x2 p = f32x2{x.at(s, j), x.at(s, j + 1)} * alpha;
+              const f32x2 q = (s == KS - 1 && j >= 4)
+                                  ? __builtin_convertvector(__builtin_convertvector(p, f16x2),
+                                                            f32x2)
+                                  : f32x2{static_cast<float>(xh[s][j]),
+                                          static_cast<float>(xh[s][j + 1])};
+              const f32x2 e = q - p;
+              e2v = e * e + e2v;
             }
+          const float e2p = e2v[0] + e2v[1];
+          e2a = e2p + xor32_f(e2p);
+          const bool wres = d <= DP - kResidSlotOff;
+          const _Float16 rs16 = resid_f16_norm_up(
+              0.25f * __builtin_amdgcn_sqrtf(e2a * 1.0001f) * 1.000001f + float(d) * 3e-8f);
+          _Float16 nh, nl;
+          split_f16(beta_w * beta_w * nx2 * (1.f / kBiasUnit), nh, nl);
+          const _Float16 quarter = static_cast<_Float16>(0.25f);
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            f16x8 v = xh[s] * quarter;
             if (s == KS - 1) {
+              v[3] = (h && wres) ? rs16 : v[3];
               v[4] = h ? static_cast<_Float16>(kBiasUnit) : v[4];
               v[5] = h ? static_cast<_Float16>(kBiasUnit) : v[5];
               v[6] = h ? nh : v[6];
               v[7] = h ? nl : v[7];
-              v2 = v[2];
             }
             *img_frag(tile, s) = v;
-          }
-          if (wres) {  // (the slot's dword rewritten: same lane, same address, program order)
-            const float e2 = e2v[0] + e2v[1];
-            const float e2r = e2 + xor32_f(e2);
-            const f16x2 w = {v2, resid_f16_up(e2r)};
-            if (h) reinterpret_cast<f16x2*>(img_frag(tile, KS - 1))[1] = w;
           }
         }
       }
@@ -713,11 +720,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
       unsure = valid && (!(b2 - b1 > tt) || !(nx2_s < 1048576.f));
       // image passes: the refined test on the row's own residual (kmeans_frag.h refined_tt;
       // wave-uniform: the residual's exchange needs both halves)
-      if (IMG && refine && __ballot(unsure) != 0ull) {
-        const float em = static_cast<float>(xh[KS - 1][3]);
-        const float eo = xor32_f(em);
+      if ((IMG || (COST && !XB)) && refine && __ballot(unsure) != 0ull) {
+        float exn;
+        if constexpr (IMG) {
+          const float em = static_cast<float>(xh[KS - 1][3]);
+          const float eo = xor32_f(em);
+          exn = h ? em : eo;
+        } else {
+          exn = __builtin_amdgcn_sqrtf(e2a * 1.0001f) * 1.001f + 1e-30f;
+        }
         const float rest = thr_k + 5e-5f * nx2_s + 2.5e-4f * fabsf(b2);
-        const float tr = refined_tt(b1, b2, tt, rest, nx2_s, h ? em : eo, r2max);
+        const float tr = refined_tt(b1, b2, tt, rest, nx2_s, exn, r2max);
         unsure = unsure && !(b1 >= 0.f && b2 - b1 > tr && nx2_s < 1048576.f);
       }
     } else {
