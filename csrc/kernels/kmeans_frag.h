@@ -134,6 +134,7 @@ __device__ inline float plane_resid2(const float* __restrict__ centers, int dp, 
   float m = 0.f;
   for (int c = tid; c < k; c += nt) {
     float e2 = 0.f;
+#pragma unroll 8
     for (int f = 0; f < d; ++f) {
       const float p = -2.f * alpha * centers[size_t(c) * dp + f];
       const float e = static_cast<float>(static_cast<_Float16>(p)) - p;

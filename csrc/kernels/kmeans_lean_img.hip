@@ -170,14 +170,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const float a2 = alpha * alpha;
   const float inv_a2 = ufl(1.f / a2);  // (a power of two)
   // ---- the plane c' = [-2 alpha c, 0 .., hi, lo (alpha^2 |c|^2 / 16), 16, 16] (kmeans_lloyd.hip)
+  // (unconditional loads, unrolled: a thread's loads in flight together — centers are kpad x DP
+  // and cnorm kpad, every slot addressable)
+#pragma unroll 4
   for (int idx = tid; idx < kpad * DP; idx += NT) {
     const int c = idx / DP, f = idx - c * DP;
+    const float cv = a.centers[idx], cnv = a.cnorm[c];
     _Float16 v;
     if (f < d) {
-      v = static_cast<_Float16>(-2.f * alpha * a.centers[idx]);
+      v = static_cast<_Float16>(-2.f * alpha * cv);
     } else if (f == DP - 4 || f == DP - 3) {
       _Float16 hi, lo;
-      split_h((c < k) ? a2 * a.cnorm[c] * (1.f / kBias) : 60000.f, hi, lo);
+      split_h((c < k) ? a2 * cnv * (1.f / kBias) : 60000.f, hi, lo);
       v = (f == DP - 4) ? hi : lo;
     } else {
       v = static_cast<_Float16>(f >= DP - 2 ? kBias : 0.f);

@@ -215,15 +215,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   // by the choice of KS), i.e. in the h = 1 lanes' j = 4..7 of the last k-step for every d: the
   // per-tile operand build then patches two fixed dwords instead of testing every slot against
   // a lane-dependent position (24 hoisted lane masks -> SGPR spills -> v_readlane per use)
+  // (unconditional loads, unrolled: a thread's loads in flight together)
+#pragma unroll 4
   for (int idx = tid; idx < kpad * DP; idx += NT) {
     const int c = idx / DP, f = idx - c * DP;
+    const float cv = a.centers[idx], cnv = a.cnorm[c];
     _Float16 v;
     if (f < d) {
-      v = static_cast<_Float16>(-2.f * alpha * a.centers[idx]);
+      v = static_cast<_Float16>(-2.f * alpha * cv);
     } else if (f == DP - 4 || f == DP - 3) {
       _Float16 hi, lo;
       // padded centers: the largest finite bias (their distance never wins)
-      split_f16((c < k) ? a2 * a.cnorm[c] * (1.f / kBiasUnit) : 60000.f, hi, lo);
+      split_f16((c < k) ? a2 * cnv * (1.f / kBiasUnit) : 60000.f, hi, lo);
       v = (f == DP - 4) ? hi : lo;
     } else {
       v = static_cast<_Float16>(f >= DP - 2 ? kBiasUnit : 0.f);
@@ -1052,10 +1055,12 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   constexpr int NT = EW * 64;
+  // (the sub-segment counts loaded in parallel, then summed in LDS: one load latency, not 16)
+  if (tid < a.row_subs) pref[tid + 1] = a.row_count[blockIdx.x * kDeferSubs + tid];
+  __syncthreads();
   if (tid == 0) {
     pref[0] = 0u;
-    for (int w = 0; w < a.row_subs; ++w)
-      pref[w + 1] = pref[w] + a.row_count[blockIdx.x * kDeferSubs + w];
+    for (int w = 0; w < a.row_subs; ++w) pref[w + 1] += pref[w];
   }
   __syncthreads();
   const unsigned total = pref[a.row_subs];
@@ -1063,6 +1068,7 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
     if (tid == 0 && a.cost_slab) a.cost_slab[blockIdx.x] = 0.0;
     return;
   }
+#pragma unroll 8
   for (int i = tid; i < kpad * DP; i += NT) {
     const int c = i / DP, f = i - c * DP;
     ct[c * CS + f] = a.centers[i];
@@ -1330,10 +1336,12 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   int* cl = reinterpret_cast<int*>(smem + L.cl) + wave * 64 * kCandList + lane;  // [slot * 64]
+  // (the sub-segment counts loaded in parallel, then summed in LDS: one load latency, not 16)
+  if (tid < a.row_subs) pref[tid + 1] = a.row_count[blockIdx.x * kDeferSubs + tid];
+  __syncthreads();
   if (tid == 0) {
     pref[0] = 0u;
-    for (int w = 0; w < a.row_subs; ++w)
-      pref[w + 1] = pref[w] + a.row_count[blockIdx.x * kDeferSubs + w];
+    for (int w = 0; w < a.row_subs; ++w) pref[w + 1] += pref[w];
   }
   __syncthreads();
   const unsigned total = pref[a.row_subs];
@@ -1347,14 +1355,17 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
   const float inv_a2 = 1.f / a2;  // (a power of two)
   // the tier-1 plane exactly as the lean first pass stages it (c' = [-2 alpha c, .., hi, lo
   // (alpha^2 |c|^2 / 16), 16, 16])
+  // (unconditional loads, unrolled: a thread's loads in flight together)
+#pragma unroll 4
   for (int idx = tid; idx < kpad * DP; idx += NT) {
     const int c = idx / DP, f = idx - c * DP;
+    const float cv = a.centers[idx], cnv = a.cnorm[c];
     _Float16 v;
     if (f < d) {
-      v = static_cast<_Float16>(-2.f * alpha * a.centers[idx]);
+      v = static_cast<_Float16>(-2.f * alpha * cv);
     } else if (f == DP - 4 || f == DP - 3) {
       _Float16 hi, lo;
-      split_f16((c < k) ? a2 * a.cnorm[c] * (1.f / kBiasUnit) : 60000.f, hi, lo);
+      split_f16((c < k) ? a2 * cnv * (1.f / kBiasUnit) : 60000.f, hi, lo);
       v = (f == DP - 4) ? hi : lo;
     } else {
       v = static_cast<_Float16>(f >= DP - 2 ? kBiasUnit : 0.f);
