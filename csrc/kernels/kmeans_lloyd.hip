@@ -1277,7 +1277,7 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
 // for the Hamerly lower bound is min(the exact second among the candidates, best + tt / alpha^2),
 // a valid lower bound for every center left out.  Accumulation, labels, bounds, cost: as
 // oap_kmeans_exact_rows.
-constexpr int kCandWaves = 8;   // 2 per SIMD: the row in registers twice (own + other half)
+constexpr int kCandWaves = 12;  // 3 per SIMD: latency-bound rows (the row in registers twice)
 constexpr int kCandList = 8;    // per-lane candidate slots (LDS); more -> the lane takes all
 
 struct CandSmem {
