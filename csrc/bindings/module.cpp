@@ -546,7 +546,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("k") = 2, py::arg("max_iter") = 20, py::arg("tol") = 1e-4,
       py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1,
       py::arg("precise") = false, py::arg("prune") = true, py::arg("delta") = true,
-      py::arg("phase_events") = true);
+      py::arg("phase_events") = false);
   m.def(
       "kmeans_fit_streamed",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,

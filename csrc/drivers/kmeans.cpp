@@ -316,6 +316,8 @@ struct AssignReq {
   double* sq_slab = nullptr;
   unsigned* bound_flag = nullptr;
   float bound_inf = 0.f;
+  // batched fits with a tolerance: the kernels stand down once the fit converged
+  const int* halt = nullptr;
 };
 
 // The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
@@ -431,6 +433,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
             "kmeans pruning needs the fast path (d <= 128) and persistent labels");
   a.xnorm = req.xnorm;
   a.ablate = req.ablate;
+  a.halt = req.halt;
   const int kmax = kern::kmeans_lds_kmax(x.cols, req.precise);
   if (x.rows > 0 && lean_applies(x, g.k, g.kpad, req)) {
     // ---- lean tier-1 pass, then the general kernel re-decides the deferred rows exactly
@@ -1530,18 +1533,20 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // Provisional fixed-point bounds (fit_bounds): the lean single-launch fit's first full pass
   // checks every row against them (and sums |x|^2 for the final cost), so no pass over the rows
   // runs before the first iteration.  Decided from the shape and parameters (rank-uniform).
+  // (a feature that is 0 in every initial center has bound 0, which every row would fail: the
+  // check could only flag and restart, so such a fit takes the column maxima up front — the
+  // rule fit_bounds evaluates then is the same on every engine)
   const char* am_env = std::getenv("OAP_KMEANS_ABSMAX_PASS");
-  const bool provisional = !p.absmax_pass && !(am_env && *am_env == '1') && delta_all &&
-                           provisional_allowed(x.global_rows, d) &&
-                           x.dtype == DType::F32 && lean_applies(x, k, g.kpad, req);
   double cb_min = std::numeric_limits<double>::infinity();
   for (int f = 0; f < d; ++f) cb_min = std::min(cb_min, cbound[f]);
-  Buffer bflag_b, bflag_h, sq_slab_b;
+  const bool provisional = !p.absmax_pass && !(am_env && *am_env == '1') && delta_all &&
+                           provisional_allowed(x.global_rows, d) && cb_min > 0.0 &&
+                           x.dtype == DType::F32 && lean_applies(x, k, g.kpad, req);
+  Buffer bflag_b, sq_slab_b;
   if (provisional) {
     fp = fixed_point_scales(cbound, x.global_rows, max_local);
     res.scale_source = "centers";
     bflag_b = ctx.alloc(2 * sizeof(unsigned));  // [flag, largest fp32 |x|^2 (bits)]
-    bflag_h = ctx.alloc_pinned(2 * sizeof(unsigned));
     ctx.memset(bflag_b.data(), 0, 2 * sizeof(unsigned), s);
   } else {
     bounds_from_absmax();
@@ -1703,9 +1708,19 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   bool delta_on = true;
   bool probing = false;  // delta_on was set by a probe: scan one iteration, then decide
   int delta_probe = 0;
-  const int probe_gap0 = p.tol < 0 ? 1 : 4;  // (batches of kBatch iterations vs single ones)
+  // With a tolerance (tol >= 0) the fit batches too where every kernel of an iteration can stand
+  // down on the device: the finalize of a converged iteration sets `halt`, and the lean / image /
+  // exact / scan kernels, the finalize and the guarded copies of the iterations enqueued behind
+  // it return at once — so the host reads the flags once per batch, not once per iteration.
+  // That needs the delta form of the lean path: the local statistics persist and reach the
+  // global ones by an out-of-place reduction (or a copy before an in-place one), so an iteration
+  // that does nothing leaves every result as the converged one left it.  (A host communicator
+  // still syncs inside each allreduce; batching saves it the per-iteration flag read-backs and
+  // scalar collectives.)  Rank-uniform: delta_all and req.fast1 (decided from allreduced values)
+  // are the same on every rank.
+  const bool tol_batch_ok = p.tol >= 0 && delta_all;
+  const int probe_gap0 = p.tol < 0 || tol_batch_ok ? 1 : 4;  // (batches vs single iterations)
   int probe_gap = probe_gap0;
-  u64 pruned_seen = 0;
 
   kern::KMeansFinalizeArgs fa;
   // a single-rank delta fit finalizes straight from its local statistics (no copy into the
@@ -1735,7 +1750,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // iteration on a 12.5M-row shard
   const bool pev = p.phase_events;
 
-  u64 tier2_seen = 0;
   RcclComm* rccl = dynamic_cast<RcclComm*>(&comm);
   const int64_t flops_per_iter = 2 * int64_t(x.rows) * k * d;
   // With a tolerance the host must see each iteration's convergence flag before deciding to
@@ -1746,25 +1760,40 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // (32: a 20-iteration fit has 2 batch boundaries — each a host round trip, ~130 us with its
   // read-backs; flags_d slots)
   constexpr int kBatch = 32;
-  const int B = p.tol < 0 ? kBatch : 1;
+  auto batch_size = [&]() { return p.tol < 0 || (tol_batch_ok && req.fast1) ? kBatch : 1; };
+  Buffer halt_b;
+  if (tol_batch_ok) {
+    halt_b = ctx.alloc(sizeof(int) * 4);
+    ctx.memset(halt_b.data(), 0, sizeof(int) * 4, s);
+  }
+  // the batch's adaptive controls (kern::kmeans_ctl), Max-allreduced with its last iteration
+  Buffer ctl_b = ctx.alloc(sizeof(double) * 8);
+  Buffer ctl_snap = ctx.alloc(sizeof(u64) * 4);
+  Buffer ctl_h = ctx.alloc_pinned(sizeof(double) * 8);
+  ctx.memset(ctl_snap.data(), 0, sizeof(u64) * 4, s);
   struct IterEvents {
     Event e0, e1, e2, e3;
   };
-  std::vector<IterEvents> ev(B);
-  Buffer flags_hb = ctx.alloc_pinned(sizeof(kern::KMeansFlags) * B);
+  std::vector<IterEvents> ev(kBatch);
+  Buffer flags_hb = ctx.alloc_pinned(sizeof(kern::KMeansFlags) * kBatch);
   auto* flh = flags_hb.as<kern::KMeansFlags>();
   bool stop = false;
   bool restart = false;  // the provisional fixed-point bounds failed (see prov_pending)
   int scan_iters = 0;  // scan passes in the current batch
-  std::vector<char> it_scanned(B, 0), it_costless(B, 0);
+  std::vector<char> it_scanned(kBatch, 0), it_costless(kBatch, 0);
   bool last_costless = false;  // the last iteration computed no cost (rank-uniform)
   hm.mark("buffers");
   for (int it0 = 0, nb_it = 0; it0 < p.max_iter && !stop; it0 += nb_it) {
     // the first batch is short so the adaptive choices (tier, scan) are made early
     // (with the scan on, the first batch ends after the first delta iteration: its moved-row
     // share gates the first scan probe)
-    nb_it = std::min(it0 == 0 && B > 3 ? (scan_all ? 2 : 3) : B, p.max_iter - it0);
+    const int Bn = batch_size();
+    nb_it = std::min(it0 == 0 && Bn > 3 ? (scan_all ? 2 : 3) : Bn, p.max_iter - it0);
     scan_iters = 0;
+    // (the halt word applies to batches of more than one iteration with a tolerance)
+    int* const halt = tol_batch_ok && Bn > 1 ? halt_b.as<int>() : nullptr;
+    req.halt = halt;
+    fa.halt = halt;
     for (int b = 0; b < nb_it; ++b) {
       const int it = it0 + b;
       maybe_inject_fault(comm.rank(), "kmeans_iter", it);
@@ -1827,7 +1856,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         OAP_CHECK(xnorm_ready, "kmeans scan before any full pass");
         kern::kmeans_lean_scan(x.rows, k, d, lgrid, req.bounds, req.labels, xnorm_full,
                                req.drift, req.drift_max, g.cstat.as<float>(),
-                               dlist_b.as<int32_t>(), dcount, req.pruned_tiles, s);
+                               dlist_b.as<int32_t>(), dcount, req.pruned_tiles, s, halt);
         req.tile_list = dlist_b.as<int32_t>();
         req.tile_count = dcount;
       } else if (!chunked) {
@@ -1852,7 +1881,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         kern::kmeans_lean_scan_rows(x.rows, k, d, lgrid, bounds_full, req.labels, xnorm_full,
                                     drift_b.as<float>(), drift_b.as<float>() + k,
                                     g.cstat.as<float>(), rlist_b.as<int32_t>(), rcount,
-                                    rpruned_b.as<u64>(), s);
+                                    rpruned_b.as<u64>(), s, halt);
         req.img_rows = rlist_b.as<int32_t>();
         req.img_row_count = rcount;
       }
@@ -1905,16 +1934,38 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           OAP_HIP_CHECK(hipMemcpyAsync(stats.data(), loc_b.data(), sizeof(u64) * (kd + k),
                                        hipMemcpyDeviceToDevice, s));
         // the centers this iteration assigned against, for the final exact-cost pass — only
-        // when it may follow this iteration (a convergence test, or the last iteration)
-        if (p.tol >= 0 || it == p.max_iter - 1)
-          OAP_HIP_CHECK(hipMemcpyAsync(cbak_b.data(), g.c32.data(),
-                                       sizeof(float) * size_t(g.kpad) * g.dp,
-                                       hipMemcpyDeviceToDevice, s));
+        // when it may follow this iteration (a convergence test, or the last iteration); in a
+        // batch behind a converged iteration it must keep that iteration's centers
+        if (p.tol >= 0 || it == p.max_iter - 1) {
+          if (halt)
+            kern::copy_guarded(cbak_b.data(), g.c32.data(), sizeof(float) * size_t(g.kpad) * g.dp,
+                               halt, s);
+          else
+            OAP_HIP_CHECK(hipMemcpyAsync(cbak_b.data(), g.c32.data(),
+                                         sizeof(float) * size_t(g.kpad) * g.dp,
+                                         hipMemcpyDeviceToDevice, s));
+        }
       }
       // (otherwise cost_d holds the zero the last finalize left: a costless iteration's cost
       // is not reported)
       if (nb > 0) kern::sum_f64(slab.as<double>(), nb, cost_d.as<double>(), s);
       if (pev) ev[b].e1.record(s);
+      // the batch's adaptive controls, from the device counters, ride its last allreduce
+      const bool ctl_it = b == nb_it - 1;
+      if (ctl_it) {
+        kern::KMeansCtlArgs ca;
+        ca.refine = refine_d.as<u64>();
+        ca.ldstat = ldstat_b.data() ? ldstat_b.as<u64>() : nullptr;
+        ca.pruned = scan ? pruned_d.as<u64>() : nullptr;
+        ca.bound_flag = prov_pending ? bflag_b.as<unsigned>() : nullptr;
+        ca.snap = ctl_snap.as<u64>();
+        ca.out = ctl_b.as<double>();
+        ca.rows = x.rows;
+        ca.nb_it = nb_it;
+        ca.scan_iters = scan_iters;
+        ca.scan_local = scan ? 1 : 0;
+        kern::kmeans_ctl(ca, s);
+      }
       if (!comm.trivial()) {
         if (comm.on_device()) {
           if (rccl) rccl->group_start();
@@ -1924,10 +1975,12 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
           else
             comm.allreduce(stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
           comm.allreduce(cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+          if (ctl_it) comm.allreduce(ctl_b.data(), 5, DType::F64, ReduceOp::Max, s);
           if (rccl) rccl->group_end();
         } else {
           comm_allreduce(ctx, comm, stats.data(), kd + k, DType::I64, ReduceOp::Sum, s);
           comm_allreduce(ctx, comm, cost_d.data(), 1, DType::F64, ReduceOp::Sum, s);
+          if (ctl_it) comm_allreduce(ctx, comm, ctl_b.data(), 5, DType::F64, ReduceOp::Max, s);
         }
       }
       if (pev) ev[b].e2.record(s);
@@ -1942,15 +1995,11 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         hipMemcpyAsync(counts_h.data(), fin_counts, sizeof(u64) * k, hipMemcpyDeviceToHost, s));
     OAP_HIP_CHECK(hipMemcpyAsync(refine_h.data(), refine_d.data(), 2 * sizeof(u64),
                                  hipMemcpyDeviceToHost, s));
+    OAP_HIP_CHECK(
+        hipMemcpyAsync(ctl_h.data(), ctl_b.data(), 5 * sizeof(double), hipMemcpyDeviceToHost, s));
+    const double* ctl = ctl_h.as<double>();
     if (ldstat_b.data())
       OAP_HIP_CHECK(hipMemcpyAsync(ldstat_h.data(), ldstat_b.data(), 5 * sizeof(u64),
-                                   hipMemcpyDeviceToHost, s));
-    u64 pruned_now = 0;
-    if (scan)
-      OAP_HIP_CHECK(hipMemcpyAsync(&pruned_now, pruned_d.data(), sizeof(u64),
-                                   hipMemcpyDeviceToHost, s));
-    if (prov_pending)
-      OAP_HIP_CHECK(hipMemcpyAsync(bflag_h.data(), bflag_b.data(), 2 * sizeof(unsigned),
                                    hipMemcpyDeviceToHost, s));
     comm.wait(s);
     if (prov_pending) {
@@ -1958,15 +2007,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // row costs one column-maxima pass, which evaluates the rule exactly — the bounds either
       // hold (continue) or the fit restarts from its initial centers with the column maxima
       prov_pending = false;
-      double fl = double(bflag_h.as<unsigned>()[0]);
-      float nmax = 0.f;
-      std::memcpy(&nmax, bflag_h.as<unsigned>() + 1, sizeof(float));
-      // every row's norm on every rank: the largest fp32 |x|^2 (relative error <= (d + 1) 2^-24)
-      double ncap = std::sqrt(double(nmax) * (1.0 + 1e-5));
-      if (!comm.trivial()) {
-        fl = comm_allreduce_scalar(ctx, comm, fl, ReduceOp::Max);
-        ncap = comm_allreduce_scalar(ctx, comm, ncap, ReduceOp::Max);
-      }
+      // (allreduced with the batch: the flag, and every row's norm on every rank — the largest
+      // fp32 |x|^2, relative error <= (d + 1) 2^-24, kern::kmeans_ctl)
+      const double fl = ctl[3];
+      const double ncap = ctl[4];
       if (std::isfinite(ncap)) row_norm_cap = std::min(row_norm_cap, ncap);
       if (fl > 0.0) {
         absmax = global_column_absmax(ctx, comm, x);
@@ -2015,8 +2059,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       res.cost_history.push_back(c_it);
       res.shift_history.push_back(std::sqrt(std::max(fl.max_shift2, 0.0)));
       res.num_iter = it + 1;
-      if (fl.converged && p.tol >= 0) {  // (B == 1 here: nothing was enqueued past it)
+      if (fl.converged && p.tol >= 0) {
+        // (iterations enqueued past it in the batch stood down on the device: halt)
         res.converged = true;
+        last_costless = it_costless[b];
         stop = true;
         break;
       }
@@ -2025,13 +2071,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // adaptive tier (rank-uniform: the largest local share decides): tier-1 first pays off
       // only while the re-decisions it leaves stay rare — tier-3 tile re-runs (general kernel)
       // or deferred rows (lean kernel)
-      const u64 t2 = refine_h.as<u64>()[1];
-      const double tiles = double((x.rows + 31) / 32) * nb_it;
-      double share = tiles > 0 ? double(t2 - tier2_seen) / (0.02 * tiles) : 0.0;
-      if (ldstat_b.data() && x.rows > 0)
-        share = std::max(share, double(ldstat_h.as<u64>()[0] - deferred_seen) /
-                                    (0.25 * double(x.rows) * nb_it));
-      tier2_seen = t2;
+      // (the batch's largest local share over the ranks, kern::kmeans_ctl)
+      const double share = ctl[0];
       if (ldstat_b.data() && Logger::instance().level() <= LogLevel::Info) {
         Logger::instance().log(
             LogLevel::Info, "kmeans/batch_rows",
@@ -2043,7 +2084,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         deferred_seen = ldstat_h.as<u64>()[0];
         moved_seen = ldstat_h.as<u64>()[1];
       }
-      if (!comm.trivial()) share = comm_allreduce_scalar(ctx, comm, share, ReduceOp::Max);
       if (share > 1.0) {
         req.fast1 = false;
         Logger::instance().log(LogLevel::Info, "kmeans/tier1_off",
@@ -2053,14 +2093,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     if (scan_all && !stop) {  // adaptive scan (decided per batch from its pruned share);
       // rank-uniform: ranks see the same drift but their own rows, so the smallest local share
       // decides (a rank without rows reports 1)
-      double frac = 0.0;
-      if (scan_iters > 0) {
-        frac = scan ? double(pruned_now - pruned_seen) /
-                          (double((x.rows + 31) / 32) * scan_iters + 1e-9)
-                    : 1.0;
-        frac = comm_allreduce_scalar(ctx, comm, frac, ReduceOp::Min);
-      }
-      pruned_seen = pruned_now;
+      // (the smallest local pruned share over the ranks, kern::kmeans_ctl)
+      const double frac = scan_iters > 0 ? -ctl[1] : 0.0;
       // (one scan right after a large move says little: turn off on two, or on a hopeless one)
       const bool was_probe = probing;
       probing = false;
@@ -2069,9 +2103,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // first scan would prune almost nothing (overlapping clusters) and costs a bound write,
       // a scan and a listed pass: back off as after a hopeless probe
       if (it0 == 0 && scan_iters == 0 && delta_on && nb_it >= 2) {  // (rank-uniform)
-        double mv = ldstat_b.data() && x.rows > 0
-                        ? double(ldstat_h.as<u64>()[1]) / double(x.rows) : 0.0;
-        if (!comm.trivial()) mv = comm_allreduce_scalar(ctx, comm, mv, ReduceOp::Max);
+        const double mv = ctl[2];  // (the largest moved share over the ranks)
         if (mv > 0.03) {
           delta_on = false;
           delta_probe = 0;
@@ -2089,7 +2121,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
         probe_gap = probe_gap0;
       } else if (!delta_on && ++delta_probe >= probe_gap) {
         delta_on = true;  // probe: the centers may have settled
-        probing = B > 1;
+        probing = batch_size() > 1;
       }
     }
   }

@@ -41,7 +41,8 @@ struct KMeansParams {
   bool delta = true;
   // per-iteration phase events (kmeans/assign_kernel and kmeans/allreduce metrics); off: one
   // event pair per batch of iterations (kmeans/iteration only), no event gaps between phases
-  bool phase_events = true;
+  // (each record is a ~10 us gap in the stream, so the default is off)
+  bool phase_events = false;
   // internal: the fixed-point bounds come from a column-maxima pass up front (set on the
   // restart after a failed provisional check, see kmeans.cpp fit_bounds)
   bool absmax_pass = false;

@@ -175,6 +175,9 @@ struct KMeansAssignArgs {
   double* sq_slab = nullptr;
   unsigned* bound_flag = nullptr;
   float bound_inf = 0.f;
+  // Batched fits with a tolerance: a device word the finalize sets once the fit has converged;
+  // the lean / image / exact / scan kernels of later iterations in the batch return at once.
+  const int* halt = nullptr;
 };
 // Lean tier-1 Lloyd kernel (kmeans_lloyd.hip): applicable when the centroid hi plane + the
 // fixed-point accumulator fit LDS and d + 4 bias features fit the padded width.
@@ -211,7 +214,8 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
 void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
                            const int32_t* labels, const float* xnorm, const float* drift,
                            const float* drift_max, const float* cstat, int32_t* row_list,
-                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s);
+                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s,
+                           const int* halt = nullptr);
 // Largest centroid chunks (multiples of 32) of the chunked lean pass at dimension d: the lean
 // kernel's fp16 plane and the exact kernel's fp32 centers (0: d not supported).
 int kmeans_lloyd_chunk_kmax(int d);
@@ -232,7 +236,8 @@ int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid);
 void kmeans_lean_scan(int64_t n, int k, int d, int lean_grid, float* bounds,
                       const int32_t* labels, const float* xnorm, const float* drift,
                       const float* drift_max, const float* cstat, int32_t* tile_list,
-                      unsigned* tile_count, unsigned long long* pruned, hipStream_t s);
+                      unsigned* tile_count, unsigned long long* pruned, hipStream_t s,
+                      const int* halt = nullptr);
 
 // Delta-mode pruning scan (single launch): per 32-row tile, tests every row's bounds (labels,
 // xnorm, the centers' drift) exactly as the assign kernel's own pruning test does.  Tiles that
@@ -310,7 +315,32 @@ struct KMeansFinalizeArgs {
   unsigned* done = nullptr;
   // optional: zeroed once its value is in the flags (the next iteration's cost accumulator)
   double* cost_reset = nullptr;
+  // optional (batched fits, tol >= 0): the finalize returns at once when *halt is set and sets it
+  // when this iteration converged, so the iterations enqueued behind it change nothing
+  int* halt = nullptr;
 };
+// dst = src (bytes, a multiple of 4) unless *halt is set (halt may be null).
+void copy_guarded(void* dst, const void* src, size_t bytes, const int* halt, hipStream_t s);
+// The adaptive controls of a K-Means batch (kmeans_fit), on the device so that they ride the
+// batch's last grouped allreduce (Max over ranks) instead of scalar host round trips:
+// out[0] = the share of re-decisions (tier-3 tile re-runs of the general kernel / deferred rows
+// of the lean kernel) over the batch against their budgets, out[1] = -(pruned tile share of the
+// batch's scan passes), out[2] = moved rows / rows, out[3] = the provisional bound flag, out[4] =
+// sqrt of the largest fp32 |x|^2 (rounded up).  snap[3] holds the counters at the batch start
+// (updated here).  Null counters count as 0.
+struct KMeansCtlArgs {
+  const unsigned long long* refine = nullptr;   // [1] = tier-3 tile re-runs
+  const unsigned long long* ldstat = nullptr;   // [0] deferred rows, [1] moved rows
+  const unsigned long long* pruned = nullptr;   // tiles pruned by the tile scan
+  const unsigned* bound_flag = nullptr;         // [flag, largest |x|^2 bits]
+  unsigned long long* snap = nullptr;           // [3] in/out
+  double* out = nullptr;                        // [5]
+  int64_t rows = 0;
+  int nb_it = 1;
+  int scan_iters = 0;
+  int scan_local = 0;  // this rank runs the tile scan (else its pruned share counts as 1)
+};
+void kmeans_ctl(const KMeansCtlArgs& a, hipStream_t s);
 struct KMeansFlags {
   int converged;
   int nonempty;

@@ -525,6 +525,7 @@ __global__ __launch_bounds__(kBinThreads) void oap_kmeans_bin_scatter_e(const in
 }
 
 __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a) {
+  if (a.halt && *a.halt) return;
   __shared__ int s_conv, s_nonempty;
   __shared__ double s_shift[4];
   __shared__ float s_norm[4], s_drift[4];
@@ -595,6 +596,7 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize(KMeansFinalizeArgs a)
     if (a.cost_reset) a.cost_reset[0] = 0.0;
     if (a.cstat) a.cstat[0] = nm * 1.0000001f;
     if (a.drift) a.drift[a.k] = dm;
+    if (a.halt && s_conv && a.tol >= 0.0) a.halt[0] = 1;
   }
 }
 
@@ -649,6 +651,7 @@ __device__ void finalize_flags_block(const KMeansFinalizeArgs& a) {
     fl->max_shift2 = mx;
     if (a.cost_reset) a.cost_reset[0] = 0.0;
     if (a.cstat) a.cstat[0] = nm * 1.0000001f;
+    if (a.halt && s_conv && a.tol >= 0.0) a.halt[0] = 1;
   }
 }
 
@@ -657,6 +660,7 @@ __device__ void finalize_flags_block(const KMeansFinalizeArgs& a) {
 // oap_kmeans_finalize_flags).  The fp64 sums keep the single-block kernel's sequential feature
 // order (lane 0), so results are bitwise unchanged.
 __global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinalizeArgs a) {
+  if (a.halt && *a.halt) return;  // (every block: the done counter stays untouched)
   __shared__ double s_df[4][256];
   __shared__ float s_dv[4][256], s_v[4][256];
   __shared__ bool s_last;
@@ -718,7 +722,50 @@ __global__ __launch_bounds__(256) void oap_kmeans_finalize_clusters(KMeansFinali
 }
 
 __global__ __launch_bounds__(256) void oap_kmeans_finalize_flags(KMeansFinalizeArgs a) {
+  if (a.halt && *a.halt) return;
   finalize_flags_block(a);
+}
+
+__global__ __launch_bounds__(256) void oap_copy_guarded(uint4* __restrict__ dst,
+                                                        const uint4* __restrict__ src, int64_t n16,
+                                                        unsigned* __restrict__ dst4,
+                                                        const unsigned* __restrict__ src4, int n4,
+                                                        const int* __restrict__ halt) {
+  if (halt && *halt) return;
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n16) dst[i] = src[i];
+  if (blockIdx.x == 0 && threadIdx.x < n4) dst4[threadIdx.x] = src4[threadIdx.x];
+}
+
+// (one thread: a handful of counters per batch)
+__global__ void oap_kmeans_ctl(KMeansCtlArgs a) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t2 = a.refine ? a.refine[1] : 0ull;
+  const unsigned long long df = a.ldstat ? a.ldstat[0] : 0ull;
+  const unsigned long long mv = a.ldstat ? a.ldstat[1] : 0ull;
+  const unsigned long long pr = a.pruned ? a.pruned[0] : 0ull;
+  const double tiles = double((a.rows + 31) / 32);
+  double share = 0.0, frac = 1.0, mvf = 0.0;
+  if (a.rows > 0) {
+    share = double(t2 - a.snap[0]) / (0.02 * tiles * a.nb_it);
+    if (a.ldstat) share = fmax(share, double(df - a.snap[1]) / (0.25 * double(a.rows) * a.nb_it));
+    if (a.scan_iters > 0 && a.scan_local)
+      frac = double(pr - a.snap[2]) / (tiles * a.scan_iters + 1e-9);
+    mvf = double(mv) / double(a.rows);
+  }
+  a.snap[0] = t2;
+  a.snap[1] = df;
+  a.snap[2] = pr;
+  a.out[0] = share;
+  a.out[1] = -frac;
+  a.out[2] = mvf;
+  double fl = 0.0, ncap = 0.0;
+  if (a.bound_flag) {
+    fl = double(a.bound_flag[0]);
+    ncap = sqrt(double(__uint_as_float(a.bound_flag[1])) * (1.0 + 1e-5));
+  }
+  a.out[3] = fl;
+  a.out[4] = ncap;
 }
 
 __global__ void oap_kmeans_prepare_centers(const double* c64, int k, int d, int dp, float* c32,
@@ -1129,6 +1176,28 @@ void kmeans_finalize(const KMeansFinalizeArgs& a, hipStream_t s) {
   } else {
     hipLaunchKernelGGL(oap_kmeans_finalize, dim3(1), dim3(256), 0, s, a);
   }
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void copy_guarded(void* dst, const void* src, size_t bytes, const int* halt, hipStream_t s) {
+  OAP_CHECK(bytes % 4 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(src) % 16 == 0,
+            "copy_guarded: 16-byte aligned buffers of whole dwords");
+  if (bytes == 0) return;
+  const int64_t n16 = int64_t(bytes / 16);
+  const int n4 = int((bytes % 16) / 4);
+  const int grid = int(n16 > 0 ? (n16 + 255) / 256 : 1);
+  hipLaunchKernelGGL(oap_copy_guarded, dim3(grid), dim3(256), 0, s, static_cast<uint4*>(dst),
+                     static_cast<const uint4*>(src), n16,
+                     reinterpret_cast<unsigned*>(static_cast<char*>(dst) + n16 * 16),
+                     reinterpret_cast<const unsigned*>(static_cast<const char*>(src) + n16 * 16),
+                     n4, halt);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+void kmeans_ctl(const KMeansCtlArgs& a, hipStream_t s) {
+  OAP_CHECK(a.snap && a.out && a.nb_it >= 1, "kmeans_ctl: bad arguments");
+  hipLaunchKernelGGL(oap_kmeans_ctl, dim3(1), dim3(64), 0, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 

@@ -80,6 +80,7 @@ struct ImgArgs {
   int movers;  // row-scan passes: the mover stage (RM 3)
   int refine;  // the refined deferral test (kmeans_frag.h refined_tt; OAP_KMEANS_REFINE=0: off)
   int32_t* mlist;  // RM 3: per-wave lists of the rows the mover stage left, [grid][seg_cap]
+  const int* halt;  // batched fits: set once the fit converged (the pass then does nothing)
 };
 
 struct ImgSmem {
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   constexpr bool NO_LOAD = (CFG & 32) != 0, NO_ACC = (CFG & 64) != 0, NO_ST = (CFG & 128) != 0;
   constexpr int DP = 16 * KS, NT = WAVES * 64, RS = DP + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.halt && *a.halt) return;
   const float cmax = a.cstat[0];
   const float alpha = a.img_beta[0];
   if (!(alpha * cmax <= 512.f)) return;  // (kmeans_lloyd img_mode 3 takes this pass)
@@ -979,7 +981,9 @@ __global__ __launch_bounds__(kScanRowThreads) void oap_kmeans_lean_scan_rows(
     const int32_t* __restrict__ labels, const float* __restrict__ xnorm,
     const float* __restrict__ drift, const float* __restrict__ drift_max,
     const float* __restrict__ cstat, int32_t* __restrict__ row_list,
-    unsigned* __restrict__ row_count, unsigned long long* __restrict__ pruned) {
+    unsigned* __restrict__ row_count, unsigned long long* __restrict__ pruned,
+    const int* __restrict__ halt) {
+  if (halt && *halt) return;
   constexpr int W = kScanRowThreads / 64;
   __shared__ float dr[1024];
   __shared__ unsigned wcnt[2][W];
@@ -1040,13 +1044,14 @@ __global__ __launch_bounds__(kScanRowThreads) void oap_kmeans_lean_scan_rows(
 void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
                            const int32_t* labels, const float* xnorm, const float* drift,
                            const float* drift_max, const float* cstat, int32_t* row_list,
-                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s) {
+                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s,
+                           const int* halt) {
   OAP_CHECK(k <= 1024 && lean_grid >= 1, "kmeans_lean_scan_rows: k <= 1024");
   if (n <= 0) return;
   hipLaunchKernelGGL(oap_kmeans_lean_scan_rows, dim3(lean_grid), dim3(kScanRowThreads), 0, s, n, k,
                      d, kmeans_lloyd_tiles_per_block(n, lean_grid),
                      reinterpret_cast<float2*>(bounds), labels, xnorm, drift, drift_max, cstat,
-                     row_list, row_count, pruned_rows);
+                     row_list, row_count, pruned_rows, halt);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
@@ -1109,6 +1114,7 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.movers = scan && a.img_movers ? 1 : 0;
   l.refine = kmeans_refine_default() ? 1 : 0;
   l.mlist = a.img_mover_list;
+  l.halt = a.halt;
   OAP_CHECK(!l.movers || l.mlist, "kmeans_lean_img: the mover stage needs its row lists");
   if (waves == 12)
     launch_img_w<12>(l, grid, cfg < 0 ? kImgDefaultCfg : cfg, s);

@@ -99,6 +99,7 @@ struct LeanArgs {
   double* sq_slab;
   unsigned* bound_flag;
   float bound_inf;
+  const int* halt;  // batched fits: set once the fit converged (the pass then does nothing)
 };
 
 struct LeanSmem {
@@ -165,6 +166,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   constexpr int PD = WAVES == 12 ? 2 : 1;
   using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.halt && *a.halt) return;
   const int kpad = a.kpad, k = a.k, d = a.d;
   // chunked passes: keys carry global center indices (kbase + in-chunk offset, < 1024); the
   // first and middle chunks only merge into the running keys, the last one finishes the rows
@@ -1037,6 +1039,7 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
   constexpr int CS = DP + 4;
   using F = Frag<KS, XB>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.halt && *a.halt) return;
   const int k = a.k, d = a.d, kpad = a.kpad;
   // chunked passes: the running (best, second, index) of each deferred row lives in xstate
   // between the chunk launches; the last chunk finishes the rows against every center
@@ -1321,6 +1324,7 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
   constexpr int NT = EW * 64;
   using F = Frag<KS, false>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (a.halt && *a.halt) return;
   const int k = a.k, d = a.d, kpad = a.kpad;
   const bool accumulate = a.accumulate;
   const CandSmem L = cand_plan(kpad, k, d, accumulate, a.sums_too);
@@ -1689,7 +1693,9 @@ __global__ __launch_bounds__(256) void oap_kmeans_lean_scan(
     const int32_t* __restrict__ labels, const float* __restrict__ xnorm,
     const float* __restrict__ drift, const float* __restrict__ drift_max,
     const float* __restrict__ cstat, int32_t* __restrict__ tile_list,
-    unsigned* __restrict__ tile_count, unsigned long long* __restrict__ pruned) {
+    unsigned* __restrict__ tile_count, unsigned long long* __restrict__ pruned,
+    const int* __restrict__ halt) {
+  if (halt && *halt) return;
   __shared__ unsigned wcnt[4], wbase[4];
   __shared__ unsigned long long bpruned;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
@@ -1885,6 +1891,7 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
   l.sq_slab = a.sq_slab;
   l.bound_flag = a.bound_flag;
   l.bound_inf = a.bound_inf;
+  l.halt = a.halt;
   // the exact per-row cost is computed when a cost or mindist is asked for
   const bool cost = a.cost_slab != nullptr || a.mindist != nullptr;
   if (a.xbf16)
@@ -1935,13 +1942,14 @@ void kmeans_exact_rows(const KMeansAssignArgs& a, int grid, hipStream_t s) {
 void kmeans_lean_scan(int64_t n, int k, int d, int lean_grid, float* bounds,
                       const int32_t* labels, const float* xnorm, const float* drift,
                       const float* drift_max, const float* cstat, int32_t* tile_list,
-                      unsigned* tile_count, unsigned long long* pruned, hipStream_t s) {
+                      unsigned* tile_count, unsigned long long* pruned, hipStream_t s,
+                      const int* halt) {
   if (n <= 0) return;
   OAP_HIP_CHECK(hipMemsetAsync(tile_count, 0, sizeof(unsigned) * lean_grid, s));
   hipLaunchKernelGGL(oap_kmeans_lean_scan, dim3(lean_grid * kScanSplit), dim3(256), 0, s, n, k, d,
                      lean_grid, kmeans_lloyd_tiles_per_block(n, lean_grid),
                      reinterpret_cast<float2*>(bounds), labels, xnorm, drift, drift_max, cstat,
-                     tile_list, tile_count, pruned);
+                     tile_list, tile_count, pruned, halt);
   OAP_HIP_CHECK(hipGetLastError());
 }
 

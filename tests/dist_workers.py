@@ -36,8 +36,9 @@ def kmeans_native(n=4000, d=6, k=5, seed=7, device="cpu", use_rccl=True, init_mo
 def kmeans_uneven(n=200000, d=16, k=20, seed=11, sigma=3.0, max_iter=12, tol=0.0,
                   empty_rank=-1, no_image_rank=-1, device="gpu", use_rccl=False):
     """Ranks that differ in what the row scan needs: one rank without rows (empty_rank) or one
-    without the fp16 operand image (no_image_rank: OAP_KMEANS_IMAGE=0 there), with tol >= 0 so
-    every iteration is its own batch and every per-batch collective must pair up across ranks."""
+    without the fp16 operand image (no_image_rank: OAP_KMEANS_IMAGE=0 there), with tol >= 0 (the
+    batched form: a converged iteration halts the rest of its batch on the device) — every
+    per-batch collective must pair up across ranks."""
     import oap_mllib_amd as O
     from oap_mllib_amd import _loader
 

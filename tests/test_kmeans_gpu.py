@@ -138,20 +138,69 @@ def test_gpu_world_two_ranks_host_comm_bitwise():
         assert abs(o["cost"] - ref["cost"]) <= 1e-9 * ref["cost"]
 
 
-@pytest.mark.parametrize("case", [{"empty_rank": 1}, {"no_image_rank": 1}])
+@pytest.mark.parametrize("case", [{"empty_rank": 1}, {"no_image_rank": 1},
+                                  {"empty_rank": 1, "tol": 0.2, "max_iter": 40},
+                                  {"no_image_rank": 1, "tol": 0.2, "max_iter": 40}])
 def test_two_ranks_uneven_scan_state(case):
     """A rank without rows, or without room for the operand image, takes different per-row
-    scan paths than its peer; the per-batch collectives must still pair up (tol >= 0: one
-    iteration per batch) and the fit must equal the one-rank fit of the same rows."""
+    scan paths than its peer; the batch's collectives (its control tail included) must still
+    pair up and the fit must equal the one-rank fit of the same rows.  With a tolerance the fit
+    converges inside a batch: the iterations enqueued behind it stand down on the device on
+    both ranks (halt), so the result is the converged iteration's."""
     from dist_workers import kmeans_uneven
 
     rc, outs = run_world("dist_workers", "kmeans_uneven", nproc=2, timeout=240, **case)
     assert rc == 0, outs
     O.shutdown_world()
-    ref = kmeans_uneven()
+    ref = kmeans_uneven(**{k: v for k, v in case.items() if k in ("tol", "max_iter")})
+    if "tol" in case:
+        assert 3 < ref["iters"] < case["max_iter"], ref["iters"]  # (early convergence)
     for o in outs:
         assert o["comm"] == "host" and o["iters"] == ref["iters"]
         assert np.array_equal(np.array(o["centers"]), np.array(ref["centers"]))
+        assert abs(o["cost"] - ref["cost"]) <= 1e-9 * abs(ref["cost"])
+
+
+@pytest.mark.parametrize("force_rccl", [False, True])
+def test_tolerance_fit_batches_and_stands_down(native, force_rccl):
+    """A fit with a tolerance enqueues its iterations in batches; the finalize of the converged
+    iteration sets the device halt word and every kernel of the iterations behind it returns at
+    once.  The result must be exactly the converged iteration's: the fit of exactly that many
+    iterations (tol < 0) gives the same centers, counts and shifts bitwise, the shift history
+    crosses the tolerance exactly there, no image pass ran past it, and the iteration count is
+    the CPU engine's (fp64; the data overlap, so its near-tie labels may differ from fp32's)."""
+    n, d, k = 300000, 12, 16
+    rng = np.random.default_rng(21)
+    C = rng.uniform(-10, 10, size=(k, d))
+    X = (C[rng.integers(0, k, n)] + rng.normal(0, 2.0, size=(n, d)))
+    X = X.astype(np.float32).astype(np.float64)
+    init = X[rng.choice(n, k, replace=False)].copy()
+    O.shutdown_world()
+    w = O.init_world(O.get_config().replace(device="gpu", device_id=0,
+                                            force_device_comm=force_rccl),
+                     rank=0, size=1, local_rank=0)
+    g, comm = w.ctx, w.comm
+    assert (comm.name == "rccl") == force_rccl, comm.name
+    t = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
+    c = native.Context(-1)
+    tc = native.upload_dense(c, X, "f64", d)
+    for tol in (1e-1, 1e-2):  # (CPU engine: 7 and 48 iterations)
+        rg = native.kmeans_fit(g, comm, t, init, k, 60, tol)
+        rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, 60, tol)
+        it = rg["num_iter"]
+        assert rg["converged"] and 2 < it < 60, it
+        assert it == rc["num_iter"]
+        sh = rg["shift_history"]
+        assert len(sh) == it and sh[-1] <= tol < min(sh[:-1]), sh
+        rf = native.kmeans_fit(g, comm, t, init, k, it, -1.0)  # exactly `it` iterations
+        assert rf["num_iter"] == it and not rf["converged"]
+        assert rg["last_counts"] == rf["last_counts"]
+        assert np.array_equal(rg["centers"], rf["centers"])
+        assert rg["shift_history"] == rf["shift_history"]
+        assert abs(rg["cost"] - rf["cost"]) <= 1e-6 * rf["cost"]
+        assert rg["image_passes"] <= it
+    del t
+    O.shutdown_world()
 
 
 @pytest.mark.parametrize("d,k", [(50, 200), (16, 64), (100, 30)])
@@ -691,6 +740,31 @@ def test_provisional_fixed_point_bounds(native, monkeypatch, case):
             assert re["num_iter"] == rg["num_iter"] and rg["last_counts"] == re["last_counts"]
             assert np.array_equal(rg["centers"], re["centers"])
             np.testing.assert_allclose(rg["cost"], re["cost"], rtol=1e-6)
+
+
+def test_zero_center_column_takes_column_maxima(native, monkeypatch):
+    """A feature that is 0 in every initial center has provisional bound 0, which no row can
+    satisfy: the fit must take the column maxima up front (scale_source "absmax"), not flag
+    every row and restart, and give the eager rule's and the CPU engine's fit bitwise."""
+    monkeypatch.setenv("OAP_KMEANS_PROVISIONAL_MIN", "0")
+    n, d, k = 60000, 10, 12
+    rng = np.random.default_rng(11)
+    C = rng.uniform(-10, 10, size=(k, d))
+    lab = rng.integers(0, k, n)
+    X = C[lab] + rng.normal(0, 0.3, size=(n, d))
+    X[:, 4] = 0.0  # constant-zero column (one-hot / sparse features)
+    X = X.astype(np.float32).astype(np.float64)
+    init = X[[int(np.argmax(lab == j)) for j in range(k)]].copy()
+    g = native.Context(0, 0.5, 0)
+    tg = native.upload_dense(g, X, "f32", native.kmeans_ld(d))
+    rg = native.kmeans_fit(g, native.LocalComm(True), tg, init, k, 8, -1.0)
+    assert rg["scale_source"] == "absmax", rg["scale_source"]
+    c = native.Context(-1)
+    tc = native.upload_dense(c, X, "f64", d)
+    rc = native.kmeans_fit(c, native.LocalComm(False), tc, init, k, 8, -1.0)
+    assert rg["last_counts"] == rc["last_counts"]
+    assert np.array_equal(rg["centers"], rc["centers"])
+    assert np.all(np.asarray(rg["centers"]).reshape(k, d)[:, 4] == 0.0)
 
 
 @pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (44, 96)])
