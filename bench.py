@@ -187,6 +187,12 @@ def bench_kmeans(args, w):
                                          "it could not prune (gathered from the row-major "
                                          "operand image) + exact fp32 re-decision; delta "
                                          "accumulation of moved rows",
+        "lean_img_kernel_delta_fused_rowscan_gated": "per iteration, a sample of the rows' "
+                                                     "bounds picks (on the device) the image "
+                                                     "kernel with the row-level Hamerly scan "
+                                                     "fused in or the dense pipelined image "
+                                                     "kernel; exact fp32 re-decision; delta "
+                                                     "accumulation of moved rows",
         "lean_img_kernel_delta_fused_rowscan": "image kernel with the row-level Hamerly scan "
                                                "fused in (per-wave LDS ring of the rows it "
                                                "cannot prune) + exact fp32 re-decision; delta "

@@ -485,8 +485,9 @@ PYBIND11_MODULE(_native, m) {
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm, std::shared_ptr<DenseTable> t,
          py::object init_centers, int k, int max_iter, double tol, const std::string& init_mode,
          int init_steps, uint64_t seed, bool precise, bool prune, bool delta,
-         bool phase_events) {
+         bool phase_events, double scan_min_prune) {
         KMeansParams p;
+        p.scan_min_prune = scan_min_prune;
         p.precise = precise;
         p.prune = prune;
         p.delta = delta;
@@ -546,7 +547,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("k") = 2, py::arg("max_iter") = 20, py::arg("tol") = 1e-4,
       py::arg("init_mode") = "k-means||", py::arg("init_steps") = 2, py::arg("seed") = 1,
       py::arg("precise") = false, py::arg("prune") = true, py::arg("delta") = true,
-      py::arg("phase_events") = false);
+      py::arg("phase_events") = false, py::arg("scan_min_prune") = 0.2);
   m.def(
       "kmeans_fit_streamed",
       [](std::shared_ptr<Context> ctx, std::shared_ptr<Comm> comm,

@@ -318,6 +318,9 @@ struct AssignReq {
   float bound_inf = 0.f;
   // batched fits with a tolerance: the kernels stand down once the fit converged
   const int* halt = nullptr;
+  // fused row-scan image passes: a device word (kern::kmeans_scan_decide) picks the scan (1) or
+  // the dense pass (0); both are enqueued (KMeansAssignArgs::img_gate)
+  const int* img_gate = nullptr;
 };
 
 // The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
@@ -492,13 +495,31 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
       const int cfg = req.img_cfg >= 0                         ? req.img_cfg
                       : a.img_scan_xnorm && scan_cfg_default() >= 0 ? scan_cfg_default()
                                                                     : img_cfg_default();
-      kern::kmeans_lean_img(a, grid, lw, cfg, s);
+      if (a.img_scan_xnorm && req.img_gate && !a.img_movers) {
+        // the scan pass and the dense pass, one of which runs (the device gate)
+        kern::KMeansAssignArgs as = a;
+        as.img_gate = req.img_gate;
+        as.img_gate_on = 1;
+        kern::kmeans_lean_img(as, grid, lw, cfg, s);
+        kern::KMeansAssignArgs ad = a;
+        ad.img_scan_xnorm = nullptr;
+        ad.img_scan_drift = nullptr;
+        ad.img_scan_pruned = nullptr;
+        ad.img_gate = req.img_gate;
+        ad.img_gate_on = 0;
+        kern::kmeans_lean_img(ad, grid, lw, req.img_cfg >= 0 ? req.img_cfg : img_cfg_default(),
+                              s);
+      } else {
+        kern::kmeans_lean_img(a, grid, lw, cfg, s);
+      }
       if (req.img_fallback) {
         kern::KMeansAssignArgs f = a;
         f.img_mode = 3;
         kern::kmeans_lloyd(f, grid, lv, s);
       }
       t_assign_path = a.img_movers       ? "lean_img_kernel_delta_rowscan_movers"
+                      : a.img_scan_xnorm && req.img_gate
+                          ? "lean_img_kernel_delta_fused_rowscan_gated"
                       : a.img_scan_xnorm ? "lean_img_kernel_delta_fused_rowscan"
                       : a.img_rows     ? "lean_img_kernel_delta_rowscan"
                       : req.tile_list  ? "lean_img_kernel_delta_scan"
@@ -1583,13 +1604,15 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // tests its own rows and queues the unpruned ones in LDS) where the kernel's LDS plan has room
   // for it; OAP_KMEANS_ROW_SCAN=2 takes the separate scan kernel + row list through HBM instead,
   // =0 the tile scan.
-  Buffer rlist_b, rpruned_b;
+  Buffer rlist_b, rpruned_b, scan_gate_b;
   const char* rs_env = std::getenv("OAP_KMEANS_ROW_SCAN");
   const bool row_scan = scan && !chunked && !(rs_env && *rs_env == '0');
   bool row_scan_fused = row_scan && !(rs_env && *rs_env == '2');
   if (row_scan) {
     rpruned_b = ctx.alloc(sizeof(u64));
     ctx.memset(rpruned_b.data(), 0, sizeof(u64), s);
+    scan_gate_b = ctx.alloc(sizeof(int) * 4);
+    ctx.memset(scan_gate_b.data(), 0, sizeof(int) * 4, s);
   }
   unsigned* dcount =
       scan ? reinterpret_cast<unsigned*>(dlist_b.as<int32_t>() + size_t(lgrid) * size_t(ltiles))
@@ -1871,11 +1894,19 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       req.img_scan_xnorm = nullptr;
       req.img_scan_drift = nullptr;
       req.img_scan_pruned = nullptr;
+      req.img_gate = nullptr;
       if (row_scan_it && row_scan_fused) {
         OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
         req.img_scan_xnorm = xnorm_full;
         req.img_scan_drift = drift_b.as<float>();
         req.img_scan_pruned = rpruned_b.as<u64>();
+        if (p.scan_min_prune > 0.0 && !req.img_movers) {
+          // scan or dense, decided on the device from a sample of the rows
+          kern::kmeans_scan_decide(x.rows, k, d, bounds_full, req.labels, xnorm_full,
+                                   drift_b.as<float>(), g.cstat.as<float>(),
+                                   float(p.scan_min_prune), scan_gate_b.as<int>(), halt, s);
+          req.img_gate = scan_gate_b.as<int>();
+        }
       } else if (row_scan_it) {
         OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
         kern::kmeans_lean_scan_rows(x.rows, k, d, lgrid, bounds_full, req.labels, xnorm_full,

@@ -43,6 +43,11 @@ struct KMeansParams {
   // event pair per batch of iterations (kmeans/iteration only), no event gaps between phases
   // (each record is a ~10 us gap in the stream, so the default is off)
   bool phase_events = false;
+  // row-scan image passes: a sample of the rows (kern::kmeans_scan_decide) estimates the share
+  // the Hamerly test would prune; below this share the pass runs dense (the pipelined image
+  // kernel, ~15% faster than a scan pass that prunes nothing).  Result-neutral (either pass
+  // writes every label and bound), so a local, per-rank choice.  0: always scan.
+  double scan_min_prune = 0.2;
   // internal: the fixed-point bounds come from a column-maxima pass up front (set on the
   // restart after a failed provisional check, see kmeans.cpp fit_bounds)
   bool absmax_pass = false;

@@ -178,6 +178,11 @@ struct KMeansAssignArgs {
   // Batched fits with a tolerance: a device word the finalize sets once the fit has converged;
   // the lean / image / exact / scan kernels of later iterations in the batch return at once.
   const int* halt = nullptr;
+  // Image pass gate (kmeans_lean_img): the pass runs only when *img_gate == img_gate_on — a
+  // row-scan pass (1) and a dense pass (0) are both enqueued and kmeans_scan_decide picks one on
+  // the device.  Either writes every row's label and bounds, so the choice changes no result.
+  const int* img_gate = nullptr;
+  int img_gate_on = 0;
 };
 // Lean tier-1 Lloyd kernel (kmeans_lloyd.hip): applicable when the centroid hi plane + the
 // fixed-point accumulator fit LDS and d + 4 bias features fit the padded width.
@@ -211,6 +216,14 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
 // max |x|^2 in the margin); pruned rows have their bounds advanced in place (no write once no
 // center moves), the others are appended in row order to b's segment of row_list
 // ([lean_grid][32 tiles_per_block], count row_count[b]).  *pruned_rows (optional) counts.
+// The scan-vs-dense choice of a row-scan image pass, on the device: the row scan's own Hamerly
+// test on an even sample of the rows (bounds, labels, the drift the last finalize wrote); *gate
+// = 1 (scan) when at least min_frac of the sample is prunable, else 0 (the dense pipelined pass,
+// cheaper when few rows prune).  gate: [4] ints, gate[2..3] zero before the first call (the
+// kernel's scratch).  Returns at once when *halt is set.
+void kmeans_scan_decide(int64_t n, int k, int d, const float* bounds, const int32_t* labels,
+                        const float* xnorm, const float* drift, const float* cstat,
+                        float min_frac, int* gate, const int* halt, hipStream_t s);
 void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
                            const int32_t* labels, const float* xnorm, const float* drift,
                            const float* drift_max, const float* cstat, int32_t* row_list,

@@ -81,6 +81,8 @@ struct ImgArgs {
   int refine;  // the refined deferral test (kmeans_frag.h refined_tt; OAP_KMEANS_REFINE=0: off)
   int32_t* mlist;  // RM 3: per-wave lists of the rows the mover stage left, [grid][seg_cap]
   const int* halt;  // batched fits: set once the fit converged (the pass then does nothing)
+  const int* gate;  // optional: the pass runs only when *gate == gate_on (kmeans_scan_decide)
+  int gate_on;
 };
 
 struct ImgSmem {
@@ -157,6 +159,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   constexpr int DP = 16 * KS, NT = WAVES * 64, RS = DP + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (a.halt && *a.halt) return;
+  if (a.gate && *a.gate != a.gate_on) return;
   const float cmax = a.cstat[0];
   const float alpha = a.img_beta[0];
   if (!(alpha * cmax <= 512.f)) return;  // (kmeans_lloyd img_mode 3 takes this pass)
@@ -1039,7 +1042,81 @@ __global__ __launch_bounds__(kScanRowThreads) void oap_kmeans_lean_scan_rows(
   }
 }
 
+constexpr int kDecideBlocks = 64;
+constexpr int kDecideThreads = 256;
+constexpr int kDecidePerThread = 4;  // 65536 sampled rows, every load of a thread in flight
+
+// scratch[0]: blocks done, scratch[1]: prunable samples (zero on entry; the last block resets)
+__global__ __launch_bounds__(kDecideThreads) void oap_kmeans_scan_decide(
+    int64_t n, int k, int d, const float2* __restrict__ bounds,
+    const int32_t* __restrict__ labels, const float* __restrict__ xnorm,
+    const float* __restrict__ drift, const float* __restrict__ cstat, float min_frac,
+    int* __restrict__ gate, unsigned* __restrict__ scratch, const int* __restrict__ halt) {
+  if (halt && *halt) return;
+  __shared__ unsigned wsum[kDecideThreads / 64];
+  __shared__ bool s_last;
+  const int tid = threadIdx.x;
+  const float dmax = drift[k];
+  const float cmax = cstat[0];
+  const float mrel = 4e-7f * float(d + 8);
+  constexpr int64_t kS = int64_t(kDecideBlocks) * kDecideThreads * kDecidePerThread;
+  const int64_t S = n < kS ? n : kS;
+  float2 b[kDecidePerThread];
+  int lab[kDecidePerThread];
+  float xn[kDecidePerThread];
+  bool in[kDecidePerThread];
+#pragma unroll
+  for (int j = 0; j < kDecidePerThread; ++j) {
+    const int64_t i = (int64_t(j) * kDecideBlocks + blockIdx.x) * kDecideThreads + tid;
+    in[j] = i < S;
+    const int64_t row = in[j] ? static_cast<int64_t>((double(i) + 0.5) * double(n) / double(S))
+                              : 0;
+    b[j] = bounds[row];
+    lab[j] = labels[row];
+    xn[j] = xnorm[row >> 5];
+  }
+  unsigned ok_n = 0;
+#pragma unroll
+  for (int j = 0; j < kDecidePerThread; ++j) {
+    const float u = b[j].x + drift[min(max(lab[j], 0), k - 1)];
+    const float lk = b[j].y - dmax;
+    ok_n += (in[j] && lk > 0.f && (lk - u) * (lk + u) > mrel * (xn[j] + cmax * cmax)) ? 1u : 0u;
+  }
+  for (int m = 32; m >= 1; m >>= 1) ok_n += __shfl_xor(ok_n, m, 64);
+  if ((tid & 63) == 0) wsum[tid >> 6] = ok_n;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned t = 0;
+    for (int w = 0; w < kDecideThreads / 64; ++w) t += wsum[w];
+    if (t) atomicAdd(&scratch[1], t);
+    __threadfence();
+    s_last = atomicAdd(&scratch[0], 1u) == kDecideBlocks - 1;
+  }
+  __syncthreads();
+  if (s_last && tid == 0) {
+    __threadfence();
+    const unsigned tot = atomicAdd(&scratch[1], 0u);
+    gate[0] = double(tot) >= double(min_frac) * double(S) ? 1 : 0;
+    scratch[0] = 0u;
+    scratch[1] = 0u;
+  }
+}
+
 }  // namespace
+
+void kmeans_scan_decide(int64_t n, int k, int d, const float* bounds, const int32_t* labels,
+                        const float* xnorm, const float* drift, const float* cstat,
+                        float min_frac, int* gate, const int* halt, hipStream_t s) {
+  OAP_CHECK(k >= 1 && gate && bounds && labels && xnorm && drift && cstat,
+            "kmeans_scan_decide: bad arguments");
+  if (n <= 0) return;
+  // gate[0]: the choice; gate[2..3]: the kernel's block counter and sum (zeroed by the caller
+  // once, reset by the kernel's last block)
+  hipLaunchKernelGGL(oap_kmeans_scan_decide, dim3(kDecideBlocks), dim3(kDecideThreads), 0, s, n,
+                     k, d, reinterpret_cast<const float2*>(bounds), labels, xnorm, drift, cstat,
+                     min_frac, gate, reinterpret_cast<unsigned*>(gate + 2), halt);
+  OAP_HIP_CHECK(hipGetLastError());
+}
 
 void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
                            const int32_t* labels, const float* xnorm, const float* drift,
@@ -1115,6 +1192,8 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.refine = kmeans_refine_default() ? 1 : 0;
   l.mlist = a.img_mover_list;
   l.halt = a.halt;
+  l.gate = a.img_gate;
+  l.gate_on = a.img_gate_on;
   OAP_CHECK(!l.movers || l.mlist, "kmeans_lean_img: the mover stage needs its row lists");
   if (waves == 12)
     launch_img_w<12>(l, grid, cfg < 0 ? kImgDefaultCfg : cfg, s);

@@ -767,6 +767,30 @@ def test_zero_center_column_takes_column_maxima(native, monkeypatch):
     assert np.all(np.asarray(rg["centers"]).reshape(k, d)[:, 4] == 0.0)
 
 
+@pytest.mark.parametrize("d,k", [(50, 200), (20, 44)])
+def test_scan_or_dense_gate_is_exact(native, d, k):
+    """Row-scan iterations enqueue a scan pass and a dense pass; kmeans_scan_decide picks one on
+    the device from a sample of the rows (scan_min_prune).  Either writes every label and bound,
+    so always-scan (0), always-dense (2) and the sampled choice (0.2) give the unpruned fit's
+    centers and counts bitwise, and the scan prunes rows only when it runs."""
+    n = 1_500_000
+    g = native.Context(0, 0.5, 0)
+    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, 8.0, 91)
+    comm = native.LocalComm(True)
+    init = native.kmeans_init(g, comm, t, k, "k-means||", 2, 3)
+    ref = native.kmeans_fit(g, comm, t, init, k, 16, -1.0, prune=False)
+    runs = {m: native.kmeans_fit(g, comm, t, init, k, 16, -1.0, scan_min_prune=m)
+            for m in (0.0, 0.2, 2.0)}
+    for m, r in runs.items():
+        assert np.array_equal(r["centers"], ref["centers"]), m
+        assert r["last_counts"] == ref["last_counts"], m
+        assert abs(r["cost"] - ref["cost"]) <= 1e-7 * ref["cost"], m
+    assert runs[2.0]["pruned_rows"] == 0
+    assert runs[0.0]["pruned_rows"] >= runs[0.2]["pruned_rows"] > 0
+    assert runs[0.0]["assign_path"] == "lean_img_kernel_delta_fused_rowscan"
+    assert runs[0.2]["assign_path"] == "lean_img_kernel_delta_fused_rowscan_gated"
+
+
 @pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (44, 96)])
 def test_mover_stage_is_exact(native, monkeypatch, d, k):
     """The row scan's mover stage (rows the Hamerly test cannot prune are bounded against the 32
@@ -784,7 +808,7 @@ def test_mover_stage_is_exact(native, monkeypatch, d, k):
     off = native.kmeans_fit(g, comm, t, init, k, 14, -1.0)
     ref = native.kmeans_fit(g, comm, t, init, k, 14, -1.0, prune=False)
     assert on["assign_path"] == "lean_img_kernel_delta_rowscan_movers", on["assign_path"]
-    assert off["assign_path"] == "lean_img_kernel_delta_fused_rowscan"
+    assert off["assign_path"] == "lean_img_kernel_delta_fused_rowscan_gated"
     for r in (on, off):
         assert np.array_equal(r["centers"], ref["centers"])
         assert r["last_counts"] == ref["last_counts"]
