@@ -230,9 +230,6 @@ def bench_kmeans(args, w):
              "moved_rows_per_iter": r.get("moved_rows", 0) / max(args.steps, 1),
              # Lloyd passes that streamed the fp16 operand image instead of the f32 rows
              "image_passes": r.get("image_passes", 0),
-             # row-scan passes with the mover stage: rows it bounded, rows it left to the full pass
-             "mover_rows_per_iter": r.get("mover_rows", 0) / max(args.steps, 1),
-             "mover_listed_rows_per_iter": r.get("mover_listed_rows", 0) / max(args.steps, 1),
              "scale_source": r.get("scale_source"),
              "final_cost_path": r.get("final_cost_path"),
              "refine_tiles_per_iter": r["refine_tiles"] / max(args.steps, 1),

@@ -16,6 +16,7 @@
 #include "drivers/kmeans.h"
 #include "kernels/kernels.h"
 #include "runtime/context.h"
+#include "runtime/knobs.h"
 #include "runtime/table.h"
 
 namespace py = pybind11;
@@ -186,6 +187,23 @@ PYBIND11_MODULE(_native, m) {
         Logger::instance().configure(rank, device, l, path);
       },
       py::arg("rank"), py::arg("device"), py::arg("level") = "warn", py::arg("path") = "");
+  // the native knob registry (runtime/knobs.h): Config.native_knobs installs overrides
+  m.def("set_knob", &set_knob, py::arg("name"), py::arg("value"),
+        "install (value non-empty) or remove (empty) a native knob override");
+  m.def("clear_knobs", &clear_knobs);
+  m.def("knob_value", [](const std::string& name) { return knob_str(name.c_str()); },
+        py::arg("name"));
+  m.def("knob_table", []() {
+    py::list out;
+    for (const KnobInfo& k : knob_table()) {
+      py::dict d;
+      d["name"] = k.name;
+      d["default"] = k.def;
+      d["doc"] = k.doc;
+      out.append(d);
+    }
+    return out;
+  });
   m.def("log", [](const std::string& level, const std::string& phase, const std::string& fields) {
     LogLevel l = level == "error" ? LogLevel::Error
                  : level == "warn" ? LogLevel::Warn
@@ -539,8 +557,6 @@ PYBIND11_MODULE(_native, m) {
         out["image_bytes"] = r.image_bytes;
         out["final_cost_path"] = r.final_cost_path;
         out["scale_source"] = r.scale_source;
-        out["mover_rows"] = r.mover_rows;
-        out["mover_listed_rows"] = r.mover_listed_rows;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("init_centers") = py::none(),

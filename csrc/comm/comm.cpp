@@ -1,4 +1,5 @@
 #include "comm/comm.h"
+#include "runtime/knobs.h"
 
 #include <rccl/rccl.h>
 #include <unistd.h>
@@ -160,8 +161,7 @@ void RcclComm::alltoallv(const void* send, const std::vector<size_t>& send_count
   // (OAP_RCCL_A2A_CHUNK_BYTES overrides the 256 MiB round size: tests drive several rounds
   // with small uneven counts)
   const size_t kChunk = [] {  // (read per call: tests set it mid-process)
-    const char* e = std::getenv("OAP_RCCL_A2A_CHUNK_BYTES");
-    const long long v = e ? std::atoll(e) : 0;
+    const int64_t v = knob_int("OAP_RCCL_A2A_CHUNK_BYTES");
     return v > 0 ? size_t(v) : size_t(1) << 28;
   }();
   const size_t chunk = std::max<size_t>(1, kChunk / es);
@@ -401,17 +401,18 @@ std::vector<int64_t> comm_allgather_i64(Context& ctx, Comm& comm, int64_t v) {
 
 // ------------------------------------------------------------------------- fault injection
 void maybe_inject_fault(int rank, const char* phase, int iteration) {
-  static const char* spec = std::getenv("OAP_MLLIB_FAULT");
-  if (!spec || !*spec) return;
+  const std::string spec_s = knob_str("OAP_MLLIB_FAULT");
+  if (spec_s.empty()) return;
+  const char* spec = spec_s.c_str();
   int r = -1, it = -1;
   char ph[64] = {0};
   if (std::sscanf(spec, "%d:%63[^:]:%d", &r, ph, &it) != 3) return;
   if (r != rank || it != iteration || std::strcmp(ph, phase) != 0) return;
-  const char* mode = std::getenv("OAP_MLLIB_FAULT_MODE");
+  const std::string mode = knob_str("OAP_MLLIB_FAULT_MODE");
   std::ostringstream os;
-  os << "\"iteration\":" << iteration << ",\"mode\":\"" << (mode ? mode : "raise") << "\"";
+  os << "\"iteration\":" << iteration << ",\"mode\":\"" << mode << "\"";
   Logger::instance().log(LogLevel::Error, std::string("fault/") + phase, os.str());
-  if (mode && std::strcmp(mode, "exit") == 0) _exit(17);
+  if (mode == "exit") _exit(17);
   OAP_THROW(CommError, "injected fault at rank " << rank << " phase " << phase << " iteration "
                                                    << iteration);
 }

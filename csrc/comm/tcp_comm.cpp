@@ -14,6 +14,7 @@
 #include <thread>
 
 #include "runtime/log.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 
@@ -278,8 +279,7 @@ void TcpComm::alltoallv(const void* send, const std::vector<size_t>& send_counts
   const size_t es = dtype_size(dt);
   // (OAP_TCP_PIECE_BYTES overrides the 64 MiB forwarding piece: tests drive several pieces)
   const size_t kPiece = [] {  // (read per call: tests set it mid-process)
-    const char* e = std::getenv("OAP_TCP_PIECE_BYTES");
-    const long long v = e ? std::atoll(e) : 0;
+    const int64_t v = knob_int("OAP_TCP_PIECE_BYTES");
     return v > 0 ? size_t(v) : size_t(64) << 20;
   }();
   std::vector<size_t> soff(P + 1, 0), roff(P + 1, 0);

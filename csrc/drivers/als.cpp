@@ -14,6 +14,7 @@
 #include "kernels/rng.h"
 #include "linalg/eigen.h"
 #include "runtime/log.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 
@@ -395,8 +396,8 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   // it upward (timing experiments: whole 128-byte lines per gathered row)
   const int r = p.rank;
   int ld = int(round_up(size_t(r), 16));
-  if (const char* e = std::getenv("OAP_ALS_LD")) {
-    const int v = std::atoi(e);
+  {
+    const int v = int(knob_int("OAP_ALS_LD"));
     if (v >= ld && v % 16 == 0 && v <= 128) ld = v;
   }
   AlsResult res;
@@ -413,7 +414,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
   // (host_engine: the fp64 host solver on a GPU world, e.g. ranks beyond the GPU kernels; the
   // GPU context only stages the collectives)
   const bool gpu_engine = ctx.is_gpu() && !p.host_engine && !p.nonnegative;
-  if (gpu_engine && !std::getenv("OAP_ALS_HOST_SETUP")) {
+  if (gpu_engine && !knob_on("OAP_ALS_HOST_SETUP")) {
     ctx.activate();
     if (local)
       on_device = kern::als_device_setup(ctx, users, items, ratings, n, ctx.compute(), &dev_setup);
@@ -545,16 +546,10 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
     const int C = local ? 1 : 4;
     // implicit rows with <= 64 ratings: low-rank (Woodbury) solve in the eigenbasis of Y^T Y
     // (kernels/als_lowrank.hip); OAP_ALS_LOWRANK=0 sends every row to the direct r x r solve
-    const bool lowrank = [] {
-      const char* e = std::getenv("OAP_ALS_LOWRANK");
-      return !e || std::atoi(e) != 0;
-    }();
+    const bool lowrank = knob_int("OAP_ALS_LOWRANK") != 0;
     // long-row chunks: split-fp16 Gramian (kernels/als.hip); OAP_ALS_GRAM=fp32 keeps the
     // exact-fp32 MFMA products
-    const bool x3_gram = [] {
-      const char* e = std::getenv("OAP_ALS_GRAM");
-      return !e || std::string(e) != "fp32";
-    }();
+    const bool x3_gram = knob_str("OAP_ALS_GRAM") != "fp32";
     struct Dev {
       Buffer f, ptr, col, val;
       Buffer short_rows, long_rows, long_chunk_ptr, chunk_begin, chunk_end, partials;
@@ -571,10 +566,7 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
       std::vector<int64_t> x3n;
     } dU, dI;
     // direct rows at most this long keep the fp32 Gramian (OAP_ALS_X3_MIN_LEN)
-    const int64_t x3_min = [] {
-      const char* e = std::getenv("OAP_ALS_X3_MIN_LEN");
-      return e ? std::atoll(e) : int64_t(128);
-    }();
+    const int64_t x3_min = knob_int("OAP_ALS_X3_MIN_LEN");
     // rows longer than kLong ratings are split into kLong-sized chunks (partial Gramians)
     constexpr int64_t kLong = 4096;
     auto upload_side = [&](Side& S, Dev& D, kern::AlsDeviceCsr* dc) {

@@ -18,6 +18,7 @@
 #include "kernels/kernels.h"
 #include "kernels/kmeans_init.h"
 #include "kernels/kmeans_wide.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 
@@ -128,8 +129,7 @@ std::vector<double> center_bounds(const std::vector<double>& centers, int k, int
 // maxima; they apply only where the pass they save is worth it: datasets of at least
 // OAP_KMEANS_PROVISIONAL_MIN elements (global rows x features, default 2^28 — 1 GiB of f32).
 bool provisional_allowed(int64_t global_rows, int d) {
-  const char* e = std::getenv("OAP_KMEANS_PROVISIONAL_MIN");  // (read per fit: tests set it)
-  const double lim = e ? std::atof(e) : double(int64_t(1) << 28);
+  const double lim = knob_float("OAP_KMEANS_PROVISIONAL_MIN");  // (read per fit: tests set it)
   return double(global_rows) * double(d) >= lim;
 }
 
@@ -299,19 +299,13 @@ struct AssignReq {
   // kernel, for the case the image's scale cannot hold the current centers (the host clears it
   // once the rows' norms prove that impossible)
   bool img_fallback = true;
-  int img_kernel = -1;      // -1: OAP_KMEANS_IMG_KERNEL (default on), 0 kmeans_lloyd, 1 lean_img
-  int img_cfg = -1;         // oap_kmeans_lean_img configuration (-1: OAP_KMEANS_IMG_CFG / default)
+  int img_kernel = -1;      // timing probes: 0 kmeans_lloyd's image branch, else the image kernel
+  int img_cfg = -1;         // timing probes: oap_kmeans_lean_img configuration (0 / 1; -1 default)
   bool skip_exact = false;  // timing probes: the lean pass only
-  // image passes after a row-level scan (kmeans_lean_scan_rows): the rows it could not prune
-  const int32_t* img_rows = nullptr;
-  const unsigned* img_row_count = nullptr;
   // image passes with the row scan fused into the image kernel (KMeansAssignArgs::img_scan_*)
   const float* img_scan_xnorm = nullptr;
   const float* img_scan_drift = nullptr;
   u64* img_scan_pruned = nullptr;
-  // fused row-scan image passes: the mover stage (KMeansAssignArgs::img_movers)
-  bool img_movers = false;
-  int32_t* img_mover_list = nullptr;
   // lean full pass: per-workgroup sum |x|^2 and the provisional-bound check (KMeansAssignArgs)
   double* sq_slab = nullptr;
   unsigned* bound_flag = nullptr;
@@ -323,57 +317,19 @@ struct AssignReq {
   const int* img_gate = nullptr;
 };
 
-// The steady-state image pass runs as its own kernel (kmeans_lean_img.hip) unless
-// OAP_KMEANS_IMG_KERNEL=0; OAP_KMEANS_IMG_CFG picks a configuration (timing probes).
-bool img_kernel_default() {
-  static const bool on = [] {
-    const char* e = std::getenv("OAP_KMEANS_IMG_KERNEL");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-int img_cfg_default() {
-  static const int c = [] {
-    const char* e = std::getenv("OAP_KMEANS_IMG_CFG");
-    return e ? std::atoi(e) : -1;
-  }();
-  return c;
-}
-
-// configuration of the fused row-scan passes (OAP_KMEANS_SCAN_CFG): 0, the chunk loop without
-// software pipelining — the scan's prefetched bounds fit its registers (105 VGPRs, no spill)
-// where the pipelined loop would spill 64 B per lane (r4h: 4.66 vs 5.14 ms/step)
-int scan_cfg_default() {
-  static const int c = [] {
-    const char* e = std::getenv("OAP_KMEANS_SCAN_CFG");
-    return e ? std::atoi(e) : 0;
-  }();
-  return c;
-}
-
-int& lean_variant_ref() {  // -1: by width (below)
-  static int v = [] {
-    const char* e = std::getenv("OAP_KMEANS_LEAN_VARIANT");
-    return e ? std::atoi(e) : -1;
-  }();
+int& lean_variant_ref() {  // -1: by width (below); kmeans_set_lean_variant (timing probes)
+  static int v = -1;
   return v;
 }
-// Workgroup shape of the lean kernel: 16 waves (4 per SIMD, 128 registers) unless the rows are
-// 7-8 k-steps wide, where 128 registers spill (config 5, d = 100: 232 B/lane of scratch) and 12
-// waves (168 registers) measured 3.5% faster (396 -> 382 ms/iter at 1B rows).  Rows of <= 4
-// k-steps whose plane fits 7-8 chunks of 32 centroids (k <= 224 at d <= 60) can take the
-// register-resident plane (variant 11, 8 waves, no LDS reads in the distance loop) with
-// OAP_KMEANS_REG_PLANE=1.
+// Workgroup shape of the lean kernel: variant 6 (16 waves, 4 per SIMD, 128 registers, fragment
+// reads grouped ahead of each MFMA chain) unless the rows are 7-8 k-steps wide, where 128
+// registers spill (config 5, d = 100: 232 B/lane of scratch) and variant 8 (12 waves, 168
+// registers) measured 3.5% faster (396 -> 382 ms/iter at 1B rows).
 int lean_variant(int d, int kpad) {
+  (void)kpad;
   const int v = lean_variant_ref();
-  const int rch = kern::kmeans_lloyd_rch(d);
-  const bool reg_ok = rch > 0 && kpad <= 32 * rch;
-  if (v >= 0) return (v == 11 && !reg_ok) ? 0 : v;
-  const char* e = std::getenv("OAP_KMEANS_REG_PLANE");
-  if (reg_ok && e && *e == '1') return 11;
-  // (variant 6 — fragment reads grouped ahead of each MFMA chain — measured ~1% ahead of 0 on
-  // the headline shape in two runs; the register plane 6% behind: profiles/r3/lean_variants_*)
-  return d + 4 > 96 ? 8 : 6;  // (wide rows: 12 waves, grouped fragment reads — config 5 -2%)
+  if (v == 6 || v == 8) return v;
+  return d + 4 > 96 ? 8 : 6;
 }
 
 // Whether gpu_assign takes the lean path for this request.
@@ -387,7 +343,7 @@ bool lean_applies(const DenseTable& x, int k, int kpad, const AssignReq& req) {
 // kernel, but small enough for 10-bit key indices; no pruning state (full passes).
 bool lean_chunked_applies(const DenseTable& x, const GpuCenters& g, const AssignReq& req,
                           int kmax) {
-  const bool off = std::getenv("OAP_KMEANS_NO_LEAN_CHUNKED") != nullptr;
+  const bool off = knob_on("OAP_KMEANS_NO_LEAN_CHUNKED");
   return !off && req.lean && req.fast1 && !req.precise && !req.mindist_seeded && !req.bounds &&
          !req.delta && x.cols <= 128 && g.kpad > kmax && g.kpad <= 1024 &&
          kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
@@ -461,13 +417,9 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     a.ximg = req.ximg;
     a.img_beta = req.img_beta;
     a.img_mode = req.img_mode;
-    a.img_rows = req.img_mode == 2 ? req.img_rows : nullptr;
-    a.img_row_count = req.img_mode == 2 ? req.img_row_count : nullptr;
     a.img_scan_xnorm = req.img_mode == 2 ? req.img_scan_xnorm : nullptr;
     a.img_scan_drift = req.img_mode == 2 ? req.img_scan_drift : nullptr;
     a.img_scan_pruned = req.img_mode == 2 ? req.img_scan_pruned : nullptr;
-    a.img_movers = req.img_mode == 2 && req.img_scan_xnorm && req.img_movers;
-    a.img_mover_list = req.img_mover_list;
     a.sq_slab = req.sq_slab;
     a.bound_flag = req.bound_flag;
     a.bound_inf = req.bound_inf;
@@ -487,15 +439,15 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
                                 : "lean_fp16";
     const int lv = lean_variant(x.cols, a.kpad);
     const int lw = kern::kmeans_lloyd_waves(lv);
-    const bool img_k = req.img_kernel >= 0 ? req.img_kernel == 1 : img_kernel_default();
-    // (variants 3 / 10 have no image branch: their img_mode 3 would not be a fallback only)
-    if (req.img_mode == 2 && img_k && lv != 3 && lv != 10 &&
-        kern::kmeans_lean_img_supported(x.cols, g.k, lw, a.img_scan_xnorm != nullptr,
-                                        a.img_movers)) {
-      const int cfg = req.img_cfg >= 0                         ? req.img_cfg
-                      : a.img_scan_xnorm && scan_cfg_default() >= 0 ? scan_cfg_default()
-                                                                    : img_cfg_default();
-      if (a.img_scan_xnorm && req.img_gate && !a.img_movers) {
+    const bool img_k = req.img_kernel != 0;
+    if (req.img_mode == 2 && img_k &&
+        kern::kmeans_lean_img_supported(x.cols, g.k, lw, a.img_scan_xnorm != nullptr)) {
+      // configurations: 0 for row-scan passes (the scan's prefetched bounds fit the non-pipelined
+      // loop's registers; the pipelined one spills 64 B/lane, 4.66 vs 5.14 ms/step), 1 (the
+      // pipelined chunk loop) for dense passes
+      const int dense_cfg = req.img_cfg >= 0 ? req.img_cfg : 1;
+      const int cfg = req.img_cfg >= 0 ? req.img_cfg : a.img_scan_xnorm ? 0 : 1;
+      if (a.img_scan_xnorm && req.img_gate) {
         // the scan pass and the dense pass, one of which runs (the device gate)
         kern::KMeansAssignArgs as = a;
         as.img_gate = req.img_gate;
@@ -507,8 +459,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
         ad.img_scan_pruned = nullptr;
         ad.img_gate = req.img_gate;
         ad.img_gate_on = 0;
-        kern::kmeans_lean_img(ad, grid, lw, req.img_cfg >= 0 ? req.img_cfg : img_cfg_default(),
-                              s);
+        kern::kmeans_lean_img(ad, grid, lw, dense_cfg, s);
       } else {
         kern::kmeans_lean_img(a, grid, lw, cfg, s);
       }
@@ -517,16 +468,13 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
         f.img_mode = 3;
         kern::kmeans_lloyd(f, grid, lv, s);
       }
-      t_assign_path = a.img_movers       ? "lean_img_kernel_delta_rowscan_movers"
-                      : a.img_scan_xnorm && req.img_gate
+      t_assign_path = a.img_scan_xnorm && req.img_gate
                           ? "lean_img_kernel_delta_fused_rowscan_gated"
                       : a.img_scan_xnorm ? "lean_img_kernel_delta_fused_rowscan"
-                      : a.img_rows     ? "lean_img_kernel_delta_rowscan"
-                      : req.tile_list  ? "lean_img_kernel_delta_scan"
-                                       : "lean_img_kernel_delta";
+                      : req.tile_list    ? "lean_img_kernel_delta_scan"
+                                         : "lean_img_kernel_delta";
     } else {
-      OAP_CHECK(!a.img_rows && !a.img_scan_xnorm,
-                "kmeans: a row-list / row-scan image pass needs the image kernel");
+      OAP_CHECK(!a.img_scan_xnorm, "kmeans: a row-scan image pass needs the image kernel");
       kern::kmeans_lloyd(a, grid, lv, s);
     }
     if (req.skip_exact) return 0;
@@ -542,8 +490,6 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
     b.tile_list = nullptr;
     b.tile_count = nullptr;
     b.xnorm = nullptr;
-    b.img_rows = nullptr;
-    b.img_row_count = nullptr;
     b.img_scan_xnorm = nullptr;
     b.img_scan_drift = nullptr;
     b.img_scan_pruned = nullptr;
@@ -555,7 +501,7 @@ int gpu_assign(Context& ctx, const DenseTable& x, const GpuCenters& g, const Ass
   }
   if (x.cols > 128 && x.rows > 0 && req.fast1 && !req.precise && !req.mindist_seeded &&
       !req.delta && kern::kmeans_wide_supported(x.cols, g.k) &&
-      !std::getenv("OAP_KMEANS_NO_WIDE")) {
+      !knob_on("OAP_KMEANS_NO_WIDE")) {
     // ---- wide rows on MFMA (kmeans_wide.hip): tier-1 labels + exact re-decision, then the
     // label-driven accumulation and (when asked) the per-row cost
     Buffer lab, dbuf;
@@ -818,7 +764,7 @@ void check_gpu_table(const DenseTable& x) {
 // 133 -> 85 ms.  Both are exact-argmin paths; per-row fp32 distances may differ in the last
 // ulp between them (direct vs expanded form), which can move a Bernoulli draw, so
 // OAP_KMEANS_INIT_PRECISE=1 keeps the previous path for A/B runs.
-bool init_fast() { return std::getenv("OAP_KMEANS_INIT_PRECISE") == nullptr; }
+bool init_fast() { return !knob_on("OAP_KMEANS_INIT_PRECISE"); }
 
 // Candidate sets beyond one LDS plan take super-chunks of at most 1024 candidates on the lean
 // pass (the centroid-chunked one where a super-chunk still exceeds the plan), the per-row exact
@@ -826,8 +772,9 @@ bool init_fast() { return std::getenv("OAP_KMEANS_INIT_PRECISE") == nullptr; }
 // bf16x3 tiers: config 5's ~2000-4000 candidates.  OAP_KMEANS_INIT_SUPER=0: the previous path.
 // (debug: =1 cost updates only, =2 candidate counts only)
 bool init_super(const DenseTable& x, int m, int which) {
-  const char* e = std::getenv("OAP_KMEANS_INIT_SUPER");
-  if (e && (*e == '0' || (*e == '1' && which != 1) || (*e == '2' && which != 2))) return false;
+  const std::string e = knob_str("OAP_KMEANS_INIT_SUPER");
+  if (!e.empty() && (e[0] == '0' || (e[0] == '1' && which != 1) || (e[0] == '2' && which != 2)))
+    return false;
   return init_fast() && x.cols <= 128 && x.rows > 0 &&
          int(round_up(size_t(m), 32)) > kern::kmeans_lds_kmax(x.cols, false) &&
          kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
@@ -1286,8 +1233,7 @@ struct HostMarks {
   std::chrono::steady_clock::time_point t0;
   std::string out;
   HostMarks() {
-    const char* e = std::getenv("OAP_KMEANS_HOST_MARKS");
-    on = e && *e == '1';
+    on = knob_on("OAP_KMEANS_HOST_MARKS");
     t0 = std::chrono::steady_clock::now();
   }
   void mark(const char* what) {
@@ -1476,7 +1422,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   req.counts = counts;
   req.cost_slab = slab.as<double>();
   req.refine_tiles = refine_d.as<u64>();
-  if (const char* e = std::getenv("OAP_KMEANS_CHUNK_DEFER")) req.defer = std::atoi(e) != 0;
+  if (!knob_str("OAP_KMEANS_CHUNK_DEFER").empty())
+    req.defer = knob_int("OAP_KMEANS_CHUNK_DEFER") != 0;
   // chunked (large-k) path: labels/mindist persist across iterations to seed the merge passes
   Buffer lab_keep, mind_keep;
   const bool chunked = x.cols <= 128 && g.kpad > kern::kmeans_lds_kmax(x.cols, p.precise);
@@ -1488,7 +1435,7 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   }
   // the centroid-chunked lean pass runs full passes (no pruning state)
   const bool lean_chunked =
-      chunked && !p.precise && g.kpad <= 1024 && !std::getenv("OAP_KMEANS_NO_LEAN_CHUNKED") &&
+      chunked && !p.precise && g.kpad <= 1024 && !knob_on("OAP_KMEANS_NO_LEAN_CHUNKED") &&
       kern::kmeans_lloyd_chunk_kmax(x.cols) >= 32 && kern::kmeans_exact_chunk_kmax(x.cols) >= 32;
   // pruning: per-row bounds (+ labels) persist across iterations, finalize reports the drift
   const bool prune = p.prune && !p.precise && x.cols <= 128 && x.rows > 0 && !lean_chunked;
@@ -1557,10 +1504,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // (a feature that is 0 in every initial center has bound 0, which every row would fail: the
   // check could only flag and restart, so such a fit takes the column maxima up front — the
   // rule fit_bounds evaluates then is the same on every engine)
-  const char* am_env = std::getenv("OAP_KMEANS_ABSMAX_PASS");
   double cb_min = std::numeric_limits<double>::infinity();
   for (int f = 0; f < d; ++f) cb_min = std::min(cb_min, cbound[f]);
-  const bool provisional = !p.absmax_pass && !(am_env && *am_env == '1') && delta_all &&
+  const bool provisional = !p.absmax_pass && !knob_on("OAP_KMEANS_ABSMAX_PASS") && delta_all &&
                            provisional_allowed(x.global_rows, d) && cb_min > 0.0 &&
                            x.dtype == DType::F32 && lean_applies(x, k, g.kpad, req);
   Buffer bflag_b, sq_slab_b;
@@ -1602,12 +1548,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // (headline data: tiles 0-13% prunable, rows up to 93%: profiles/r4/row_prune_potential.jsonl).
   // Bounds are then written by every pass.  The scan runs inside the image kernel (each wave
   // tests its own rows and queues the unpruned ones in LDS) where the kernel's LDS plan has room
-  // for it; OAP_KMEANS_ROW_SCAN=2 takes the separate scan kernel + row list through HBM instead,
-  // =0 the tile scan.
-  Buffer rlist_b, rpruned_b, scan_gate_b;
-  const char* rs_env = std::getenv("OAP_KMEANS_ROW_SCAN");
-  const bool row_scan = scan && !chunked && !(rs_env && *rs_env == '0');
-  bool row_scan_fused = row_scan && !(rs_env && *rs_env == '2');
+  // for it; knob OAP_KMEANS_ROW_SCAN=0 takes the tile scan.  (A separate scan kernel writing
+  // row lists through HBM cost more than it saved: profiles/r4/trace_bench_r4f_separate_scan.txt.)
+  Buffer rpruned_b, scan_gate_b;
+  const bool row_scan = scan && !chunked && knob_int("OAP_KMEANS_ROW_SCAN") != 0;
   if (row_scan) {
     rpruned_b = ctx.alloc(sizeof(u64));
     ctx.memset(rpruned_b.data(), 0, sizeof(u64), s);
@@ -1630,7 +1574,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   }
   if (x.rows > 0 && (req.defer_rows || lean_chunked)) {
     // [deferred rows, moved rows staged, passes that read the operand image]
-    // (+ [3] rows into the mover stage, [4] rows it listed for the full pass)
     ldstat_b = ctx.alloc(5 * sizeof(u64));
     ldstat_h = ctx.alloc_pinned(5 * sizeof(u64));
     ctx.memset(ldstat_b.data(), 0, 5 * sizeof(u64), s);
@@ -1662,10 +1605,10 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     init_cmax = std::max(init_cmax, std::sqrt(s2));
   }
   {
-    const char* e = std::getenv("OAP_KMEANS_IMAGE");
     const size_t ib = kern::kmeans_lloyd_image_bytes(x.rows, x.cols);
     DeviceArena* ar = ctx.backend() == Backend::GPU ? ctx.arena() : nullptr;
-    if (delta && req.defer_rows && x.dtype == DType::F32 && ib > 0 && !(e && *e == '0') && ar &&
+    if (delta && req.defer_rows && x.dtype == DType::F32 && ib > 0 &&
+        knob_int("OAP_KMEANS_IMAGE") != 0 && ar &&
         ar->used() + ib + ar->budget() / 4 <= ar->budget()) {
       img_b = ctx.alloc(ib);
       img_beta_b = ctx.alloc(sizeof(float) * 4);
@@ -1675,12 +1618,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   // (row-scan mode needs the image and the image kernel at this shape; rank-uniform in practice:
   // every rank decides from the same shape, and a rank without rows scans nothing)
   bool row_scan_ok = false;
-  if (row_scan && img_b.data() && img_kernel_default()) {
-    const int lv = lean_variant(d, g.kpad);
-    const int lw = kern::kmeans_lloyd_waves(lv);
-    row_scan_ok = lv != 3 && lv != 10 && kern::kmeans_lean_img_supported(d, k, lw);
-    row_scan_fused =
-        row_scan_fused && row_scan_ok && kern::kmeans_lean_img_supported(d, k, lw, true);
+  if (row_scan && img_b.data()) {
+    const int lw = kern::kmeans_lloyd_waves(lean_variant(d, g.kpad));
+    row_scan_ok = kern::kmeans_lean_img_supported(d, k, lw, true);
   }
   // the same decision for the whole world (it changes which iterations compute a cost and
   // scan tiles, and so which collectives run): every rank with rows must have the image and the
@@ -1691,32 +1631,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   const bool row_scan_all = scan_all && !chunked && rs_vote > 0.5 &&
                             (row_scan_ok || x.rows == 0 || !comm.trivial());
   row_scan_ok = row_scan_ok && row_scan_all;
-  row_scan_fused = row_scan_fused && row_scan_ok;
-  // the mover stage of the fused row scan (OAP_KMEANS_MOVERS=1: on; a local choice — it
-  // changes no collective and no result, only which rows take the full pass).  Off by default:
-  // at the headline it bounds 81M rows a pass and lists 26M for the full pass (64% of the rows
-  // pruned instead of 25%), but the extra image read of every bounded row and the looser bounds
-  // it leaves make the fit slower: 5.52 vs 4.38 ms/step (profiles/r5/bench_movers_r5f.json)
-  {
-    const char* e = std::getenv("OAP_KMEANS_MOVERS");
-    const int lw = kern::kmeans_lloyd_waves(lean_variant(d, g.kpad));
-    req.img_movers = row_scan_fused && (e && *e == '1') &&
-                     kern::kmeans_lean_img_supported(d, k, lw, true, true);
-  }
-  Buffer mlist_b;  // the mover stage's per-wave row lists ([grid][seg_cap], like the deferrals)
-  if (req.img_movers) {
-    const int64_t scap = kern::kmeans_lloyd_seg_cap(
-        x.rows, lgrid, kern::kmeans_lloyd_waves(lean_variant(d, g.kpad)));
-    mlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(scap) + 64);
-    req.img_mover_list = mlist_b.as<int32_t>();
-  }
-  if (row_scan_ok && !row_scan_fused)
-    rlist_b = ctx.alloc(sizeof(int32_t) * size_t(lgrid) * size_t(ltiles) * 32 +
-                        sizeof(unsigned) * size_t(lgrid) + 64);
-  unsigned* rcount =
-      rlist_b.data()
-          ? reinterpret_cast<unsigned*>(rlist_b.as<int32_t>() + size_t(lgrid) * size_t(ltiles) * 32)
-          : nullptr;
   // with the adaptive scan off, full passes write the per-row bounds (8 B/row) only where a
   // following iteration may scan, and the per-tile max |x|^2 (constant) once
   float* const bounds_full = req.bounds;
@@ -1889,32 +1803,22 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
       // row-level scan ahead of an image pass (the drift finalize wrote for the previous step)
       const bool row_scan_it = row_scan_ok && delta_it && it > 1 && img_ready && !cost_it &&
                                req.fast1 && !req.tile_list;
-      req.img_rows = nullptr;
-      req.img_row_count = nullptr;
       req.img_scan_xnorm = nullptr;
       req.img_scan_drift = nullptr;
       req.img_scan_pruned = nullptr;
       req.img_gate = nullptr;
-      if (row_scan_it && row_scan_fused) {
+      if (row_scan_it) {
         OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
         req.img_scan_xnorm = xnorm_full;
         req.img_scan_drift = drift_b.as<float>();
         req.img_scan_pruned = rpruned_b.as<u64>();
-        if (p.scan_min_prune > 0.0 && !req.img_movers) {
+        if (p.scan_min_prune > 0.0) {
           // scan or dense, decided on the device from a sample of the rows
           kern::kmeans_scan_decide(x.rows, k, d, bounds_full, req.labels, xnorm_full,
                                    drift_b.as<float>(), g.cstat.as<float>(),
                                    float(p.scan_min_prune), scan_gate_b.as<int>(), halt, s);
           req.img_gate = scan_gate_b.as<int>();
         }
-      } else if (row_scan_it) {
-        OAP_CHECK(xnorm_ready && bounds_full, "kmeans row scan before any full pass");
-        kern::kmeans_lean_scan_rows(x.rows, k, d, lgrid, bounds_full, req.labels, xnorm_full,
-                                    drift_b.as<float>(), drift_b.as<float>() + k,
-                                    g.cstat.as<float>(), rlist_b.as<int32_t>(), rcount,
-                                    rpruned_b.as<u64>(), s, halt);
-        req.img_rows = rlist_b.as<int32_t>();
-        req.img_row_count = rcount;
       }
       // operand image: written by the first full lean pass, read by costless delta passes
       req.ximg = img_b.data();
@@ -2181,8 +2085,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     Buffer md;  // outlives the copy_to_host below (which synchronizes the stream)
     // (rank-uniform: the dtype, the shape and the env are; the helper's inputs are global)
     double c_stats = 0.0;
-    const char* fc_env = std::getenv("OAP_KMEANS_FINAL_COST");  // "rows": the per-row pass
-    const bool try_stats = delta_all && x.dtype == DType::F32 && !(fc_env && *fc_env == 'r');
+    // (knob OAP_KMEANS_FINAL_COST=rows: the per-row pass)
+    const bool try_stats =
+        delta_all && x.dtype == DType::F32 && knob_str("OAP_KMEANS_FINAL_COST")[0] != 'r';
     double fused_T[2] = {0.0, 0.0};  // {sum |x|^2 of the local rows, its relative bound}
     const bool fused = sq_ready || x.rows == 0;
     if (sq_ready) {
@@ -2257,8 +2162,6 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   if (ldstat_b.data()) {
     u64 dr[5] = {0, 0, 0, 0, 0};
     ctx.copy_to_host(dr, ldstat_b.data(), 5 * sizeof(u64), s);
-    res.mover_rows = static_cast<int64_t>(dr[3]);
-    res.mover_listed_rows = static_cast<int64_t>(dr[4]);
     res.deferred_rows = static_cast<int64_t>(dr[0]);
     res.moved_rows = static_cast<int64_t>(dr[1]) + cmoved;
     res.image_passes = static_cast<int>(dr[2]);  // counted by the passes that read the image

@@ -74,8 +74,6 @@ struct KMeansResult {
   int64_t moved_rows = 0;     // rows the lean delta passes moved between clusters
   int64_t pruned_rows = 0;    // rows the row-level scan proved unchanged (summed over passes)
   int image_passes = 0;       // lean passes that took their operands from the fp16 row image
-  int64_t mover_rows = 0;          // rows the row scan sent to the mover stage (summed)
-  int64_t mover_listed_rows = 0;   // of those, rows the mover bound left to the full pass
   int64_t image_bytes = 0;    // HBM of that image (0: not allocated)
   std::string assign_path = "cpu";  // the distance kernel path of the last iteration (GPU)
   // how a last assignment that computed no cost in its pass got one: "stats" (from the fit's

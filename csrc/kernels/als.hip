@@ -35,6 +35,7 @@
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 namespace kern {
@@ -572,11 +573,7 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
   a.implicit = s.implicit ? 1 : 0;
   a.dst = s.dst;
   a.fail = s.fail;
-  static const int ablate = [] {
-    const char* e = std::getenv("OAP_ALS_ABLATE");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.ablate = ablate;
+  a.ablate = int(knob_int("OAP_ALS_ABLATE"));
   // rows of the low-rank path (the tail of short_rows) are solved by als_solve_lowrank
   const int64_t n_direct = (s.lr_off[4] > s.lr_off[0]) ? s.lr_off[0] : s.n_short;
   if (n_direct > 0) {
@@ -585,10 +582,7 @@ void run(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
     a.nrows = n_direct;
     a.queue = s.queue;
     // split-fp16 Gramian for the direct rows too (OAP_ALS_DIRECT_X3=0: exact-fp32 products)
-    static const bool direct_x3 = [] {
-      const char* e = std::getenv("OAP_ALS_DIRECT_X3");
-      return !e || std::atoi(e) != 0;
-    }();
+    const bool direct_x3 = knob_int("OAP_ALS_DIRECT_X3") != 0;
     a.absmax = direct_x3 ? s.absmax : nullptr;
     // the longest rows on the split-fp16 Gramian, the short tail on the fp32 one at two waves
     // per SIMD (its rows are Cholesky-bound: 30 vs 38 ms per user half at 1B ratings)

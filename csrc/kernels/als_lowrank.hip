@@ -31,6 +31,7 @@
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 namespace kern {
@@ -331,15 +332,9 @@ void lowrank_classes(const AlsSolveArgs& s, int num_cus, hipStream_t st) {
   a.alpha = s.alpha;
   a.lambda = s.lambda;
   a.fail = s.fail;
-  static const int ablate = [] {
-    const char* e = std::getenv("OAP_ALS_ABLATE");
-    return e ? std::atoi(e) : 0;
-  }();
-  a.ablate = ablate;
-  static const int lr3_occ = [] {  // waves/SIMD of the 33-48-rating class (timing experiments)
-    const char* e = std::getenv("OAP_ALS_LR3_OCC");
-    return e ? std::atoi(e) : 0;
-  }();
+  a.ablate = int(knob_int("OAP_ALS_ABLATE"));
+  // waves/SIMD of the 33-48-rating class (timing experiments)
+  const int lr3_occ = int(knob_int("OAP_ALS_LR3_OCC"));
   // class j: rows [lr_off[j], lr_off[j+1]) of short_rows hold 16 (4 - j) - 15 .. 16 (4 - j) ratings
   for (int j = 0; j < 4; ++j) {
     const int64_t b = s.lr_off[j], e = s.lr_off[j + 1];
@@ -553,10 +548,7 @@ void als_rotate(const float* in, const int32_t* in_rows, float* out, const int32
   if (n <= 0) return;
   OAP_CHECK(ld % 16 == 0 && ld >= 16 && ld <= 128,
             "als_rotate: ld must be 16..128, multiple of 16");
-  static const bool valu = [] {
-    const char* e = std::getenv("OAP_ALS_ROTATE_VALU");
-    return e && *e == '1';
-  }();
+  const bool valu = knob_on("OAP_ALS_ROTATE_VALU");
   if (!valu) {
     switch (ld / 16) {
       case 1: launch_rotate_mfma<1>(in, in_rows, out, out_rows, n, R, num_cus, s); return;

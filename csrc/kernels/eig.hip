@@ -22,6 +22,7 @@
 
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 namespace kern {
@@ -779,10 +780,7 @@ size_t eig_tridiag_lds_bytes(int n, int G) {
 int eig_tridiag_grid(int n, int num_cus) {
   // one workgroup per CU (cooperative: all co-resident), at most n of them; fewer workgroups
   // (OAP_EIG_GRID) trade fused-pass parallelism for barrier traffic
-  static const int cap = [] {
-    const char* e = std::getenv("OAP_EIG_GRID");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int cap = int(knob_int("OAP_EIG_GRID"));
   int g = n < num_cus ? n : num_cus;
   if (cap > 0 && cap < g) g = cap;
   while (g > 1 && (n + g - 1) / g > kEigMaxRows) ++g;  // (cannot exceed num_cus for n <= 2048)

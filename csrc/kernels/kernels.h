@@ -117,10 +117,6 @@ struct KMeansAssignArgs {
   // row's previous label.
   const int32_t* row_list = nullptr;
   const unsigned* row_count = nullptr;  // [grid][16]: rows per sub-segment
-  // Row-list image pass (kmeans_lean_img): the rows the row scan left, [grid][32 tiles/block]
-  // in row order, count [grid] (kmeans_lean_scan_rows)
-  const int32_t* img_rows = nullptr;
-  const unsigned* img_row_count = nullptr;
   // Row-scan image pass (kmeans_lean_img, fused): the kernel applies the row scan's Hamerly test
   // to every row itself and runs only the rows it cannot prune.  img_scan_xnorm: per-tile max
   // |x|^2 (set: the fused scan is on); img_scan_drift: the centers' drift [k] and its maximum at
@@ -128,11 +124,6 @@ struct KMeansAssignArgs {
   const float* img_scan_xnorm = nullptr;
   const float* img_scan_drift = nullptr;
   unsigned long long* img_scan_pruned = nullptr;
-  // row-scan image passes: the mover stage (kmeans_lean_img.hip RM 3) — rows the scan cannot
-  // prune are first bounded against the 32 centers that moved most (one MFMA chunk); only the
-  // rows that bound cannot decide take the full pass
-  bool img_movers = false;
-  int32_t* img_mover_list = nullptr;  // [grid][row_seg_cap] rows (the mover stage's lists)
   int64_t row_seg_cap = 0;
   int row_subs = 1;  // sub-segments per workgroup segment (each row_seg_cap / row_subs long)
   // Lean tier-1 kernel output: rows whose tier-1 top-2 gap is inside the tier's error bound are
@@ -191,13 +182,10 @@ int kmeans_lloyd_grid(int64_t n, int num_cus);
 // Waves per workgroup of a lean-kernel variant; per-workgroup capacity of its deferral list
 // (rows; `waves` sub-segments of seg_cap / waves each, counts [grid][16]).
 int kmeans_lloyd_waves(int variant);
-// Chunks of 32 centroids the register-resident-plane variant (11) holds at width d (0: none).
-int kmeans_lloyd_rch(int d);
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves);
 // One pass: rows whose tier-1 answer is sure are finished (labels / mindist / bounds / cost /
 // fixed-point statistics, delta mode over tile_list); the others go to a.defer_rows.  variant
-// selects the workgroup shape (0: 16 waves; tuning: 1-3).  Writes `grid`
-// cost partials.
+// selects the workgroup shape (6: 16 waves, 8: 12 waves).  Writes `grid` cost partials.
 int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s);
 // Bytes of the lean kernel's fp16 operand image of n f32 rows of width d (0: not applicable).
 size_t kmeans_lloyd_image_bytes(int64_t n, int d);
@@ -209,13 +197,8 @@ size_t kmeans_lloyd_image_bytes(int64_t n, int d);
 // the refined tier-1 deferral test of the image passes (kmeans_frag.h refined_tt): on unless
 // OAP_KMEANS_REFINE=0 (timing A/B; labels and statistics are the same either way)
 bool kmeans_refine_default();
-bool kmeans_lean_img_supported(int d, int k, int waves, bool scan = false, bool movers = false);
+bool kmeans_lean_img_supported(int d, int k, int waves, bool scan = false);
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s);
-// Row-level bound scan for the image passes: every row of lean workgroup b's range gets the
-// Hamerly test of kmeans_lean_scan (u + drift[label] against l - max drift, with the tile's
-// max |x|^2 in the margin); pruned rows have their bounds advanced in place (no write once no
-// center moves), the others are appended in row order to b's segment of row_list
-// ([lean_grid][32 tiles_per_block], count row_count[b]).  *pruned_rows (optional) counts.
 // The scan-vs-dense choice of a row-scan image pass, on the device: the row scan's own Hamerly
 // test on an even sample of the rows (bounds, labels, the drift the last finalize wrote); *gate
 // = 1 (scan) when at least min_frac of the sample is prunable, else 0 (the dense pipelined pass,
@@ -224,11 +207,6 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
 void kmeans_scan_decide(int64_t n, int k, int d, const float* bounds, const int32_t* labels,
                         const float* xnorm, const float* drift, const float* cstat,
                         float min_frac, int* gate, const int* halt, hipStream_t s);
-void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
-                           const int32_t* labels, const float* xnorm, const float* drift,
-                           const float* drift_max, const float* cstat, int32_t* row_list,
-                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s,
-                           const int* halt = nullptr);
 // Largest centroid chunks (multiples of 32) of the chunked lean pass at dimension d: the lean
 // kernel's fp16 plane and the exact kernel's fp32 centers (0: d not supported).
 int kmeans_lloyd_chunk_kmax(int d);

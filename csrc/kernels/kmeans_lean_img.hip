@@ -35,6 +35,7 @@
 
 #include "kernels/kmeans_frag.h"
 #include "kernels/kmeans_internal.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 namespace kern {
@@ -67,9 +68,7 @@ struct ImgArgs {
   const unsigned* tile_count;
   int32_t* defer_rows;
   unsigned* defer_row_count;
-  u64* stat;  // optional [deferred rows, moved rows, image passes, mover rows, mover-listed rows]
-  const int32_t* rows;  // row-list passes: [grid][32 tiles_per_block] rows in order, count [grid]
-  const unsigned* row_count;
+  u64* stat;  // optional [deferred rows, moved rows, image passes]
   // row-scan passes: per-tile max |x|^2 (global tile index), the centers' drift [k] and its
   // maximum at [k], and the counter of pruned rows
   const float* scan_xnorm;
@@ -77,27 +76,19 @@ struct ImgArgs {
   u64* pruned;
   int64_t n, seg_cap, tiles_per_block;
   int ld, d, k, kpad;
-  int movers;  // row-scan passes: the mover stage (RM 3)
   int refine;  // the refined deferral test (kmeans_frag.h refined_tt; OAP_KMEANS_REFINE=0: off)
-  int32_t* mlist;  // RM 3: per-wave lists of the rows the mover stage left, [grid][seg_cap]
   const int* halt;  // batched fits: set once the fit converged (the pass then does nothing)
   const int* gate;  // optional: the pass runs only when *gate == gate_on (kmeans_scan_decide)
   int gate_on;
 };
 
 struct ImgSmem {
-  size_t plane, sc, acc, cnt, mv, dr, ring, mp, mvi, slot, ringb, total;
+  size_t plane, sc, acc, cnt, mv, dr, ring, total;
 };
-
-// Mover stage (RM 3): the 32 centers that moved most since the last pass, one fp16 chunk
-constexpr int kMovers = 32;
 
 // fp16 plane; fixed-point accumulator rows of DP + 1 doubles (odd: conflict-free ds_add_f64; the
 // padded features add zeros into their own columns, so the moved-row adds need no predicate)
-// (mover passes: accumulator rows of d | 1 doubles — still odd — with predicated pad features, to
-// make room for the mover plane and the second ring)
-__host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, bool scan,
-                                            bool movers = false, int d = 0) {
+__host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, bool scan) {
   ImgSmem m;
   size_t off = 0;
   m.plane = 0;
@@ -105,7 +96,7 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, 
   m.sc = off;  // scales [dp], then per-wave 2 max |e_c| (kmdev::plane_resid2)
   off = round16(off + size_t(dp + kmdev::kResidSlots) * 4);
   m.acc = off;
-  off = round16(off + size_t(k) * size_t(movers ? (d | 1) : dp + 1) * 8);
+  off = round16(off + size_t(k) * size_t(dp + 1) * 8);
   m.cnt = off;
   off = round16(off + size_t(k) * 4);
   m.mv = off;
@@ -114,15 +105,6 @@ __host__ __device__ inline ImgSmem img_plan(int dp, int kpad, int k, int waves, 
   off = scan ? round16(off + size_t(k) * 4) : off;
   m.ring = off;
   off += scan ? size_t(waves) * kRing * 4 : 0;
-  off = round16(off);
-  m.mp = off;  // mover plane [32][stride] fp16, then its center indices, the center -> slot map
-  off += movers ? size_t(kMovers) * stride_bf16(dp) * 2 : 0;
-  off = round16(off);
-  m.mvi = off;
-  off += movers ? size_t(kMovers + 4) * 4 : 0;
-  m.slot = off;
-  off += movers ? size_t(k) * 4 : 0;
-  m.ringb = off;
   m.total = round16(off);
   return m;
 }
@@ -143,19 +125,20 @@ __device__ inline void split_h(float v, _Float16& hi, _Float16& lo) {
   lo = static_cast<_Float16>(v - static_cast<float>(hi));
 }
 
-// CFG: bit 0 software-pipelined chunk loop; bit 1 operands two tiles ahead (else one); bits 2+
-// timing ablations (probe builds only): 4 no epilogue, 8 no MFMA, 16 no plane reads, 32 no image
-// loads, 64 no moved-row accumulation, 128 no per-row stores.
-// RM (row mode): 0 dense tiles of 32 consecutive rows; 1 (LIST) 32 consecutive entries of this
-// workgroup's row list (the rows kmeans_lean_scan_rows could not prune), gathered from the
-// row-major image; 2 (SCAN) the fused row scan: 32 consecutive entries of the wave's LDS ring.
+// CFG: 1 software-pipelined chunk loop (dense passes), 0 not (row-scan passes); operands one
+// tile ahead.  (The timing ablation builds of rounds 3-5 — no epilogue, MFMA, plane reads, image
+// loads, accumulation or stores; operands two tiles ahead — live in git history.)
+// RM (row mode): 0 dense tiles of 32 consecutive rows; 2 (SCAN) the fused row scan: 32
+// consecutive entries of the wave's LDS ring (the rows its Hamerly test cannot prune).
+// (Measured dead ends kept in git history only: RM 1, a separate row-scan kernel writing row
+// lists through HBM, 5.30 vs 5.06 ms/step; RM 3, a mover stage against the 32 centers that moved
+// most, 5.52 vs 4.38 ms/step.)
 template <int KS, int WAVES, int CFG, int RM>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) {
-  constexpr bool LIST = RM == 1, SCAN = RM == 2, MOV = RM == 3;
+  constexpr bool SCAN = RM == 2;
+  static_assert(RM == 0 || RM == 2, "row modes: dense (0) or fused row scan (2)");
   constexpr bool PIPE = (CFG & 1) != 0;
-  constexpr int PD = (LIST || !(CFG & 2)) ? 1 : 2;
-  constexpr bool NO_EPI = (CFG & 4) != 0, NO_MFMA = (CFG & 8) != 0, NO_LDS = (CFG & 16) != 0;
-  constexpr bool NO_LOAD = (CFG & 32) != 0, NO_ACC = (CFG & 64) != 0, NO_ST = (CFG & 128) != 0;
+  static_assert(CFG == 0 || CFG == 1, "configurations: 0, 1 (pipelined chunk loop)");
   constexpr int DP = 16 * KS, NT = WAVES * 64, RS = DP + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (a.halt && *a.halt) return;
@@ -164,8 +147,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const float alpha = a.img_beta[0];
   if (!(alpha * cmax <= 512.f)) return;  // (kmeans_lloyd img_mode 3 takes this pass)
   const int k = a.k, kpad = a.kpad, d = a.d;
-  const ImgSmem L = img_plan(DP, kpad, k, WAVES, SCAN || MOV, MOV, d);
-  const int rs = MOV ? (d | 1) : RS;  // accumulator row stride (doubles)
+  const ImgSmem L = img_plan(DP, kpad, k, WAVES, SCAN);
+  constexpr int rs = RS;  // accumulator row stride (doubles)
   const int sb = stride_bf16(DP);
   _Float16* ph = reinterpret_cast<_Float16*>(smem + L.plane);
   float* sc_l = reinterpret_cast<float*>(smem + L.sc);
@@ -203,42 +186,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   for (int i = tid; i < k * rs; i += NT) acc_l[i] = 0.0;
   for (int i = tid; i < k; i += NT) cnt_l[i] = 0;
   float* dr_l = reinterpret_cast<float*>(smem + L.dr);
-  if constexpr (SCAN || MOV)
+  if constexpr (SCAN)
     for (int i = tid; i < k; i += NT) dr_l[i] = a.drift[i];
   __syncthreads();
-  // ---- mover stage (RM 3): the kMovers centers with the largest drift (ties: lower index) get
-  // their own fp16 chunk; the largest drift among the others bounds how far every other center
-  // moved.  On overlapping clusters a few centers move a lot while the median barely moves
-  // (headline: max 12-24, median 0.02-0.4 after the first iterations), so a row whose Hamerly
-  // test fails on the largest drift is usually decided by its distance to those few.
-  _Float16* mp = reinterpret_cast<_Float16*>(smem + L.mp);
-  int* mvi = reinterpret_cast<int*>(smem + L.mvi);
-  int* slot_l = reinterpret_cast<int*>(smem + L.slot);
-  if constexpr (MOV) {
-    for (int i = tid; i < k; i += NT) {
-      const float di = dr_l[i];
-      int rk = 0;
-      for (int j = 0; j < k; ++j) {
-        const float dj = dr_l[j];
-        rk += (dj > di || (dj == di && j < i)) ? 1 : 0;
-      }
-      slot_l[i] = rk < kMovers ? rk : -1;
-      if (rk < kMovers) mvi[rk] = i;
-      if (rk == kMovers) mvi[kMovers] = __float_as_int(di);  // the largest non-mover drift
-    }
-    if (tid == 0 && k <= kMovers) mvi[kMovers] = 0;  // (every center is a mover)
-    for (int i = k + tid; i < kMovers; i += NT) mvi[i] = kpad - 1;  // (a padded plane row)
-    __syncthreads();
-    for (int idx = tid; idx < kMovers * DP; idx += NT) {
-      const int m = idx / DP, f = idx - m * DP;
-      const int c = mvi[m];
-      mp[m * sb + f] = (m < k) ? ph[c * sb + f]
-                               : static_cast<_Float16>(f == DP - 4 ? 60000.f
-                                                       : (f >= DP - 2 ? kBias : 0.f));
-    }
-    __syncthreads();
-  }
-
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   int2* mv_l = reinterpret_cast<int2*>(smem + L.mv) + wave * kMv;
@@ -259,12 +209,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   const bool listed = a.tile_list != nullptr;
   const int64_t T = a.tiles_per_block;
   const int64_t t0 = int64_t(blockIdx.x) * T;
-  const unsigned lcnt = LIST ? a.row_count[blockIdx.x] : 0u;  // (row-list passes)
-  const int32_t* rseg = LIST ? a.rows + blockIdx.x * (T * 32) : nullptr;
   const int64_t dense_pos = t0 < ntiles_all ? (ntiles_all - t0 < T ? ntiles_all - t0 : T) : 0;
-  const int64_t npos = LIST     ? (int64_t(lcnt) + 31) / 32
-                       : listed ? int64_t(a.tile_count[blockIdx.x])
-                                : dense_pos;
+  const int64_t npos = listed ? int64_t(a.tile_count[blockIdx.x]) : dense_pos;
   const int32_t* seg = listed ? a.tile_list + blockIdx.x * T : nullptr;
   constexpr int64_t stride = WAVES;
   const int64_t sub_cap = a.seg_cap / WAVES;
@@ -297,18 +243,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
   // resource over this workgroup's rows: a 32-bit offset per lane instead of a 64-bit pointer
   // (the pipelined loop has no VGPRs to spare)
   auto load_img_row = [&](int64_t row, f16x8(&dst)[KS]) OAP_AI {
-    if constexpr (!NO_LOAD) {
-      const uint32_t off = uint32_t(row - row0) * uint32_t(32 * KS) + 16u * uint32_t(h);
+    const uint32_t off = uint32_t(row - row0) * uint32_t(32 * KS) + 16u * uint32_t(h);
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        dst[s] = __builtin_bit_cast(
-            f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_img, off + 32u * s, 0, 0));
-    }
-  };
-  // row-list passes: this lane's row of list tile q (-1 past the count)
-  auto rid_of = [&](int64_t q) OAP_AI -> int32_t {
-    const int64_t i = q * 32 + r;
-    return i < int64_t(lcnt) ? rseg[i] : -1;
+    for (int s = 0; s < KS; ++s)
+      dst[s] = __builtin_bit_cast(
+          f16x8, __builtin_amdgcn_raw_buffer_load_b128(rs_img, off + 32u * s, 0, 0));
   };
 
   // ---- moved rows: staged (row, new | old << 16) in the wave's LDS slots, accumulated 32 at a
@@ -353,7 +292,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
         const float scv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
         for (int j = 0; j < 8; ++j) {  // (features >= d: scale 0, a zero into a pad column)
-          if (MOV && 16 * s + 8 * h + j >= d) continue;  // (rows of d | 1)
           const double v = static_cast<double>(rintf(xv[s][j] * scv[j]));
           atomicAdd(ap + 16 * s + j, v);
           atomicAdd(aq + 16 * s + j, -v);
@@ -372,20 +310,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   };
 
-  // ---- one tile: X holds its operands (landed or in flight), pf receives tile pos + PD stride
+  // ---- one tile: X holds its operands (landed or in flight), pf receives tile pos + stride
   // row: this lane's row (-1: none); pf_row: the row whose operands go to pf (a real row)
-  // rid_next: row-list passes — the list entry of tile pos + 2 stride, loaded here (ahead of
-  // this tile's own loads, so waiting for it never waits for them)
   auto body = [&](auto pf_t, const int64_t pos, const int64_t row, const int64_t pf_row,
-                  int32_t* rid_next, f16x8(&X)[KS], f16x8(&pf)[KS]) OAP_AI {
+                  f16x8(&X)[KS], f16x8(&pf)[KS]) OAP_AI {
     constexpr bool PFON = decltype(pf_t)::value;  // (false: no next-tile prefetch)
-    if constexpr (!NO_ACC) {
-      if (n_mv >= 32) {  // (before this tile's loads are issued)
-        flush(n_mv);
-        n_mv -= 32;
-      }
+    if (n_mv >= 32) {  // (before this tile's loads are issued)
+      flush(n_mv);
+      n_mv -= 32;
     }
-    if constexpr (LIST) *rid_next = rid_of(pos + 2 * stride);
     const bool valid = pos < npos && row >= 0 && row < a.n;
     const uint32_t roff = uint32_t(row - row0);
     int old = buf_load_b32(rs_lab, roff * 4, valid);
@@ -397,39 +330,21 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     const float nx2_s = h ? mine : other;
     int k1 = 0x7fffffff, k2 = 0x7fffffff;
     auto frags = [&](int c0, f16x8(&av)[KS]) OAP_AI {
-      if constexpr (NO_LDS) {
+      const _Float16* ap = ph + size_t(c0 + r) * sb + 8 * h;
 #pragma unroll
-        for (int s = 0; s < KS; ++s) av[s] = X[(s + 1) % KS];
-      } else {
-        const _Float16* ap = ph + size_t(c0 + r) * sb + 8 * h;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
-      }
+      for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
     };
     auto chain = [&](const f16x8(&av)[KS], f32x16& acc) OAP_AI {
-      if constexpr (NO_MFMA) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], X[0], f32x16{}, 0, 0, 0);
 #pragma unroll
-        for (int q = 0; q < 4 && q < KS; ++q) {
-          const f32x4 w = __builtin_bit_cast(f32x4, av[q]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[4 * q + e] = w[e];
-        }
-      } else {
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], X[0], f32x16{}, 0, 0, 0);
-#pragma unroll
-        for (int s = 1; s < KS; ++s)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], X[s], acc, 0, 0, 0);
-      }
+      for (int s = 1; s < KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], X[s], acc, 0, 0, 0);
     };
     // keys: the distance's bits with the low 10 mantissa bits replaced by the centroid's offset
     // (value order, lowest index first); padded centroids carry the largest finite bias and
     // never win.  NG groups of 8 centroids (4 per lane); the pair fold is 3 VALU per 2 keys.
     auto epi = [&](auto ng_t, int c0, const f32x16& acc) OAP_AI {
       constexpr int NG = decltype(ng_t)::value;
-      if constexpr (NO_EPI) {
-        k1 = min(k1, (__float_as_int(acc[0]) & ~0x3ff) | (c0 + 4 * h));
-        return;
-      }
       int key[4 * NG];
 #pragma unroll
       for (int e = 0; e < 4 * NG; ++e)
@@ -516,13 +431,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
     // ---- defer unsure rows (wave-private sub-segment, in tile order)
     const unsigned long long um = __ballot(unsure && h == 0);
     buf_store_b32(rs_def, (n_def + lanes_below(um)) * 4u,
-                  static_cast<int32_t>(row), !NO_ST && unsure && h == 0);
+                  static_cast<int32_t>(row), unsure && h == 0);
     n_def += static_cast<unsigned>(__popcll(um));
     const bool done = valid && !unsure;
     int b = k1 & 0x3ff;
     b = (b < k) ? b : 0;  // only for degenerate (NaN / all-inf) inputs
     const bool moved = done && old >= 0 && old != b;
-    if constexpr (!NO_ACC) {
+    {
       const unsigned long long mm = __ballot(moved && h == 0);
       if (mm) {
         if (moved && h == 0)
@@ -532,7 +447,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       }
     }
     // labels: only the rows that moved (the others already hold theirs)
-    buf_store_b32(rs_lab, roff * 4, b, !NO_ST && moved && h == 0);
+    buf_store_b32(rs_lab, roff * 4, b, moved && h == 0);
     // bounds (when a following iteration may scan): the pick's alpha^2 distance is <= b1 + tt,
     // every other one >= b2 - tt
     float2 bnd = make_float2(0.f, 0.f);
@@ -542,27 +457,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       bnd = make_float2(__builtin_amdgcn_sqrtf(fmaxf(up, 0.f)) * (1.f + 1e-6f) + 1e-30f,
                         __builtin_amdgcn_sqrtf(fmaxf(lo, 0.f)) * (1.f - 1e-6f));
     }
-    buf_store_f2(rs_bnd, roff * 8, bnd, !NO_ST && done && h == 0);
+    buf_store_f2(rs_bnd, roff * 8, bnd, done && h == 0);
   };
 
   int64_t t = wave;
   unsigned n_pruned = 0;  // (row-scan passes; wave-uniform)
-  unsigned n_mvr = 0, n_lst = 0;  // (mover passes: rows into the mover stage, rows it listed)
   auto trow = [&](int64_t q) OAP_AI -> int64_t { return tile_of(q) * 32 + r; };  // (dense)
-  if constexpr (LIST) {
-    // rows of tiles t, t + stride in ra, rb; each body loads the list entry two tiles ahead
-    const int64_t rfix = row0;  // (a real row of this workgroup: the operands of padding lanes)
-    int32_t ra = rid_of(t), rb = rid_of(t + stride), rc = -1;
-    f16x8 xa[KS], xb[KS];
-    load_img_row(ra >= 0 ? ra : rfix, xa);
-    for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      body(std::true_type{}, t, ra, rb >= 0 ? rb : rfix, &rc, xa, xb);
-      ra = rc;  // (tile t + 2 stride)
-      if (t + stride >= npos) break;
-      body(std::true_type{}, t + stride, rb, ra >= 0 ? ra : rfix, &rc, xb, xa);
-      rb = rc;  // (tile t + 3 stride)
-    }
-  } else if constexpr (SCAN) {
+  if constexpr (SCAN) {
     // The wave's dense tiles (t = wave + j stride) are scanned two at a time (h = 0 lanes the
     // first, h = 1 the second): the Hamerly test of kmeans_lean_scan_rows per row.  A pruned
     // row keeps its label and has its bounds advanced in place (rounded outward; no write once
@@ -638,242 +539,36 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
       refill();
       {
         const int64_t nx = ring_row(head + 32u);
-        body(std::true_type{}, 0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xa, xb);
+        body(std::true_type{}, 0, ring_row(head), nx >= 0 ? nx : rfix, xa, xb);
       }
       head = tail - head > 32u ? head + 32u : tail;
       if (head == tail) break;
       refill();
       {
         const int64_t nx = ring_row(head + 32u);
-        body(std::true_type{}, 0, ring_row(head), nx >= 0 ? nx : rfix, nullptr, xb, xa);
+        body(std::true_type{}, 0, ring_row(head), nx >= 0 ? nx : rfix, xb, xa);
       }
       head = tail - head > 32u ? head + 32u : tail;
     }
-  } else if constexpr (MOV) {
-    // Phase 1 — the fused row scan of RM 2 (Hamerly test on the largest drift, bounds only),
-    // then a mover stage for the rows it could not prune: one MFMA chunk against the kMovers
-    // centers that moved most gives each row a lower bound on its distance to every mover
-    // (tier-1 value minus its error bound, its own center left out); with the others' largest
-    // drift dS it bounds the distance to every other center: min(l - dS, l_movers).  A row whose
-    // upper bound stays below that (the scan's fp32 margin) keeps its label and gets the new
-    // bounds; the others are appended to the wave's own list in HBM.  Phase 2 — the full chunk
-    // loop over the wave's list, 32 rows a tile, operands prefetched a tile ahead (the phases
-    // share no registers: neither pays for the other's).
-    int* ring = reinterpret_cast<int*>(smem + L.ring) + wave * kRing;
-    const float dmax = ufl(a.drift[k]);
-    const float cm2 = ufl(cmax * cmax);
-    const float dS = ufl(__int_as_float(mvi[kMovers]));
-    typedef const float __attribute__((address_space(4)))* xn_cptr;
-    const xn_cptr xn_seg = (xn_cptr)(a.scan_xnorm + t0);
-    // the wave's list: rows of its own tiles only (wave + j stride), so ceil(T / WAVES) x 32
-    const uint32_t wcap = uint32_t((T + WAVES - 1) / WAVES * 32);
-    // (workgroup segments of seg_cap = WAVES x wcap entries: the deferral lists' layout)
-    const __amdgpu_buffer_rsrc_t rs_ml =
-        buf_rsrc(a.mlist + blockIdx.x * a.seg_cap + int64_t(wave) * wcap, wcap * 4u);
-    unsigned nl = 0;              // entries the wave appended (wave-uniform)
-    unsigned head = 0, tail = 0;  // ring [head, tail) (wave-uniform)
-    int64_t sq = wave;
-    u32x2 pbw;
-    int plab;
-    float pxn0, pxn1;
-    auto issue = [&]() OAP_AI {
-      const int64_t q = sq + h * stride;
-      const uint32_t roff = uint32_t(q * 32 + r);
-      const bool in = q < dense_pos && int64_t(roff) < wrows;
-      pbw = __builtin_bit_cast(
-          u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, in ? roff * 8u : kBufOff, 0, 0));
-      plab = buf_load_b32(rs_lab, roff * 4u, in);
-      const int64_t q0 = sq < dense_pos ? sq : dense_pos - 1;
-      const int64_t q1 = sq + stride < dense_pos ? sq + stride : dense_pos - 1;
-      pxn0 = xn_seg[q0 < 0 ? 0 : q0];
-      pxn1 = xn_seg[q1 < 0 ? 0 : q1];
-    };
-    auto refill = [&]() OAP_AI {
-      while (tail - head < 64u && sq < dense_pos) {
-        const int64_t q = sq + h * stride;
-        const uint32_t roff = uint32_t(q * 32 + r);
-        const bool in = q < dense_pos && int64_t(roff) < wrows;
-        const float u = __uint_as_float(pbw[0]) + dr_l[min(max(plab, 0), k - 1)];
-        const float lk = __uint_as_float(pbw[1]) - dmax;
-        const float xn = h ? pxn1 : pxn0;
-        const bool ok = in && lk > 0.f && (lk - u) * (lk + u) > mrel * (xn + cm2);
-        buf_store_f2(rs_bnd, roff * 8u, make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f)),
-                     ok && dmax > 0.f);
-        const bool act = in && !ok;
-        const unsigned long long m = __ballot(act);
-        if (act) ring[(tail + lanes_below(m)) & (kRing - 1)] = static_cast<int>(roff);
-        tail += static_cast<unsigned>(__popcll(m));
-        n_pruned += static_cast<unsigned>(__popcll(__ballot(ok)));
-        sq += 2 * stride;
-        issue();
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    auto ring_row = [&](unsigned i) OAP_AI -> int64_t {
-      const int e = ring[(i + unsigned(r)) & (kRing - 1)];
-      return i + unsigned(r) < tail ? row0 + e : int64_t(-1);
-    };
-    const int64_t rfix = row0;
-    // one ring tile (its label and bounds come with it: loaded a tile ahead into ol_n / bw_n)
-    auto mover = [&](const int64_t row, const int64_t pf_row, f16x8(&X)[KS], f16x8(&pf)[KS],
-                     int& ol_c, u32x2& bw_c) OAP_AI {
-      const bool valid = row >= 0 && row < a.n;
-      const uint32_t roff = uint32_t(row - row0);
-      const int ol = min(max(ol_c, 0), k - 1);
-      const u32x2 bw = bw_c;
-      {  // the next tile's label and bounds, then its operands (in flight under this tile)
-        const bool vn = pf_row >= 0 && pf_row < a.n;
-        const uint32_t rn = uint32_t(pf_row - row0);
-        ol_c = buf_load_b32(rs_lab, rn * 4u, vn);
-        bw_c = __builtin_bit_cast(
-            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, vn ? rn * 8u : kBufOff, 0, 0));
-      }
-      load_img_row(pf_row, pf);
-      const float mine =
-          kBias * (static_cast<float>(X[KS - 1][6]) + static_cast<float>(X[KS - 1][7]));
-      const float other = xor32_f(mine);
-      const float nx2_s = h ? mine : other;
-      f16x8 av[KS];
-      const _Float16* ap = mp + size_t(r) * sb + 8 * h;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
-      f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], X[0], f32x16{}, 0, 0, 0);
-#pragma unroll
-      for (int s = 1; s < KS; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], X[s], acc, 0, 0, 0);
-      int key[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        key[e] = (__float_as_int(acc[e]) & ~0x3ff) | (8 * (e >> 2) + (e & 3));
-      int t1 = min(key[0], key[1]), t2 = max(key[0], key[1]);
-#pragma unroll
-      for (int e = 2; e < 16; e += 2) {
-        t2 = min(t2, med3_i32_pure(t1, key[e], key[e + 1]));
-        t1 = min(min(t1, key[e]), key[e + 1]);
-      }
-      int k1 = t1 | (4 * h), k2 = t2 | (4 * h);
-      const int o1 = xor32_i(k1), o2 = xor32_i(k2);
-      k2 = min(max(k1, o1), min(k2, o2));
-      k1 = min(k1, o1);
-      const int own = slot_l[ol];  // (-1: the row's center is not a mover)
-      const int kb = ((k1 & 0x3ff) == own) ? k2 : k1;
-      const float bm = __int_as_float(kb & ~0x3ff);  // (truncated: <= the tier-1 value)
-      const float tt = fmaf(thr_c, __builtin_amdgcn_sqrtf(nx2_s), thr_k) + 5e-5f * nx2_s +
-                       2.5e-4f * fabsf(bm);
-      const float mg = fmaf(mrel, nx2_s, mg_c);
-      const float lm =
-          __builtin_amdgcn_sqrtf(fmaxf((bm - (tt + mg)) * inv_a2, 0.f)) * (1.f - 1e-6f);
-      const float u = __uint_as_float(bw[0]) + dr_l[ol];
-      const float lk = fminf(__uint_as_float(bw[1]) - dS, lm);
-      const float xn = nx2_s * inv_a2 * 1.001f;  // (the row's |x|^2 from its bias pair)
-      const bool ok = valid && lk > 0.f && (lk - u) * (lk + u) > mrel * (xn + cm2);
-      buf_store_f2(rs_bnd, roff * 8u, make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f)),
-                   ok && h == 0);
-      n_pruned += static_cast<unsigned>(__popcll(__ballot(ok && h == 0)));
-      const bool fail = valid && !ok && h == 0;
-      const unsigned long long fm = __ballot(fail);
-      buf_store_b32(rs_ml, (nl + lanes_below(fm)) * 4u, static_cast<int>(roff), fail);
-      nl += static_cast<unsigned>(__popcll(fm));
-      n_mvr += static_cast<unsigned>(__popcll(__ballot(valid && h == 0)));
-    };
-    issue();
-    {
-      f16x8 xa[KS], xb[KS];
-      int ola = 0;
-      u32x2 bwa = {0u, 0u};
-      refill();
-      {
-        const int64_t r0v = ring_row(head);
-        const bool v0 = r0v >= 0;
-        const uint32_t rn = uint32_t((v0 ? r0v : rfix) - row0);
-        ola = buf_load_b32(rs_lab, rn * 4u, v0);
-        bwa = __builtin_bit_cast(
-            u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs_bnd, v0 ? rn * 8u : kBufOff, 0, 0));
-        load_img_row(v0 ? r0v : rfix, xa);
-      }
-      while (head < tail) {  // (wave-uniform)
-        refill();
-        {
-          const int64_t nx = ring_row(head + 32u);
-          mover(ring_row(head), nx >= 0 ? nx : rfix, xa, xb, ola, bwa);
-        }
-        head = tail - head > 32u ? head + 32u : tail;
-        if (head == tail) break;
-        refill();
-        {
-          const int64_t nx = ring_row(head + 32u);
-          mover(ring_row(head), nx >= 0 ? nx : rfix, xb, xa, ola, bwa);
-        }
-        head = tail - head > 32u ? head + 32u : tail;
-      }
-    }
-    n_lst = nl;
-    // ---- phase 2: the wave's list (its own stores: drained, then read back from L2)
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    const int64_t nlt = (int64_t(nl) + 31) / 32;
-    auto lrow = [&](int64_t q) OAP_AI -> int64_t {
-      const uint32_t i = uint32_t(q * 32 + r);
-      // (sc0 sc1: read through to the wave's own stores)
-      const int e = __builtin_amdgcn_raw_buffer_load_b32(rs_ml, i < nl ? i * 4u : kBufOff, 0, 17);
-      return i < nl ? row0 + e : int64_t(-1);
-    };
-    {
-      f16x8 xa[KS], xb[KS];
-      int64_t ra = lrow(0), rb = lrow(1);
-      load_img_row(ra >= 0 ? ra : rfix, xa);
-      for (int64_t q = 0; q < nlt; q += 2) {  // (wave-uniform)
-        body(std::true_type{}, 0, ra, rb >= 0 ? rb : rfix, nullptr, xa, xb);
-        ra = lrow(q + 2);
-        if (q + 1 >= nlt) break;
-        body(std::true_type{}, 0, rb, ra >= 0 ? ra : rfix, nullptr, xb, xa);
-        rb = lrow(q + 3);
-      }
-    }
-  } else if constexpr (PD == 1) {
+  } else {
     f16x8 xa[KS], xb[KS];
     load_img_row(trow(t), xa);
-    if constexpr (NO_LOAD) {
-#pragma unroll
-      for (int s = 0; s < KS; ++s) xa[s] = xb[s] = f16x8{};
-    }
     for (; t < npos; t += 2 * stride) {  // t is wave-uniform: every branch stays uniform
-      body(std::true_type{}, t, trow(t), trow(t + stride), nullptr, xa, xb);
+      body(std::true_type{}, t, trow(t), trow(t + stride), xa, xb);
       if (t + stride >= npos) break;
-      body(std::true_type{}, t + stride, trow(t + stride), trow(t + 2 * stride), nullptr, xb, xa);
-    }
-  } else {
-    f16x8 xa[KS], xb[KS], xc[KS];
-    load_img_row(trow(t), xa);
-    load_img_row(trow(t + stride), xb);
-    if constexpr (NO_LOAD) {
-#pragma unroll
-      for (int s = 0; s < KS; ++s) xa[s] = xb[s] = xc[s] = f16x8{};
-    }
-    for (; t < npos; t += 3 * stride) {
-      body(std::true_type{}, t, trow(t), trow(t + 2 * stride), nullptr, xa, xc);
-      if (t + stride >= npos) break;
-      body(std::true_type{}, t + stride, trow(t + stride), trow(t + 3 * stride), nullptr, xb, xa);
-      if (t + 2 * stride >= npos) break;
-      body(std::true_type{}, t + 2 * stride, trow(t + 2 * stride), trow(t + 4 * stride), nullptr,
-           xc, xb);
+      body(std::true_type{}, t + stride, trow(t + stride), trow(t + 2 * stride), xb, xa);
     }
   }
-  if constexpr (!NO_ACC) {
-    while (n_mv) {  // (at most 63 staged)
-      flush(n_mv);
-      n_mv = n_mv > 32 ? n_mv - 32 : 0;
-    }
+  while (n_mv) {  // (at most 63 staged)
+    flush(n_mv);
+    n_mv = n_mv > 32 ? n_mv - 32 : 0;
   }
   if (lane == 0) {
     if (a.stat && blockIdx.x == 0 && wave == 0) atomicAdd(a.stat + 2, 1ull);  // (image passes)
     a.defer_row_count[blockIdx.x * kDeferSubs + wave] = n_def;
     if (a.stat && n_def) atomicAdd(a.stat, u64(n_def));
     if (a.stat && moved_total) atomicAdd(a.stat + 1, moved_total);
-    if ((SCAN || MOV) && a.pruned && n_pruned) atomicAdd(a.pruned, u64(n_pruned));
-    if (MOV && a.stat && n_mvr) atomicAdd(a.stat + 3, u64(n_mvr));
-    if (MOV && a.stat && n_lst) atomicAdd(a.stat + 4, u64(n_lst));
+    if (SCAN && a.pruned && n_pruned) atomicAdd(a.pruned, u64(n_pruned));
   }
   __syncthreads();
   for (int i = tid; i < k * d; i += NT) {
@@ -889,7 +584,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lean_img(ImgArgs a) 
 
 template <int KS, int WAVES, int CFG, int RM>
 void launch_img_l(const ImgArgs& a, int grid, hipStream_t s) {
-  const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES, RM >= 2, RM == 3, a.d);
+  const ImgSmem L = img_plan(16 * KS, a.kpad, a.k, WAVES, RM == 2);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
@@ -904,55 +599,27 @@ void launch_img_l(const ImgArgs& a, int grid, hipStream_t s) {
 
 template <int KS, int WAVES, int CFG>
 void launch_img(const ImgArgs& a, int grid, hipStream_t s) {
-  if constexpr ((CFG & ~1) == 0) {  // (row-list / row-scan passes: production configurations)
-    if (a.rows) {
-      launch_img_l<KS, WAVES, CFG, 1>(a, grid, s);
-      return;
-    }
-    if (a.scan_xnorm && a.movers) {
-      launch_img_l<KS, WAVES, CFG, 3>(a, grid, s);
-      return;
-    }
-    if (a.scan_xnorm) {
-      launch_img_l<KS, WAVES, CFG, 2>(a, grid, s);
-      return;
-    }
-  } else {
-    OAP_CHECK(!a.rows && !a.scan_xnorm,
-              "kmeans_lean_img: row-list / row-scan passes take configuration 0 or 1");
-  }
-  launch_img_l<KS, WAVES, CFG, 0>(a, grid, s);
+  if (a.scan_xnorm)
+    launch_img_l<KS, WAVES, CFG, 2>(a, grid, s);
+  else
+    launch_img_l<KS, WAVES, CFG, 0>(a, grid, s);
 }
 
 constexpr int kImgDefaultCfg = 1;  // pipelined chunk loop, operands one tile ahead
 
+// Production configurations: 0 (row-scan passes: the scan's prefetched bounds fit the
+// non-pipelined loop's registers) and 1 (dense passes: the pipelined chunk loop).  The timing
+// ablation builds of rounds 3-5 (no epilogue / MFMA / plane reads / loads / accumulation / stores,
+// operands two tiles ahead) live in git history.
 template <int KS, int WAVES>
 void launch_img_cfg(const ImgArgs& a, int grid, int cfg, hipStream_t s) {
-  if constexpr (KS == 4 && WAVES == 16) {  // the headline shape: every probe configuration
-    switch (cfg) {
-      case 0: launch_img<4, 16, 0>(a, grid, s); return;
-      case 1: launch_img<4, 16, 1>(a, grid, s); return;
-      case 2: launch_img<4, 16, 2>(a, grid, s); return;
-      case 3: launch_img<4, 16, 3>(a, grid, s); return;
-      case 1 | 4: launch_img<4, 16, 1 | 4>(a, grid, s); return;
-      case 1 | 8: launch_img<4, 16, 1 | 8>(a, grid, s); return;
-      case 1 | 16: launch_img<4, 16, 1 | 16>(a, grid, s); return;
-      case 1 | 32: launch_img<4, 16, 1 | 32>(a, grid, s); return;
-      case 1 | 64: launch_img<4, 16, 1 | 64>(a, grid, s); return;
-      case 1 | 128: launch_img<4, 16, 1 | 128>(a, grid, s); return;
-      case 1 | 4 | 8 | 16: launch_img<4, 16, 1 | 4 | 8 | 16>(a, grid, s); return;
-      case 1 | 4 | 64 | 128: launch_img<4, 16, 1 | 4 | 64 | 128>(a, grid, s); return;
-      case 1 | 8 | 64 | 128: launch_img<4, 16, 1 | 8 | 64 | 128>(a, grid, s); return;
-      case 1 | 4 | 16 | 64 | 128: launch_img<4, 16, 1 | 4 | 16 | 64 | 128>(a, grid, s); return;
-      case 1 | 4 | 32 | 64 | 128: launch_img<4, 16, 1 | 4 | 32 | 64 | 128>(a, grid, s); return;
-      case 4 | 64 | 128: launch_img<4, 16, 4 | 64 | 128>(a, grid, s); return;
-      case 1 | 4 | 8 | 16 | 64 | 128:
-        launch_img<4, 16, 1 | 4 | 8 | 16 | 64 | 128>(a, grid, s);
-        return;
-      default: break;
-    }
-  }
-  launch_img<KS, WAVES, kImgDefaultCfg>(a, grid, s);
+  OAP_CHECK(cfg == 0 || cfg == 1, "kmeans_lean_img: configuration " << cfg << " (0 or 1)");
+  if (cfg == 0 && a.scan_xnorm)
+    launch_img<KS, WAVES, 0>(a, grid, s);
+  else if (cfg == 0)
+    launch_img<KS, WAVES, 0>(a, grid, s);
+  else
+    launch_img<KS, WAVES, 1>(a, grid, s);
 }
 
 template <int WAVES>
@@ -967,78 +634,6 @@ void launch_img_w(const ImgArgs& a, int grid, int cfg, hipStream_t s) {
     case 7: launch_img_cfg<7, WAVES>(a, grid, cfg, s); break;
     case 8: launch_img_cfg<8, WAVES>(a, grid, cfg, s); break;
     default: OAP_THROW(ConfigError, "kmeans_lean_img: unsupported d=" << a.d);
-  }
-}
-
-// ---------------------------------------------------------------- row-level bound scan
-// Lean workgroup b's rows, 1024 per step, one block per lean workgroup: the Hamerly test of
-// kmeans_lean_scan (kmeans_lloyd.hip) per ROW.  A pruned row keeps its label (the exact-fp32
-// argmin cannot change: its stored upper bound plus its center's drift stays below its lower
-// bound minus the largest drift, with the fp32 evaluation margin) and has its bounds advanced in
-// place, rounded outward; the other rows are appended in row order to b's segment (wave ballots
-// + one LDS prefix per step: deterministic, no atomics on the list).
-constexpr int kScanRowThreads = 1024;
-
-__global__ __launch_bounds__(kScanRowThreads) void oap_kmeans_lean_scan_rows(
-    int64_t n, int k, int d, int64_t tiles_per_block, float2* __restrict__ bounds,
-    const int32_t* __restrict__ labels, const float* __restrict__ xnorm,
-    const float* __restrict__ drift, const float* __restrict__ drift_max,
-    const float* __restrict__ cstat, int32_t* __restrict__ row_list,
-    unsigned* __restrict__ row_count, unsigned long long* __restrict__ pruned,
-    const int* __restrict__ halt) {
-  if (halt && *halt) return;
-  constexpr int W = kScanRowThreads / 64;
-  __shared__ float dr[1024];
-  __shared__ unsigned wcnt[2][W];
-  __shared__ unsigned long long bpr;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int j = tid; j < k && j < 1024; j += kScanRowThreads) dr[j] = drift[j];
-  if (tid == 0) bpr = 0;
-  const float dmax = drift_max[0];
-  const float cmax = cstat[0];
-  const float mrel = 4e-7f * float(d + 8);
-  const int64_t span = tiles_per_block * 32;
-  const int64_t r0 = int64_t(blockIdx.x) * span;
-  const int64_t r1 = r0 + span < n ? r0 + span : n;
-  int32_t* seg = row_list + int64_t(blockIdx.x) * span;
-  unsigned base = 0;  // (block-uniform) entries written so far
-  unsigned long long npr = 0;
-  __syncthreads();
-  int par = 0;
-  for (int64_t c = r0; c < r1; c += kScanRowThreads, par ^= 1) {  // block-uniform trip count
-    const int64_t row = c + tid;
-    bool active = false;
-    if (row < r1) {
-      const float2 b = bounds[row];
-      const int lab = min(max(labels[row], 0), k - 1);
-      const float u = b.x + dr[lab];
-      const float lk = b.y - dmax;
-      const bool ok =
-          lk > 0.f && (lk - u) * (lk + u) > mrel * (xnorm[row >> 5] + cmax * cmax);
-      if (ok) {
-        ++npr;
-        if (dmax > 0.f) bounds[row] = make_float2(u * (1.f + 2.5e-7f), lk * (1.f - 2.5e-7f));
-      } else {
-        active = true;
-      }
-    }
-    const unsigned long long m = __ballot(active);
-    if (lane == 0) wcnt[par][wave] = static_cast<unsigned>(__popcll(m));
-    __syncthreads();  // (wcnt alternates by step parity: one barrier per step)
-    unsigned off = base, tot = 0;
-    for (int w = 0; w < W; ++w) {
-      const unsigned cw = wcnt[par][w];
-      off += w < wave ? cw : 0u;
-      tot += cw;
-    }
-    if (active) seg[off + lanes_below(m)] = static_cast<int32_t>(row);
-    base += tot;
-  }
-  if (npr) atomicAdd(&bpr, npr);
-  __syncthreads();
-  if (tid == 0) {
-    row_count[blockIdx.x] = base;
-    if (pruned && bpr) atomicAdd(pruned, bpr);
   }
 }
 
@@ -1118,45 +713,29 @@ void kmeans_scan_decide(int64_t n, int k, int d, const float* bounds, const int3
   OAP_HIP_CHECK(hipGetLastError());
 }
 
-void kmeans_lean_scan_rows(int64_t n, int k, int d, int lean_grid, float* bounds,
-                           const int32_t* labels, const float* xnorm, const float* drift,
-                           const float* drift_max, const float* cstat, int32_t* row_list,
-                           unsigned* row_count, unsigned long long* pruned_rows, hipStream_t s,
-                           const int* halt) {
-  OAP_CHECK(k <= 1024 && lean_grid >= 1, "kmeans_lean_scan_rows: k <= 1024");
-  if (n <= 0) return;
-  hipLaunchKernelGGL(oap_kmeans_lean_scan_rows, dim3(lean_grid), dim3(kScanRowThreads), 0, s, n, k,
-                     d, kmeans_lloyd_tiles_per_block(n, lean_grid),
-                     reinterpret_cast<float2*>(bounds), labels, xnorm, drift, drift_max, cstat,
-                     row_list, row_count, pruned_rows, halt);
-  OAP_HIP_CHECK(hipGetLastError());
-}
-
 bool kmeans_refine_default() {  // (read per launch: tests switch it within a process)
-  const char* e = std::getenv("OAP_KMEANS_REFINE");
-  return !(e && *e == '0');
+  return knob_int("OAP_KMEANS_REFINE") != 0;
 }
 
-bool kmeans_lean_img_supported(int d, int k, int waves, bool scan, bool movers) {
+bool kmeans_lean_img_supported(int d, int k, int waves, bool scan) {
   if (d + 4 > 128 || k < 1 || (waves != 12 && waves != 16)) return false;
   const int dp = (d + 4 + 15) / 16 * 16;
   if (dp != kmeans_dp(d)) return false;
   const int kpad = (k + 31) / 32 * 32;
   if (kpad > 1024) return false;
-  return img_plan(dp, kpad, k, waves, scan || movers, movers, d).total <= kLdsLimit;
+  return img_plan(dp, kpad, k, waves, scan).total <= kLdsLimit;
 }
 
 void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hipStream_t s) {
   const bool scan = a.img_scan_xnorm != nullptr;
-  OAP_CHECK(kmeans_lean_img_supported(a.d, a.k, waves, scan, scan && a.img_movers) && !a.xbf16 &&
+  OAP_CHECK(kmeans_lean_img_supported(a.d, a.k, waves, scan) && !a.xbf16 &&
                 a.ximg && a.img_beta &&
                 a.delta && a.labels && a.scale && a.sums && a.counts && a.accumulate &&
                 a.sums_too && a.defer_rows && a.defer_row_count && a.cstat && !a.xnorm &&
                 !a.cost_slab && !a.mindist && !a.centers_all && a.chunk_mode == 0 &&
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, waves) &&
                 a.ld == kmeans_ld(a.d, false) && (!a.tile_list || a.tile_count) &&
-                (!a.img_rows || (a.img_row_count && !a.tile_list)) &&
-                (!scan || (a.img_scan_drift && a.bounds && !a.img_rows && !a.tile_list)),
+                (!scan || (a.img_scan_drift && a.bounds && !a.tile_list)),
             "kmeans_lean_img: unsupported arguments");
   if (a.n == 0) return;
   ImgArgs l;
@@ -1176,8 +755,6 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.defer_rows = a.defer_rows;
   l.defer_row_count = a.defer_row_count;
   l.stat = a.deferred_rows;
-  l.rows = a.img_rows;
-  l.row_count = a.img_row_count;
   l.scan_xnorm = a.img_scan_xnorm;
   l.drift = a.img_scan_drift;
   l.pruned = a.img_scan_pruned;
@@ -1188,13 +765,10 @@ void kmeans_lean_img(const KMeansAssignArgs& a, int grid, int waves, int cfg, hi
   l.d = a.d;
   l.k = a.k;
   l.kpad = a.kpad;
-  l.movers = scan && a.img_movers ? 1 : 0;
   l.refine = kmeans_refine_default() ? 1 : 0;
-  l.mlist = a.img_mover_list;
   l.halt = a.halt;
   l.gate = a.img_gate;
   l.gate_on = a.img_gate_on;
-  OAP_CHECK(!l.movers || l.mlist, "kmeans_lean_img: the mover stage needs its row lists");
   if (waves == 12)
     launch_img_w<12>(l, grid, cfg < 0 ? kImgDefaultCfg : cfg, s);
   else

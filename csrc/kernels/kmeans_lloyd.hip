@@ -41,6 +41,7 @@
 
 #include "kernels/kmeans_frag.h"
 #include "kernels/kmeans_internal.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 namespace kern {
@@ -151,14 +152,12 @@ __device__ inline void split_f16(float v, _Float16& hi, _Float16& lo) {
 // the row's f32 values are not needed after its fp16 operands are built (rows that accumulate
 // re-read theirs), so PF 2 can reuse their registers, and the bounds' upper half comes from the
 // tier-1 distance plus its error bound.
-// U: k chunks per step of the distance loop (1 or 2).
-// RCH > 0: register-resident plane — every wave copies the whole fp16 plane (kpad <= 32 RCH
-// centroids, RCH x KS fragments of 4 registers) out of LDS once, so the distance loop reads no
-// LDS at all (the LDS plane otherwise costs each tile 7 x 4 ds_read_b128 per wave, as many LDS
-// cycles as MFMA cycles at 4 waves/SIMD, and exposes their latency before every MFMA); chunk
-// c + 1's MFMA chain is issued before chunk c's epilogue (two accumulators), so one wave keeps
-// the matrix pipe busy under its own VALU.  Run at 2 waves/SIMD (8 per workgroup).
-template <int KS, bool XB, int WAVES, int PF, bool COST, int U, bool SG = false, int RCH = 0>
+// SG: all KS fragment reads of a chunk in flight before its first MFMA.
+// (Measured dead ends, in git history: two chunks per step, software-pipelined fragment reads,
+// an accumulator-pipelined chunk loop (config 5: 293 vs 290 ms/iter, profiles/r5/
+// cfg5_r5h_v12.json), a register-resident plane at 2 waves/SIMD (6% slower, profiles/r3/
+// lean_variants_r3n_v11.json).)
+template <int KS, bool XB, int WAVES, int PF, bool COST, bool SG = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a) {
   constexpr int DP = 16 * KS;
   constexpr int NT = WAVES * 64;
@@ -254,17 +253,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
 
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (uniform)
   const int r = lane & 31, h = lane >> 5;
-  // register-resident plane: this lane's A fragments of every chunk (zero past kpad)
-  f16x8 pr[RCH > 0 ? RCH : 1][KS];
-  if constexpr (RCH > 0) {
-#pragma unroll
-    for (int c = 0; c < RCH; ++c)
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        pr[c][s] = (32 * c < kpad) ? *reinterpret_cast<const f16x8*>(
-                                         ph + size_t(32 * c + r) * sb + 8 * h + 16 * s)
-                                   : f16x8{};
-  }
   // tier-1 bound on two candidates' distance error (alpha^2 units): the cross term
   // 2 x 2 x 2^-10 |alpha c||alpha x| (fp16 products), fp16 subnormals d 2^-14, the bias pairs
   // 2^-21 (|c|^2 + |x|^2), fp32 accumulation 4e-5 (cmax^2 + |x|^2), plus the key truncation
@@ -622,87 +610,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
     float b1 = 0.f, b2 = 0.f, tt = 0.f;
     if (IMG || do_dist) {
       int c0 = 0;
-      if constexpr (RCH > 0) {
-        // software-pipelined over chunks: issue chunk c's MFMA chain, then fold chunk c - 1
-        f32x16 accA, accB;
-        auto chain = [&](int c, f32x16& acc) OAP_AI {
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr[c][0], xh[0], f32x16{}, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(pr[c][s], xh[s], acc, 0, 0, 0);
-        };
-        const int nch = kpad >> 5;  // <= RCH (kmeans_lloyd checks)
-#pragma unroll
-        for (int c = 0; c <= RCH; ++c) {
-          if (c < RCH && c < nch) chain(c, (c & 1) ? accB : accA);
-          if (c >= 1 && c - 1 < nch) epilogue(32 * (c - 1), ((c - 1) & 1) ? accB : accA);
-        }
-        c0 = kpad;
-      }
-      if constexpr (U == 2) {
-        // two chunks per step: all 2 KS fragment reads issue together, two independent MFMA
-        // chains, then both epilogues (ILP the single-chunk loop lacks)
-        for (; c0 + 32 < kpad; c0 += 64) {
-          const _Float16* apA = ph + size_t(c0 + r) * sb + 8 * h;
-          const _Float16* apB = apA + size_t(32) * sb;
-          f16x8 avA[KS], avB[KS];
-#pragma unroll
-          for (int s = 0; s < KS; ++s) {
-            avA[s] = *reinterpret_cast<const f16x8*>(apA + 16 * s);
-            avB[s] = *reinterpret_cast<const f16x8*>(apB + 16 * s);
-          }
-          f32x16 accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(avA[0], xh[0], f32x16{}, 0, 0, 0);
-          f32x16 accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(avB[0], xh[0], f32x16{}, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s) {
-            accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(avA[s], xh[s], accA, 0, 0, 0);
-            accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(avB[s], xh[s], accB, 0, 0, 0);
-          }
-          epilogue(c0, accA);
-          epilogue(c0 + 32, accB);
-        }
-      }
-      if constexpr (U == 3) {
-        // software-pipelined: the next chunk's fragments are read under this chunk's epilogue
-        f16x8 av[KS];
-        const _Float16* ap = ph + size_t(r) * sb + 8 * h;
-#pragma unroll
-        for (int s = 0; s < KS; ++s) av[s] = *reinterpret_cast<const f16x8*>(ap + 16 * s);
-        for (; c0 < kpad; c0 += 32) {
-          f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[0], xh[0], f32x16{}, 0, 0, 0);
-#pragma unroll
-          for (int s = 1; s < KS; ++s)
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[s], xh[s], acc, 0, 0, 0);
-          ap += size_t(32) * sb;
-          const bool more = c0 + 32 < kpad;  // wave-uniform
-#pragma unroll
-          for (int s = 0; s < KS; ++s)
-            av[s] = more ? *reinterpret_cast<const f16x8*>(ap + 16 * s) : av[s];
-          __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
-          epilogue(c0, acc);
-        }
-      }
-      if constexpr (U == 4) {
-        // accumulator-pipelined: chunk c + 1's MFMA chain is issued before chunk c's epilogue
-        // (into the other accumulator), so this wave's own VALU runs under its matrix work — an
-        // MFMA holds the SIMD's vector issue for 8 of its 32 cycles, so a 32-centroid epilogue
-        // (~45 VALU) fits under a chain of KS MFMAs
-        f32x16 accA, accB;
-        int c = 0;
-        mfma_chunk(0, accA);
-        while (true) {  // invariant: accA holds chunk c (issued)
-          if (c + 32 < kpad) mfma_chunk(c + 32, accB);
-          epilogue(c, accA);
-          c += 32;
-          if (c >= kpad) break;
-          if (c + 32 < kpad) mfma_chunk(c + 32, accA);
-          epilogue(c, accB);
-          c += 32;
-          if (c >= kpad) break;
-        }
-        c0 = kpad;
-      }
       for (; c0 < kpad; c0 += 32) {  // other waves' MFMAs overlap this epilogue
         f32x16 acc;
         mfma_chunk(c0, acc);
@@ -899,74 +806,34 @@ __global__ __launch_bounds__(WAVES * 64, 1) void oap_kmeans_lloyd_t1(LeanArgs a)
   }
 }
 
-template <int KS, bool XB, int WAVES, int PF, bool COST, int U = 1, bool SG = false, int RCH = 0>
+template <int KS, bool XB, int WAVES, int PF, bool COST, bool SG = false>
 void launch_lean(const LeanArgs& a, int grid, hipStream_t s) {
   const LeanSmem L =
       lean_plan(16 * KS, a.kpad, a.k, a.d, a.accumulate, a.sums_too, WAVES, a.delta != 0);
   static bool attr_set = false;
   if (!attr_set) {
     OAP_HIP_CHECK(hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG, RCH>),
+        reinterpret_cast<const void*>(&oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, SG>),
         hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kLdsLimit)));
     attr_set = true;
   }
-  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, U, SG, RCH>), dim3(grid),
+  hipLaunchKernelGGL((oap_kmeans_lloyd_t1<KS, XB, WAVES, PF, COST, SG>), dim3(grid),
                      dim3(WAVES * 64), L.total, s, a);
   OAP_HIP_CHECK(hipGetLastError());
 }
 
+// Workgroup shapes (one workgroup per CU: the LDS plan), fragment reads grouped ahead of each
+// MFMA chain: variant 6, 4 waves/SIMD; variant 8, 3 waves/SIMD (rows of 7-8 k-steps, where 128
+// registers spill).  With the cost the rows stay in registers; without, the next tile is
+// prefetched into them (PF 2).
 template <int KS, bool XB>
 void launch_lean_v(const LeanArgs& a, int grid, int variant, bool cost, hipStream_t s) {
-  // workgroup shape (one workgroup per CU: the LDS plan); with the cost: rows stay in
-  // registers; without: the next tile is prefetched into them (PF 2)
-  switch (variant) {
-    case 3:  // 3 waves/SIMD, no prefetch
-      if (cost) launch_lean<KS, XB, 12, 0, true>(a, grid, s);
-      else launch_lean<KS, XB, 12, 0, false>(a, grid, s);
-      break;
-    case 5:  // 3 waves/SIMD, prefetch
-      if (cost) launch_lean<KS, XB, 12, 2, true>(a, grid, s);
-      else launch_lean<KS, XB, 12, 2, false>(a, grid, s);
-      break;
-    case 6:  // 4 waves/SIMD, fragment reads grouped ahead of the MFMAs
-      if (cost) launch_lean<KS, XB, 16, 0, true, 1, true>(a, grid, s);
-      else launch_lean<KS, XB, 16, 2, false, 1, true>(a, grid, s);
-      break;
-    case 8:  // 3 waves/SIMD, grouped fragment reads
-      if (cost) launch_lean<KS, XB, 12, 0, true, 1, true>(a, grid, s);
-      else launch_lean<KS, XB, 12, 2, false, 1, true>(a, grid, s);
-      break;
-    case 9:  // 3 waves/SIMD, software-pipelined fragment reads
-      if (cost) launch_lean<KS, XB, 12, 0, true, 3>(a, grid, s);
-      else launch_lean<KS, XB, 12, 2, false, 3>(a, grid, s);
-      break;
-    case 10:  // 4 waves/SIMD, software-pipelined fragment reads, no prefetch
-      if (cost) launch_lean<KS, XB, 16, 0, true, 3>(a, grid, s);
-      else launch_lean<KS, XB, 16, 0, false, 3>(a, grid, s);
-      break;
-    case 11:  // 2 waves/SIMD, register-resident plane (kpad <= 32 kmeans_lloyd_rch(d))
-      if constexpr (KS <= 4) {
-        constexpr int R = KS == 4 ? 7 : 8;
-        if (cost) launch_lean<KS, XB, 8, 0, true, 1, false, R>(a, grid, s);
-        else launch_lean<KS, XB, 8, 2, false, 1, false, R>(a, grid, s);
-      }
-      break;  // (other widths: rejected by kmeans_lloyd)
-    case 7:  // 3 waves/SIMD, two chunks per step, prefetch without the cost
-      if (cost) launch_lean<KS, XB, 12, 0, true, 2>(a, grid, s);
-      else launch_lean<KS, XB, 12, 2, false, 2>(a, grid, s);
-      break;
-    case 12:  // 3 waves/SIMD, accumulator-pipelined chunk loop
-      if (cost) launch_lean<KS, XB, 12, 0, true, 4>(a, grid, s);
-      else launch_lean<KS, XB, 12, 2, false, 4>(a, grid, s);
-      break;
-    case 13:  // 4 waves/SIMD, accumulator-pipelined chunk loop
-      if (cost) launch_lean<KS, XB, 16, 0, true, 4>(a, grid, s);
-      else launch_lean<KS, XB, 16, 2, false, 4>(a, grid, s);
-      break;
-    default:  // 4 waves/SIMD
-      if (cost) launch_lean<KS, XB, 16, 0, true>(a, grid, s);
-      else launch_lean<KS, XB, 16, 2, false>(a, grid, s);
-      break;
+  if (variant == 8) {
+    if (cost) launch_lean<KS, XB, 12, 0, true, true>(a, grid, s);
+    else launch_lean<KS, XB, 12, 2, false, true>(a, grid, s);
+  } else {
+    if (cost) launch_lean<KS, XB, 16, 0, true, true>(a, grid, s);
+    else launch_lean<KS, XB, 16, 2, false, true>(a, grid, s);
   }
 }
 
@@ -1796,18 +1663,7 @@ int64_t kmeans_lloyd_tiles_per_block(int64_t n, int grid) {
   return (tiles + grid - 1) / grid;
 }
 
-int kmeans_lloyd_waves(int variant) {
-  if (variant == 11) return 8;
-  return (variant == 3 || variant == 5 || variant == 7 || variant == 8 || variant == 9 ||
-          variant == 12)
-             ? 12
-             : 16;
-}
-
-int kmeans_lloyd_rch(int d) {
-  const int ks = (d + 4 + 15) / 16;
-  return ks <= 3 ? 8 : (ks == 4 ? 7 : 0);
-}
+int kmeans_lloyd_waves(int variant) { return variant == 8 ? 12 : 16; }
 
 int64_t kmeans_lloyd_seg_cap(int64_t n, int grid, int waves) {
   const int64_t per_block = kmeans_lloyd_tiles_per_block(n, grid);
@@ -1833,8 +1689,6 @@ int kmeans_lloyd(const KMeansAssignArgs& a, int grid, int variant, hipStream_t s
                 a.row_seg_cap == kmeans_lloyd_seg_cap(a.n, grid, kmeans_lloyd_waves(variant)) &&
                 a.ld == kmeans_ld(a.d, a.xbf16),
             "kmeans_lloyd: unsupported arguments");
-  OAP_CHECK(variant != 11 || (kmeans_lloyd_rch(a.d) > 0 && a.kpad <= 32 * kmeans_lloyd_rch(a.d)),
-            "kmeans_lloyd: the register-plane variant needs kpad <= 32 kmeans_lloyd_rch(d)");
   OAP_CHECK(!a.delta || a.labels, "kmeans_lloyd: delta mode needs the previous labels");
   OAP_CHECK(!a.tile_list || (a.delta && a.tile_count), "kmeans_lloyd: tile list without delta");
   // the operand image: f32 rows, one launch; written by a full pass, read without the per-tile
@@ -1914,12 +1768,12 @@ void kmeans_exact_rows(const KMeansAssignArgs& a, int grid, hipStream_t s) {
             "kmeans_exact_rows: chunked pass needs its running state and every center");
   // the candidate form: f32 rows of a single-launch pass whose centers' tier-1 plane fits (the
   // chunked and bf16 passes keep the full MFMA sweep); OAP_KMEANS_EXACT=mfma / cand force one
-  const char* fe = std::getenv("OAP_KMEANS_EXACT");  // (read per call: tests switch it)
-  const bool force_mfma = fe && fe[0] == 'm';
+  const std::string fe = knob_str("OAP_KMEANS_EXACT");  // (read per call: tests switch it)
+  const bool force_mfma = !fe.empty() && fe[0] == 'm';
   // (measured: 5-10% faster per pass at 390k rows per workgroup, the headline; 20% slower at 49k,
   // the 8-GPU shard, where staging its fp16 plane and running at 8 waves do not amortise)
   const bool big = a.n >= int64_t(grid) * 131072;
-  if ((big || (fe && fe[0] == 'c')) && !force_mfma && !a.xbf16 && a.chunk_mode == 0 &&
+  if ((big || (!fe.empty() && fe[0] == 'c')) && !force_mfma && !a.xbf16 && a.chunk_mode == 0 &&
       a.d + 4 <= 96 && a.base == 0 &&
       (a.d + 4 + 15) / 16 * 16 == kmeans_dp(a.d) &&  // (the centers' row stride)
       cand_plan(a.kpad, a.k, a.d, a.accumulate, a.sums_too).total <= kLdsLimit) {

@@ -9,6 +9,7 @@
 
 #include "kernels/kernels.h"
 #include "runtime/common.h"
+#include "runtime/knobs.h"
 
 namespace oap {
 
@@ -37,7 +38,7 @@ SymEig sym_eig_topk_gpu(Context& ctx, const double* a, int n, int k, hipStream_t
                     reinterpret_cast<unsigned*>(bar.data()), s);
   e1.record(s);
   unsigned abort_word = 0;
-  if (kern::eig_vectors_supported(n, k) && !std::getenv("OAP_EIG_HOST_INVIT")) {
+  if (kern::eig_vectors_supported(n, k) && !knob_on("OAP_EIG_HOST_INVIT")) {
     // the rest on the device (kern::eig_top_vectors): bracket, bisection, selection, inverse
     // iteration, back-transform and signs — only the results come back
     Buffer zb = ctx.alloc(sizeof(double) * size_t(n) * k);

@@ -1,4 +1,5 @@
 #include "runtime/log.h"
+#include "runtime/knobs.h"
 
 #include <dlfcn.h>
 
@@ -24,9 +25,7 @@ const char* level_name(LogLevel l) {
   }
 }
 LogLevel level_from_env() {
-  const char* v = std::getenv("OAP_MLLIB_LOG_LEVEL");
-  if (!v) return LogLevel::Warn;
-  std::string s(v);
+  const std::string s = knob_str("OAP_MLLIB_LOG_LEVEL");
   if (s == "debug") return LogLevel::Debug;
   if (s == "info") return LogLevel::Info;
   if (s == "warn") return LogLevel::Warn;
@@ -38,7 +37,7 @@ LogLevel level_from_env() {
 
 Logger::Logger() {
   level_ = level_from_env();
-  if (const char* p = std::getenv("OAP_MLLIB_LOG_FILE")) path_ = p;
+  path_ = knob_str("OAP_MLLIB_LOG_FILE");
 }
 
 Logger& Logger::instance() {
@@ -140,9 +139,7 @@ struct Roctx {
   pop_fn pop = nullptr;
   mark_fn mark = nullptr;
   Roctx() {
-    if (const char* off = std::getenv("OAP_MLLIB_NO_ROCTX")) {
-      if (off[0] == '1') return;
-    }
+    if (knob_on("OAP_MLLIB_NO_ROCTX")) return;
     const char* libs[] = {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
                           "libroctx64.so.4", "libroctx64.so"};
     for (const char* l : libs) {

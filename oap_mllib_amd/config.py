@@ -68,12 +68,26 @@ class Config:
     #: installed pyspark's, else 3.1.1.  The reference builds one jar per Spark profile
     #: (3.0.0, 3.0.1, 3.0.2, 3.1.1, mllib-dal/pom.xml:151-224); here it is one knob.
     spark_version: str = ""
+    #: native-layer tuning / diagnostic knobs ({"OAP_KMEANS_ROW_SCAN": "0", ...}), installed by
+    #: init_world; the complete documented list is ``_native.knob_table()`` (runtime/knobs.cpp,
+    #: docs/ARCHITECTURE.md "Knobs").  A knob not given here falls back to the environment
+    #: variable of the same name.  From the environment / Spark conf: "NAME=value,NAME=value".
+    native_knobs: dict = dataclasses.field(default_factory=dict)
 
     def replace(self, **kw) -> "Config":
         return dataclasses.replace(self, **kw)
 
 
 def _coerce(field: dataclasses.Field, value: Any) -> Any:
+    if field.name == "native_knobs":
+        if isinstance(value, Mapping):
+            return {str(k): str(v) for k, v in value.items()}
+        out = {}
+        for item in str(value).split(","):
+            if item.strip():
+                k, _, v = item.partition("=")
+                out[k.strip()] = v.strip()
+        return out
     t = field.type if isinstance(field.type, type) else {"str": str, "int": int, "float": float,
                                                          "bool": bool}.get(str(field.type), str)
     if t is bool:

@@ -161,6 +161,9 @@ def init_world(config: Config | None = None, rank: int | None = None,
               config=cfg, _owns_pg=owns_pg)
     if backend != "vanilla":
         N = _loader.load()
+        N.clear_knobs()
+        for name, value in (cfg.native_knobs or {}).items():
+            N.set_knob(str(name), str(value))
         N.configure_logging(rank, device, cfg.log_level, cfg.log_file)
         w.ctx = N.Context(device, cfg.hbm_fraction, cfg.cpu_threads)
         if size == 1 and not (backend == "gpu" and cfg.force_device_comm):

@@ -369,11 +369,13 @@ def test_pruning_is_exact(native, monkeypatch, d, k, dtype, n):
     init = bf16_round(init) if dtype == "bf16" else init.astype(np.float32).astype(np.float64)
     g = native.Context(0, 0.5, 0)
     t = native.upload_dense(g, X, dtype, native.kmeans_ld(d, dtype))
-    rp = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
+    # (scan_min_prune 0: every row-scan iteration scans, whatever the sampled prunable share)
+    rp = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True,
+                           scan_min_prune=0.0)
     ru = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=False)
     rn = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True,
                            delta=False)
-    # (f32 fits with the operand image prune per row: kmeans_lean_scan_rows)
+    # (f32 fits with the operand image prune per row: the image kernel's fused row scan)
     assert ru["pruned_tiles"] == 0 and ru["pruned_rows"] == 0 and rn["pruned_tiles"] > 0
     assert rp["pruned_tiles"] + rp["pruned_rows"] > 0
     if dtype == "f32" and k == 200:  # the tile-level scan (OAP_KMEANS_ROW_SCAN=0) still exact
@@ -382,19 +384,7 @@ def test_pruning_is_exact(native, monkeypatch, d, k, dtype, n):
         assert rt["pruned_rows"] == 0 and rt["pruned_tiles"] > 0 and rp["pruned_rows"] > 0
         assert rt["last_counts"] == ru["last_counts"]
         assert np.array_equal(rt["centers"], ru["centers"])
-        # the separate scan kernel + row list (=2) prunes exactly the rows the fused scan does
-        # without its mover stage (which prunes more)
-        monkeypatch.setenv("OAP_KMEANS_ROW_SCAN", "2")
-        r2 = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
         monkeypatch.delenv("OAP_KMEANS_ROW_SCAN")
-        monkeypatch.setenv("OAP_KMEANS_MOVERS", "1")
-        r1 = native.kmeans_fit(g, native.LocalComm(True), t, init, k, 10, -1.0, prune=True)
-        monkeypatch.delenv("OAP_KMEANS_MOVERS")
-        assert r2["pruned_rows"] == rp["pruned_rows"] and r2["pruned_tiles"] == 0
-        assert rp["pruned_rows"] <= r1["pruned_rows"]
-        assert np.array_equal(r1["centers"], ru["centers"])
-        assert r2["last_counts"] == ru["last_counts"]
-        assert np.array_equal(r2["centers"], ru["centers"])
     for r in (rp, rn):
         assert r["last_counts"] == ru["last_counts"]
         assert np.array_equal(r["centers"], ru["centers"])
@@ -789,31 +779,6 @@ def test_scan_or_dense_gate_is_exact(native, d, k):
     assert runs[0.0]["pruned_rows"] >= runs[0.2]["pruned_rows"] > 0
     assert runs[0.0]["assign_path"] == "lean_img_kernel_delta_fused_rowscan"
     assert runs[0.2]["assign_path"] == "lean_img_kernel_delta_fused_rowscan_gated"
-
-
-@pytest.mark.parametrize("d,k", [(50, 200), (20, 24), (44, 96)])
-def test_mover_stage_is_exact(native, monkeypatch, d, k):
-    """The row scan's mover stage (rows the Hamerly test cannot prune are bounded against the 32
-    centers that moved most, kmeans_lean_img.hip RM 3) skips full passes but never changes a
-    label: centers, counts and cost history are bitwise those of the fit without it, which are
-    bitwise the unpruned fit's; it prunes at least as many rows."""
-    n = 1_500_000
-    g = native.Context(0, 0.5, 0)
-    t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, 8.0, 77)
-    comm = native.LocalComm(True)
-    init = native.kmeans_init(g, comm, t, k, "k-means||", 2, 3)
-    monkeypatch.setenv("OAP_KMEANS_MOVERS", "1")  # (off by default: see kmeans.cpp)
-    on = native.kmeans_fit(g, comm, t, init, k, 14, -1.0)
-    monkeypatch.delenv("OAP_KMEANS_MOVERS")
-    off = native.kmeans_fit(g, comm, t, init, k, 14, -1.0)
-    ref = native.kmeans_fit(g, comm, t, init, k, 14, -1.0, prune=False)
-    assert on["assign_path"] == "lean_img_kernel_delta_rowscan_movers", on["assign_path"]
-    assert off["assign_path"] == "lean_img_kernel_delta_fused_rowscan_gated"
-    for r in (on, off):
-        assert np.array_equal(r["centers"], ref["centers"])
-        assert r["last_counts"] == ref["last_counts"]
-    assert on["pruned_rows"] >= off["pruned_rows"]
-    assert abs(on["cost"] - ref["cost"]) <= 1e-7 * ref["cost"]
 
 
 @pytest.mark.parametrize("d,k,sigma", [(50, 200, 8.0), (20, 24, 3.0), (44, 96, 12.0)])

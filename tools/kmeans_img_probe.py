@@ -23,7 +23,7 @@ N = _loader.load()
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
 sigma = float(sys.argv[2]) if len(sys.argv) > 2 else 8.0
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 5
-cfgs = sys.argv[4].split(",") if len(sys.argv) > 4 else ["old", "-1", "0", "2", "3"]
+cfgs = sys.argv[4].split(",") if len(sys.argv) > 4 else ["old", "-1", "0", "1"]
 d, k = int(os.environ.get("PROBE_D", "50")), int(os.environ.get("PROBE_K", "200"))
 g = N.Context(0, 0.9, 0)
 t = N.synth_blobs(g, rows, d, N.kmeans_ld(d), 0, k, 10.0, sigma, 20240917)

@@ -18,7 +18,7 @@ N = _loader.load()
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 50_000_000
 sigma = float(sys.argv[2]) if len(sys.argv) > 2 else 8.0
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 10
-variant = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+variant = int(sys.argv[4]) if len(sys.argv) > 4 else 6  # (6 or 8)
 abls = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [0, 1, 2, 3, 8, 11]
 d, k = 50, 200
 g = N.Context(0, 0.9, 0)

@@ -48,7 +48,7 @@ for sg in sigmas:
             C = r["centers"]
     # full single pass on the final centers, with ablations (ms per 100M rows)
     abl = {}
-    for v in (1, 2, 3, 0):
+    for v in (6, 8):
         N.kmeans_set_lean_variant(v)
         abl[f"lean_v{v}"] = round(N.kmeans_assign_timing(g, t, C, 5, False, 64) * 100e6 / rows, 3)
     for name, precise, ab in [("lean", False, 64), ("lean_no_acc", False, 65),
