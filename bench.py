@@ -142,7 +142,7 @@ def bench_kmeans(args, w):
         ms_unpruned = el_u / args.steps * 1e3
         assert np.array_equal(ru["centers"], r["centers"]), "pruning changed the result"
     # end-to-end fit(): init + Lloyd to convergence (maxIter 20, tol 1e-4)
-    fit_s = fit_iters = None
+    fit_s = fit_iters = tol_ms = None
     if not args.skip_fit:
         _barrier_sync(w)
         t1 = time.perf_counter()
@@ -150,6 +150,10 @@ def bench_kmeans(args, w):
         _barrier_sync(w)
         fit_s = float(w.allreduce_np(np.array([time.perf_counter() - t1]), "max")[0])
         fit_iters = rf["num_iter"]
+        # its Lloyd phase per iteration (tol >= 0: batched, a converged iteration halts the rest
+        # of its batch on the device) — against the timed tol = -1 step
+        tol_ms = float(w.allreduce_np(np.array([rf["iter_seconds"] / max(fit_iters, 1) * 1e3]),
+                                      "max")[0])
     ak = m.get("kmeans/assign_kernel", {"total_us": 0, "count": 1})
     ar = m.get("kmeans/allreduce", {"total_us": 0, "count": 1})
     itr = m.get("kmeans/iteration", {"total_us": 0, "count": 1})
@@ -205,6 +209,7 @@ def bench_kmeans(args, w):
     path = r.get("assign_path", "unknown")
     path_desc = described.get(path, path)
     extra = {"fit_wall_s_end_to_end": fit_s, "fit_iters": fit_iters,
+             "fit_tol1e-4_lloyd_ms_per_iter": tol_ms,
              "init_kmeans_parallel_s": init_s, "init_phases_ms": init_phases,
              "ingest_synth_s": ingest_s,
              "data_sigma": args.sigma, "data_box": args.box,

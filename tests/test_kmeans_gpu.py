@@ -644,7 +644,7 @@ def test_image_kernel_matches_lloyd_image_branch(native, d, k, sigma):
     """The dedicated steady-state image kernel (kmeans_lean_img.hip) gives the general lean
     kernel's image branch bitwise: labels, fixed-point statistics, deferred and moved rows (one
     delta pass at the next Lloyd step's centers; partial last chunks, one chunk, 12-wave rows),
-    in each of its configurations, with and without the f32-row fallback launch."""
+    in both its configurations (0, 1), with and without the f32-row fallback launch."""
     n = 120000
     g = native.Context(0, 0.5, 0)
     t = native.synth_blobs(g, n, d, native.kmeans_ld(d), 0, k, 10.0, sigma, 17)
@@ -654,7 +654,7 @@ def test_image_kernel_matches_lloyd_image_branch(native, d, k, sigma):
     cb = np.asarray(native.kmeans_fit(g, comm, t, ca, k, 1, -1.0)["centers"]).reshape(k, d)
     ref = native.kmeans_image_timing(g, t, ca, cb, 1, 0, -1, True)
     assert ref["image_passes"] > 0 and ref["moved_rows"] > 0
-    for cfg, fb in ((-1, True), (-1, False), (0, True), (2, True), (3, False)):
+    for cfg, fb in ((-1, True), (-1, False), (0, True), (1, False)):
         r = native.kmeans_image_timing(g, t, ca, cb, 1, 1, cfg, fb)
         assert r["path"].startswith("lean_img_kernel"), r["path"]
         assert r["image_passes"] == ref["image_passes"]
