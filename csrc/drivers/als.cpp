@@ -289,10 +289,12 @@ bool chol_solve(std::vector<double>& A, std::vector<double>& b, int r) {
 // (A = lower triangle of an SPD r x r matrix, row-major), by the Lawson-Hanson active set: the
 // strictly convex problem has one minimiser, the one Spark's projected-CG NNLS
 // (mllib/optimization/NNLS.scala, ALS.scala:1718-1800 with nonnegative = true) converges to.
-// Each passive-set solve is a Cholesky of the passive block.  x gets the solution; false when a
-// passive block is not SPD.
-bool nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int r,
-                std::vector<double>& x) {
+// Each passive-set solve is a Cholesky of the passive block.  x gets the solution.  Returns
+// kNnlsOk, kNnlsCapped (the iteration cap: x holds the last feasible, nearly optimal iterate —
+// usable, but reported) or kNnlsNotSpd (a passive block is not SPD: x is not usable).
+enum NnlsStatus : int { kNnlsOk = 0, kNnlsCapped = 1, kNnlsNotSpd = 2 };
+NnlsStatus nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int r,
+                      std::vector<double>& x) {
   auto a = [&](int i, int j) { return i >= j ? A[size_t(i) * r + j] : A[size_t(j) * r + i]; };
   x.assign(r, 0.0);
   std::vector<char> passive(r, 0);
@@ -335,10 +337,10 @@ bool nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int 
         jbest = j;
       }
     }
-    if (jbest < 0) return true;
+    if (jbest < 0) return kNnlsOk;
     passive[jbest] = 1;
     for (int inner = 0; inner < 3 * r + 10; ++inner) {
-      if (!solve_passive()) return false;
+      if (!solve_passive()) return kNnlsNotSpd;
       double alpha = 1.0;
       bool feasible = true;
       for (int i = 0; i < r; ++i)
@@ -365,7 +367,7 @@ bool nnls_solve(const std::vector<double>& A, const std::vector<double>& b, int 
       std::fill(blocked.begin(), blocked.end(), 0);
     }
   }
-  return false;  // iteration cap: not reported as converged (the caller counts a failed row)
+  return kNnlsCapped;  // (the caller keeps x and counts the row as failed)
 }
 
 // Rows of X (global user order, stride ld) whose id appears in the caller's initial factors
@@ -939,10 +941,10 @@ AlsResult als_fit(Context& ctx, Comm& comm, const int32_t* users, const int32_t*
           for (int i = 0; i < r; ++i) A[size_t(i) * r + i] += lam;
           float* out = &mine[size_t(row) * ld];
           if (p.nonnegative) {
-            if (nnls_solve(A, bv, r, y))
+            const NnlsStatus st = nnls_solve(A, bv, r, y);
+            if (st != kNnlsNotSpd)  // (capped: the feasible iterate, still counted below)
               for (int f = 0; f < r; ++f) out[f] = float(y[f]);
-            else
-              ++fail_part[ci];
+            if (st != kNnlsOk) ++fail_part[ci];
           } else if (chol_solve(A, bv, r)) {
             for (int f = 0; f < r; ++f) out[f] = float(bv[f]);
           } else {

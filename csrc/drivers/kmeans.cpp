@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <limits>
 #include <map>
@@ -1228,6 +1229,16 @@ constexpr double kStatsCostRel = 1e-5;
 // OAP_KMEANS_HOST_MARKS=1: host timestamps at the fit's phase boundaries, to stderr (where a
 // fit's wall clock goes when its kernels do not fill it: allocations, syncs, read-backs)
 namespace {
+// Drains a stream when the scope unwinds by an exception: the pooled pinned buffers a fit reads
+// back into (flags, counters) go back to the pool on destruction, and an async copy still in
+// flight must not land in a block another caller already holds (runtime/memory.h contract).
+struct StreamDrainOnUnwind {
+  hipStream_t s;
+  int n0 = std::uncaught_exceptions();
+  ~StreamDrainOnUnwind() {
+    if (std::uncaught_exceptions() > n0) (void)hipStreamSynchronize(s);
+  }
+};
 struct HostMarks {
   bool on = false;
   std::chrono::steady_clock::time_point t0;
@@ -1295,8 +1306,12 @@ static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const
   return true;
 }
 
-KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
-                        const std::vector<double>& init_centers, const KMeansParams& p) {
+// One fit attempt.  When the provisional fixed-point bounds fail (a row past its column's bound)
+// it stores the initial centers in *restart and returns at once; kmeans_fit then reruns the fit
+// with the column maxima's scales after this frame — and every buffer it held — has unwound.
+static KMeansResult kmeans_fit_once(Context& ctx, Comm& comm, DenseTable& x,
+                                    const std::vector<double>& init_centers,
+                                    const KMeansParams& p, std::vector<double>* restart) {
   OAP_CHECK(p.k > 1 || p.init == KMeansInit::Given, "k must be > 1");
   OAP_CHECK(p.max_iter >= 0, "maxIter must be >= 0");
   if (ctx.is_gpu()) check_gpu_table(x);
@@ -1713,6 +1728,8 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
   };
   std::vector<IterEvents> ev(kBatch);
   Buffer flags_hb = ctx.alloc_pinned(sizeof(kern::KMeansFlags) * kBatch);
+  // (declared after every pinned read-back buffer of the fit: destroyed before them)
+  StreamDrainOnUnwind drain_on_unwind{s};
   auto* flh = flags_hb.as<kern::KMeansFlags>();
   bool stop = false;
   bool restart = false;  // the provisional fixed-point bounds failed (see prov_pending)
@@ -2066,17 +2083,9 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
     // fit runs again from its initial centers with the column maxima's scales (rare: rows
     // far outside every initial center's coordinate range)
     OAP_HIP_CHECK(hipStreamSynchronize(s));
-    img_b.reset();
-    ldefer_b.reset();
-    bounds_b.reset();
-    lab_keep.reset();
-    KMeansParams q = p;
-    q.absmax_pass = true;
-    q.init = KMeansInit::Given;
-    KMeansResult r = kmeans_fit(ctx, comm, x, centers, q);
-    r.init_seconds = res.init_seconds;
-    r.scale_source = "restart";
-    return r;
+    OAP_CHECK(restart != nullptr, "kmeans: the restarted fit failed its bounds again");
+    *restart = centers;
+    return res;
   }
   if ((delta_all || cfree_all) && last_costless && res.num_iter > 1) {
     // exact cost of a last scan iteration: every row against the centers it was assigned to,
@@ -2174,6 +2183,23 @@ KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
               res.iter_seconds > 0 ? double(x.global_rows) * res.num_iter / res.iter_seconds : 0);
   res.assign_path = t_assign_path;
   return res;
+}
+
+KMeansResult kmeans_fit(Context& ctx, Comm& comm, DenseTable& x,
+                        const std::vector<double>& init_centers, const KMeansParams& p) {
+  std::vector<double> again;
+  KMeansResult r = kmeans_fit_once(ctx, comm, x, init_centers, p, &again);
+  if (again.empty()) return r;
+  // a row past the provisional bounds: the first batch's integers may have wrapped — the fit
+  // runs again from its initial centers with the column maxima's scales (rare: rows far outside
+  // every initial center's coordinate range), after the first attempt released its buffers
+  KMeansParams q = p;
+  q.absmax_pass = true;
+  q.init = KMeansInit::Given;
+  KMeansResult r2 = kmeans_fit_once(ctx, comm, x, again, q, nullptr);
+  r2.init_seconds = r.init_seconds;
+  r2.scale_source = "restart";
+  return r2;
 }
 
 void kmeans_predict_device(Context& ctx, const DenseTable& x, const std::vector<double>& centers,

@@ -49,16 +49,56 @@ __device__ inline int fresh_lane() {
   return lane;
 }
 
+// One step of the diagonal block's factorisation, lane (mod 16) = row: the pivot and column J of
+// L come from DPP row broadcasts (v_mov_b32_dpp row_newbcast, lane K of every 16-lane row to that
+// row) — a plain VALU operand, where v_readlane round-trips each value through an SGPR (with
+// its hazard wait) — 16 broadcasts a step instead of 16 readlanes.  Every 16-lane row of the
+// wave holds a copy of the block (rows of lane & 15); only lanes 0..15 store it.
+template <int J>
+__device__ inline float row_bcast(float v) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + J, 0xF, 0xF, false));
+}
+// t[K] -= lij L[K][J] as ONE instruction: v_fmac_f32 with the DPP broadcast on its first source
+// (lane K of the row's t[J]) — the compiler keeps a v_mov_b32_dpp apart from the FMA that uses
+// it.  fma(b, -lij, t) is bitwise fma(-lij, b, t).  The caller waits 2 states after writing tj
+// (VALU write -> DPP read); the updates write other registers than they broadcast.
+template <int J, int K>
+__device__ inline void diag_update(float (&t)[16], float nlij, float tj) {
+  if constexpr (K < 16) {
+    asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(t[K])
+                 : "v"(tj), "v"(nlij), "i"(K));
+    diag_update<J, K + 1>(t, nlij, tj);
+  }
+}
+template <int J>
+__device__ inline void diag_steps(float (&t)[16], int rl, bool& ok) {
+  if constexpr (J < 16) {
+    const float piv = row_bcast<J>(t[J]);
+    ok = ok && (piv > 0.f);
+    const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
+    t[J] = (rl > J) ? t[J] * inv : (rl == J ? dj : t[J]);
+    const float nlij = (rl > J) ? -t[J] : 0.f;
+    if constexpr (J + 1 < 16) {
+      const float tj = t[J];
+      asm volatile("s_nop 1" ::"v"(tj));  // (VALU write -> DPP read: 2 wait states)
+      diag_update<J, J + 1>(t, nlij, tj);
+    }
+    diag_steps<J + 1>(t, rl, ok);
+  }
+}
+
 template <int NB, int RS = kBS>
 __device__ inline bool chol_factor(float* M, int first = 0) {
   constexpr int RP = 16 * NB;
   const int lane = fresh_lane();
   for (int jb = first; jb < NB; ++jb) {
     const int o = 16 * jb;
-    // (1) diagonal block: lanes 0..15 own its rows, in registers
+    // (1) diagonal block: lanes 0..15 own its rows, in registers (copies in the other rows)
     float t[16];
+    const int rl = lane & 15;
     {
-      const int rl = lane & 15;
 #pragma unroll
       for (int m = 0; m < 16; m += 4) {
         const float4 v = *reinterpret_cast<const float4*>(&M[mi<RS>(o + rl, o + m)]);
@@ -69,19 +109,7 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
       }
     }
     bool ok = true;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float piv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), j));
-      ok = ok && (piv > 0.f);
-      const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
-      t[j] = (lane > j) ? t[j] * inv : (lane == j ? dj : t[j]);
-      const float lij = (lane > j) ? t[j] : 0.f;
-#pragma unroll
-      for (int k = j + 1; k < 16; ++k) {
-        const float lkj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[j]), k));
-        t[k] = fmaf(-lij, lkj, t[k]);
-      }
-    }
+    diag_steps<0>(t, rl, ok);
     if (!ok) return false;
     if (lane < 16) {
 #pragma unroll
@@ -150,6 +178,28 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
   return true;
 }
 
+// Diagonal-block steps of the triangular solves: the value of step J is meaningful at lane
+// base + J (L_jj there; v_rcp_f32, 1 ulp, instead of the ~10-instruction IEEE division) and
+// reaches the block's other rows by a DPP row broadcast (the block occupies one 16-lane row).
+template <int J>
+__device__ inline void fwd_steps(const float (&t)[16], float& vd, int rl, bool mine) {
+  if constexpr (J < 16) {
+    const float zj = row_bcast<J>(vd * __builtin_amdgcn_rcpf(t[J]));
+    if (rl == J) vd = zj;
+    else if (mine && rl > J) vd = fmaf(-t[J], zj, vd);
+    fwd_steps<J + 1>(t, vd, rl, mine);
+  }
+}
+template <int J>
+__device__ inline void bwd_steps(const float (&c)[16], float& vd, int rl, bool mine) {
+  if constexpr (J >= 0) {
+    const float xj = row_bcast<J>(vd * __builtin_amdgcn_rcpf(c[J]));
+    if (rl == J) vd = xj;
+    else if (mine && rl < J) vd = fmaf(-c[J], xj, vd);
+    bwd_steps<J - 1>(c, vd, rl, mine);
+  }
+}
+
 // L L^T x = b with the factor from chol_factor.  Right-hand side in registers: lane l holds rows
 // l and l + 64 (v0, v1; v1 only when NB > 4).  Per 16-row block the diagonal solve runs in
 // registers (16 sequential steps, readlane broadcasts) and the off-diagonal part is one
@@ -176,16 +226,13 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
       t[m + 3] = q.w;
     }
     float vd = (o < 64) ? v0 : v1;
+    // the serial chain on the block's own 16-lane row (DPP row broadcasts), then z to every lane
+    // (lane base + j holds z_j) by independent readlanes off the chain
+    fwd_steps<0>(t, vd, rl, mine);
     float z[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      // meaningful at lane base + j (t[j] = L_jj there); v_rcp_f32 (1 ulp) instead of the
-      // ~10-instruction IEEE division
-      const float zl = vd * __builtin_amdgcn_rcpf(t[j]);
-      z[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zl), base + j));
-      if (rl == j) vd = z[j];
-      else if (mine && rl > j) vd = fmaf(-t[j], z[j], vd);
-    }
+    for (int j = 0; j < 16; ++j)
+      z[j] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vd), base + j));
     if (o < 64) v0 = vd;
     else v1 = vd;
     if (jb + 1 < NB) {
@@ -233,13 +280,7 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
     const int cp = mine ? rl : 0;
 #pragma unroll
     for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi<RS>(o + mm, o + cp)];
-#pragma unroll
-    for (int j = 15; j >= 0; --j) {
-      const float xl = vd * __builtin_amdgcn_rcpf(c[j]);  // meaningful at lane base + j
-      const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xl), base + j));
-      if (rl == j) vd = xj;
-      else if (mine && rl < j) vd = fmaf(-c[j], xj, vd);
-    }
+    bwd_steps<15>(c, vd, rl, mine);
     if (o < 64) v0 = vd;
     else v1 = vd;
   }

@@ -71,6 +71,9 @@ enum class MemKind : int { Host = 0, Device = 1, Pinned = 2, View = 3, PinnedPoo
 // flags, counters, per-fit read-backs) from a process-wide pool of power-of-two blocks, since a
 // hipHostMalloc / hipHostFree pair costs far more than the copies such a buffer serves (a fit
 // allocated six of them: ~0.2 ms of host time on every call).
+// Contract of a pooled pinned buffer: no async copy into or out of it may still be in flight when
+// it is destroyed (hipHostFree used to wait for the device; the pool does not) — the owner drains
+// the stream first, on the exception path too (kmeans.cpp StreamDrainOnUnwind).
 class Buffer {
  public:
   Buffer() = default;

@@ -62,6 +62,13 @@ class KMeansSummary:
     over the labels of the final model straight from the device pass over the still-resident
     rows, and the counts it made (``clusterSizes``, global over the ranks); the ``predictions``
     frame is only assembled when it is read, so a fit on 100M rows creates no per-row objects.
+
+    ``trainingCost`` accuracy class (GPU engine): the cost of the last assignment, either summed
+    from the rows' exact-assignment fp32 distances in fp64 or — when the last pass computed none
+    (row-scan fits) — from the fit's own statistics, ``sum|x|^2 - 2 sum c.S + sum n |c|^2``, taken
+    only when its rigorous error bound (fp32 row norms, fixed-point sums, fp64 rounding) is within
+    1e-5 of the result (drivers/kmeans.cpp kStatsCostRel); otherwise one exact pass over the rows
+    runs.  Both are within 1e-5 relative of the fp64 cost Spark reports (typically ~1e-8).
     """
 
     def __init__(self, predictions, predictionCol: str, featuresCol: str, k: int,  # noqa: N803
