@@ -1307,11 +1307,11 @@ static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const
 }
 
 // One fit attempt.  When the provisional fixed-point bounds fail (a row past its column's bound)
-// it stores the initial centers in *restart and returns at once; kmeans_fit then reruns the fit
+// it stores the initial centers in *restart_with and returns at once; kmeans_fit then reruns the fit
 // with the column maxima's scales after this frame — and every buffer it held — has unwound.
 static KMeansResult kmeans_fit_once(Context& ctx, Comm& comm, DenseTable& x,
                                     const std::vector<double>& init_centers,
-                                    const KMeansParams& p, std::vector<double>* restart) {
+                                    const KMeansParams& p, std::vector<double>* restart_with) {
   OAP_CHECK(p.k > 1 || p.init == KMeansInit::Given, "k must be > 1");
   OAP_CHECK(p.max_iter >= 0, "maxIter must be >= 0");
   if (ctx.is_gpu()) check_gpu_table(x);
@@ -2083,8 +2083,8 @@ static KMeansResult kmeans_fit_once(Context& ctx, Comm& comm, DenseTable& x,
     // fit runs again from its initial centers with the column maxima's scales (rare: rows
     // far outside every initial center's coordinate range)
     OAP_HIP_CHECK(hipStreamSynchronize(s));
-    OAP_CHECK(restart != nullptr, "kmeans: the restarted fit failed its bounds again");
-    *restart = centers;
+    OAP_CHECK(restart_with != nullptr, "kmeans: the restarted fit failed its bounds again");
+    *restart_with = centers;
     return res;
   }
   if ((delta_all || cfree_all) && last_costless && res.num_iter > 1) {
