@@ -1014,15 +1014,22 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
       }
   };
   double my_cost = 0.0;
+  // the previous labels of a group's rows (delta passes), gathered with its rows: a group ahead
+  auto load_old = [&](int64_t gg) -> int {
+    const int64_t ii = gg * 32 + r;
+    return (a.delta && ii < int64_t(total)) ? a.labels[row_at(ii)] : -1;
+  };
   F xa, xb;
   int64_t g = wave;
   load_rows(g, xa);
+  int olda = load_old(g);
   for (; g < ngroups; g += EW) {  // wave-uniform
     const int64_t i = g * 32 + r;
     const bool valid = i < int64_t(total);
     const int64_t row = row_at(i);
     F& x = xa;
     load_rows(g + EW, xb);  // next group: in flight under this one's MFMAs
+    const int oldb = load_old(g + EW);
     // exact argmin with the best and second-best exact distances (the second for the bounds)
     float best = INFINITY, second = INFINITY;
     int bidx = 0x7fffffff;
@@ -1077,11 +1084,11 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
     if (st_out) {  // not the last chunk: carry the state to the next one
       if (valid && h == 0) xst[slot] = make_float2(best, __int_as_float(bidx));
       xa = xb;
+      olda = oldb;
       continue;
     }
     const int b = (bidx >= 0 && bidx < kglob) ? bidx : 0;
-    int old = -1;
-    if (a.delta && valid) old = a.labels[row];
+    const int old = valid ? olda : -1;
     // exact cost and |x|^2 in the assign kernels' lane order
     float part = 0.f, px = 0.f;
     const float* cb = a.chunk_mode ? a.centers_all + size_t(b) * DP + 8 * h
@@ -1112,6 +1119,7 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
       my_cost += double(rowcost);
     }
     xa = xb;
+    olda = oldb;
   }
   const double ws = wave_sum_f64(my_cost);
   if (lane == 0) wc[wave] = ws;
@@ -1304,15 +1312,22 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
       }
   };
   double my_cost = 0.0;
+  // the previous labels of a group's rows (delta passes), gathered with its rows: a group ahead
+  auto load_old = [&](int64_t gg) -> int {
+    const int64_t ii = gg * 32 + r;
+    return (a.delta && ii < int64_t(total)) ? a.labels[row_at(ii)] : -1;
+  };
   F xa, xb;
   int64_t g = wave;
   load_rows(g, xa);
+  int olda = load_old(g);
   for (; g < ngroups; g += EW) {  // wave-uniform
     const int64_t i = g * 32 + r;
     const bool valid = i < int64_t(total);
     const int64_t row = row_at(i);
     F& x = xa;
     load_rows(g + EW, xb);  // next group: in flight under this one
+    const int oldb = load_old(g + EW);
     // the whole row in h-normalised order: x0 = features 16 s + j (j < 8), x1 = 16 s + 8 + j
     float x0[KS][8], x1[KS][8];
 #pragma unroll
@@ -1450,8 +1465,7 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
     // centers left out: exact distance > best + tt / alpha^2
     if (!every) second = fminf(second, best + tt * inv_a2);
     const int b = (bidx >= 0 && bidx < k) ? bidx : 0;
-    int old = -1;
-    if (a.delta && valid) old = a.labels[row];
+    const int old = valid ? olda : -1;
     float part = 0.f, px = 0.f;
     const float* cb = a.centers + size_t(b) * DP + 8 * h;
 #pragma unroll
@@ -1480,6 +1494,7 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
       my_cost += double(rowcost);
     }
     xa = xb;
+    olda = oldb;
   }
   const double ws = wave_sum_f64(my_cost);
   if (lane == 0) wc[wave] = ws;
