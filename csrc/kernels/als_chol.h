@@ -77,7 +77,8 @@ __device__ inline void diag_steps(float (&t)[16], int rl, bool& ok) {
   if constexpr (J < 16) {
     const float piv = row_bcast<J>(t[J]);
     ok = ok && (piv > 0.f);
-    const float dj = sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
+    // (v_sqrt_f32, 1 ulp: the IEEE-exact sqrtf expands to ~10 VALU on the serial chain)
+    const float dj = __builtin_amdgcn_sqrtf(fmaxf(piv, 1e-30f)), inv = __builtin_amdgcn_rcpf(dj);
     t[J] = (rl > J) ? t[J] * inv : (rl == J ? dj : t[J]);
     const float nlij = (rl > J) ? -t[J] : 0.f;
     if constexpr (J + 1 < 16) {
@@ -178,25 +179,35 @@ __device__ inline bool chol_factor(float* M, int first = 0) {
   return true;
 }
 
-// Diagonal-block steps of the triangular solves: the value of step J is meaningful at lane
-// base + J (L_jj there; v_rcp_f32, 1 ulp, instead of the ~10-instruction IEEE division) and
-// reaches the block's other rows by a DPP row broadcast (the block occupies one 16-lane row).
+// Diagonal-block steps of the triangular solves.  Step J's value z_J = vd / L_JJ is meaningful at
+// lane base + J and reaches the block's other rows by a DPP row broadcast (the block occupies one
+// 16-lane row), fused into the update as ONE v_fmac_f32_dpp: vd += m_J z_J with the per-lane
+// coefficient m_J = -L[row][J] below the diagonal, 1 on it (where vd was zeroed first: vd = z_J)
+// and 0 elsewhere — three VALU a step (multiply, select, fused update) instead of six.  The
+// reciprocals and coefficients are formed before the chain.  (fma(-l, z, v) is bitwise the
+// original update; a zero coefficient leaves vd exactly.)
 template <int J>
-__device__ inline void fwd_steps(const float (&t)[16], float& vd, int rl, bool mine) {
+__device__ inline void solve_steps_fwd(const float (&rt)[16], const float (&m)[16], float& vd,
+                                       int rl) {
   if constexpr (J < 16) {
-    const float zj = row_bcast<J>(vd * __builtin_amdgcn_rcpf(t[J]));
-    if (rl == J) vd = zj;
-    else if (mine && rl > J) vd = fmaf(-t[J], zj, vd);
-    fwd_steps<J + 1>(t, vd, rl, mine);
+    const float zl = vd * rt[J];
+    vd = (rl == J) ? 0.f : vd;
+    asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(vd)
+                 : "v"(zl), "v"(m[J]), "i"(J));
+    solve_steps_fwd<J + 1>(rt, m, vd, rl);
   }
 }
 template <int J>
-__device__ inline void bwd_steps(const float (&c)[16], float& vd, int rl, bool mine) {
+__device__ inline void solve_steps_bwd(const float (&rt)[16], const float (&m)[16], float& vd,
+                                       int rl) {
   if constexpr (J >= 0) {
-    const float xj = row_bcast<J>(vd * __builtin_amdgcn_rcpf(c[J]));
-    if (rl == J) vd = xj;
-    else if (mine && rl < J) vd = fmaf(-c[J], xj, vd);
-    bwd_steps<J - 1>(c, vd, rl, mine);
+    const float xl = vd * rt[J];
+    vd = (rl == J) ? 0.f : vd;
+    asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(vd)
+                 : "v"(xl), "v"(m[J]), "i"(J));
+    solve_steps_bwd<J - 1>(rt, m, vd, rl);
   }
 }
 
@@ -228,7 +239,15 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
     float vd = (o < 64) ? v0 : v1;
     // the serial chain on the block's own 16-lane row (DPP row broadcasts), then z to every lane
     // (lane base + j holds z_j) by independent readlanes off the chain
-    fwd_steps<0>(t, vd, rl, mine);
+    {
+      float rt[16], m[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        rt[j] = __builtin_amdgcn_rcpf(t[j]);
+        m[j] = rl == j ? 1.f : ((mine && rl > j) ? -t[j] : 0.f);
+      }
+      solve_steps_fwd<0>(rt, m, vd, rl);
+    }
     float z[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j)
@@ -280,7 +299,15 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
     const int cp = mine ? rl : 0;
 #pragma unroll
     for (int mm = 0; mm < 16; ++mm) c[mm] = M[mi<RS>(o + mm, o + cp)];
-    bwd_steps<15>(c, vd, rl, mine);
+    {
+      float rt[16], m[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        rt[j] = __builtin_amdgcn_rcpf(c[j]);
+        m[j] = rl == j ? 1.f : ((mine && rl < j) ? -c[j] : 0.f);
+      }
+      solve_steps_bwd<15>(rt, m, vd, rl);
+    }
     if (o < 64) v0 = vd;
     else v1 = vd;
   }
