@@ -32,6 +32,8 @@ def main(argv=None):
     ap.add_argument("--precision", default="both", choices=["exact", "fast", "fast4", "both"],
                     help="exact: fp64 products + sums (fp64 MFMA, the reference's precision); "
                     "fast: bf16x3 split products; fast4: bf16x4; both: exact (headline) + fast")
+    ap.add_argument("--no-fp64-compare", action="store_true",
+                    help="skip the exact fit on the fp64-MFMA engine (extra.exact_fp64_engine)")
     a = ap.parse_args(argv)
     from bench_common import init_world, self_launch, shard
 
@@ -70,12 +72,25 @@ def main(argv=None):
                 "allreduce_ms": r["allreduce_ms"], "eig_ms": r["eig_ms"],
                 "native_total_ms": r["total_ms"],
                 "syrk_tflops": flops / (r["stats_ms"] * 1e-3) / 1e12, "all_wall_s": wall,
+                "stats_engine": r["engine"], "err_bound": r["err_bound"],
                 "explained_variance_head": list(r["explained_variance"][:5])}, r
 
     modes = ["exact", "fast"] if a.precision == "both" else [a.precision]
     res = {m: run(m) for m in modes}
+    fp64_cmp = None
+    if "exact" in modes and not a.no_fp64_compare:  # the same exact fit on the fp64 MFMA
+        N.set_knob("OAP_PCA_EXACT_ENGINE", "fp64")
+        try:
+            fp64_cmp = run("exact")
+        finally:
+            N.set_knob("OAP_PCA_EXACT_ENGINE", "")
     head = modes[0]
-    dtype = {"exact": "fp32 in, fp64 products + fp64 accumulate (v_mfma_f64_16x16x4_f64)",
+    dtype = {"exact": ("fp32 in, exact statistics: 7 base-128 int8 digits per centred element, "
+                       "v_mfma_i32_32x32x32_i8 digit products (exact int32 sums), fp64 combine, "
+                       "a priori error bound reported (extra.err_bound)"
+                       if res["exact"][0]["stats_engine"] == "int8_digits" else
+                       "fp32 in, fp64 products + fp64 accumulate (v_mfma_f64_16x16x4_f64)")
+             if "exact" in res else None,
              "fast": "fp32 in, bf16x3 MFMA, fp64 accumulate",
              "fast4": "fp32 in, bf16x4 MFMA, fp64 accumulate"}[head]
     if w.rank == 0:
@@ -92,6 +107,12 @@ def main(argv=None):
 
             cpu = pca_proxy(t.to_numpy(w.ctx, 0, min(a.cpu_rows, n_loc)), a.k, a.rows)
             extra["cpu_baseline"] = cpu
+        if fp64_cmp is not None:
+            extra["exact_fp64_engine"] = fp64_cmp[0]
+            ev_a = np.asarray(res["exact"][1]["explained_variance"])
+            ev_b = np.asarray(fp64_cmp[1]["explained_variance"])
+            extra["exact_fp64_engine"]["max_abs_ev_diff_vs_int8"] = float(
+                np.max(np.abs(ev_a - ev_b)))
         for m in modes[1:]:
             extra[m + "_mode"] = res[m][0]
             ev_a = np.asarray(res[head][1]["explained_variance"])

@@ -54,6 +54,8 @@ void register_pca(py::module_& m) {
         out["eig_tridiag_ms"] = r.eig_tridiag_ms;
         out["eig_host_ms"] = r.eig_host_ms;
         out["eig_backtransform_ms"] = r.eig_backtransform_ms;
+        out["engine"] = r.engine;
+        out["err_bound"] = r.err_bound;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("k"),
@@ -76,6 +78,8 @@ void register_pca(py::module_& m) {
         out["n"] = c.n;
         out["stats_ms"] = c.stats_ms;
         out["allreduce_ms"] = c.allreduce_ms;
+        out["engine"] = c.engine;
+        out["err_bound"] = c.err_bound;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("precise") = false,

@@ -1307,8 +1307,8 @@ static bool final_cost_from_stats(Context& ctx, Comm& comm, DenseTable& x, const
 }
 
 // One fit attempt.  When the provisional fixed-point bounds fail (a row past its column's bound)
-// it stores the initial centers in *restart_with and returns at once; kmeans_fit then reruns the fit
-// with the column maxima's scales after this frame — and every buffer it held — has unwound.
+// it stores the initial centers in *restart_with and returns at once; kmeans_fit then reruns the
+// fit with the column maxima's scales after this frame — and every buffer it held — has unwound.
 static KMeansResult kmeans_fit_once(Context& ctx, Comm& comm, DenseTable& x,
                                     const std::vector<double>& init_centers,
                                     const KMeansParams& p, std::vector<double>* restart_with) {

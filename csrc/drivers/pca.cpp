@@ -7,6 +7,7 @@
 #include "kernels/kernels.h"
 #include "linalg/eigen.h"
 #include "linalg/eigen_gpu.h"
+#include "runtime/knobs.h"
 #include "runtime/log.h"
 
 namespace oap {
@@ -90,52 +91,87 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
               "GPU PCA expects an f32 table (f32 or f64 in exact mode)");
     ctx.activate();
     hipStream_t s = ctx.compute();
-    const kern::PcaPlan plan = p.exact ? kern::pca_syrk_plan_f64(x.rows, d, ctx.info().cu_count)
-                                       : kern::pca_syrk_plan(x.rows, d, ctx.info().cu_count);
-    Buffer part = ctx.alloc(plan.part_elems * sizeof(double));
-    Buffer cpart = ctx.alloc(plan.cpart_elems * sizeof(double));
-    Buffer shf = ctx.alloc(plan.shift_elems * sizeof(double));
-    Buffer out = ctx.alloc(cnt * sizeof(double));
-    if (p.exact) {  // the fp64 shift itself (no fp32 rounding: exact mode subtracts in fp64)
-      std::vector<double> hs(plan.shift_elems, 0.0);
-      for (int c = 0; c < d; ++c) hs[c] = shift[c];
-      ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(double), s);
+    // exact mode on f32 rows: the int8 digit products (kernels/pca_ozaki.hip); the fp64 MFMA
+    // for f64 rows (their 53-bit inputs would need more digits) or when the knob says so
+    const bool digits = p.exact && x.dtype == DType::F32 &&
+                        knob_str("OAP_PCA_EXACT_ENGINE") != "fp64";
+    res.engine = !p.exact ? "bf16_split" : digits ? "int8_digits" : "fp64_mfma";
+    // [S | c | bound]: the bound rides in the one allreduce (summed over the ranks)
+    const size_t cnt_x = cnt + (digits ? 1 : 0);
+    Buffer out = ctx.alloc(cnt_x * sizeof(double));
+    Buffer part, cpart, shf, ws;
+    kern::PcaPlan plan;
+    kern::PcaOzakiPlan oplan;
+    if (digits) {
+      size_t free_b = 0, total_b = 0;
+      OAP_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      // digit planes of one row chunk (7 bytes per padded element): at most 16 GiB (knob) and a
+      // third of what is free (the 40 GB bench table takes 5 chunks)
+      const size_t cap = std::min<size_t>(size_t(knob_int("OAP_PCA_DIGIT_CHUNK_BYTES")),
+                                          free_b / 3);
+      oplan = kern::pca_ozaki_plan(x.rows, d, ctx.info().cu_count, cap);
+      ws = ctx.alloc(oplan.ws_bytes);
     } else {
-      std::vector<float> hs(plan.shift_elems, 0.f);
-      for (int c = 0; c < d; ++c) hs[c] = float(shift[c]);
-      ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(float), s);
+      plan = p.exact ? kern::pca_syrk_plan_f64(x.rows, d, ctx.info().cu_count)
+                     : kern::pca_syrk_plan(x.rows, d, ctx.info().cu_count);
+      part = ctx.alloc(plan.part_elems * sizeof(double));
+      cpart = ctx.alloc(plan.cpart_elems * sizeof(double));
+      shf = ctx.alloc(plan.shift_elems * sizeof(double));
+      if (p.exact) {  // the fp64 shift itself (no fp32 rounding: exact mode subtracts in fp64)
+        std::vector<double> hs(plan.shift_elems, 0.0);
+        for (int c = 0; c < d; ++c) hs[c] = shift[c];
+        ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(double), s);
+      } else {
+        std::vector<float> hs(plan.shift_elems, 0.f);
+        for (int c = 0; c < d; ++c) hs[c] = float(shift[c]);
+        ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(float), s);
+      }
     }
     Event e0, e1, e2;
     e0.record(s);
     {
       TraceRange k(&ctx.metrics(), "pca/syrk_launch");
-      if (p.exact)
-        kern::pca_syrk_f64(x.data.data(), x.dtype == DType::F64, x.rows, x.ld, d,
-                           shf.as<double>(), plan, part.as<double>(), cpart.as<double>(), s);
-      else
-        kern::pca_syrk(x.data.as<float>(), x.rows, x.ld, d, shf.as<float>(), plan,
-                       part.as<double>(), cpart.as<double>(), p.precise, p.flush_rows, s);
-      kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), d, out.as<double>(),
-                       out.as<double>() + size_t(d) * d, s);
+      if (digits) {
+        kern::pca_syrk_ozaki(x.data.as<float>(), x.ld, shift.data(), oplan, ws.data(),
+                             out.as<double>(), out.as<double>() + size_t(d) * d,
+                             out.as<double>() + cnt, s);
+      } else {
+        if (p.exact)
+          kern::pca_syrk_f64(x.data.data(), x.dtype == DType::F64, x.rows, x.ld, d,
+                             shf.as<double>(), plan, part.as<double>(), cpart.as<double>(), s);
+        else
+          kern::pca_syrk(x.data.as<float>(), x.rows, x.ld, d, shf.as<float>(), plan,
+                         part.as<double>(), cpart.as<double>(), p.precise, p.flush_rows, s);
+        kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), d, out.as<double>(),
+                         out.as<double>() + size_t(d) * d, s);
+      }
     }
     e1.record(s);
-    comm_allreduce(ctx, comm, out.data(), cnt, DType::F64, ReduceOp::Sum, s);
+    comm_allreduce(ctx, comm, out.data(), cnt_x, DType::F64, ReduceOp::Sum, s);
     if (comm.on_device()) comm.wait(s);
     e2.record(s);
+    double bound_s = 0.0;
     if (device_cov) {  // the covariance stays on the device; only c comes back (the mean)
       res.dev_cov = ctx.alloc(sizeof(double) * size_t(d) * d);
       kern::pca_cov(out.as<double>(), d, res.n, res.dev_cov.as<double>(), s);
-      ctx.copy_to_host(stats.data() + size_t(d) * d, out.as<double>() + size_t(d) * d,
-                       size_t(d) * sizeof(double));
+      std::vector<double> tail(size_t(d) + (digits ? 1 : 0));
+      ctx.copy_to_host(tail.data(), out.as<double>() + size_t(d) * d, tail.size() * sizeof(double));
+      std::copy(tail.begin(), tail.begin() + d, stats.begin() + size_t(d) * d);
+      if (digits) bound_s = tail[d];
     } else {
-      ctx.copy_to_host(stats.data(), out.data(), cnt * sizeof(double));
+      std::vector<double> all(cnt_x);
+      ctx.copy_to_host(all.data(), out.data(), cnt_x * sizeof(double));
+      std::copy(all.begin(), all.begin() + cnt, stats.begin());
+      if (digits) bound_s = all[cnt];
     }
+    res.err_bound = bound_s / double(res.n - 1);
     res.stats_ms = Event::elapsed_ms(e0, e1);
     res.allreduce_ms = Event::elapsed_ms(e1, e2);
     ctx.metrics().add("pca/syrk_kernel", res.stats_ms * 1e3,
                       int64_t(x.rows) * x.ld * int64_t(sizeof(float)));
     ctx.metrics().add("pca/allreduce", res.allreduce_ms * 1e3, int64_t(cnt * sizeof(double)));
   } else {
+    res.engine = "cpu";
     auto t0 = std::chrono::steady_clock::now();
     cpu_stats(ctx, x, shift, stats);
     res.stats_ms = ms_since(t0);
@@ -171,6 +207,8 @@ PcaResult pca_fit(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p) {
   r.mean = cv.mean;
   r.stats_ms = cv.stats_ms;
   r.allreduce_ms = cv.allreduce_ms;
+  r.engine = cv.engine;
+  r.err_bound = cv.err_bound;
   auto t1 = std::chrono::steady_clock::now();
   SymEig eg;
   {

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 #include "comm/comm.h"
@@ -39,6 +40,12 @@ struct PcaCovariance {
   // GPU engine with device_cov requested: `cov` stays empty and the covariance is here instead
   // ([d][d] doubles on the device; the GPU eigensolver reads it without a host round trip)
   Buffer dev_cov;
+  // which kernel formed S: "int8_digits" (exact mode, f32 rows: kernels/pca_ozaki.hip),
+  // "fp64_mfma" (exact mode, f64 rows or OAP_PCA_EXACT_ENGINE=fp64), "bf16_split" (fast), "cpu"
+  std::string engine;
+  // int8_digits: a bound on max_jk |cov_jk - cov_exact_jk| from the digit products (the
+  // statistics' own error; the fp64 correction c c^T / n is the fp64 path's); else 0
+  double err_bound = 0.0;
 };
 
 struct PcaResult {
@@ -51,6 +58,8 @@ struct PcaResult {
   double stats_ms = 0.0, allreduce_ms = 0.0, eig_ms = 0.0, total_ms = 0.0;
   bool eig_on_gpu = false;
   double eig_tridiag_ms = 0.0, eig_host_ms = 0.0, eig_backtransform_ms = 0.0;
+  std::string engine;       // PcaCovariance::engine
+  double err_bound = 0.0;   // PcaCovariance::err_bound
 };
 
 PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p,

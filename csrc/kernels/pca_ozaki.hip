@@ -1,0 +1,433 @@
+// PCA exact-mode statistics on the int8 matrix cores (integer-sliced, Ozaki-style SYRK).
+//
+// The reference forms every product (x_i - s_i)(x_j - s_j) and its sum in fp64 (oneDAL
+// step1Local, mllib-dal/src/main/native/PCADALImpl.cpp:31,63-69).  The fp64 MFMA path
+// (pca.hip, oap_pca_syrk_f64) does the same at ~78 TFLOP/s peak.  Here the centred rows are
+// written as 7 signed base-128 digits per element, relative to a per-column power of two, and the
+// products of digits run on v_mfma_i32_32x32x32_i8 (int8 in, int32 accumulate: exact), 64x the
+// fp64 MFMA rate per instruction; 28 digit products (p + q <= 6) replace one fp64 product.
+//
+//   v = x - s (fp64),  M_j = max_i |v_ij| < 2^E_j,
+//   v = 2^(E-6) (t_0 + t_1 2^-7 + ... + t_6 2^-42 + rho),   t_p in [-64, 64],  |rho| <= 2^-43
+//   S_jk = sum_i v_ij v_ik ~= 2^(E_j + E_k - 12) sum_{L=0..6} 2^(-7L) sum_{p+q=L} sum_i t_p t_q
+//
+// Error per row (the bound pca.cpp reports, docs/ARCHITECTURE.md "PCA exact"):
+//   |v_j v_k - approx| <= 2^(E_j+E_k-49) (2 [representation] + 6.04 [dropped p+q >= 7])
+// i.e. <= 8.05 * 2^-49 * 4 M_j M_k, plus the fp64 rounding of v and of the slab sums that the fp64
+// path has too.  The level sums are exact integers: |t_p t_q| <= 2^12, at most 7 products per
+// level and row, so 2048 row blocks (65536 rows) stay below 2^31 before an fp64 flush.
+//
+// Kernels (one fit = one minmax pass over all rows, then per row chunk: slice + SYRK):
+//   oap_oz_minmax   column min / max of x per row group (fp32, exact)
+//   oap_oz_exponent E_j and the scale 2^(6 - E_j) from max(xmax - s, s - xmin) (fp64)
+//   oap_oz_slice    the 7 digit planes [p][row block][feature][32 rows] int8 + fp64 column sums
+//   oap_oz_syrk     128 x 64 output tile per 4-wave workgroup (each wave 32 x 64: 7 levels x 2
+//                   blocks of 32 x 32 int32 accumulators = 224 registers); the digit fragments of
+//                   one 32-row block are 16-byte loads straight from the planes (a fragment is a
+//                   contiguous 1 KB), double-buffered in registers one row block ahead
+//   oap_oz_reduce   sum of the split slabs (fixed order), times 2^(E_i + E_j - 12), both halves
+#include "kernels/device_utils.h"
+#include "kernels/kernels.h"
+#include "runtime/common.h"
+
+namespace oap {
+namespace kern {
+
+namespace {
+
+constexpr int kOzDigits = 7;
+constexpr int kOzRB = 32;          // rows per row block (the MFMA's k)
+constexpr int kOzTI = 128, kOzTJ = 64;
+constexpr int kOzThreads = 256;
+constexpr int kOzFlush = 2048;     // row blocks per int32 flush (7 * 2^12 * 32 * 2048 < 2^31)
+constexpr int kOzRowGroup = 2048;  // rows per minmax partial
+constexpr int kOzSliceRB = 16;     // row blocks per slice-kernel block (one column-sum partial)
+constexpr int kOzFeat = 256;       // features per minmax / slice block
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(kOzFeat) void oap_oz_minmax(const float* __restrict__ x, int64_t n,
+                                                          int64_t ld, int d, int dp,
+                                                          float2* __restrict__ mm) {
+  const int f = blockIdx.y * kOzFeat + threadIdx.x;
+  const int64_t r0 = int64_t(blockIdx.x) * kOzRowGroup;
+  const int64_t r1 = min(n, r0 + kOzRowGroup);
+  float lo = INFINITY, hi = -INFINITY;
+  if (f < d) {
+    const float* p = x + r0 * ld + f;
+    int64_t r = r0;
+    for (; r + 8 <= r1; r += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(r - r0 + u) * ld];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        lo = fminf(lo, v[u]);
+        hi = fmaxf(hi, v[u]);
+      }
+    }
+    for (; r < r1; ++r) {
+      const float v = p[(r - r0) * ld];
+      lo = fminf(lo, v);
+      hi = fmaxf(hi, v);
+    }
+  }
+  if (f < dp) mm[size_t(blockIdx.x) * dp + f] = make_float2(lo, hi);
+}
+
+__global__ __launch_bounds__(256) void oap_oz_exponent(const float2* __restrict__ mm, int groups,
+                                                        int d, int dp,
+                                                        const double* __restrict__ shift,
+                                                        int* __restrict__ E,
+                                                        double* __restrict__ sc) {
+  __shared__ float slo[256], shi[256];
+  const int f = blockIdx.x;
+  float lo = INFINITY, hi = -INFINITY;
+  if (f < d)
+    for (int g = threadIdx.x; g < groups; g += 256) {
+      const float2 v = mm[size_t(g) * dp + f];
+      lo = fminf(lo, v.x);
+      hi = fmaxf(hi, v.y);
+    }
+  slo[threadIdx.x] = lo;
+  shi[threadIdx.x] = hi;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      slo[threadIdx.x] = fminf(slo[threadIdx.x], slo[threadIdx.x + w]);
+      shi[threadIdx.x] = fmaxf(shi[threadIdx.x], shi[threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int e = 0;
+    if (f < d && groups > 0) {
+      // the slice kernel's v = (double)x - s is monotone in x: its extreme values are these
+      const double s = shift[f];
+      const double m = fmax(double(shi[0]) - s, s - double(slo[0]));
+      if (m > 0.0 && m <= 1.7e308) e = min(max(ilogb(m) + 1, -900), 1000);  // m < 2^e
+    }
+    E[f] = e;
+    sc[f] = ldexp(1.0, 6 - e);
+  }
+}
+
+// digits of 32 rows of one feature per thread: 7 x 32 bytes (two 16-byte stores per digit plane)
+__global__ __launch_bounds__(kOzFeat) void oap_oz_slice(
+    const float* __restrict__ x, int64_t n, int64_t ld, int d, int dp, int64_t row0,
+    int64_t nrb, const double* __restrict__ shift, const double* __restrict__ sc,
+    int8_t* __restrict__ planes, double* __restrict__ cpart, int64_t group0) {
+  const int f = blockIdx.y * kOzFeat + threadIdx.x;
+  if (f >= dp) return;
+  const int64_t rb0 = int64_t(blockIdx.x) * kOzSliceRB;
+  const int64_t rb1 = min(nrb, rb0 + kOzSliceRB);
+  const bool okf = f < d;
+  const double s = okf ? shift[f] : 0.0, scale = okf ? sc[f] : 0.0;
+  const size_t plane = size_t(nrb) * dp * kOzRB;
+  double csum = 0.0;
+  for (int64_t rb = rb0; rb < rb1; ++rb) {
+    const int64_t r = row0 + rb * kOzRB;
+    float xv[kOzRB];
+#pragma unroll
+    for (int i = 0; i < kOzRB; ++i)
+      xv[i] = (okf && r + i < n) ? x[(r + i) * ld + f] : 0.f;
+    unsigned pk[kOzDigits][kOzRB / 4];
+#pragma unroll
+    for (int p = 0; p < kOzDigits; ++p)
+#pragma unroll
+      for (int q = 0; q < kOzRB / 4; ++q) pk[p][q] = 0u;
+#pragma unroll
+    for (int i = 0; i < kOzRB; ++i) {
+      const bool ok = okf && r + i < n;
+      const double v = ok ? double(xv[i]) - s : 0.0;
+      csum += v;
+      double w = v * scale;  // exact (power of two), |w| < 64
+      double t = __builtin_rint(w);
+      pk[0][i >> 2] |= (unsigned(int(t)) & 0xffu) << (8 * (i & 3));
+      w -= t;  // exact: |w| <= 1/2
+#pragma unroll
+      for (int p = 1; p < kOzDigits; ++p) {
+        w *= 128.0;
+        t = __builtin_rint(w);
+        pk[p][i >> 2] |= (unsigned(int(t)) & 0xffu) << (8 * (i & 3));
+        w -= t;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kOzDigits; ++p) {
+      v4i* o = reinterpret_cast<v4i*>(planes + p * plane + (size_t(rb) * dp + f) * kOzRB);
+      o[0] = v4i{int(pk[p][0]), int(pk[p][1]), int(pk[p][2]), int(pk[p][3])};
+      o[1] = v4i{int(pk[p][4]), int(pk[p][5]), int(pk[p][6]), int(pk[p][7])};
+    }
+  }
+  cpart[size_t(group0 + blockIdx.x) * dp + f] = csum;
+}
+
+struct OzArgs {
+  const int8_t* planes;  // [7][nrb][dp][32]
+  int64_t nrb;
+  int dp, nbj, tiles;
+  int64_t rb_per_split;
+  double* slab;  // [splits][tiles][128][64], accumulated (+=)
+};
+
+__device__ inline void oz_tile(int tile, int nbj, int& bi, int& bj) {
+  int t = tile, b = 0;
+  while (t >= nbj - 2 * b) {
+    t -= nbj - 2 * b;
+    ++b;
+  }
+  bi = b;
+  bj = 2 * b + t;
+}
+
+__global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
+  const int G = gridDim.x;
+  const int per = G / 8;  // XCD-aware: the tiles of one split share an XCD (its L2)
+  const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  const int split = L / a.tiles, tile = L - split * a.tiles;
+  const int64_t rb0 = int64_t(split) * a.rb_per_split;
+  const int64_t rb1 = min(a.nrb, rb0 + a.rb_per_split);
+  if (rb0 >= rb1) return;
+  int bi, bj;
+  oz_tile(tile, a.nbj, bi, bj);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const size_t plane = size_t(a.nrb) * a.dp * kOzRB;
+  const size_t rbs = size_t(a.dp) * kOzRB;
+  // fragment: lane l holds feature f0 + (l & 31), rows 16 (l >> 5) .. + 15 of the row block —
+  // the same k order for A and B, which is all the sum over k needs.  Uniform bases + one
+  // per-lane 32-bit offset: every load is saddr + voffset (no 64-bit address per load).
+  const unsigned loff = unsigned(lane & 31) * kOzRB + 16u * unsigned(lane >> 5);
+  const int8_t* pa = a.planes + size_t(bi * kOzTI + 32 * wave) * kOzRB;
+  const int8_t* pb = a.planes + size_t(bj * kOzTJ) * kOzRB;
+
+  v16i acc[kOzDigits][2];
+#pragma unroll
+  for (int l = 0; l < kOzDigits; ++l)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[l][y][e] = 0;
+
+  double* slab = a.slab + (size_t(split) * a.tiles + tile) * (kOzTI * kOzTJ);
+  auto flush = [&]() {
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        double v = double(acc[kOzDigits - 1][y][e]);
+#pragma unroll
+        for (int l = kOzDigits - 2; l >= 0; --l) v = fma(v, 0x1p-7, double(acc[l][y][e]));
+        const int row = 32 * wave + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        const int col = 32 * y + (lane & 31);
+        slab[row * kOzTJ + col] += v;
+      }
+#pragma unroll
+    for (int l = 0; l < kOzDigits; ++l)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[l][y][e] = 0;
+  };
+
+  v4i fa[2][kOzDigits], fb[2][kOzDigits][2];
+  // unconditional (the block index is clamped to the split's last): no divergent joins
+  auto load = [&](int64_t rb, v4i (&A)[kOzDigits], v4i (&B)[kOzDigits][2]) {
+    const size_t o = size_t(min(rb, rb1 - 1)) * rbs;
+#pragma unroll
+    for (int p = 0; p < kOzDigits; ++p) {
+      const int8_t* ba = pa + p * plane + o;
+      const int8_t* bb = pb + p * plane + o;
+      A[p] = *reinterpret_cast<const v4i*>(ba + loff);
+      B[p][0] = *reinterpret_cast<const v4i*>(bb + loff);
+      B[p][1] = *reinterpret_cast<const v4i*>(bb + loff + 32 * kOzRB);
+    }
+  };
+  auto step = [&](const v4i (&A)[kOzDigits], const v4i (&B)[kOzDigits][2]) {
+#pragma unroll
+    for (int l = 0; l < kOzDigits; ++l)
+#pragma unroll
+      for (int p = 0; p <= l; ++p)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+          acc[l][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[p], B[l - p][y], acc[l][y], 0, 0, 0);
+  };
+  // int32 sums over at most kOzFlush row blocks, then one fp64 flush (no fragment is live across
+  // it: each run of blocks loads its own first one)
+  for (int64_t c0 = rb0; c0 < rb1; c0 += kOzFlush) {
+    const int64_t c1 = min(rb1, c0 + kOzFlush);
+    load(c0, fa[0], fb[0]);
+    for (int64_t rb = c0; rb < c1; rb += 2) {
+      load(min(rb + 1, c1 - 1), fa[1], fb[1]);
+      step(fa[0], fb[0]);
+      const bool two = rb + 1 < c1;
+      load(min(rb + 2, c1 - 1), fa[0], fb[0]);
+      if (two) step(fa[1], fb[1]);
+    }
+    flush();
+  }
+}
+
+__global__ __launch_bounds__(256) void oap_oz_reduce(const double* __restrict__ slab, int splits,
+                                                      int tiles, int nbj, int d,
+                                                      const int* __restrict__ E,
+                                                      double* __restrict__ out) {
+  const int64_t total = int64_t(d) * d;
+  for (int64_t idx = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * blockDim.x) {
+    const int i = static_cast<int>(idx / d), j = static_cast<int>(idx - int64_t(i) * d);
+    if (i > j) continue;
+    const int bi = i / kOzTI, bj = j / kOzTJ;
+    const int tile = bi * nbj - bi * (bi - 1) + (bj - 2 * bi);
+    const size_t e = size_t(i - bi * kOzTI) * kOzTJ + (j - bj * kOzTJ);
+    double s = 0.0;
+    for (int sp = 0; sp < splits; ++sp)
+      s += slab[(size_t(sp) * tiles + tile) * (kOzTI * kOzTJ) + e];
+    const double v = ldexp(s, E[i] + E[j] - 12);
+    out[size_t(i) * d + j] = v;
+    out[size_t(j) * d + i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void oap_oz_colsum(const double* __restrict__ cpart,
+                                                      int64_t groups, int dp,
+                                                      double* __restrict__ colsum) {
+  __shared__ double sh[256];
+  const int f = blockIdx.x;
+  double s = 0.0;
+  for (int64_t g = threadIdx.x; g < groups; g += 256) s += cpart[size_t(g) * dp + f];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) colsum[f] = sh[0];
+}
+
+// *bound = rows * 2^(2 max_j E_j) * coef: the per-entry bound on |S - S_exact| (pca.cpp)
+__global__ __launch_bounds__(256) void oap_oz_bound(const int* __restrict__ E, int d, double rows,
+                                                     double coef, double* __restrict__ bound) {
+  __shared__ int sh[256];
+  int m = INT_MIN;
+  for (int f = threadIdx.x; f < d; f += 256) m = max(m, E[f]);
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) sh[threadIdx.x] = max(sh[threadIdx.x], sh[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bound[0] = rows > 0 ? ldexp(rows * coef, 2 * sh[0]) : 0.0;
+}
+
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+}  // namespace
+
+PcaOzakiPlan pca_ozaki_plan(int64_t n, int d, int num_cus, size_t max_plane_bytes) {
+  PcaOzakiPlan p;
+  p.n = n;
+  p.d = d;
+  p.dp = int(round_up(size_t(std::max(d, 1)), kOzTI));
+  p.nbj = p.dp / kOzTJ;
+  p.tiles = 0;
+  for (int b = 0; b < p.dp / kOzTI; ++b) p.tiles += p.nbj - 2 * b;
+  p.nrb = (n + kOzRB - 1) / kOzRB;
+  p.groups = (n + kOzRowGroup - 1) / kOzRowGroup;
+  // row blocks per chunk: the digit planes of one chunk within max_plane_bytes, whole slice
+  // groups (so the column-sum partials of all chunks tile one array)
+  const size_t per_rb = size_t(kOzDigits) * p.dp * kOzRB;
+  int64_t crb = int64_t(std::max<size_t>(1, max_plane_bytes / per_rb));
+  crb = std::max<int64_t>(kOzSliceRB, crb / kOzSliceRB * kOzSliceRB);
+  p.chunk_rb = std::min<int64_t>(round_up(size_t(std::max<int64_t>(p.nrb, 1)), kOzSliceRB), crb);
+  p.chunks = std::max<int64_t>(1, (p.nrb + p.chunk_rb - 1) / p.chunk_rb);
+  p.cgroups = (p.nrb + kOzSliceRB - 1) / kOzSliceRB;
+  // one 256-thread workgroup per CU (~400 registers per lane): splits x tiles in whole rounds of
+  // the CUs, at least two rounds when the rows allow
+  const int64_t R = std::max(num_cus, 64);
+  const int64_t s_lo = std::max<int64_t>(1, (2 * R + p.tiles - 1) / p.tiles);
+  int64_t s = s_lo;
+  double best = 1e30;
+  for (int64_t c = s_lo; c <= 4 * s_lo; ++c) {
+    const int64_t g = c * p.tiles;
+    const double waste = double((g + R - 1) / R * R) / double(g);
+    if (waste < best - 1e-9) {
+      best = waste;
+      s = c;
+    }
+  }
+  s = std::max<int64_t>(1, std::min<int64_t>(s, std::max<int64_t>(1, p.chunk_rb / 8)));
+  p.splits = int(s);
+  // longest chain of fp64 additions into one output: the slab flushes of a split over all
+  // chunks, the sum over splits, the final scaling
+  const int64_t rps = (p.chunk_rb + s - 1) / s;
+  p.fp64_adds = int(p.chunks * ((rps + kOzFlush - 1) / kOzFlush) + s + 2);
+  p.slab_elems = size_t(p.splits) * p.tiles * kOzTI * kOzTJ;
+  // workspace: planes | slab | minmax partials | E | scale | shift | column-sum partials
+  p.off_slab = align256(size_t(p.chunk_rb) * per_rb);
+  p.off_mm = p.off_slab + align256(p.slab_elems * sizeof(double));
+  p.off_e = p.off_mm + align256(size_t(std::max<int64_t>(p.groups, 1)) * p.dp * sizeof(float2));
+  p.off_sc = p.off_e + align256(size_t(p.dp) * sizeof(int));
+  p.off_shift = p.off_sc + align256(size_t(p.dp) * sizeof(double));
+  p.off_cpart = p.off_shift + align256(size_t(p.dp) * sizeof(double));
+  p.ws_bytes =
+      p.off_cpart + align256(size_t(std::max<int64_t>(p.cgroups, 1)) * p.dp * sizeof(double));
+  return p;
+}
+
+void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const PcaOzakiPlan& p,
+                    void* ws, double* out, double* colsum, double* bound, hipStream_t s) {
+  OAP_CHECK(ld >= p.d, "pca_syrk_ozaki: bad ld");
+  char* w = static_cast<char*>(ws);
+  int8_t* planes = reinterpret_cast<int8_t*>(w);
+  double* slab = reinterpret_cast<double*>(w + p.off_slab);
+  float2* mm = reinterpret_cast<float2*>(w + p.off_mm);
+  int* E = reinterpret_cast<int*>(w + p.off_e);
+  double* sc = reinterpret_cast<double*>(w + p.off_sc);
+  double* shift = reinterpret_cast<double*>(w + p.off_shift);
+  double* cpart = reinterpret_cast<double*>(w + p.off_cpart);
+  OAP_HIP_CHECK(hipMemcpyAsync(shift, shift_host, size_t(p.d) * sizeof(double),
+                               hipMemcpyHostToDevice, s));
+  OAP_HIP_CHECK(hipMemsetAsync(slab, 0, p.slab_elems * sizeof(double), s));
+  const int fblocks = p.dp / kOzFeat + (p.dp % kOzFeat ? 1 : 0);
+  if (p.groups > 0)
+    hipLaunchKernelGGL(oap_oz_minmax, dim3(unsigned(p.groups), fblocks), dim3(kOzFeat), 0, s, x,
+                       p.n, ld, p.d, p.dp, mm);
+  hipLaunchKernelGGL(oap_oz_exponent, dim3(p.dp), dim3(256), 0, s, mm, int(p.groups), p.d, p.dp,
+                     shift, E, sc);
+  OAP_HIP_CHECK(hipGetLastError());
+  const int64_t G = round_up(size_t(p.splits) * p.tiles, 8);
+  for (int64_t c = 0; c < p.chunks; ++c) {
+    const int64_t rb0 = c * p.chunk_rb;
+    const int64_t nrb = std::min<int64_t>(p.chunk_rb, p.nrb - rb0);
+    if (nrb <= 0) break;
+    const int64_t sg = (nrb + kOzSliceRB - 1) / kOzSliceRB;
+    hipLaunchKernelGGL(oap_oz_slice, dim3(unsigned(sg), fblocks), dim3(kOzFeat), 0, s, x, p.n,
+                       ld, p.d, p.dp, rb0 * kOzRB, nrb, shift, sc, planes, cpart,
+                       rb0 / kOzSliceRB);
+    OzArgs a;
+    a.planes = planes;
+    a.nrb = nrb;
+    a.dp = p.dp;
+    a.nbj = p.nbj;
+    a.tiles = p.tiles;
+    a.rb_per_split = (nrb + p.splits - 1) / p.splits;
+    a.slab = slab;
+    hipLaunchKernelGGL(oap_oz_syrk, dim3(unsigned(G)), dim3(kOzThreads), 0, s, a);
+    OAP_HIP_CHECK(hipGetLastError());
+  }
+  const int64_t total = int64_t(p.d) * p.d;
+  hipLaunchKernelGGL(oap_oz_reduce, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s, slab,
+                     p.splits, p.tiles, p.nbj, p.d, E, out);
+  hipLaunchKernelGGL(oap_oz_colsum, dim3(p.d), dim3(256), 0, s, cpart, p.cgroups, p.dp, colsum);
+  // per row: 2^(E_j+E_k-49) (2 representation + 6.04 dropped digit products + 2^-4 rounding of
+  // v) + 2^(E_j+E_k-53) per fp64 addition of the longest chain
+  const double coef = 0x1p-49 * (8.04 + 0.0625) + 0x1p-53 * p.fp64_adds;
+  hipLaunchKernelGGL(oap_oz_bound, dim3(1), dim3(256), 0, s, E, p.d, double(p.n), coef, bound);
+  OAP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace kern
+}  // namespace oap

@@ -47,7 +47,13 @@ const std::vector<KnobInfo> kKnobs = {
     {"OAP_ALS_ABLATE", "0", "timing ablations of the ALS solve kernels (bit mask)"},
     {"OAP_ALS_LR3_OCC", "0", "waves per SIMD of the 33-48-rating low-rank class (0: default)"},
     {"OAP_ALS_ROTATE_VALU", "0", "1: factor rotations on the VALU instead of MFMA"},
-    // ---- PCA eigensolver
+    // ---- PCA
+    {"OAP_PCA_EXACT_ENGINE", "int8",
+     "exact mode on f32 rows: 'int8' digit products on the int8 MFMA (error bound reported), "
+     "'fp64' fp64 products on the fp64 MFMA"},
+    {"OAP_PCA_DIGIT_CHUNK_BYTES", "17179869184",
+     "int8 exact engine: digit planes of one row chunk at most this many bytes (and a third of "
+     "the free HBM)"},
     {"OAP_EIG_GRID", "0", "workgroups of the fused tridiagonalisation (0: one per CU)"},
     {"OAP_EIG_HOST_INVIT", "0", "1: inverse iteration on the host thread pool"},
     // ---- collectives, fault injection, logging

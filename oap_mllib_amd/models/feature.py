@@ -94,7 +94,9 @@ class PCA(_PCAParams, Estimator, DefaultParamsPersistence):
             extra["precision"] = precision
             extra["device_rows_dtype"] = table.dtype
             pc, ev = np.asarray(r["pc"]), np.asarray(r["explained_variance"])
-            extra.update({k_: r[k_] for k_ in ("stats_ms", "allreduce_ms", "eig_ms", "total_ms")})
+            extra.update({k_: r[k_] for k_ in ("stats_ms", "allreduce_ms", "eig_ms", "total_ms",
+                                               "err_bound")})
+            extra["stats_engine"] = r["engine"]  # int8_digits | fp64_mfma | bf16_split
         model = PCAModel(uid=self.uid, pc=DenseMatrix.from_array(pc),
                          explainedVariance=DenseVector(ev))
         self._copyValues(model)

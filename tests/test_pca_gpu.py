@@ -180,3 +180,73 @@ def test_exact_f64_rows_beyond_budget_go_up_as_f32(gpu_world):
         np.testing.assert_allclose(f.explainedVariance.toArray(), wr[:3] / wr.sum(), rtol=1e-10)
     finally:
         O.set_config(O.get_config().replace(hbm_budget_bytes=0))
+
+
+# ------------------------------------------------- exact mode on the int8 matrix cores (Ozaki)
+def _cov_exact_full(native, w, X):
+    from oap_mllib_amd.models.clustering import upload_table
+
+    t = upload_table(w, X, layout="pca_exact")
+    return native.pca_covariance(w.ctx, w.comm, t, False, exact=True)
+
+
+@pytest.mark.parametrize("n,d,offset,spread", [(7, 3, 0.0, 1.0), (3001, 50, 5.0, 1.0),
+                                               (4099, 129, 3e3, 1.0), (2500, 300, 0.0, 1e3),
+                                               (20000, 1000, 1.0, 1.0)])
+def test_exact_int8_digits_within_bound(native, gpu_world, n, d, offset, spread):
+    """f32 rows in exact mode run on the int8 digit products (kernels/pca_ozaki.hip): the error
+    against np.cov of the same rows stays inside the bound the kernel reports, the bound itself
+    is far below the 1e-12 the exact-mode tests ask for, and the fp64-MFMA engine agrees."""
+    rng = np.random.default_rng(n + d)
+    X = (rng.normal(size=(n, d)) * np.geomspace(1.0, spread, d) + offset).astype(np.float32)
+    r = _cov_exact_full(native, gpu_world, X)
+    assert r["engine"] == "int8_digits"
+    C = np.asarray(r["cov"])
+    Cr = np.cov(X.astype(np.float64).T, ddof=1)
+    err = np.max(np.abs(C - Cr))
+    scale = np.max(np.abs(Cr))
+    assert err / scale < 1e-12, err / scale
+    assert 0 < r["err_bound"] < 1e-10 * scale
+    # np.cov's own rounding (fp64 sums of n products) is the slack next to the bound
+    M = np.abs(X.astype(np.float64) - X.mean(0)).max()
+    assert err <= r["err_bound"] + n * 2.0 ** -52 * M * M / (n - 1)
+    native.set_knob("OAP_PCA_EXACT_ENGINE", "fp64")
+    try:
+        f = _cov_exact_full(native, gpu_world, X)
+    finally:
+        native.set_knob("OAP_PCA_EXACT_ENGINE", "")
+    assert f["engine"] == "fp64_mfma"
+    assert np.max(np.abs(np.asarray(f["cov"]) - C)) / scale < 1e-12
+    assert np.array_equal(C, C.T)
+
+
+def test_exact_int8_digits_row_chunks_and_determinism(native, gpu_world):
+    """Several digit-plane row chunks (a small chunk budget) give the statistics of one chunk to
+    fp64 rounding, and repeated fits are bitwise equal."""
+    rng = np.random.default_rng(77)
+    X = (rng.normal(size=(9000, 70)) * 3 + 2).astype(np.float32)
+    one = _cov_exact_full(native, gpu_world, X)
+    native.set_knob("OAP_PCA_DIGIT_CHUNK_BYTES", str(1 << 20))  # 1 MiB: 5 chunks of 2048 rows
+    try:
+        many = _cov_exact_full(native, gpu_world, X)
+        again = _cov_exact_full(native, gpu_world, X)
+    finally:
+        native.set_knob("OAP_PCA_DIGIT_CHUNK_BYTES", "")
+    a, b = np.asarray(one["cov"]), np.asarray(many["cov"])
+    assert np.max(np.abs(a - b)) / np.max(np.abs(a)) < 1e-14
+    assert np.array_equal(b, np.asarray(again["cov"]))
+    np.testing.assert_allclose(many["mean"], X.astype(np.float64).mean(0), rtol=0, atol=1e-12 * 10)
+
+
+def test_exact_int8_digits_constant_and_zero_columns(native, gpu_world):
+    """A constant column (zero range: no exponent) and an all-zero column give exact zeros in
+    their rows and columns of the covariance."""
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(5000, 40)).astype(np.float32)
+    X[:, 5] = 7.25
+    X[:, 17] = 0.0
+    r = _cov_exact_full(native, gpu_world, X)
+    C = np.asarray(r["cov"])
+    assert np.all(C[5] == 0) and np.all(C[:, 17] == 0)
+    Cr = np.cov(X.astype(np.float64).T, ddof=1)
+    assert np.max(np.abs(C - Cr)) / np.max(np.abs(Cr)) < 1e-12

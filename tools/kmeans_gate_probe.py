@@ -40,6 +40,6 @@ for rep in range(reps):
         tol = kw.pop("tol", -1.0)
         r = N.kmeans_fit(g, comm, t, init, k, 20, tol, **kw)
         out[name].append((time.perf_counter() - t0) / r["num_iter"] * 1e3)
-print(json.dumps({"rows": rows, "comm": comm.name, "ms_per_step_median": {n: round(sorted(v)[len(v) // 2], 4)
-                                                       for n, v in out.items()},
+med = {n: round(sorted(v)[len(v) // 2], 4) for n, v in out.items()}
+print(json.dumps({"rows": rows, "comm": comm.name, "ms_per_step_median": med,
                   "all": out}, indent=1))
