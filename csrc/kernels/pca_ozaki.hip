@@ -23,8 +23,8 @@
 //   oap_oz_slice    the 7 digit planes [p][row block][feature][32 rows] int8 + fp64 column sums
 //   oap_oz_syrk     128 x 64 output tile per 4-wave workgroup (each wave 32 x 64: 7 levels x 2
 //                   blocks of 32 x 32 int32 accumulators = 224 registers); the digit fragments of
-//                   one 32-row block are 16-byte loads straight from the planes (a fragment is a
-//                   contiguous 1 KB), double-buffered in registers one row block ahead
+//                   a 32-row block (each a contiguous 1 KB of a plane) stage through LDS by
+//                   global_load_lds, three blocks deep, the B fragments shared by the 4 waves
 //   oap_oz_reduce   sum of the split slabs (fixed order), times 2^(E_i + E_j - 12), both halves
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
@@ -42,7 +42,13 @@ constexpr int kOzThreads = 256;
 constexpr int kOzFlush = 2048;     // row blocks per int32 flush (7 * 2^12 * 32 * 2048 < 2^31)
 constexpr int kOzRowGroup = 2048;  // rows per minmax partial
 constexpr int kOzSliceRB = 16;     // row blocks per slice-kernel block (one column-sum partial)
-constexpr int kOzFeat = 256;       // features per minmax / slice block
+constexpr int kOzFeat = 256;       // features per minmax block
+constexpr int kOzSliceFeat = 128;  // features per slice block (two threads each)
+
+constexpr int kOzGlds = kOzDigits + 4;                   // LDS-DMA loads per wave and stage
+constexpr int kOzStage = (4 * kOzDigits + 2 * kOzDigits) * 1024;  // 42 KB: A 4 x 7, B 2 x 7
+// s_waitcnt vmcnt(kOzGlds) (expcnt / lgkmcnt not waited): one stage may stay in flight
+constexpr int kOzVmcntStage = (kOzGlds & 15) | ((kOzGlds >> 4) << 14) | (7 << 4) | (15 << 8);
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
@@ -113,32 +119,38 @@ __global__ __launch_bounds__(256) void oap_oz_exponent(const float2* __restrict_
   }
 }
 
-// digits of 32 rows of one feature per thread: 7 x 32 bytes (two 16-byte stores per digit plane)
-__global__ __launch_bounds__(kOzFeat) void oap_oz_slice(
+// digits of 16 rows of one feature per thread, two threads (adjacent lanes) per feature: lane l
+// covers feature f0 + l / 2, rows 16 (l & 1) .. + 15 of each row block, so one wave's store of a
+// digit plane is a contiguous 1 KB (32 features x 32 bytes)
+__global__ __launch_bounds__(256) void oap_oz_slice(
     const float* __restrict__ x, int64_t n, int64_t ld, int d, int dp, int64_t row0,
     int64_t nrb, const double* __restrict__ shift, const double* __restrict__ sc,
     int8_t* __restrict__ planes, double* __restrict__ cpart, int64_t group0) {
-  const int f = blockIdx.y * kOzFeat + threadIdx.x;
-  if (f >= dp) return;
+  const int f = blockIdx.y * kOzSliceFeat + (threadIdx.x >> 1);
+  const int half = threadIdx.x & 1;
   const int64_t rb0 = int64_t(blockIdx.x) * kOzSliceRB;
   const int64_t rb1 = min(nrb, rb0 + kOzSliceRB);
   const bool okf = f < d;
   const double s = okf ? shift[f] : 0.0, scale = okf ? sc[f] : 0.0;
   const size_t plane = size_t(nrb) * dp * kOzRB;
   double csum = 0.0;
-  for (int64_t rb = rb0; rb < rb1; ++rb) {
-    const int64_t r = row0 + rb * kOzRB;
-    float xv[kOzRB];
+  // rows of block rb + 1 in flight while block rb is digitised (unconditional loads: rows
+  // clamped to n - 1, features to 0; masked below)
+  const int fl = okf ? f : 0;
+  auto load = [&](int64_t rb, float (&v)[16]) {
+    const int64_t r = row0 + min(rb, rb1 - 1) * kOzRB + 16 * half;
 #pragma unroll
-    for (int i = 0; i < kOzRB; ++i)
-      xv[i] = (okf && r + i < n) ? x[(r + i) * ld + f] : 0.f;
-    unsigned pk[kOzDigits][kOzRB / 4];
+    for (int i = 0; i < 16; ++i) v[i] = x[min(r + i, n - 1) * ld + fl];
+  };
+  auto digitise = [&](int64_t rb, const float (&xv)[16]) {
+    const int64_t r = row0 + rb * kOzRB + 16 * half;
+    unsigned pk[kOzDigits][4];
 #pragma unroll
     for (int p = 0; p < kOzDigits; ++p)
 #pragma unroll
-      for (int q = 0; q < kOzRB / 4; ++q) pk[p][q] = 0u;
+      for (int q = 0; q < 4; ++q) pk[p][q] = 0u;
 #pragma unroll
-    for (int i = 0; i < kOzRB; ++i) {
+    for (int i = 0; i < 16; ++i) {
       const bool ok = okf && r + i < n;
       const double v = ok ? double(xv[i]) - s : 0.0;
       csum += v;
@@ -155,13 +167,21 @@ __global__ __launch_bounds__(kOzFeat) void oap_oz_slice(
       }
     }
 #pragma unroll
-    for (int p = 0; p < kOzDigits; ++p) {
-      v4i* o = reinterpret_cast<v4i*>(planes + p * plane + (size_t(rb) * dp + f) * kOzRB);
-      o[0] = v4i{int(pk[p][0]), int(pk[p][1]), int(pk[p][2]), int(pk[p][3])};
-      o[1] = v4i{int(pk[p][4]), int(pk[p][5]), int(pk[p][6]), int(pk[p][7])};
-    }
+    for (int p = 0; p < kOzDigits; ++p)
+      *reinterpret_cast<v4i*>(planes + p * plane + (size_t(rb) * dp + f) * kOzRB + 16 * half) =
+          v4i{int(pk[p][0]), int(pk[p][1]), int(pk[p][2]), int(pk[p][3])};
+  };
+  float xa[16], xb[16];
+  load(rb0, xa);
+  for (int64_t rb = rb0; rb < rb1; rb += 2) {
+    load(rb + 1, xb);
+    digitise(rb, xa);
+    if (rb + 1 >= rb1) break;
+    load(rb + 2, xa);
+    digitise(rb + 1, xb);
   }
-  cpart[size_t(group0 + blockIdx.x) * dp + f] = csum;
+  csum += __shfl_xor(csum, 1, 64);  // (the two halves of the feature, fixed order)
+  if (half == 0) cpart[size_t(group0 + blockIdx.x) * dp + f] = csum;
 }
 
 struct OzArgs {
@@ -182,7 +202,11 @@ __device__ inline void oz_tile(int tile, int nbj, int& bi, int& bj) {
   bj = 2 * b + t;
 }
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef const __attribute__((address_space(1))) void* glb_ptr_t;
+
 __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
+  __shared__ __attribute__((aligned(1024))) int oz_lds[3 * kOzStage / 4];  // the only LDS object
   const int G = gridDim.x;
   const int per = G / 8;  // XCD-aware: the tiles of one split share an XCD (its L2)
   const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -197,9 +221,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
   const size_t plane = size_t(a.nrb) * a.dp * kOzRB;
   const size_t rbs = size_t(a.dp) * kOzRB;
   // fragment: lane l holds feature f0 + (l & 31), rows 16 (l >> 5) .. + 15 of the row block —
-  // the same k order for A and B, which is all the sum over k needs.  Uniform bases + one
-  // per-lane 32-bit offset: every load is saddr + voffset (no 64-bit address per load).
-  const unsigned loff = unsigned(lane & 31) * kOzRB + 16u * unsigned(lane >> 5);
+  // the same k order for A and B, which is all the sum over k needs
   const int8_t* pa = a.planes + size_t(bi * kOzTI + 32 * wave) * kOzRB;
   const int8_t* pb = a.planes + size_t(bj * kOzTJ) * kOzRB;
 
@@ -213,6 +235,10 @@ __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
 
   double* slab = a.slab + (size_t(split) * a.tiles + tile) * (kOzTI * kOzTJ);
   auto flush = [&]() {
+    // laundered per-lane base: keeps the 32 element addresses from being hoisted out of the row
+    // loop as live registers; 4 read-modify-writes in flight at a time
+    double* base = slab + (32 * wave + 4 * (lane >> 5)) * kOzTJ + (lane & 31);
+    asm volatile("" : "+v"(base));
 #pragma unroll
     for (int y = 0; y < 2; ++y)
 #pragma unroll
@@ -220,9 +246,9 @@ __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
         double v = double(acc[kOzDigits - 1][y][e]);
 #pragma unroll
         for (int l = kOzDigits - 2; l >= 0; --l) v = fma(v, 0x1p-7, double(acc[l][y][e]));
-        const int row = 32 * wave + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        const int col = 32 * y + (lane & 31);
-        slab[row * kOzTJ + col] += v;
+        double* q = base + ((e & 3) + 8 * (e >> 2)) * kOzTJ + 32 * y;
+        *q += v;
+        if ((e & 3) == 3) asm volatile("" ::: "memory");
       }
 #pragma unroll
     for (int l = 0; l < kOzDigits; ++l)
@@ -232,42 +258,90 @@ __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
         for (int e = 0; e < 16; ++e) acc[l][y][e] = 0;
   };
 
-  v4i fa[2][kOzDigits], fb[2][kOzDigits][2];
-  // unconditional (the block index is clamped to the split's last): no divergent joins
-  auto load = [&](int64_t rb, v4i (&A)[kOzDigits], v4i (&B)[kOzDigits][2]) {
-    const size_t o = size_t(min(rb, rb1 - 1)) * rbs;
+  // Digit fragments stage through LDS by global_load_lds, three row blocks deep: block rb + 2 is
+  // in flight while rb + 1 lands and rb feeds the MFMAs.  A stage holds the 4 waves' A fragments
+  // (slots w*7 + p) and the shared B fragments (slots 28 + 7y + p), 1 KB each; lane l fetches
+  // byte g(l) = (l & 31) * 32 + 16 (l >> 5) of a fragment into LDS byte 16 l, so the MFMA lane l
+  // reads its operand at 16 l.  Every wave issues exactly kOzGlds loads per stage (its 7 A
+  // fragments and 4 of the 14 B fragments; waves 2, 3 repeat one of theirs) so one counted
+  // vmcnt retires a stage.  Only raw s_barriers in the loop (a __syncthreads would drain the
+  // in-flight stage).
+  char* st0 = reinterpret_cast<char*>(oz_lds);
+  const size_t gl = size_t(lane & 31) * kOzRB + 16 * (lane >> 5);
+  auto issue = [&](int64_t rb, int stg) {
+    const size_t o = size_t(min(rb, rb1 - 1)) * rbs + gl;
+    char* sb = st0 + stg * kOzStage;
 #pragma unroll
-    for (int p = 0; p < kOzDigits; ++p) {
-      const int8_t* ba = pa + p * plane + o;
-      const int8_t* bb = pb + p * plane + o;
-      A[p] = *reinterpret_cast<const v4i*>(ba + loff);
-      B[p][0] = *reinterpret_cast<const v4i*>(bb + loff);
-      B[p][1] = *reinterpret_cast<const v4i*>(bb + loff + 32 * kOzRB);
+    for (int p = 0; p < kOzDigits; ++p)
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(pa + p * plane + o),
+                                       (lds_ptr_t)(sb + (wave * kOzDigits + p) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int j = wave + 4 * i;
+      j = j < 2 * kOzDigits ? j : j - 4;
+      const int y = j / kOzDigits, p = j - y * kOzDigits;
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(pb + p * plane + o + y * 32 * kOzRB),
+                                       (lds_ptr_t)(sb + (4 * kOzDigits + j) * 1024), 16, 0, 0);
     }
   };
-  auto step = [&](const v4i (&A)[kOzDigits], const v4i (&B)[kOzDigits][2]) {
-#pragma unroll
-    for (int l = 0; l < kOzDigits; ++l)
+  // one staged block: its fragments are read in level order (A_p, B_p) and the MFMAs run level by
+  // level, pinned by scheduling barriers, so level L waits only for the reads of digits <= L
+  // (in-order LDS returns) instead of all 21 (the compiler otherwise hoists every read and waits
+  // lgkmcnt(0) once)
+  auto compute = [&](int stg) {
+    const char* sb = st0 + stg * kOzStage + 16 * lane;
+    v4i A[kOzDigits], B[kOzDigits][2];
+    auto rd = [&](int p) {
+      A[p] = *reinterpret_cast<const v4i*>(sb + (wave * kOzDigits + p) * 1024);
+      B[p][0] = *reinterpret_cast<const v4i*>(sb + (4 * kOzDigits + p) * 1024);
+      B[p][1] = *reinterpret_cast<const v4i*>(sb + (5 * kOzDigits + p) * 1024);
+    };
+    auto lvl = [&](int l) {
 #pragma unroll
       for (int p = 0; p <= l; ++p)
 #pragma unroll
         for (int y = 0; y < 2; ++y)
           acc[l][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[p], B[l - p][y], acc[l][y], 0, 0, 0);
+    };
+    // reads in three groups (digits 0-1, 2-3, 4-6), each issued one group of MFMAs ahead: the
+    // 4 waves read their 21 KB right after the barrier, and LDS at 128 B/clk would otherwise
+    // hold every MFMA back by ~650 cycles (the compiler hoists all reads and waits once)
+    rd(0);
+    rd(1);
+    rd(2);
+    rd(3);
+    __builtin_amdgcn_sched_barrier(0);
+    lvl(0);
+    lvl(1);
+    rd(4);
+    rd(5);
+    rd(6);
+    __builtin_amdgcn_sched_barrier(0);
+    lvl(2);
+    lvl(3);
+    __builtin_amdgcn_sched_barrier(0);
+    lvl(4);
+    lvl(5);
+    lvl(6);
   };
-  // int32 sums over at most kOzFlush row blocks, then one fp64 flush (no fragment is live across
-  // it: each run of blocks loads its own first one)
-  for (int64_t c0 = rb0; c0 < rb1; c0 += kOzFlush) {
-    const int64_t c1 = min(rb1, c0 + kOzFlush);
-    load(c0, fa[0], fb[0]);
-    for (int64_t rb = c0; rb < c1; rb += 2) {
-      load(min(rb + 1, c1 - 1), fa[1], fb[1]);
-      step(fa[0], fb[0]);
-      const bool two = rb + 1 < c1;
-      load(min(rb + 2, c1 - 1), fa[0], fb[0]);
-      if (two) step(fa[1], fb[1]);
+  issue(rb0, 0);
+  issue(rb0 + 1, 1);
+  int stg = 0, since = 0;
+  for (int64_t rb = rb0; rb < rb1; ++rb) {
+    // this wave's loads of block rb have landed (rb + 1's may still be in flight), then
+    // everyone's; the barrier also frees the stage block rb - 1 was read from
+    __builtin_amdgcn_s_waitcnt(kOzVmcntStage);
+    __builtin_amdgcn_s_barrier();
+    issue(rb + 2, stg == 0 ? 2 : stg - 1);
+    compute(stg);
+    stg = stg == 2 ? 0 : stg + 1;
+    if (++since == kOzFlush) {
+      flush();
+      since = 0;
     }
-    flush();
   }
+  if (since > 0) flush();
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): nothing in flight at exit
 }
 
 __global__ __launch_bounds__(256) void oap_oz_reduce(const double* __restrict__ slab, int splits,
@@ -404,8 +478,8 @@ void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const 
     const int64_t nrb = std::min<int64_t>(p.chunk_rb, p.nrb - rb0);
     if (nrb <= 0) break;
     const int64_t sg = (nrb + kOzSliceRB - 1) / kOzSliceRB;
-    hipLaunchKernelGGL(oap_oz_slice, dim3(unsigned(sg), fblocks), dim3(kOzFeat), 0, s, x, p.n,
-                       ld, p.d, p.dp, rb0 * kOzRB, nrb, shift, sc, planes, cpart,
+    hipLaunchKernelGGL(oap_oz_slice, dim3(unsigned(sg), p.dp / kOzSliceFeat), dim3(256), 0, s, x,
+                       p.n, ld, p.d, p.dp, rb0 * kOzRB, nrb, shift, sc, planes, cpart,
                        rb0 / kOzSliceRB);
     OzArgs a;
     a.planes = planes;
