@@ -80,6 +80,9 @@ void register_pca(py::module_& m) {
         out["allreduce_ms"] = c.allreduce_ms;
         out["engine"] = c.engine;
         out["err_bound"] = c.err_bound;
+        out["scales_redone"] = c.scales_redone;
+        out["fallback_fp64"] = c.fallback_fp64;
+        out["int8_rel_bound"] = c.int8_rel_bound;
         return out;
       },
       py::arg("ctx"), py::arg("comm"), py::arg("table"), py::arg("precise") = false,

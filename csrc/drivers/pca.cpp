@@ -73,6 +73,9 @@ void cpu_stats(Context& ctx, const DenseTable& x, const std::vector<double>& shi
 
 }  // namespace
 
+// int8 exact engine: largest accepted err_bound relative to the largest variance
+constexpr double kExactRelBound = 1e-10;
+
 PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaParams& p,
                              bool device_cov) {
   TraceRange tr(&ctx.metrics(), "pca/covariance");
@@ -93,8 +96,8 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
     hipStream_t s = ctx.compute();
     // exact mode on f32 rows: the int8 digit products (kernels/pca_ozaki.hip); the fp64 MFMA
     // for f64 rows (their 53-bit inputs would need more digits) or when the knob says so
-    const bool digits = p.exact && x.dtype == DType::F32 &&
-                        knob_str("OAP_PCA_EXACT_ENGINE") != "fp64";
+    bool digits = p.exact && x.dtype == DType::F32 &&
+                  knob_str("OAP_PCA_EXACT_ENGINE") != "fp64";
     res.engine = !p.exact ? "bf16_split" : digits ? "int8_digits" : "fp64_mfma";
     // [S | c | bound]: the bound rides in the one allreduce (summed over the ranks)
     const size_t cnt_x = cnt + (digits ? 1 : 0);
@@ -102,16 +105,7 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
     Buffer part, cpart, shf, ws;
     kern::PcaPlan plan;
     kern::PcaOzakiPlan oplan;
-    if (digits) {
-      size_t free_b = 0, total_b = 0;
-      OAP_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-      // digit planes of one row chunk (7 bytes per padded element): at most 16 GiB (knob) and a
-      // third of what is free (the 40 GB bench table takes 5 chunks)
-      const size_t cap = std::min<size_t>(size_t(knob_int("OAP_PCA_DIGIT_CHUNK_BYTES")),
-                                          free_b / 3);
-      oplan = kern::pca_ozaki_plan(x.rows, d, ctx.info().cu_count, cap);
-      ws = ctx.alloc(oplan.ws_bytes);
-    } else {
+    auto setup_mfma = [&]() {  // the fp64 (exact) or bf16-split (fast) SYRK's plan and slabs
       plan = p.exact ? kern::pca_syrk_plan_f64(x.rows, d, ctx.info().cu_count)
                      : kern::pca_syrk_plan(x.rows, d, ctx.info().cu_count);
       part = ctx.alloc(plan.part_elems * sizeof(double));
@@ -126,45 +120,95 @@ PcaCovariance pca_covariance(Context& ctx, Comm& comm, DenseTable& x, const PcaP
         for (int c = 0; c < d; ++c) hs[c] = float(shift[c]);
         ctx.copy_to_backend(shf.data(), hs.data(), hs.size() * sizeof(float), s);
       }
+    };
+    if (digits) {
+      size_t free_b = 0, total_b = 0;
+      OAP_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      // digit planes of one row chunk (7 bytes per padded element): at most 16 GiB (knob) and a
+      // third of what is free (the 40 GB bench table takes 5 chunks)
+      const size_t cap = std::min<size_t>(size_t(knob_int("OAP_PCA_DIGIT_CHUNK_BYTES")),
+                                          free_b / 3);
+      oplan = kern::pca_ozaki_plan(x.rows, d, ctx.info().cu_count, cap);
+      ws = ctx.alloc(oplan.ws_bytes);
+    } else {
+      setup_mfma();
     }
     Event e0, e1, e2;
-    e0.record(s);
-    {
-      TraceRange k(&ctx.metrics(), "pca/syrk_launch");
-      if (digits) {
-        kern::pca_syrk_ozaki(x.data.as<float>(), x.ld, shift.data(), oplan, ws.data(),
-                             out.as<double>(), out.as<double>() + size_t(d) * d,
-                             out.as<double>() + cnt, s);
+    double bound_s = 0.0;
+    // one pass: statistics, the one allreduce, the host copy; with the int8 engine a negative
+    // allreduced bound means some rank's sampled column scales were too small — every rank sees
+    // it and redoes the pass with exact scales (the same decision everywhere)
+    auto run = [&](bool exact_scales) {
+      e0.record(s);
+      {
+        TraceRange k(&ctx.metrics(), "pca/syrk_launch");
+        if (digits) {
+          kern::pca_syrk_ozaki(x.data.as<float>(), x.ld, shift.data(), oplan, ws.data(),
+                               out.as<double>(), out.as<double>() + size_t(d) * d,
+                               out.as<double>() + cnt, exact_scales, s);
+        } else {
+          if (p.exact)
+            kern::pca_syrk_f64(x.data.data(), x.dtype == DType::F64, x.rows, x.ld, d,
+                               shf.as<double>(), plan, part.as<double>(), cpart.as<double>(), s);
+          else
+            kern::pca_syrk(x.data.as<float>(), x.rows, x.ld, d, shf.as<float>(), plan,
+                           part.as<double>(), cpart.as<double>(), p.precise, p.flush_rows, s);
+          kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), d, out.as<double>(),
+                           out.as<double>() + size_t(d) * d, s);
+        }
+      }
+      e1.record(s);
+      comm_allreduce(ctx, comm, out.data(), digits ? cnt_x : cnt, DType::F64, ReduceOp::Sum, s);
+      if (comm.on_device()) comm.wait(s);
+      e2.record(s);
+      if (device_cov) {  // the covariance stays on the device; only c comes back (the mean)
+        if (!res.dev_cov.data()) res.dev_cov = ctx.alloc(sizeof(double) * size_t(d) * d);
+        kern::pca_cov(out.as<double>(), d, res.n, res.dev_cov.as<double>(), s);
+        std::vector<double> tail(size_t(d) + (digits ? 1 : 0));
+        ctx.copy_to_host(tail.data(), out.as<double>() + size_t(d) * d,
+                         tail.size() * sizeof(double));
+        std::copy(tail.begin(), tail.begin() + d, stats.begin() + size_t(d) * d);
+        if (digits) bound_s = tail[d];
       } else {
-        if (p.exact)
-          kern::pca_syrk_f64(x.data.data(), x.dtype == DType::F64, x.rows, x.ld, d,
-                             shf.as<double>(), plan, part.as<double>(), cpart.as<double>(), s);
-        else
-          kern::pca_syrk(x.data.as<float>(), x.rows, x.ld, d, shf.as<float>(), plan,
-                         part.as<double>(), cpart.as<double>(), p.precise, p.flush_rows, s);
-        kern::pca_reduce(plan, part.as<double>(), cpart.as<double>(), d, out.as<double>(),
-                         out.as<double>() + size_t(d) * d, s);
+        std::vector<double> all(digits ? cnt_x : cnt);
+        ctx.copy_to_host(all.data(), out.data(), all.size() * sizeof(double));
+        std::copy(all.begin(), all.begin() + cnt, stats.begin());
+        if (digits) bound_s = all[cnt];
+      }
+    };
+    run(false);
+    if (digits && bound_s < 0) {
+      res.scales_redone = true;
+      run(true);
+    }
+    res.err_bound = digits ? bound_s / double(res.n - 1) : 0.0;
+    if (digits) {
+      // The bound is relative to the column ranges (max |v_j| max |v_k|), not to each product: a
+      // column whose range dwarfs its spread (a far outlier) can leave it above fp64 accuracy.
+      // Then the pass is redone on the fp64 MFMA (same decision on every rank: S, c and the
+      // bound are allreduced).
+      std::vector<double> sdiag(d);
+      OAP_HIP_CHECK(hipMemcpy2DAsync(sdiag.data(), sizeof(double), out.data(),
+                                     size_t(d + 1) * sizeof(double), sizeof(double), d,
+                                     hipMemcpyDeviceToHost, s));
+      OAP_HIP_CHECK(hipStreamSynchronize(s));
+      const double nn = double(res.n);
+      double vmax = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double cj = stats[size_t(d) * d + j];
+        vmax = std::max(vmax, (sdiag[j] - cj * cj / nn) / (nn - 1.0));
+      }
+      res.int8_rel_bound = vmax > 0 ? res.err_bound / vmax : 0.0;
+      if (!(res.err_bound <= kExactRelBound * vmax)) {
+        res.fallback_fp64 = true;
+        digits = false;
+        res.engine = "fp64_mfma";
+        res.err_bound = 0.0;
+        ws = Buffer();
+        setup_mfma();
+        run(false);
       }
     }
-    e1.record(s);
-    comm_allreduce(ctx, comm, out.data(), cnt_x, DType::F64, ReduceOp::Sum, s);
-    if (comm.on_device()) comm.wait(s);
-    e2.record(s);
-    double bound_s = 0.0;
-    if (device_cov) {  // the covariance stays on the device; only c comes back (the mean)
-      res.dev_cov = ctx.alloc(sizeof(double) * size_t(d) * d);
-      kern::pca_cov(out.as<double>(), d, res.n, res.dev_cov.as<double>(), s);
-      std::vector<double> tail(size_t(d) + (digits ? 1 : 0));
-      ctx.copy_to_host(tail.data(), out.as<double>() + size_t(d) * d, tail.size() * sizeof(double));
-      std::copy(tail.begin(), tail.begin() + d, stats.begin() + size_t(d) * d);
-      if (digits) bound_s = tail[d];
-    } else {
-      std::vector<double> all(cnt_x);
-      ctx.copy_to_host(all.data(), out.data(), cnt_x * sizeof(double));
-      std::copy(all.begin(), all.begin() + cnt, stats.begin());
-      if (digits) bound_s = all[cnt];
-    }
-    res.err_bound = bound_s / double(res.n - 1);
     res.stats_ms = Event::elapsed_ms(e0, e1);
     res.allreduce_ms = Event::elapsed_ms(e1, e2);
     ctx.metrics().add("pca/syrk_kernel", res.stats_ms * 1e3,

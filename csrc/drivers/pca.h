@@ -46,6 +46,12 @@ struct PcaCovariance {
   // int8_digits: a bound on max_jk |cov_jk - cov_exact_jk| from the digit products (the
   // statistics' own error; the fp64 correction c c^T / n is the fp64 path's); else 0
   double err_bound = 0.0;
+  // int8_digits: the column scales sampled from 65536 rows proved too small (a digit overflowed)
+  // and the pass was redone with scales from every row
+  bool scales_redone = false;
+  // int8_digits gave a bound above 1e-10 of the largest variance: redone on the fp64 MFMA
+  bool fallback_fp64 = false;
+  double int8_rel_bound = 0.0;  // the int8 engine's err_bound / largest variance (diagnostic)
 };
 
 struct PcaResult {

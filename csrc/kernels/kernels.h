@@ -369,9 +369,10 @@ void pca_syrk_f64(const void* x, bool x_f64, int64_t n, int64_t ld, int d, const
 // differs from the exact S by at most n 2^(E_j + E_k - 49) (8.05 + fp64 rounding) per entry.
 struct PcaOzakiPlan {
   int64_t n = 0;
-  int d = 0, dp = 0, nbj = 0, tiles = 0, splits = 0;
+  int d = 0, dp = 0, nb = 0, tiles = 0, splits = 0;
   int64_t nrb = 0, groups = 0, chunk_rb = 0, chunks = 0, cgroups = 0;
-  int fp64_adds = 0;  // longest chain of fp64 additions into one output (error bound)
+  int split_group = 1;  // the reduce sums the splits in groups of this many
+  int fp64_adds = 0;    // longest chain of fp64 additions into one output (error bound)
   size_t slab_elems = 0;
   size_t off_slab = 0, off_mm = 0, off_e = 0, off_sc = 0, off_shift = 0, off_cpart = 0;
   size_t ws_bytes = 0;  // one device workspace (digit planes of one row chunk first)
@@ -379,9 +380,12 @@ struct PcaOzakiPlan {
 // max_plane_bytes bounds the digit planes of one row chunk (7 d_pad bytes per row)
 PcaOzakiPlan pca_ozaki_plan(int64_t n, int d, int num_cus, size_t max_plane_bytes);
 // out: d x d S (both triangles), colsum: [d]; shift_host: fp64 [d] (read before the call
-// returns); bound (device, 1 double): the bound on max |S - S_exact| over the entries
+// returns); bound (device, 1 double): the bound on max |S - S_exact| over the entries, negative
+// when the column scales taken from a row sample (exact_scales false, > 65536 rows) proved too
+// small — then call again with exact_scales
 void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const PcaOzakiPlan& p,
-                    void* ws, double* out, double* colsum, double* bound, hipStream_t s);
+                    void* ws, double* out, double* colsum, double* bound, bool exact_scales,
+                    hipStream_t s);
 // ---- ALS (kernels/als.hip) -------------------------------------------------------------------
 struct AlsSolveArgs {
   const int64_t* rowptr = nullptr;  // [nrows+1] CSR of the destination rows

@@ -18,7 +18,9 @@
 // level and row, so 2048 row blocks (65536 rows) stay below 2^31 before an fp64 flush.
 //
 // Kernels (one fit = one minmax pass over all rows, then per row chunk: slice + SYRK):
-//   oap_oz_minmax   column min / max of x per row group (fp32, exact)
+//   oap_oz_minmax   column min / max of x per row group (fp32, exact), over every row or an
+//                   even sample of 65536 rows (then one bit of margin, and the digitising pass
+//                   flags any digit past [-64, 64]: the caller redoes the pass with exact scales)
 //   oap_oz_exponent E_j and the scale 2^(6 - E_j) from max(xmax - s, s - xmin) (fp64)
 //   oap_oz_slice    the 7 digit planes [p][row block][feature][32 rows] int8 + fp64 column sums
 //   oap_oz_syrk     128 x 64 output tile per 4-wave workgroup (each wave 32 x 64: 7 levels x 2
@@ -26,6 +28,9 @@
 //                   a 32-row block (each a contiguous 1 KB of a plane) stage through LDS by
 //                   global_load_lds, three blocks deep, the B fragments shared by the 4 waves
 //   oap_oz_reduce   sum of the split slabs (fixed order), times 2^(E_i + E_j - 12), both halves
+#include <algorithm>
+#include <cmath>
+
 #include "kernels/device_utils.h"
 #include "kernels/kernels.h"
 #include "runtime/common.h"
@@ -37,36 +42,37 @@ namespace {
 
 constexpr int kOzDigits = 7;
 constexpr int kOzRB = 32;          // rows per row block (the MFMA's k)
-constexpr int kOzTI = 128, kOzTJ = 64;
+constexpr int kOzTile = 64;        // output tile (64 x 64 per workgroup)
 constexpr int kOzThreads = 256;
 constexpr int kOzFlush = 2048;     // row blocks per int32 flush (7 * 2^12 * 32 * 2048 < 2^31)
 constexpr int kOzRowGroup = 2048;  // rows per minmax partial
+constexpr int kOzSample = 65536;   // rows of the sampled column ranges
 constexpr int kOzSliceRB = 16;     // row blocks per slice-kernel block (one column-sum partial)
 constexpr int kOzFeat = 256;       // features per minmax block
 constexpr int kOzSliceFeat = 128;  // features per slice block (two threads each)
 
-constexpr int kOzGlds = kOzDigits + 4;                   // LDS-DMA loads per wave and stage
-constexpr int kOzStage = (4 * kOzDigits + 2 * kOzDigits) * 1024;  // 42 KB: A 4 x 7, B 2 x 7
-// s_waitcnt vmcnt(kOzGlds) (expcnt / lgkmcnt not waited): one stage may stay in flight
-constexpr int kOzVmcntStage = (kOzGlds & 15) | ((kOzGlds >> 4) << 14) | (7 << 4) | (15 << 8);
+constexpr int kOzStage = 4 * kOzDigits * 1024;  // 28 KB: A 2 x 7, B 2 x 7 fragments
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-__global__ __launch_bounds__(kOzFeat) void oap_oz_minmax(const float* __restrict__ x, int64_t n,
-                                                          int64_t ld, int d, int dp,
+// rows idx * rstride for idx in [g * per, (g + 1) * per) of the n_s sampled rows (rstride 1: all)
+__global__ __launch_bounds__(kOzFeat) void oap_oz_minmax(const float* __restrict__ x, int64_t n_s,
+                                                          int64_t rstride, int per, int64_t ld,
+                                                          int d, int dp,
                                                           float2* __restrict__ mm) {
   const int f = blockIdx.y * kOzFeat + threadIdx.x;
-  const int64_t r0 = int64_t(blockIdx.x) * kOzRowGroup;
-  const int64_t r1 = min(n, r0 + kOzRowGroup);
+  const int64_t r0 = int64_t(blockIdx.x) * per;
+  const int64_t r1 = min(n_s, r0 + per);
   float lo = INFINITY, hi = -INFINITY;
   if (f < d) {
-    const float* p = x + r0 * ld + f;
+    const float* p = x + f;
+    const int64_t st = rstride * ld;
     int64_t r = r0;
     for (; r + 8 <= r1; r += 8) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p[(r - r0 + u) * ld];
+      for (int u = 0; u < 8; ++u) v[u] = p[(r + u) * st];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         lo = fminf(lo, v[u]);
@@ -74,7 +80,7 @@ __global__ __launch_bounds__(kOzFeat) void oap_oz_minmax(const float* __restrict
       }
     }
     for (; r < r1; ++r) {
-      const float v = p[(r - r0) * ld];
+      const float v = p[r * st];
       lo = fminf(lo, v);
       hi = fmaxf(hi, v);
     }
@@ -83,7 +89,7 @@ __global__ __launch_bounds__(kOzFeat) void oap_oz_minmax(const float* __restrict
 }
 
 __global__ __launch_bounds__(256) void oap_oz_exponent(const float2* __restrict__ mm, int groups,
-                                                        int d, int dp,
+                                                        int d, int dp, int margin,
                                                         const double* __restrict__ shift,
                                                         int* __restrict__ E,
                                                         double* __restrict__ sc) {
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(256) void oap_oz_exponent(const float2* __restrict_
       // the slice kernel's v = (double)x - s is monotone in x: its extreme values are these
       const double s = shift[f];
       const double m = fmax(double(shi[0]) - s, s - double(slo[0]));
-      if (m > 0.0 && m <= 1.7e308) e = min(max(ilogb(m) + 1, -900), 1000);  // m < 2^e
+      if (m > 0.0 && m <= 1.7e308) e = min(max(ilogb(m) + 1 + margin, -900), 1000);  // m < 2^e
     }
     E[f] = e;
     sc[f] = ldexp(1.0, 6 - e);
@@ -125,7 +131,8 @@ __global__ __launch_bounds__(256) void oap_oz_exponent(const float2* __restrict_
 __global__ __launch_bounds__(256) void oap_oz_slice(
     const float* __restrict__ x, int64_t n, int64_t ld, int d, int dp, int64_t row0,
     int64_t nrb, const double* __restrict__ shift, const double* __restrict__ sc,
-    int8_t* __restrict__ planes, double* __restrict__ cpart, int64_t group0) {
+    int8_t* __restrict__ planes, double* __restrict__ cpart, int64_t group0,
+    int* __restrict__ ovf) {
   const int f = blockIdx.y * kOzSliceFeat + (threadIdx.x >> 1);
   const int half = threadIdx.x & 1;
   const int64_t rb0 = int64_t(blockIdx.x) * kOzSliceRB;
@@ -134,6 +141,7 @@ __global__ __launch_bounds__(256) void oap_oz_slice(
   const double s = okf ? shift[f] : 0.0, scale = okf ? sc[f] : 0.0;
   const size_t plane = size_t(nrb) * dp * kOzRB;
   double csum = 0.0;
+  bool over = false;  // a digit past [-64, 64]: the sampled scales were too small
   // rows of block rb + 1 in flight while block rb is digitised (unconditional loads: rows
   // clamped to n - 1, features to 0; masked below)
   const int fl = okf ? f : 0;
@@ -154,7 +162,8 @@ __global__ __launch_bounds__(256) void oap_oz_slice(
       const bool ok = okf && r + i < n;
       const double v = ok ? double(xv[i]) - s : 0.0;
       csum += v;
-      double w = v * scale;  // exact (power of two), |w| < 64
+      double w = v * scale;  // exact (power of two), |w| < 64 (checked)
+      over |= !(fabs(w) < 64.0);
       double t = __builtin_rint(w);
       pk[0][i >> 2] |= (unsigned(int(t)) & 0xffu) << (8 * (i & 3));
       w -= t;  // exact: |w| <= 1/2
@@ -180,6 +189,7 @@ __global__ __launch_bounds__(256) void oap_oz_slice(
     load(rb + 2, xa);
     digitise(rb + 1, xb);
   }
+  if (over) atomicOr(ovf, 1);
   csum += __shfl_xor(csum, 1, 64);  // (the two halves of the feature, fixed order)
   if (half == 0) cpart[size_t(group0 + blockIdx.x) * dp + f] = csum;
 }
@@ -187,26 +197,30 @@ __global__ __launch_bounds__(256) void oap_oz_slice(
 struct OzArgs {
   const int8_t* planes;  // [7][nrb][dp][32]
   int64_t nrb;
-  int dp, nbj, tiles;
+  int dp, nb, tiles;
   int64_t rb_per_split;
-  double* slab;  // [splits][tiles][128][64], accumulated (+=)
+  double* slab;  // [splits][tiles][64][64], accumulated (+=)
 };
 
-__device__ inline void oz_tile(int tile, int nbj, int& bi, int& bj) {
+// upper-triangular 64 x 64 tile t of nb blocks -> (bi, bj), bj >= bi
+__device__ inline void oz_tile(int tile, int nb, int& bi, int& bj) {
   int t = tile, b = 0;
-  while (t >= nbj - 2 * b) {
-    t -= nbj - 2 * b;
+  while (t >= nb - b) {
+    t -= nb - b;
     ++b;
   }
   bi = b;
-  bj = 2 * b + t;
+  bj = b + t;
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef const __attribute__((address_space(1))) void* glb_ptr_t;
 
-__global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
-  __shared__ __attribute__((aligned(1024))) int oz_lds[3 * kOzStage / 4];  // the only LDS object
+// 64 x 64 output tile per 4-wave workgroup, each wave one 32 x 32 block (wave (wi, wj)) with its
+// 7 level accumulators (112 AGPRs): ~200 registers, so two workgroups share a CU (two waves per
+// SIMD) and one's LDS reads and barrier waits hide under the other's MFMAs.
+__global__ __launch_bounds__(kOzThreads, 2) void oap_oz_syrk(OzArgs a) {
+  __shared__ __attribute__((aligned(1024))) int oz_lds[2 * kOzStage / 4];  // the only LDS object
   const int G = gridDim.x;
   const int per = G / 8;  // XCD-aware: the tiles of one split share an XCD (its L2)
   const int L = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -215,126 +229,82 @@ __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
   const int64_t rb1 = min(a.nrb, rb0 + a.rb_per_split);
   if (rb0 >= rb1) return;
   int bi, bj;
-  oz_tile(tile, a.nbj, bi, bj);
+  oz_tile(tile, a.nb, bi, bj);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wi = wave >> 1, wj = wave & 1;
   const size_t plane = size_t(a.nrb) * a.dp * kOzRB;
   const size_t rbs = size_t(a.dp) * kOzRB;
-  // fragment: lane l holds feature f0 + (l & 31), rows 16 (l >> 5) .. + 15 of the row block —
-  // the same k order for A and B, which is all the sum over k needs
-  const int8_t* pa = a.planes + size_t(bi * kOzTI + 32 * wave) * kOzRB;
-  const int8_t* pb = a.planes + size_t(bj * kOzTJ) * kOzRB;
 
-  v16i acc[kOzDigits][2];
+  v16i acc[kOzDigits];
 #pragma unroll
   for (int l = 0; l < kOzDigits; ++l)
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[l][y][e] = 0;
+    for (int e = 0; e < 16; ++e) acc[l][e] = 0;
 
-  double* slab = a.slab + (size_t(split) * a.tiles + tile) * (kOzTI * kOzTJ);
+  double* slab = a.slab + (size_t(split) * a.tiles + tile) * (kOzTile * kOzTile);
   auto flush = [&]() {
-    // laundered per-lane base: keeps the 32 element addresses from being hoisted out of the row
+    // laundered per-lane base: keeps the 16 element addresses from being hoisted out of the row
     // loop as live registers; 4 read-modify-writes in flight at a time
-    double* base = slab + (32 * wave + 4 * (lane >> 5)) * kOzTJ + (lane & 31);
+    double* base = slab + (32 * wi + 4 * (lane >> 5)) * kOzTile + 32 * wj + (lane & 31);
     asm volatile("" : "+v"(base));
 #pragma unroll
-    for (int y = 0; y < 2; ++y)
+    for (int e = 0; e < 16; ++e) {
+      double v = double(acc[kOzDigits - 1][e]);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        double v = double(acc[kOzDigits - 1][y][e]);
-#pragma unroll
-        for (int l = kOzDigits - 2; l >= 0; --l) v = fma(v, 0x1p-7, double(acc[l][y][e]));
-        double* q = base + ((e & 3) + 8 * (e >> 2)) * kOzTJ + 32 * y;
-        *q += v;
-        if ((e & 3) == 3) asm volatile("" ::: "memory");
-      }
+      for (int l = kOzDigits - 2; l >= 0; --l) v = fma(v, 0x1p-7, double(acc[l][e]));
+      double* q = base + ((e & 3) + 8 * (e >> 2)) * kOzTile;
+      *q += v;
+      if ((e & 3) == 3) asm volatile("" ::: "memory");
+    }
 #pragma unroll
     for (int l = 0; l < kOzDigits; ++l)
 #pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[l][y][e] = 0;
+      for (int e = 0; e < 16; ++e) acc[l][e] = 0;
   };
 
-  // Digit fragments stage through LDS by global_load_lds, three row blocks deep: block rb + 2 is
-  // in flight while rb + 1 lands and rb feeds the MFMAs.  A stage holds the 4 waves' A fragments
-  // (slots w*7 + p) and the shared B fragments (slots 28 + 7y + p), 1 KB each; lane l fetches
-  // byte g(l) = (l & 31) * 32 + 16 (l >> 5) of a fragment into LDS byte 16 l, so the MFMA lane l
-  // reads its operand at 16 l.  Every wave issues exactly kOzGlds loads per stage (its 7 A
-  // fragments and 4 of the 14 B fragments; waves 2, 3 repeat one of theirs) so one counted
-  // vmcnt retires a stage.  Only raw s_barriers in the loop (a __syncthreads would drain the
-  // in-flight stage).
+  // Digit fragments stage through LDS by global_load_lds, two row blocks deep (block rb + 1 is
+  // in flight while rb feeds the MFMAs).  A stage holds the tile's two A blocks (slots 7 i + p)
+  // and two B blocks (slots 14 + 7 j + p), 1 KB each; wave w loads the 7 slots 7 w .. 7 w + 6
+  // (exactly 7 per wave and stage).  Lane l fetches byte g(l) = (l & 31) * 32 + 16 (l >> 5)
+  // of a fragment into LDS byte 16 l, so the MFMA lane l reads its operand at 16 l.  Only raw
+  // s_barriers in the loop (a __syncthreads would also drain the in-flight stage).
   char* st0 = reinterpret_cast<char*>(oz_lds);
   const size_t gl = size_t(lane & 31) * kOzRB + 16 * (lane >> 5);
+  const int blk = wave < 2 ? bi : bj;  // the 64-feature block wave w's slots come from
+  const int8_t* pw = a.planes + (size_t(blk) * kOzTile + 32 * (wave & 1)) * kOzRB;
   auto issue = [&](int64_t rb, int stg) {
     const size_t o = size_t(min(rb, rb1 - 1)) * rbs + gl;
-    char* sb = st0 + stg * kOzStage;
+    char* sb = st0 + stg * kOzStage + wave * kOzDigits * 1024;
 #pragma unroll
     for (int p = 0; p < kOzDigits; ++p)
-      __builtin_amdgcn_global_load_lds((glb_ptr_t)(pa + p * plane + o),
-                                       (lds_ptr_t)(sb + (wave * kOzDigits + p) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int j = wave + 4 * i;
-      j = j < 2 * kOzDigits ? j : j - 4;
-      const int y = j / kOzDigits, p = j - y * kOzDigits;
-      __builtin_amdgcn_global_load_lds((glb_ptr_t)(pb + p * plane + o + y * 32 * kOzRB),
-                                       (lds_ptr_t)(sb + (4 * kOzDigits + j) * 1024), 16, 0, 0);
-    }
+      __builtin_amdgcn_global_load_lds((glb_ptr_t)(pw + p * plane + o),
+                                       (lds_ptr_t)(sb + p * 1024), 16, 0, 0);
   };
-  // one staged block: its fragments are read in level order (A_p, B_p) and the MFMAs run level by
-  // level, pinned by scheduling barriers, so level L waits only for the reads of digits <= L
-  // (in-order LDS returns) instead of all 21 (the compiler otherwise hoists every read and waits
-  // lgkmcnt(0) once)
   auto compute = [&](int stg) {
     const char* sb = st0 + stg * kOzStage + 16 * lane;
-    v4i A[kOzDigits], B[kOzDigits][2];
-    auto rd = [&](int p) {
-      A[p] = *reinterpret_cast<const v4i*>(sb + (wave * kOzDigits + p) * 1024);
-      B[p][0] = *reinterpret_cast<const v4i*>(sb + (4 * kOzDigits + p) * 1024);
-      B[p][1] = *reinterpret_cast<const v4i*>(sb + (5 * kOzDigits + p) * 1024);
-    };
-    auto lvl = [&](int l) {
+    v4i A[kOzDigits], B[kOzDigits];
+#pragma unroll
+    for (int p = 0; p < kOzDigits; ++p) {
+      A[p] = *reinterpret_cast<const v4i*>(sb + (wi * kOzDigits + p) * 1024);
+      B[p] = *reinterpret_cast<const v4i*>(sb + ((2 + wj) * kOzDigits + p) * 1024);
+    }
+#pragma unroll
+    for (int l = 0; l < kOzDigits; ++l)
 #pragma unroll
       for (int p = 0; p <= l; ++p)
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-          acc[l][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[p], B[l - p][y], acc[l][y], 0, 0, 0);
-    };
-    // reads in three groups (digits 0-1, 2-3, 4-6), each issued one group of MFMAs ahead: the
-    // 4 waves read their 21 KB right after the barrier, and LDS at 128 B/clk would otherwise
-    // hold every MFMA back by ~650 cycles (the compiler hoists all reads and waits once)
-    rd(0);
-    rd(1);
-    rd(2);
-    rd(3);
-    __builtin_amdgcn_sched_barrier(0);
-    lvl(0);
-    lvl(1);
-    rd(4);
-    rd(5);
-    rd(6);
-    __builtin_amdgcn_sched_barrier(0);
-    lvl(2);
-    lvl(3);
-    __builtin_amdgcn_sched_barrier(0);
-    lvl(4);
-    lvl(5);
-    lvl(6);
+        acc[l] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[p], B[l - p], acc[l], 0, 0, 0);
   };
   issue(rb0, 0);
-  issue(rb0 + 1, 1);
   int stg = 0, since = 0;
   for (int64_t rb = rb0; rb < rb1; ++rb) {
-    // this wave's loads of block rb have landed (rb + 1's may still be in flight), then
-    // everyone's; the barrier also frees the stage block rb - 1 was read from
-    __builtin_amdgcn_s_waitcnt(kOzVmcntStage);
+    // this wave's loads of block rb have landed, then everyone's; the barrier also frees the
+    // stage block rb - 1 was read from (every wave's reads of it retired before its MFMAs)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __builtin_amdgcn_s_barrier();
-    issue(rb + 2, stg == 0 ? 2 : stg - 1);
+    issue(rb + 1, stg ^ 1);
     compute(stg);
-    stg = stg == 2 ? 0 : stg + 1;
+    stg ^= 1;
     if (++since == kOzFlush) {
       flush();
       since = 0;
@@ -345,7 +315,7 @@ __global__ __launch_bounds__(kOzThreads, 1) void oap_oz_syrk(OzArgs a) {
 }
 
 __global__ __launch_bounds__(256) void oap_oz_reduce(const double* __restrict__ slab, int splits,
-                                                      int tiles, int nbj, int d,
+                                                      int group, int tiles, int nb, int d,
                                                       const int* __restrict__ E,
                                                       double* __restrict__ out) {
   const int64_t total = int64_t(d) * d;
@@ -353,12 +323,19 @@ __global__ __launch_bounds__(256) void oap_oz_reduce(const double* __restrict__ 
        idx += int64_t(gridDim.x) * blockDim.x) {
     const int i = static_cast<int>(idx / d), j = static_cast<int>(idx - int64_t(i) * d);
     if (i > j) continue;
-    const int bi = i / kOzTI, bj = j / kOzTJ;
-    const int tile = bi * nbj - bi * (bi - 1) + (bj - 2 * bi);
-    const size_t e = size_t(i - bi * kOzTI) * kOzTJ + (j - bj * kOzTJ);
+    const int bi = i / kOzTile, bj = j / kOzTile;
+    const int tile = bi * nb - bi * (bi - 1) / 2 + (bj - bi);
+    const size_t e = size_t(i - bi * kOzTile) * kOzTile + (j - bj * kOzTile);
+    // two-level sum over the splits (groups of ceil(sqrt(splits)), fixed order): an fp64
+    // rounding chain of ~2 sqrt(splits) additions instead of splits
+    const double* sl = slab + size_t(tile) * (kOzTile * kOzTile) + e;
+    const size_t sstride = size_t(tiles) * (kOzTile * kOzTile);
     double s = 0.0;
-    for (int sp = 0; sp < splits; ++sp)
-      s += slab[(size_t(sp) * tiles + tile) * (kOzTI * kOzTJ) + e];
+    for (int g0 = 0; g0 < splits; g0 += group) {
+      double gs = 0.0;
+      for (int sp = g0; sp < min(splits, g0 + group); ++sp) gs += sl[sp * sstride];
+      s += gs;
+    }
     const double v = ldexp(s, E[i] + E[j] - 12);
     out[size_t(i) * d + j] = v;
     out[size_t(j) * d + i] = v;
@@ -383,7 +360,8 @@ __global__ __launch_bounds__(256) void oap_oz_colsum(const double* __restrict__ 
 
 // *bound = rows * 2^(2 max_j E_j) * coef: the per-entry bound on |S - S_exact| (pca.cpp)
 __global__ __launch_bounds__(256) void oap_oz_bound(const int* __restrict__ E, int d, double rows,
-                                                     double coef, double* __restrict__ bound) {
+                                                     double coef, const int* __restrict__ ovf,
+                                                     double* __restrict__ bound) {
   __shared__ int sh[256];
   int m = INT_MIN;
   for (int f = threadIdx.x; f < d; f += 256) m = max(m, E[f]);
@@ -393,7 +371,10 @@ __global__ __launch_bounds__(256) void oap_oz_bound(const int* __restrict__ E, i
     if (threadIdx.x < w) sh[threadIdx.x] = max(sh[threadIdx.x], sh[threadIdx.x + w]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) bound[0] = rows > 0 ? ldexp(rows * coef, 2 * sh[0]) : 0.0;
+  // an overflowed digit (sampled scales too small) poisons the bound: the caller redoes the pass
+  // with exact scales (-1e300 keeps the allreduced sum negative)
+  if (threadIdx.x == 0)
+    bound[0] = ovf[0] ? -1e300 : rows > 0 ? ldexp(rows * coef, 2 * sh[0]) : 0.0;
 }
 
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
@@ -404,10 +385,9 @@ PcaOzakiPlan pca_ozaki_plan(int64_t n, int d, int num_cus, size_t max_plane_byte
   PcaOzakiPlan p;
   p.n = n;
   p.d = d;
-  p.dp = int(round_up(size_t(std::max(d, 1)), kOzTI));
-  p.nbj = p.dp / kOzTJ;
-  p.tiles = 0;
-  for (int b = 0; b < p.dp / kOzTI; ++b) p.tiles += p.nbj - 2 * b;
+  p.dp = int(round_up(size_t(std::max(d, 1)), kOzSliceFeat));
+  p.nb = p.dp / kOzTile;
+  p.tiles = p.nb * (p.nb + 1) / 2;
   p.nrb = (n + kOzRB - 1) / kOzRB;
   p.groups = (n + kOzRowGroup - 1) / kOzRowGroup;
   // row blocks per chunk: the digit planes of one chunk within max_plane_bytes, whole slice
@@ -418,9 +398,9 @@ PcaOzakiPlan pca_ozaki_plan(int64_t n, int d, int num_cus, size_t max_plane_byte
   p.chunk_rb = std::min<int64_t>(round_up(size_t(std::max<int64_t>(p.nrb, 1)), kOzSliceRB), crb);
   p.chunks = std::max<int64_t>(1, (p.nrb + p.chunk_rb - 1) / p.chunk_rb);
   p.cgroups = (p.nrb + kOzSliceRB - 1) / kOzSliceRB;
-  // one 256-thread workgroup per CU (~400 registers per lane): splits x tiles in whole rounds of
-  // the CUs, at least two rounds when the rows allow
-  const int64_t R = std::max(num_cus, 64);
+  // two 256-thread workgroups per CU (~200 registers per lane, 56 KB of LDS each): splits x
+  // tiles in whole rounds of the resident slots, at least two rounds when the rows allow
+  const int64_t R = 2 * int64_t(std::max(num_cus, 64));
   const int64_t s_lo = std::max<int64_t>(1, (2 * R + p.tiles - 1) / p.tiles);
   int64_t s = s_lo;
   double best = 1e30;
@@ -437,13 +417,17 @@ PcaOzakiPlan pca_ozaki_plan(int64_t n, int d, int num_cus, size_t max_plane_byte
   // longest chain of fp64 additions into one output: the slab flushes of a split over all
   // chunks, the sum over splits, the final scaling
   const int64_t rps = (p.chunk_rb + s - 1) / s;
-  p.fp64_adds = int(p.chunks * ((rps + kOzFlush - 1) / kOzFlush) + s + 2);
-  p.slab_elems = size_t(p.splits) * p.tiles * kOzTI * kOzTJ;
+  p.split_group = std::max(1, int(std::ceil(std::sqrt(double(s)))));
+  p.fp64_adds = int(p.chunks * ((rps + kOzFlush - 1) / kOzFlush) + p.split_group +
+                    (s + p.split_group - 1) / p.split_group + 2);
+  p.slab_elems = size_t(p.splits) * p.tiles * kOzTile * kOzTile;
   // workspace: planes | slab | minmax partials | E | scale | shift | column-sum partials
   p.off_slab = align256(size_t(p.chunk_rb) * per_rb);
   p.off_mm = p.off_slab + align256(p.slab_elems * sizeof(double));
-  p.off_e = p.off_mm + align256(size_t(std::max<int64_t>(p.groups, 1)) * p.dp * sizeof(float2));
-  p.off_sc = p.off_e + align256(size_t(p.dp) * sizeof(int));
+  // minmax partials: every row's groups or the sample's (kOzSample / 256), whichever is more
+  const int64_t mm_groups = std::max<int64_t>({p.groups, int64_t(kOzSample / 256), 1});
+  p.off_e = p.off_mm + align256(size_t(mm_groups) * p.dp * sizeof(float2));
+  p.off_sc = p.off_e + align256(size_t(p.dp + 1) * sizeof(int));  // E | overflow flag
   p.off_shift = p.off_sc + align256(size_t(p.dp) * sizeof(double));
   p.off_cpart = p.off_shift + align256(size_t(p.dp) * sizeof(double));
   p.ws_bytes =
@@ -452,7 +436,8 @@ PcaOzakiPlan pca_ozaki_plan(int64_t n, int d, int num_cus, size_t max_plane_byte
 }
 
 void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const PcaOzakiPlan& p,
-                    void* ws, double* out, double* colsum, double* bound, hipStream_t s) {
+                    void* ws, double* out, double* colsum, double* bound, bool exact_scales,
+                    hipStream_t s) {
   OAP_CHECK(ld >= p.d, "pca_syrk_ozaki: bad ld");
   char* w = static_cast<char*>(ws);
   int8_t* planes = reinterpret_cast<int8_t*>(w);
@@ -465,12 +450,22 @@ void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const 
   OAP_HIP_CHECK(hipMemcpyAsync(shift, shift_host, size_t(p.d) * sizeof(double),
                                hipMemcpyHostToDevice, s));
   OAP_HIP_CHECK(hipMemsetAsync(slab, 0, p.slab_elems * sizeof(double), s));
+  int* ovf = E + p.dp;
+  OAP_HIP_CHECK(hipMemsetAsync(ovf, 0, sizeof(int), s));
   const int fblocks = p.dp / kOzFeat + (p.dp % kOzFeat ? 1 : 0);
-  if (p.groups > 0)
-    hipLaunchKernelGGL(oap_oz_minmax, dim3(unsigned(p.groups), fblocks), dim3(kOzFeat), 0, s, x,
-                       p.n, ld, p.d, p.dp, mm);
-  hipLaunchKernelGGL(oap_oz_exponent, dim3(p.dp), dim3(256), 0, s, mm, int(p.groups), p.d, p.dp,
-                     shift, E, sc);
+  // column exponents: from every row (exact_scales, or few rows), else from an even sample of
+  // kOzSample rows with one bit of margin — a digit past [-64, 64] then flags the pass (the
+  // caller redoes it with exact scales); the margin costs one bit of the bound
+  const bool sampled = !exact_scales && p.n > int64_t(kOzSample);
+  const int64_t n_s = sampled ? kOzSample : p.n;
+  const int64_t rstride = sampled ? p.n / kOzSample : 1;
+  const int per = sampled ? 256 : kOzRowGroup;
+  const int64_t groups = (n_s + per - 1) / per;  // (the plan sizes the partials for both)
+  if (groups > 0)
+    hipLaunchKernelGGL(oap_oz_minmax, dim3(unsigned(groups), fblocks), dim3(kOzFeat), 0, s, x,
+                       n_s, rstride, per, ld, p.d, p.dp, mm);
+  hipLaunchKernelGGL(oap_oz_exponent, dim3(p.dp), dim3(256), 0, s, mm, int(groups), p.d, p.dp,
+                     sampled ? 1 : 0, shift, E, sc);
   OAP_HIP_CHECK(hipGetLastError());
   const int64_t G = round_up(size_t(p.splits) * p.tiles, 8);
   for (int64_t c = 0; c < p.chunks; ++c) {
@@ -480,12 +475,12 @@ void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const 
     const int64_t sg = (nrb + kOzSliceRB - 1) / kOzSliceRB;
     hipLaunchKernelGGL(oap_oz_slice, dim3(unsigned(sg), p.dp / kOzSliceFeat), dim3(256), 0, s, x,
                        p.n, ld, p.d, p.dp, rb0 * kOzRB, nrb, shift, sc, planes, cpart,
-                       rb0 / kOzSliceRB);
+                       rb0 / kOzSliceRB, ovf);
     OzArgs a;
     a.planes = planes;
     a.nrb = nrb;
     a.dp = p.dp;
-    a.nbj = p.nbj;
+    a.nb = p.nb;
     a.tiles = p.tiles;
     a.rb_per_split = (nrb + p.splits - 1) / p.splits;
     a.slab = slab;
@@ -494,12 +489,13 @@ void pca_syrk_ozaki(const float* x, int64_t ld, const double* shift_host, const 
   }
   const int64_t total = int64_t(p.d) * p.d;
   hipLaunchKernelGGL(oap_oz_reduce, dim3(grid_for(total, 256, 4096)), dim3(256), 0, s, slab,
-                     p.splits, p.tiles, p.nbj, p.d, E, out);
+                     p.splits, p.split_group, p.tiles, p.nb, p.d, E, out);
   hipLaunchKernelGGL(oap_oz_colsum, dim3(p.d), dim3(256), 0, s, cpart, p.cgroups, p.dp, colsum);
   // per row: 2^(E_j+E_k-49) (2 representation + 6.04 dropped digit products + 2^-4 rounding of
   // v) + 2^(E_j+E_k-53) per fp64 addition of the longest chain
   const double coef = 0x1p-49 * (8.04 + 0.0625) + 0x1p-53 * p.fp64_adds;
-  hipLaunchKernelGGL(oap_oz_bound, dim3(1), dim3(256), 0, s, E, p.d, double(p.n), coef, bound);
+  hipLaunchKernelGGL(oap_oz_bound, dim3(1), dim3(256), 0, s, E, p.d, double(p.n), coef, ovf,
+                     bound);
   OAP_HIP_CHECK(hipGetLastError());
 }
 

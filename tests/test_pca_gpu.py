@@ -192,7 +192,7 @@ def _cov_exact_full(native, w, X):
 
 @pytest.mark.parametrize("n,d,offset,spread", [(7, 3, 0.0, 1.0), (3001, 50, 5.0, 1.0),
                                                (4099, 129, 3e3, 1.0), (2500, 300, 0.0, 1e3),
-                                               (20000, 1000, 1.0, 1.0)])
+                                               (20000, 1000, 1.0, 1.0), (150001, 70, 2.0, 10.0)])
 def test_exact_int8_digits_within_bound(native, gpu_world, n, d, offset, spread):
     """f32 rows in exact mode run on the int8 digit products (kernels/pca_ozaki.hip): the error
     against np.cov of the same rows stays inside the bound the kernel reports, the bound itself
@@ -250,3 +250,27 @@ def test_exact_int8_digits_constant_and_zero_columns(native, gpu_world):
     assert np.all(C[5] == 0) and np.all(C[:, 17] == 0)
     Cr = np.cov(X.astype(np.float64).T, ddof=1)
     assert np.max(np.abs(C - Cr)) / np.max(np.abs(Cr)) < 1e-12
+
+
+def test_exact_int8_digits_sampled_scales_redone_on_outlier(native, gpu_world):
+    """Beyond 65536 rows the column scales come from an even row sample (one bit of margin); an
+    outlier the sample misses overflows a digit, the pass is flagged and redone with scales from
+    every row, and the result is the exact covariance all the same.  A far outlier (a column
+    range 10^4 x its spread) leaves the digit bound above 1e-10 of the variance: the pass is then
+    redone on the fp64 MFMA."""
+    rng = np.random.default_rng(19)
+    n = 200_000
+    X = rng.normal(size=(n, 24)).astype(np.float32)
+    for outlier, fallback in ((40.0, False), (1e4, True)):
+        X[1, 7] = outlier  # (row 1 is not a sampled row: the sample stride is n // 65536 = 3)
+        r = _cov_exact_full(native, gpu_world, X)
+        assert r["scales_redone"] and r["fallback_fp64"] == fallback
+        assert r["engine"] == ("fp64_mfma" if fallback else "int8_digits")
+        Cr = np.cov(X.astype(np.float64).T, ddof=1)
+        C = np.asarray(r["cov"])
+        assert np.max(np.abs(C - Cr)) / np.max(np.abs(Cr)) < 1e-12
+    X[1, 7] = 0.5
+    r2 = _cov_exact_full(native, gpu_world, X)
+    assert not r2["scales_redone"] and not r2["fallback_fp64"]
+    Cr2 = np.cov(X.astype(np.float64).T, ddof=1)
+    assert np.max(np.abs(np.asarray(r2["cov"]) - Cr2)) / np.max(np.abs(Cr2)) < 1e-12
