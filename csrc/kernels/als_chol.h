@@ -243,7 +243,9 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
       float rt[16], m[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        rt[j] = __builtin_amdgcn_rcpf(t[j]);
+        // (rows of other blocks: a zero reciprocal broadcasts z = 0, so their zero coefficient
+        // leaves them bitwise untouched; 1/0 there would broadcast inf and 0 * inf = NaN)
+        rt[j] = mine ? __builtin_amdgcn_rcpf(t[j]) : 0.f;
         m[j] = rl == j ? 1.f : ((mine && rl > j) ? -t[j] : 0.f);
       }
       solve_steps_fwd<0>(rt, m, vd, rl);
@@ -303,7 +305,7 @@ __device__ inline void chol_solve(const float* M, float* bv, float& v0, float& v
       float rt[16], m[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        rt[j] = __builtin_amdgcn_rcpf(c[j]);
+        rt[j] = mine ? __builtin_amdgcn_rcpf(c[j]) : 0.f;
         m[j] = rl == j ? 1.f : ((mine && rl < j) ? -c[j] : 0.f);
       }
       solve_steps_bwd<15>(rt, m, vd, rl);
