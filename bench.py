@@ -30,8 +30,9 @@ contiguous shard directly in HBM (identical values for any N).
 the 288 GB HBM partition sizing case), same protocol.
 The timed region is bracketed by a barrier + device synchronize on both sides and the MAX over
 ranks is reported.  The untimed warmup runs max(W, K) iterations of the same fit, so every kernel
-variant the timed fit launches has had its code object loaded (HIP loads lazily, on first use).  `value` is whole-job samples/s = global_rows * K / t.  The end-to-end fit()
-wall clock (k-means|| init + Lloyd to convergence, maxIter=20, tol=1e-4) is reported alongside.
+variant the timed fit launches has had its code object loaded (HIP loads lazily, on first use).
+`value` is whole-job samples/s = global_rows * K / t.  The end-to-end fit() wall clock
+(k-means|| init + Lloyd to convergence, maxIter=20, tol=1e-4) is reported alongside.
 Other BASELINE configs: benchmarks/bench_pca.py, benchmarks/bench_als.py.
 """
 from __future__ import annotations
