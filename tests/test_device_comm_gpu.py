@@ -81,14 +81,19 @@ def test_kmeans_forced_rccl_bitwise(n, d, k):
     assert out[True][1] == out[False][1] and out[True][2] == out[False][2]
 
 
-def test_pca_forced_rccl_matches_local():
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_pca_forced_rccl_matches_local(dtype):
+    """f64 rows: the fp64-MFMA statistics; f32 rows: the int8 digit engine, whose error bound
+    rides in the one allreduce (an extra element after [S | c])."""
     rng = np.random.default_rng(9)
-    X = rng.normal(size=(40000, 40)) @ rng.normal(size=(40, 40)) + 20.0
+    X = (rng.normal(size=(40000, 40)) @ rng.normal(size=(40, 40)) + 20.0).astype(dtype)
     res = {}
     for force in (False, True):
         _world(force)
         m = O.PCA(k=6, inputCol="features").fit(X)
         assert m.fit_info["engine"] == "gpu"
+        assert m.fit_info["stats_engine"] == ("int8_digits" if dtype == np.float32
+                                              else "fp64_mfma")
         res[force] = (m.pc.toArray(), m.explainedVariance.toArray())
     O.shutdown_world()
     np.testing.assert_allclose(res[True][1], res[False][1], rtol=1e-9, atol=1e-12)
