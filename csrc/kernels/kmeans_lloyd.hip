@@ -1216,7 +1216,8 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  uint16_t* cl = reinterpret_cast<uint16_t*>(smem + L.cl) + wave * 64 * kCandList + lane;  // [slot * 64]
+  // (this lane's slots: [slot * 64])
+  uint16_t* cl = reinterpret_cast<uint16_t*>(smem + L.cl) + wave * 64 * kCandList + lane;
   // (the sub-segment counts loaded in parallel, then summed in LDS: one load latency, not 16)
   if (tid < a.row_subs) pref[tid + 1] = a.row_count[blockIdx.x * kDeferSubs + tid];
   __syncthreads();
