@@ -1076,19 +1076,28 @@ double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>&
   const size_t n = pts.size() / d;
   constexpr size_t kBlk = 512;  // points per block of the across-points loops (L1-resident sums)
   std::uniform_real_distribution<double> U(0.0, 1.0);
-  auto pick = [&](const std::vector<double>& mass) {  // Spark pickWeighted semantics
-    double tot = 0.0;
-    for (double v : mass) tot += v;
-    double r = U(rng) * tot, cum = 0.0;
-    size_t j = 0;
-    while (j < n && cum < r) cum += mass[j++];
-    return j == 0 ? size_t(0) : j - 1;
+  // Spark pickWeighted semantics: the first j with cum_j = mass_0 + .. + mass_{j-1} >= r (summed
+  // in index order), minus one.  The running sums are formed once per mass vector (prefix) and
+  // each draw is a binary search in them — the same sums in the same order, so the same pick as
+  // the per-draw scan, without a serial scan per draw.
+  std::vector<double> prefix(n + 1);
+  auto prefix_of = [&](const std::vector<double>& mass) {
+    double cum = 0.0;
+    prefix[0] = 0.0;
+    for (size_t j = 0; j < n; ++j) prefix[j + 1] = (cum += mass[j]);
+  };
+  auto pick = [&]() {  // (after prefix_of; masses are >= 0, so prefix is non-decreasing)
+    const double r = U(rng) * prefix[n];
+    const size_t j = size_t(std::lower_bound(prefix.begin(), prefix.end(), r) - prefix.begin());
+    const size_t jj = std::min(j, n);
+    return jj == 0 ? size_t(0) : jj - 1;
   };
   centers.assign(size_t(k) * d, 0.0);
   auto set_center = [&](int c, size_t i) {
     std::copy(pts.begin() + i * d, pts.begin() + (i + 1) * d, centers.begin() + size_t(c) * d);
   };
-  set_center(0, pick(w));
+  prefix_of(w);
+  set_center(0, pick());
   std::vector<double> cost(n), mass(n);
   for_points(pool, n, [&](size_t b, size_t e) {
     for (size_t i0 = b; i0 < e; i0 += kBlk)
@@ -1100,7 +1109,8 @@ double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>&
   std::vector<std::vector<double>> trial(trials, std::vector<double>(n));
   for (int c = 1; c < k; ++c) {
     for (size_t i = 0; i < n; ++i) mass[i] = w[i] * cost[i];
-    for (int t = 0; t < trials; ++t) cand[t] = pick(mass);  // same RNG order as drawing per trial
+    prefix_of(mass);
+    for (int t = 0; t < trials; ++t) cand[t] = pick();  // same RNG order as drawing per trial
     for_points(pool, n, [&](size_t b, size_t e) {
       for (int t = 0; t < trials; ++t) {
         const double* cc = pts.data() + cand[t] * d;
@@ -1114,9 +1124,13 @@ double kmeans_pp_once(const std::vector<double>& pts, const std::vector<double>&
     });
     int best_t = 0;
     double best_pot = std::numeric_limits<double>::infinity();
+    // every trial's potential summed in point order, the trials' sums interleaved (independent
+    // add chains in one sweep instead of one latency-bound chain after another)
+    std::vector<double> pots(trials, 0.0);
+    for (size_t i = 0; i < n; ++i)
+      for (int t = 0; t < trials; ++t) pots[t] += w[i] * trial[t][i];
     for (int t = 0; t < trials; ++t) {
-      double pot = 0.0;
-      for (size_t i = 0; i < n; ++i) pot += w[i] * trial[t][i];
+      const double pot = pots[t];
       if (pot < best_pot) {
         best_pot = pot;
         best_t = t;
