@@ -1156,9 +1156,7 @@ __global__ __launch_bounds__(exact_waves(KS, XB) * 64) void oap_kmeans_exact_row
 // a valid lower bound for every center left out.  Accumulation, labels, bounds, cost: as
 // oap_kmeans_exact_rows.
 constexpr int kCandWaves = 12;  // 3 per SIMD: latency-bound rows (the row in registers twice)
-constexpr int kCandList = 16;   // per-lane candidate slots (LDS, 16-bit center indices); more ->
-                                // the lane takes all its centers (a wave then loops over all of
-                                // them: 8 slots overflowed often enough to be most of the pass)
+constexpr int kCandList = 8;    // per-lane candidate slots (LDS); more -> the lane takes all
 
 struct CandSmem {
   size_t plane, cn, sc, acc, cnt, wc, pref, cl, total;
@@ -1180,7 +1178,7 @@ __host__ __device__ inline CandSmem cand_plan(int kpad, int k, int d, bool acc, 
   m.pref = off;
   off = round16(off + (kDeferSubs + 1) * 4);
   m.cl = off;
-  off = round16(off + size_t(kCandWaves) * 64 * kCandList * 2);
+  off = round16(off + size_t(kCandWaves) * 64 * kCandList * 4);
   m.acc = off;
   const size_t base = off;
   size_t accb = (acc && sums) ? size_t(k) * (d | 1) * 8 : 0;
@@ -1216,8 +1214,7 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  // (this lane's slots: [slot * 64])
-  uint16_t* cl = reinterpret_cast<uint16_t*>(smem + L.cl) + wave * 64 * kCandList + lane;
+  int* cl = reinterpret_cast<int*>(smem + L.cl) + wave * 64 * kCandList + lane;  // [slot * 64]
   // (the sub-segment counts loaded in parallel, then summed in LDS: one load latency, not 16)
   if (tid < a.row_subs) pref[tid + 1] = a.row_count[blockIdx.x * kDeferSubs + tid];
   __syncthreads();
@@ -1414,7 +1411,7 @@ __global__ __launch_bounds__(kCandWaves * 64) void oap_kmeans_exact_cand(KMeansA
         for (int e = 0; e < 16; ++e) {
           const int c = c0 + 8 * (e >> 2) + 4 * h + (e & 3);
           if (acc[e] <= T && c < k) {
-            if (ncand < kCandList) cl[ncand * 64] = static_cast<uint16_t>(c);
+            if (ncand < kCandList) cl[ncand * 64] = c;
             ++ncand;
           }
         }
