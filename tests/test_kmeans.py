@@ -192,6 +192,22 @@ def test_init_world_size_independent_draws(cpu_world, native):
     np.testing.assert_array_equal(c1, c2)
 
 
+def test_init_identical_for_any_host_pool(native):
+    """Local k-means++ (the k-means|| reduction: pool-parallel seeding trials and Lloyd sweeps,
+    every reduction over points in point order) gives the same centers for any host pool size."""
+    X, _ = blobs(4000, 12, 200, seed=5, sigma=1.5)
+    out = []
+    for threads in (1, 4):
+        O.shutdown_world()
+        w = O.init_world(O.get_config().replace(device="cpu", cpu_threads=threads), rank=0,
+                         size=1, local_rank=0)
+        t = native.upload_dense(w.ctx, X, "f64", 12)
+        out.append(np.asarray(native.kmeans_init(w.ctx, w.comm, t, 200, "k-means||", 2, 3)))
+        O.shutdown_world()
+    assert out[0].shape == (200, 12)
+    np.testing.assert_array_equal(out[0], out[1])
+
+
 # ------------------------------------------------------------------- persistence
 def test_read_write_all_params(cpu_world, tmp_path):
     df = generate_kmeans_data()
